@@ -1,0 +1,317 @@
+/*
+ * rvx.h — C ABI of the MI355X-native GNN-learned-index engine (librvx.so).
+ *
+ * This is the drop-in boundary for ruvector's hot path. Every entry point
+ * names the reference interface it replaces (paths relative to the
+ * Mu-L/ruvector checkout). Conventions:
+ *   - every function returns rvx_status (0 = RVX_OK); the status codes map
+ *     1:1 onto the reference error enums RuvectorError
+ *     (crates/ruvector-core/src/error.rs:8-60) and GnnError
+ *     (crates/ruvector-gnn/src/error.rs:12-55);
+ *   - rvx_last_error() returns the thread-local message of the last failure;
+ *   - inputs are caller-owned host pointers that the library copies on entry
+ *     (the `_device` / rvx_buffer variants take device-resident data instead);
+ *   - the library owns every handle it returns; handles are freed with the
+ *     matching *_destroy / *_free;
+ *   - search calls on one handle may run concurrently from several threads;
+ *     add/load calls need external exclusion (mirrors VectorDB's RwLock,
+ *     crates/ruvector-core/src/vector_db.rs:22-26).
+ * No torch, CUDA or compatibility types appear in these signatures.
+ */
+#ifndef RVX_RVX_H
+#define RVX_RVX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t rvx_status;
+
+enum {
+    RVX_OK = 0,
+    RVX_ERR_DIMENSION_MISMATCH = 1, /* RuvectorError::DimensionMismatch / GnnError::DimensionMismatch */
+    RVX_ERR_INVALID_PARAMETER = 2,  /* RuvectorError::InvalidParameter */
+    RVX_ERR_INDEX = 3,              /* RuvectorError::IndexError */
+    RVX_ERR_LAYER_CONFIG = 4,       /* GnnError::LayerConfig (layer.rs:100-106, :353-358) */
+    RVX_ERR_INVALID_SHAPE = 5,      /* GnnError::InvalidShape */
+    RVX_ERR_DEVICE = 6,             /* HIP runtime failure (no reference analogue) */
+    RVX_ERR_OUT_OF_MEMORY = 7,
+    RVX_ERR_UNSUPPORTED = 8,
+    RVX_ERR_SERIALIZATION = 9,      /* serde / bincode errors */
+    RVX_ERR_COMM = 10,              /* RCCL failure */
+    RVX_ERR_NOT_FOUND = 11          /* RuvectorError::VectorNotFound */
+};
+
+/* Distance metrics: crates/ruvector-core/src/types.rs:10-20 (DistanceMetric),
+ * plus the Poincaré ball distance of crates/ruvector-hyperbolic-hnsw/src/poincare.rs:227-255. */
+enum {
+    RVX_METRIC_L2 = 0,        /* Euclidean  -> distance.rs:27-43  */
+    RVX_METRIC_COSINE = 1,    /* Cosine     -> distance.rs:47-64  */
+    RVX_METRIC_DOT = 2,       /* DotProduct -> distance.rs:68-80  */
+    RVX_METRIC_L1 = 3,        /* Manhattan  -> distance.rs:84-86  */
+    RVX_METRIC_POINCARE = 4   /* poincare_distance (curvature c)  */
+};
+
+/* ------------------------------------------------------------------ */
+/* Library / device                                                    */
+/* ------------------------------------------------------------------ */
+int32_t rvx_last_error(char* buf, size_t len);     /* copies message; returns its length */
+const char* rvx_version(void);
+rvx_status rvx_device_count(int32_t* count);
+/* Select the HIP device used by the calling thread's library calls (default 0). */
+rvx_status rvx_set_device(int32_t device);
+rvx_status rvx_get_device(int32_t* device);
+/* Wait for all work the library queued on the current device. */
+rvx_status rvx_synchronize(void);
+/* Device properties: CU count, HBM bytes, arch name (e.g. "gfx950"). */
+rvx_status rvx_device_info(int32_t* num_cus, int64_t* hbm_bytes, char* arch, size_t arch_len);
+
+/* ------------------------------------------------------------------ */
+/* Device buffers (HBM-resident tensors; row-major, 256-B aligned)     */
+/* ------------------------------------------------------------------ */
+typedef struct rvx_buffer rvx_buffer;
+rvx_status rvx_buffer_alloc(int64_t bytes, rvx_buffer** out);
+rvx_status rvx_buffer_free(rvx_buffer* buf);
+int64_t    rvx_buffer_bytes(const rvx_buffer* buf);
+void*      rvx_buffer_device_ptr(rvx_buffer* buf);
+rvx_status rvx_buffer_upload(rvx_buffer* buf, const void* src, int64_t bytes, int64_t offset);
+rvx_status rvx_buffer_download(const rvx_buffer* buf, void* dst, int64_t bytes, int64_t offset);
+rvx_status rvx_buffer_zero(rvx_buffer* buf);
+
+/* Synthetic data generators (device side; the integer stream is shared with
+ * oracle/oracle.cpp so the CPU baseline sees identical inputs).
+ * uniform:  x_i = lo + (hi-lo) * u_i,  u_i = (h(seed,i) >> 40) * 2^-24
+ * normal:   Box–Muller on two uniforms (ruvector-bench DatasetGenerator,
+ *           crates/ruvector-bench/src/lib.rs:112-114)
+ * random_csr: out-degree `deg` per node, col = h(seed, i*deg+t) mod N. */
+rvx_status rvx_fill_uniform(rvx_buffer* buf, int64_t n_floats, uint64_t seed, float lo, float hi);
+rvx_status rvx_fill_normal(rvx_buffer* buf, int64_t n_floats, uint64_t seed);
+rvx_status rvx_normalize_rows(rvx_buffer* buf, int64_t rows, int32_t dim); /* L2, as hnsw_integration_test.rs:21-28 */
+rvx_status rvx_random_csr(int64_t n, int32_t deg, uint64_t seed, rvx_buffer* row_ptr_i64, rvx_buffer* col_i32);
+/* Rows [row_begin, row_begin+n_rows) of the same n_total-node random CSR
+ * (local row_ptr, global column ids): one node-range shard. */
+rvx_status rvx_random_csr_shard(int64_t n_total, int64_t row_begin, int64_t n_rows, int32_t deg, uint64_t seed,
+                                rvx_buffer* row_ptr_i64, rvx_buffer* col_i32);
+
+/* ------------------------------------------------------------------ */
+/* Graph (CSR by destination, neighbours in edge order)                */
+/* Replaces build_adjacency_list (crates/ruvector-postgres/src/gnn/     */
+/* message_passing.rs:34-50): adj[dst].push(src) in edge order, edges   */
+/* with an out-of-range endpoint dropped.                              */
+/* ------------------------------------------------------------------ */
+typedef struct rvx_graph rvx_graph;
+/* From (src,dst) edge pairs, optional per-edge weights (nullable). */
+rvx_status rvx_graph_from_edges(int64_t num_nodes, const int64_t* src, const int64_t* dst,
+                                int64_t num_edges, const float* edge_weights, rvx_graph** out);
+/* From a host CSR: row_ptr[n+1] (int64), col[E] (int32), weights[E] nullable. */
+rvx_status rvx_graph_from_csr(int64_t num_nodes, const int64_t* row_ptr, const int32_t* col,
+                              const float* edge_weights, rvx_graph** out);
+/* Adopt device-resident CSR buffers (copied by reference; caller keeps them alive). */
+rvx_status rvx_graph_from_device_csr(int64_t num_nodes, int64_t num_edges, rvx_buffer* row_ptr_i64,
+                                     rvx_buffer* col_i32, rvx_buffer* weights_f32 /*nullable*/,
+                                     rvx_graph** out);
+rvx_status rvx_graph_info(const rvx_graph* g, int64_t* num_nodes, int64_t* num_edges, int32_t* max_degree);
+rvx_status rvx_graph_destroy(rvx_graph* g);
+
+/* ------------------------------------------------------------------ */
+/* Message passing aggregators (aggregators.rs:35-92)                  */
+/* ------------------------------------------------------------------ */
+enum { RVX_AGG_SUM = 0, RVX_AGG_MEAN = 1, RVX_AGG_MAX = 2 };
+/* out[i] = agg_{j in adj(i)} (w_ij * x_j) over device buffers. Rows with no
+ * neighbours get zeros (sum/mean) or -inf (max) unless `keep_isolated`,
+ * in which case they get x_i (propagate, message_passing.rs:75-78). */
+rvx_status rvx_aggregate_device(const rvx_graph* g, int32_t agg, int32_t use_edge_weights,
+                                int32_t keep_isolated, const rvx_buffer* x, int32_t dim, rvx_buffer* out);
+
+/* ------------------------------------------------------------------ */
+/* GraphSAGE (crates/ruvector-postgres/src/gnn/graphsage.rs:25-196)    */
+/* ------------------------------------------------------------------ */
+typedef struct rvx_sage_layer rvx_sage_layer;
+enum { RVX_SAGE_MEAN = 0, RVX_SAGE_MAXPOOL = 1, RVX_SAGE_LSTM = 2 /* = mean, graphsage.rs:159 */ };
+/* w_neighbor/w_self: [in][out] row-major as GraphSAGELayer stores them; NULL
+ * for both selects the deterministic init of graphsage.rs:56-78.
+ * num_samples < max degree needs the StdRng(42) partial_shuffle sampling of
+ * graphsage.rs:92-102, which this engine rejects with RVX_ERR_UNSUPPORTED. */
+rvx_status rvx_sage_layer_create(int32_t in_features, int32_t out_features, int32_t num_samples,
+                                 int32_t aggregator, int32_t normalize, const float* w_neighbor,
+                                 const float* w_self, rvx_sage_layer** out);
+rvx_status rvx_sage_layer_destroy(rvx_sage_layer* l);
+/* GraphSAGELayer::forward (graphsage.rs:190-196) over host arrays. */
+rvx_status rvx_sage_forward(const rvx_sage_layer* l, const rvx_graph* g, const float* x, int64_t n,
+                            float* y);
+/* Same over HBM-resident buffers: x [n][in], y [n][out]. */
+rvx_status rvx_sage_forward_device(const rvx_sage_layer* l, const rvx_graph* g, const rvx_buffer* x,
+                                   rvx_buffer* y);
+/* Node-range shard: g holds this rank's destination rows
+ * [row_offset, row_offset + g.n) with GLOBAL column ids; x_full [N][in] is the
+ * all-gathered node table; y [g.n][out] receives the owned rows. */
+rvx_status rvx_sage_forward_shard_device(const rvx_sage_layer* l, const rvx_graph* g, const rvx_buffer* x_full,
+                                         int64_t row_offset, rvx_buffer* y);
+
+/* ------------------------------------------------------------------ */
+/* GCN (crates/ruvector-postgres/src/gnn/gcn.rs:12-149)                */
+/* ------------------------------------------------------------------ */
+typedef struct rvx_gcn_layer rvx_gcn_layer;
+/* weights [in][out] (NULL = deterministic init gcn.rs:32-41), bias [out] (NULL = zeros). */
+rvx_status rvx_gcn_layer_create(int32_t in_features, int32_t out_features, int32_t normalize,
+                                const float* weights, const float* bias, rvx_gcn_layer** out);
+rvx_status rvx_gcn_layer_destroy(rvx_gcn_layer* l);
+/* GCNLayer::forward (gcn.rs:93-112): propagate(_weighted) then ReLU. */
+rvx_status rvx_gcn_forward(const rvx_gcn_layer* l, const rvx_graph* g, int32_t use_edge_weights,
+                           const float* x, int64_t n, float* y);
+
+/* ------------------------------------------------------------------ */
+/* RuvectorLayer (crates/ruvector-gnn/src/layer.rs:313-457)            */
+/* ------------------------------------------------------------------ */
+typedef struct rvx_layer rvx_layer;
+/* RuvectorLayer::new (layer.rs:347-368). Weights are drawn from a seeded
+ * normal(0, sqrt(2/(in+out))) stream (the reference draws them from
+ * thread_rng, layer.rs:21-34, so they are an input for parity). */
+rvx_status rvx_gnn_layer_create(int32_t input_dim, int32_t hidden_dim, int32_t heads, float dropout,
+                                uint64_t seed, rvx_layer** out);
+/* serde_json form of RuvectorLayer (layer.rs:313-333; ndarray {v,dim,data}). */
+rvx_status rvx_gnn_layer_from_json(const char* json, rvx_layer** out);
+/* Writes the JSON into buf (NUL-terminated) if it fits; *len receives the size
+ * needed including the NUL. */
+rvx_status rvx_gnn_layer_to_json(const rvx_layer* l, char* buf, size_t* len);
+rvx_status rvx_gnn_layer_dims(const rvx_layer* l, int32_t* input_dim, int32_t* hidden_dim, int32_t* heads,
+                              float* dropout);
+rvx_status rvx_gnn_layer_destroy(rvx_layer* l);
+/* RuvectorLayer::forward for one node (layer.rs:379-418): node [in],
+ * nbrs [deg][in] contiguous, w [num_weights]. */
+rvx_status rvx_gnn_forward_one(const rvx_layer* l, const float* node, const float* nbrs, int32_t deg,
+                               const float* w, int32_t num_weights, float* out);
+/* Batched: every node i of the graph as `node`, its CSR row as neighbours
+ * (in edge order) and the CSR edge weights as `edge_weights`
+ * (nullable graph weights = empty weight slice, layer.rs:422-424). */
+rvx_status rvx_gnn_forward_graph(const rvx_layer* l, const rvx_graph* g, const float* x, int64_t n,
+                                 float* y);
+rvx_status rvx_gnn_forward_graph_device(const rvx_layer* l, const rvx_graph* g, const rvx_buffer* x,
+                                        rvx_buffer* y);
+
+/* differentiable_search (crates/ruvector-gnn/src/search.rs:56-94), batched:
+ * q [nq][d], cand [nq][c][d] -> idx [nq][k] (int64, -1 padded), w [nq][k]. */
+rvx_status rvx_differentiable_search_batch(const float* q, int64_t nq, const float* cand, int32_t c,
+                                           int32_t d, int32_t k, float temperature, int64_t* idx, float* w);
+
+/* ------------------------------------------------------------------ */
+/* Graph attention head: EdgeFeaturedAttention                         */
+/* (crates/ruvector-attention/src/graph/edge_featured.rs:87-320)       */
+/* ------------------------------------------------------------------ */
+typedef struct rvx_edge_attention rvx_edge_attention;
+typedef struct {
+    int32_t node_dim, edge_dim, num_heads; float dropout; int32_t concat_heads, add_self_loops;
+    float negative_slope;
+} rvx_edge_attention_config; /* EdgeFeaturedConfig, edge_featured.rs:11-33 */
+/* Deterministic LCG init of EdgeFeaturedAttention::new (edge_featured.rs:98-141). */
+rvx_status rvx_edge_attention_create(const rvx_edge_attention_config* cfg, rvx_edge_attention** out);
+rvx_status rvx_edge_attention_destroy(rvx_edge_attention* a);
+rvx_status rvx_edge_attention_dim(const rvx_edge_attention* a, int32_t* out_dim);
+/* compute_with_edges for one query (edge_featured.rs:196-258): keys/values [n][node_dim],
+ * edges [n][edge_dim] (NULL = zero edge features, i.e. Attention::compute, :267-288). */
+rvx_status rvx_edge_attention_compute(const rvx_edge_attention* a, const float* query, const float* keys,
+                                      const float* values, const float* edges, int32_t n, float* out);
+/* Whole graph: query = x_i, keys = values = x_j for j in adj(i),
+ * edges [E][edge_dim] in CSR order (nullable). Rows without neighbours
+ * return RVX_ERR_INVALID_PARAMETER unless add_self_loops (then key = x_i). */
+rvx_status rvx_edge_attention_forward_graph_device(const rvx_edge_attention* a, const rvx_graph* g,
+                                                   const rvx_buffer* x, const rvx_buffer* edge_feat,
+                                                   rvx_buffer* y);
+
+/* ------------------------------------------------------------------ */
+/* Vector index: VectorIndex (crates/ruvector-core/src/index.rs:11-36) */
+/*   FlatIndex (index/flat.rs) and HnswIndex (index/hnsw.rs)           */
+/* ------------------------------------------------------------------ */
+typedef struct rvx_index rvx_index;
+enum { RVX_INDEX_FLAT = 0, RVX_INDEX_HNSW = 1 };
+typedef struct {
+    int32_t kind;            /* RVX_INDEX_FLAT / RVX_INDEX_HNSW (VectorDB picks HNSW iff hnsw_config, vector_db.rs:81-98) */
+    int32_t dim;
+    int32_t metric;          /* RVX_METRIC_* */
+    int32_t m;               /* HnswConfig::m (types.rs:87-96: 32) */
+    int32_t ef_construction; /* 200 */
+    int32_t ef_search;       /* 100 */
+    int64_t max_elements;    /* 10_000_000 */
+    float   curvature;       /* POINCARE only */
+    uint64_t seed;           /* level-generator seed (the reference uses StdRng::from_entropy) */
+} rvx_index_config;
+rvx_status rvx_index_create(const rvx_index_config* cfg, rvx_index** out);
+rvx_status rvx_index_destroy(rvx_index* idx);
+/* add_batch: vecs [n][dim]; ids are the caller's dense u64 keys (VectorId). */
+rvx_status rvx_index_add_batch(rvx_index* idx, const float* vecs, const uint64_t* ids, int64_t n);
+rvx_status rvx_index_add_batch_device(rvx_index* idx, const rvx_buffer* vecs, int64_t n, uint64_t first_id);
+rvx_status rvx_index_len(const rvx_index* idx, int64_t* len);
+/* remove(id) (index/hnsw.rs:322-338): the id disappears from results; graph kept. */
+rvx_status rvx_index_remove(rvx_index* idx, uint64_t id, int32_t* removed);
+/* search (VectorIndex::search / HnswIndex::search_with_ef, index/hnsw.rs:231-260):
+ * q [nq][dim] -> out_ids [nq][k], out_dist [nq][k] ascending, out_count [nq].
+ * ef <= 0 selects cfg.ef_search. Unused slots: id UINT64_MAX, dist +inf. */
+rvx_status rvx_index_search(const rvx_index* idx, const float* q, int64_t nq, int32_t k, int32_t ef,
+                            uint64_t* out_ids, float* out_dist, int32_t* out_count);
+rvx_status rvx_index_search_device(const rvx_index* idx, const rvx_buffer* q, int64_t nq, int32_t k,
+                                   int32_t ef, rvx_buffer* out_ids_u64, rvx_buffer* out_dist_f32);
+/* Exact scan (FlatIndex::search, index/flat.rs:36-76): ties broken by id. */
+rvx_status rvx_index_brute_force(const rvx_index* idx, const float* q, int64_t nq, int32_t k,
+                                 uint64_t* out_ids, float* out_dist);
+rvx_status rvx_index_brute_force_device(const rvx_index* idx, const rvx_buffer* q, int64_t nq, int32_t k,
+                                        rvx_buffer* out_ids_u64, rvx_buffer* out_dist_f32);
+
+/* HNSW graph interchange (fixed-graph parity and GNN topology).
+ * Layer 0: CSR over all n points in stored neighbour order (hnsw_rs keeps
+ * every list sorted by distance to its owner, hnsw.rs:1186,1268).
+ * Upper layers l=1..max_level: points with level >= l, as a per-layer CSR
+ * over that sorted point list. */
+typedef struct {
+    int64_t n; int32_t max_level; int64_t entry_point;
+    const uint8_t* levels;          /* [n] */
+    const int64_t* row_ptr0;        /* [n+1] */
+    const int32_t* col0;            /* [row_ptr0[n]] */
+    const int64_t* upper_count;     /* [max_level+1], upper_count[0] unused */
+    const int32_t* const* upper_ids;      /* per layer l>=1: sorted point ids [upper_count[l]] */
+    const int64_t* const* upper_row_ptr;  /* per layer: [upper_count[l]+1] */
+    const int32_t* const* upper_col;      /* per layer */
+} rvx_hnsw_graph;
+rvx_status rvx_index_load_graph(rvx_index* idx, const rvx_hnsw_graph* g);
+/* Layer-0 adjacency export for the GNN (edge weight = stored distance). */
+rvx_status rvx_index_layer0_size(const rvx_index* idx, int64_t* n, int64_t* num_edges);
+rvx_status rvx_index_export_layer0(const rvx_index* idx, int64_t* row_ptr, int32_t* col, float* dist);
+
+/* ------------------------------------------------------------------ */
+/* Distances (distance.rs:9-107, poincare.rs:227-301)                  */
+/* ------------------------------------------------------------------ */
+/* out[i][j] = distance(q_i, x_j) for q [nq][d], x [n][d], in the reference's
+ * scalar accumulation order. */
+rvx_status rvx_distance_matrix(int32_t metric, const float* q, int64_t nq, const float* x, int64_t n,
+                               int32_t d, float curvature, float* out);
+
+/* ------------------------------------------------------------------ */
+/* Profiling: per-kernel device time measured with HIP events on the   */
+/* stream the kernels run on.                                          */
+/* ------------------------------------------------------------------ */
+rvx_status rvx_profile_enable(int32_t on);
+rvx_status rvx_profile_reset(void);
+/* Total milliseconds and launch count of every launch tagged `name`. */
+rvx_status rvx_profile_query(const char* name, double* total_ms, int64_t* launches);
+/* Comma-separated list of tags seen since the last reset. */
+rvx_status rvx_profile_names(char* buf, size_t len);
+
+/* ------------------------------------------------------------------ */
+/* Multi-GPU: node-range sharding with RCCL over xGMI   */
+/* ------------------------------------------------------------------ */
+typedef struct rvx_comm rvx_comm;
+#define RVX_COMM_ID_BYTES 128
+rvx_status rvx_comm_unique_id(uint8_t id[RVX_COMM_ID_BYTES]);
+rvx_status rvx_comm_init(const uint8_t id[RVX_COMM_ID_BYTES], int32_t nranks, int32_t rank, rvx_comm** out);
+rvx_status rvx_comm_destroy(rvx_comm* c);
+/* All-gather of equal row blocks: send [rows][cols] f32 from every rank into
+ * recv [nranks*rows][cols] (rank-major), on the library stream. */
+rvx_status rvx_comm_allgather_f32(rvx_comm* c, const rvx_buffer* send, int64_t count, rvx_buffer* recv);
+rvx_status rvx_comm_allreduce_max_f64(rvx_comm* c, double* value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RVX_RVX_H */

@@ -1,0 +1,27 @@
+"""ruvector_amd — MI355X-native GNN-learned-index hot path of ruvector.
+
+Every compute call goes through librvx.so (hand-written HIP kernels for
+gfx950, C ABI in include/rvx/rvx.h). Importing the package loads the library
+and fails loudly if it is missing; there is no CPU fallback.
+"""
+from . import _lib
+
+_lib.load()
+
+from ._lib import RvxError  # noqa: E402
+from .device import Buffer, Profiler, device_count, device_info, set_device, synchronize  # noqa: E402
+from .graph import Graph  # noqa: E402
+from .core import (DistanceMetric, FlatIndex, HnswConfig, HnswIndex, RuvectorError, SearchResult,  # noqa: E402
+                   batch_distances, distance, distance_matrix)
+from .gnn import (GCNLayer, GnnError, GraphSAGELayer, RuvectorLayer, aggregate, differentiable_search,  # noqa: E402
+                  differentiable_search_batch, hierarchical_forward)
+from .attention import EdgeFeaturedAttention, EdgeFeaturedConfig  # noqa: E402
+
+__all__ = [
+    "RvxError", "Buffer", "Profiler", "device_count", "device_info", "set_device", "synchronize", "Graph",
+    "DistanceMetric", "FlatIndex", "HnswConfig", "HnswIndex", "RuvectorError", "SearchResult", "batch_distances",
+    "distance", "distance_matrix", "GCNLayer", "GnnError", "GraphSAGELayer", "RuvectorLayer", "aggregate",
+    "differentiable_search", "differentiable_search_batch", "hierarchical_forward", "EdgeFeaturedAttention",
+    "EdgeFeaturedConfig",
+]
+__version__ = "0.1.0"

@@ -1,0 +1,189 @@
+// api_attention.cpp — EdgeFeaturedAttention (crates/ruvector-attention/src/graph/edge_featured.rs)
+// and the batched differentiable_search (crates/ruvector-gnn/src/search.rs:56-94).
+#include <cmath>
+
+#include "attn.hpp"
+#include "graph.hpp"
+#include "kernels.hpp"
+
+using namespace rvx;
+
+struct rvx_edge_attention {
+    rvx_edge_attention_config cfg{};
+    int hd = 0, D = 0;
+    std::vector<float> w_node, w_edge, a_src, a_dst, a_edge;
+    DevMem d_wnode, d_wedge, d_asrc, d_adst, d_aedge;
+};
+
+namespace {
+
+void upload_vec(DevMem& d, const std::vector<float>& v) {
+    d.reset((int64_t)std::max<size_t>(v.size(), 1) * 4);
+    d.upload(v.data(), (int64_t)v.size() * 4);
+}
+
+// One destination row per query row q of `tq`, neighbours given by rp/col.
+void run_efa(const rvx_edge_attention* a, int64_t n, const int64_t* rp, const int32_t* col, int64_t E, const float* tq,
+             const float* tk, const float* tv, const float* edges, float* out) {
+    EfaArgs ea;
+    ea.n = n; ea.heads = a->cfg.num_heads; ea.hd = a->hd; ea.edge_dim = a->cfg.edge_dim;
+    ea.concat = a->cfg.concat_heads ? 1 : 0; ea.slope = a->cfg.negative_slope;
+    ea.rp = rp; ea.col = col;
+    ea.tq = tq; ea.ldq = a->D; ea.tk = tk; ea.ldk = a->D; ea.tv = tv; ea.ldv = a->D;
+    ea.edges = (a->cfg.edge_dim > 0) ? edges : nullptr;
+    ea.w_edge = a->d_wedge.as<float>();
+    ea.a_src = a->d_asrc.as<float>(); ea.a_dst = a->d_adst.as<float>(); ea.a_edge = a->d_aedge.as<float>();
+    ea.scores = scratch_f32("efa_scores", std::max<int64_t>(E, 1) * a->cfg.num_heads);
+    ea.out = out;
+    edge_feat_attention(ea);
+}
+
+void transform(const rvx_edge_attention* a, const float* x, int64_t rows, float* t, const char* tag) {
+    // transform_node for every head at once: T = X W_node^T, W_node [heads*hd][node_dim]
+    gemm_nt(rows, a->D, GemmOperand{x, a->cfg.node_dim, a->d_wnode.as<float>(), a->cfg.node_dim, a->cfg.node_dim},
+            nullptr, GemmEpilogue(), t, a->D, tag);
+}
+
+}  // namespace
+
+extern "C" {
+
+rvx_status rvx_edge_attention_create(const rvx_edge_attention_config* cfg, rvx_edge_attention** out) {
+    return guard([&] {
+        RVX_REQUIRE(cfg && out, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(cfg->node_dim > 0 && cfg->num_heads > 0 && cfg->edge_dim >= 0, RVX_ERR_INVALID_PARAMETER,
+                    "bad EdgeFeaturedConfig");
+        RVX_REQUIRE(cfg->node_dim / cfg->num_heads > 0, RVX_ERR_INVALID_PARAMETER, "num_heads > node_dim");
+        auto a = std::make_unique<rvx_edge_attention>();
+        a->cfg = *cfg;
+        const int hd = cfg->node_dim / cfg->num_heads;  // EdgeFeaturedConfig::head_dim
+        a->hd = hd;
+        a->D = hd * cfg->num_heads;
+        // EdgeFeaturedAttention::new (edge_featured.rs:98-141): LCG seed 42.
+        const float node_scale = std::sqrt(2.0f / (float)(cfg->node_dim + hd));
+        const float edge_scale = std::sqrt(2.0f / (float)(cfg->edge_dim + hd));
+        const float attn_scale = std::sqrt(1.0f / (float)hd);
+        uint64_t seed = 42;
+        auto rnd = [&]() {
+            seed = seed * 6364136223846793005ull + 1ull;
+            return (float)seed / (float)UINT64_MAX - 0.5f;
+        };
+        const int64_t H = cfg->num_heads;
+        a->w_node.resize(H * hd * cfg->node_dim);
+        for (auto& v : a->w_node) v = rnd() * 2.0f * node_scale;
+        a->w_edge.resize(H * hd * cfg->edge_dim);
+        for (auto& v : a->w_edge) v = rnd() * 2.0f * edge_scale;
+        a->a_src.resize(H * hd);
+        for (auto& v : a->a_src) v = rnd() * 2.0f * attn_scale;
+        a->a_dst.resize(H * hd);
+        for (auto& v : a->a_dst) v = rnd() * 2.0f * attn_scale;
+        a->a_edge.resize(H * hd);
+        for (auto& v : a->a_edge) v = rnd() * 2.0f * attn_scale;
+        upload_vec(a->d_wnode, a->w_node);
+        upload_vec(a->d_wedge, a->w_edge);
+        upload_vec(a->d_asrc, a->a_src);
+        upload_vec(a->d_adst, a->a_dst);
+        upload_vec(a->d_aedge, a->a_edge);
+        *out = a.release();
+    });
+}
+
+rvx_status rvx_edge_attention_destroy(rvx_edge_attention* a) {
+    return guard([&] { delete a; });
+}
+
+rvx_status rvx_edge_attention_dim(const rvx_edge_attention* a, int32_t* out_dim) {
+    return guard([&] {
+        RVX_REQUIRE(a && out_dim, RVX_ERR_INVALID_PARAMETER, "null argument");
+        *out_dim = a->cfg.concat_heads ? a->D : a->hd;
+    });
+}
+
+rvx_status rvx_edge_attention_compute(const rvx_edge_attention* a, const float* query, const float* keys,
+                                      const float* values, const float* edges, int32_t n, float* out) {
+    return guard([&] {
+        RVX_REQUIRE(a && query && out && n >= 0, RVX_ERR_INVALID_PARAMETER, "bad arguments");
+        // Attention::compute rejects empty keys (edge_featured.rs:273-275).
+        RVX_REQUIRE(edges != nullptr || n > 0, RVX_ERR_INVALID_PARAMETER, "Empty keys");
+        RVX_REQUIRE(n == 0 || (keys && values), RVX_ERR_INVALID_PARAMETER, "null keys/values");
+        ComputeLock cl;
+        const int nd = a->cfg.node_dim, D = a->D;
+        const int64_t nn = std::max(n, 1);
+        float* dq = scratch_f32("efa1_q", nd);
+        float* dk = scratch_f32("efa1_k", nn * nd);
+        float* dv = scratch_f32("efa1_v", nn * nd);
+        float* tq = scratch_f32("efa1_tq", D);
+        float* tk = scratch_f32("efa1_tk", nn * D);
+        float* tv = scratch_f32("efa1_tv", nn * D);
+        float* de = scratch_f32("efa1_e", nn * std::max(a->cfg.edge_dim, 1));
+        float* dout = scratch_f32("efa1_out", D);
+        auto* rp = (int64_t*)scratch_bytes("efa1_rp", 16);
+        auto* col = (int32_t*)scratch_bytes("efa1_col", nn * 4);
+        std::vector<int64_t> hrp{0, n};
+        std::vector<int32_t> hcol(nn);
+        for (int j = 0; j < n; ++j) hcol[j] = j;
+        RVX_HIP(hipMemcpyAsync(dq, query, (size_t)nd * 4, hipMemcpyHostToDevice, stream()));
+        if (n) {
+            RVX_HIP(hipMemcpyAsync(dk, keys, (size_t)n * nd * 4, hipMemcpyHostToDevice, stream()));
+            RVX_HIP(hipMemcpyAsync(dv, values, (size_t)n * nd * 4, hipMemcpyHostToDevice, stream()));
+            if (edges && a->cfg.edge_dim > 0)
+                RVX_HIP(hipMemcpyAsync(de, edges, (size_t)n * a->cfg.edge_dim * 4, hipMemcpyHostToDevice, stream()));
+        }
+        RVX_HIP(hipMemcpyAsync(rp, hrp.data(), 16, hipMemcpyHostToDevice, stream()));
+        RVX_HIP(hipMemcpyAsync(col, hcol.data(), (size_t)nn * 4, hipMemcpyHostToDevice, stream()));
+        transform(a, dq, 1, tq, "efa_transform");
+        if (n) {
+            transform(a, dk, n, tk, "efa_transform");
+            transform(a, dv, n, tv, "efa_transform");
+        }
+        run_efa(a, 1, rp, col, n, tq, tk, tv, (edges && a->cfg.edge_dim > 0) ? de : nullptr, dout);
+        const int od = a->cfg.concat_heads ? D : a->hd;
+        RVX_HIP(hipMemcpyAsync(out, dout, (size_t)od * 4, hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
+rvx_status rvx_edge_attention_forward_graph_device(const rvx_edge_attention* a, const rvx_graph* g, const rvx_buffer* x,
+                                                   const rvx_buffer* ef, rvx_buffer* y) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(a && x && y, RVX_ERR_INVALID_PARAMETER, "null argument");
+        const int nd = a->cfg.node_dim;
+        const int od = a->cfg.concat_heads ? a->D : a->hd;
+        RVX_REQUIRE(x->mem.bytes >= g->n * nd * 4, RVX_ERR_DIMENSION_MISMATCH, "x smaller than n*node_dim");
+        RVX_REQUIRE(y->mem.bytes >= g->n * od * 4, RVX_ERR_DIMENSION_MISMATCH, "y smaller than n*out_dim");
+        RVX_REQUIRE(!ef || ef->mem.bytes >= g->e * a->cfg.edge_dim * 4, RVX_ERR_DIMENSION_MISMATCH,
+                    "edge features smaller than E*edge_dim");
+        ComputeLock cl;
+        float* t = scratch_f32("efa_t", g->n * (int64_t)a->D);
+        transform(a, x->mem.as<float>(), g->n, t, "efa_transform");
+        run_efa(a, g->n, g->row_ptr, g->col, g->e, t, t, t, ef ? ef->mem.as<float>() : nullptr, y->mem.as<float>());
+    });
+}
+
+rvx_status rvx_differentiable_search_batch(const float* q, int64_t nq, const float* cand, int32_t c, int32_t d, int32_t k,
+                                           float temperature, int64_t* idx, float* w) {
+    return guard([&] {
+        RVX_REQUIRE(nq >= 0 && c >= 0 && d > 0 && k >= 0, RVX_ERR_INVALID_PARAMETER, "bad sizes");
+        if (nq == 0 || k == 0) return;
+        RVX_REQUIRE(q && idx && w && (c == 0 || cand), RVX_ERR_INVALID_PARAMETER, "null argument");
+        if (c == 0) {  // empty candidates -> empty result (search.rs:62-64)
+            for (int64_t i = 0; i < nq * k; ++i) { idx[i] = -1; w[i] = 0.0f; }
+            return;
+        }
+        ComputeLock cl;
+        float* dq = scratch_f32("ds_q", nq * d);
+        float* dc = scratch_f32("ds_c", nq * c * (int64_t)d);
+        float* ds = scratch_f32("ds_s", nq * c);
+        auto* di = (int64_t*)scratch_bytes("ds_i", nq * k * 8);
+        float* dw = scratch_f32("ds_w", nq * k);
+        RVX_HIP(hipMemcpyAsync(dq, q, (size_t)(nq * d * 4), hipMemcpyHostToDevice, stream()));
+        RVX_HIP(hipMemcpyAsync(dc, cand, (size_t)(nq * c * (int64_t)d * 4), hipMemcpyHostToDevice, stream()));
+        differentiable_search(dq, nq, dc, c, d, k, temperature, ds, di, dw);
+        RVX_HIP(hipMemcpyAsync(idx, di, (size_t)(nq * k * 8), hipMemcpyDeviceToHost, stream()));
+        RVX_HIP(hipMemcpyAsync(w, dw, (size_t)(nq * k * 4), hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+// api_comm.cpp — RCCL communicator for node-range sharding over xGMI.
+// One process per GPU; the unique id travels over the host launcher's store.
+// The only data-path collective of the path is the per-layer all-gather of
+// node tables (GNN halo); HNSW shards merge per-shard top-k.
+#include <rccl/rccl.h>
+
+#include "graph.hpp"
+
+using namespace rvx;
+
+struct rvx_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 0, rank = 0;
+};
+
+#define RVX_NCCL(expr)                                                                         \
+    do {                                                                                       \
+        ncclResult_t r_ = (expr);                                                              \
+        if (r_ != ncclSuccess) ::rvx::fail(RVX_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+static_assert(sizeof(ncclUniqueId) == RVX_COMM_ID_BYTES, "ncclUniqueId size");
+
+extern "C" {
+
+rvx_status rvx_comm_unique_id(uint8_t id[RVX_COMM_ID_BYTES]) {
+    return guard([&] {
+        RVX_REQUIRE(id, RVX_ERR_INVALID_PARAMETER, "null id");
+        ncclUniqueId u;
+        RVX_NCCL(ncclGetUniqueId(&u));
+        std::memcpy(id, &u, sizeof u);
+    });
+}
+
+rvx_status rvx_comm_init(const uint8_t id[RVX_COMM_ID_BYTES], int32_t nranks, int32_t rank, rvx_comm** out) {
+    return guard([&] {
+        RVX_REQUIRE(id && out && nranks > 0 && rank >= 0 && rank < nranks, RVX_ERR_INVALID_PARAMETER, "bad comm args");
+        device();  // bind the calling thread's device first
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof u);
+        auto c = std::make_unique<rvx_comm>();
+        RVX_NCCL(ncclCommInitRank(&c->comm, nranks, u, rank));
+        c->nranks = nranks;
+        c->rank = rank;
+        *out = c.release();
+    });
+}
+
+rvx_status rvx_comm_destroy(rvx_comm* c) {
+    return guard([&] {
+        if (c && c->comm) ncclCommDestroy(c->comm);
+        delete c;
+    });
+}
+
+rvx_status rvx_comm_allgather_f32(rvx_comm* c, const rvx_buffer* send, int64_t count, rvx_buffer* recv) {
+    return guard([&] {
+        RVX_REQUIRE(c && send && recv && count >= 0, RVX_ERR_INVALID_PARAMETER, "bad all-gather args");
+        RVX_REQUIRE(send->mem.bytes >= count * 4 && recv->mem.bytes >= count * 4 * c->nranks, RVX_ERR_INVALID_PARAMETER,
+                    "all-gather buffers too small");
+        ProfScope ps("rccl_allgather");
+        RVX_NCCL(ncclAllGather(send->mem.p, recv->mem.p, (size_t)count, ncclFloat32, c->comm, stream()));
+    });
+}
+
+rvx_status rvx_comm_allreduce_max_f64(rvx_comm* c, double* value) {
+    return guard([&] {
+        RVX_REQUIRE(c && value, RVX_ERR_INVALID_PARAMETER, "null argument");
+        double* d = (double*)scratch_bytes("comm_scalar", 8);
+        RVX_HIP(hipMemcpyAsync(d, value, 8, hipMemcpyHostToDevice, stream()));
+        RVX_NCCL(ncclAllReduce(d, d, 1, ncclFloat64, ncclMax, c->comm, stream()));
+        RVX_HIP(hipMemcpyAsync(value, d, 8, hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
+}  // extern "C"

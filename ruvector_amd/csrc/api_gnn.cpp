@@ -1,0 +1,381 @@
+// api_gnn.cpp — RuvectorLayer (crates/ruvector-gnn/src/layer.rs:313-457) and
+// differentiable_search (crates/ruvector-gnn/src/search.rs:4-94) over HBM.
+//
+// Batched forward of every node of a graph (node = x_i, neighbours = its CSR
+// row in edge order, edge_weights = the row's edge weights):
+//   M    = X W_msg^T + b_msg                              GEMM   (layer.rs:392-396)
+//   QKV  = M [W_q;W_k;W_v]^T + [b_q;b_k;b_v]              GEMM   (layer.rs:135-137)
+//   ATT, WAGG = edge kernel                               K5     (layer.rs:139-207, 421-445)
+//   COMB = ATT W_o^T + b_o + WAGG                         GEMM   (layer.rs:159, 407)
+//   AGG  = COMB W_agg^T + b_agg                           GEMM   (layer.rs:408)
+//   ZR   = sigmoid(AGG [W_z;W_r]^T + M [U_z;U_r]^T + b)   GEMM   (layer.rs:257-262)
+//   RH   = R ⊙ M ;  HT = tanh(AGG W_h^T + RH U_h^T + b)  GEMM   (layer.rs:265-267)
+//   Y    = LayerNorm((1-Z)⊙M + Z⊙HT) × (1-dropout))        finish (layer.rs:270-274, 414-417)
+// Nodes without neighbours get LayerNorm(M_i) (layer.rs:385-389).
+// K/V are computed once per node instead of once per (destination, neighbour)
+// pair as the reference does; the values are the same Linear outputs.
+#include <cmath>
+#include <cstring>
+
+#include "gnn.hpp"
+#include "graph.hpp"
+#include "json.hpp"
+#include "kernels.hpp"
+
+using namespace rvx;
+
+namespace {
+
+struct HostLinear {
+    int out = 0, in = 0;
+    std::vector<float> w;  // [out][in]
+    std::vector<float> b;  // [out]
+};
+
+uint64_t sm64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// Linear::new (layer.rs:21-34): weights ~ N(0, sqrt(2/(in+out))), bias 0. The
+// reference uses thread_rng; here a seeded counter stream.
+HostLinear make_linear(int in, int out, uint64_t seed) {
+    HostLinear l;
+    l.in = in; l.out = out;
+    l.w.resize((size_t)in * out);
+    l.b.assign(out, 0.0f);
+    const double scale = std::sqrt(2.0f / (float)(in + out));
+    const uint64_t s0 = sm64(seed);
+    for (size_t i = 0; i < l.w.size(); ++i) {
+        const double u1 = ((double)(sm64(s0 + 2 * i) >> 11) + 1.0) * (1.0 / 9007199254740992.0);
+        const double u2 = (double)(sm64(s0 + 2 * i + 1) >> 11) * (1.0 / 9007199254740992.0);
+        l.w[i] = (float)(scale * std::sqrt(-2.0 * std::log(u1)) * std::cos(6.283185307179586 * u2));
+    }
+    return l;
+}
+
+}  // namespace
+
+struct rvx_layer {
+    int in = 0, H = 0, heads = 0, hd = 0;
+    float dropout = 0.0f;
+    HostLinear w_msg, w_agg, w_z, u_z, w_r, u_r, w_h, u_h, q, k, v, o;
+    std::vector<float> gamma, beta;
+    float eps = 1e-5f;
+    // device
+    DevMem d_wmsg, d_bmsg, d_wqkv, d_bqkv, d_wo, d_bo, d_wagg, d_bagg, d_wzr, d_uzr, d_bwzr, d_buzr, d_wh, d_uh, d_bwh,
+        d_buh, d_gamma, d_beta;
+};
+
+namespace {
+
+void upload(DevMem& d, const std::vector<float>& v) {
+    d.reset((int64_t)std::max<size_t>(v.size(), 1) * 4);
+    d.upload(v.data(), (int64_t)v.size() * 4);
+}
+std::vector<float> cat(std::initializer_list<const std::vector<float>*> parts) {
+    std::vector<float> r;
+    for (auto* p : parts) r.insert(r.end(), p->begin(), p->end());
+    return r;
+}
+
+void validate(const rvx_layer* l) {
+    RVX_REQUIRE(l->dropout >= 0.0f && l->dropout <= 1.0f, RVX_ERR_LAYER_CONFIG,
+                "Dropout must be between 0.0 and 1.0");
+    RVX_REQUIRE(l->heads > 0 && l->H % l->heads == 0, RVX_ERR_LAYER_CONFIG,
+                "Embedding dimension must be divisible by number of heads");
+    auto chk = [&](const HostLinear& x, int out, int in, const char* name) {
+        RVX_REQUIRE(x.out == out && x.in == in && (int64_t)x.w.size() == (int64_t)out * in && (int)x.b.size() == out,
+                    RVX_ERR_INVALID_SHAPE, std::string("bad shape for ") + name);
+    };
+    chk(l->w_msg, l->H, l->in, "w_msg");
+    for (auto* p : {&l->w_agg, &l->w_z, &l->u_z, &l->w_r, &l->u_r, &l->w_h, &l->u_h, &l->q, &l->k, &l->v, &l->o})
+        chk(*p, l->H, l->H, "hidden linear");
+    RVX_REQUIRE((int)l->gamma.size() == l->H && (int)l->beta.size() == l->H, RVX_ERR_INVALID_SHAPE, "bad norm shape");
+}
+
+void upload_layer(rvx_layer* l) {
+    upload(l->d_wmsg, l->w_msg.w); upload(l->d_bmsg, l->w_msg.b);
+    upload(l->d_wqkv, cat({&l->q.w, &l->k.w, &l->v.w})); upload(l->d_bqkv, cat({&l->q.b, &l->k.b, &l->v.b}));
+    upload(l->d_wo, l->o.w); upload(l->d_bo, l->o.b);
+    upload(l->d_wagg, l->w_agg.w); upload(l->d_bagg, l->w_agg.b);
+    upload(l->d_wzr, cat({&l->w_z.w, &l->w_r.w})); upload(l->d_uzr, cat({&l->u_z.w, &l->u_r.w}));
+    upload(l->d_bwzr, cat({&l->w_z.b, &l->w_r.b})); upload(l->d_buzr, cat({&l->u_z.b, &l->u_r.b}));
+    upload(l->d_wh, l->w_h.w); upload(l->d_uh, l->u_h.w); upload(l->d_bwh, l->w_h.b); upload(l->d_buh, l->u_h.b);
+    upload(l->d_gamma, l->gamma); upload(l->d_beta, l->beta);
+}
+
+// ---- serde JSON ------------------------------------------------------------
+std::vector<float> arr_data(const json::Value* a, std::vector<int64_t>& dim) {
+    RVX_REQUIRE(a && a->kind == json::Value::Object, RVX_ERR_SERIALIZATION, "expected ndarray object");
+    const json::Value* d = a->get("dim");
+    const json::Value* data = a->get("data");
+    RVX_REQUIRE(d && d->kind == json::Value::Array && data && data->kind == json::Value::Array, RVX_ERR_SERIALIZATION,
+                "ndarray needs dim and data");
+    dim.clear();
+    int64_t total = 1;
+    for (auto& x : d->arr) { dim.push_back((int64_t)x.num); total *= (int64_t)x.num; }
+    RVX_REQUIRE((int64_t)data->arr.size() == total, RVX_ERR_SERIALIZATION, "ndarray data length != prod(dim)");
+    std::vector<float> v(total);
+    for (int64_t i = 0; i < total; ++i)
+        v[i] = data->arr[i].kind == json::Value::Number ? (float)data->arr[i].num : NAN;
+    return v;
+}
+HostLinear linear_from(const json::Value* o, const char* name) {
+    RVX_REQUIRE(o && o->kind == json::Value::Object, RVX_ERR_SERIALIZATION, std::string("missing ") + name);
+    HostLinear l;
+    std::vector<int64_t> dw, db;
+    l.w = arr_data(o->get("weights"), dw);
+    l.b = arr_data(o->get("bias"), db);
+    RVX_REQUIRE(dw.size() == 2 && db.size() == 1, RVX_ERR_SERIALIZATION, std::string("bad dims for ") + name);
+    l.out = (int)dw[0]; l.in = (int)dw[1];
+    return l;
+}
+void put_arr(std::string& s, const std::vector<float>& v, std::initializer_list<int64_t> dim) {
+    s += "{\"v\":1,\"dim\":[";
+    bool first = true;
+    for (auto d : dim) { if (!first) s += ","; s += std::to_string(d); first = false; }
+    s += "],\"data\":[";
+    for (size_t i = 0; i < v.size(); ++i) { if (i) s += ","; json::put_f32(s, v[i]); }
+    s += "]}";
+}
+void put_linear(std::string& s, const HostLinear& l) {
+    s += "{\"weights\":"; put_arr(s, l.w, {l.out, l.in});
+    s += ",\"bias\":"; put_arr(s, l.b, {l.out});
+    s += "}";
+}
+
+// ---- batched forward ---------------------------------------------------------
+// wmode: 0 no weights, 1 raw per-edge weights (graph), 2 pre-normalised.
+void forward_dev(const rvx_layer* l, int64_t n, const int64_t* rp, const int32_t* col, int64_t E, const float* w,
+                 int wmode, const float* x, float* y) {
+    const int H = l->H;
+    float* M = scratch_f32("rvl_m", n * H);
+    float* S1 = scratch_f32("rvl_s1", n * 3 * (int64_t)H);
+    float* S2 = scratch_f32("rvl_s2", n * H);
+    float* S3 = scratch_f32("rvl_s3", n * H);
+    float* S4 = scratch_f32("rvl_s4", n * H);
+    float* scores = scratch_f32("rvl_scores", std::max<int64_t>(E, 1) * l->heads);
+
+    GemmEpilogue ep;
+    ep.bias0 = l->d_bmsg.as<float>();
+    gemm_nt(n, H, GemmOperand{x, l->in, l->d_wmsg.as<float>(), l->in, l->in}, nullptr, ep, M, H, "gnn_gemm_msg");
+    ep = GemmEpilogue();
+    ep.bias0 = l->d_bqkv.as<float>();
+    gemm_nt(n, 3 * H, GemmOperand{M, H, l->d_wqkv.as<float>(), H, H}, nullptr, ep, S1, 3 * H, "gnn_gemm_qkv");
+
+    EdgeArgs ea;
+    ea.n = n; ea.H = H; ea.heads = l->heads; ea.hd = l->hd; ea.G = edge_group_lanes(H, l->heads);
+    ea.rp = rp; ea.col = col; ea.w = w; ea.wmode = w ? wmode : 0;
+    ea.qkv = S1; ea.m = M; ea.scores = scores; ea.att = S2; ea.wagg = S3;
+    edge_attention(ea);
+
+    ep = GemmEpilogue();
+    ep.bias0 = l->d_bo.as<float>();
+    ep.addend = S3; ep.ld_addend = H;
+    gemm_nt(n, H, GemmOperand{S2, H, l->d_wo.as<float>(), H, H}, nullptr, ep, S4, H, "gnn_gemm_out");  // COMB
+    ep = GemmEpilogue();
+    ep.bias0 = l->d_bagg.as<float>();
+    gemm_nt(n, H, GemmOperand{S4, H, l->d_wagg.as<float>(), H, H}, nullptr, ep, S2, H, "gnn_gemm_agg");  // AGG
+    ep = GemmEpilogue();
+    ep.epi = GEMM_EPI_SIGMOID; ep.bias0 = l->d_bwzr.as<float>(); ep.bias1 = l->d_buzr.as<float>();
+    GemmOperand zr_b{M, H, l->d_uzr.as<float>(), H, H};
+    gemm_nt(n, 2 * H, GemmOperand{S2, H, l->d_wzr.as<float>(), H, H}, &zr_b, ep, S1, 2 * H, "gnn_gemm_zr");
+    mul_rows(S1 + H, 2 * (int64_t)H, M, S3, n, H);  // RH = r ⊙ h
+    ep = GemmEpilogue();
+    ep.epi = GEMM_EPI_TANH; ep.bias0 = l->d_bwh.as<float>(); ep.bias1 = l->d_buh.as<float>();
+    GemmOperand h_b{S3, H, l->d_uh.as<float>(), H, H};
+    gemm_nt(n, H, GemmOperand{S2, H, l->d_wh.as<float>(), H, H}, &h_b, ep, S4, H, "gnn_gemm_h");  // HT
+
+    FinishArgs fa;
+    fa.n = n; fa.H = H; fa.rp = rp; fa.m = M; fa.zr = S1; fa.ht = S4;
+    fa.gamma = l->d_gamma.as<float>(); fa.beta = l->d_beta.as<float>(); fa.eps = l->eps;
+    fa.keep = 1.0f - l->dropout;
+    fa.y = y;
+    gru_finish(fa);
+}
+
+}  // namespace
+
+extern "C" {
+
+rvx_status rvx_gnn_layer_create(int32_t in, int32_t hidden, int32_t heads, float dropout, uint64_t seed,
+                                rvx_layer** out) {
+    return guard([&] {
+        RVX_REQUIRE(out && in > 0 && hidden > 0, RVX_ERR_LAYER_CONFIG, "dimensions must be positive");
+        RVX_REQUIRE(dropout >= 0.0f && dropout <= 1.0f, RVX_ERR_LAYER_CONFIG,
+                    "Dropout must be between 0.0 and 1.0, got " + std::to_string(dropout));
+        RVX_REQUIRE(heads > 0 && hidden % heads == 0, RVX_ERR_LAYER_CONFIG,
+                    "Embedding dimension (" + std::to_string(hidden) + ") must be divisible by number of heads (" +
+                        std::to_string(heads) + ")");
+        auto l = std::make_unique<rvx_layer>();
+        l->in = in; l->H = hidden; l->heads = heads; l->hd = hidden / heads; l->dropout = dropout;
+        uint64_t s = seed * 1315423911ull;
+        l->w_msg = make_linear(in, hidden, s + 1);
+        l->w_agg = make_linear(hidden, hidden, s + 2);
+        l->w_z = make_linear(hidden, hidden, s + 3); l->u_z = make_linear(hidden, hidden, s + 4);
+        l->w_r = make_linear(hidden, hidden, s + 5); l->u_r = make_linear(hidden, hidden, s + 6);
+        l->w_h = make_linear(hidden, hidden, s + 7); l->u_h = make_linear(hidden, hidden, s + 8);
+        l->q = make_linear(hidden, hidden, s + 9); l->k = make_linear(hidden, hidden, s + 10);
+        l->v = make_linear(hidden, hidden, s + 11); l->o = make_linear(hidden, hidden, s + 12);
+        l->gamma.assign(hidden, 1.0f); l->beta.assign(hidden, 0.0f); l->eps = 1e-5f;
+        validate(l.get());
+        upload_layer(l.get());
+        *out = l.release();
+    });
+}
+
+rvx_status rvx_gnn_layer_from_json(const char* text, rvx_layer** out) {
+    return guard([&] {
+        RVX_REQUIRE(text && out, RVX_ERR_INVALID_PARAMETER, "null argument");
+        json::Value root;
+        std::string err;
+        RVX_REQUIRE(json::parse(text, root, err), RVX_ERR_SERIALIZATION, "Deserialization error: " + err);
+        RVX_REQUIRE(root.kind == json::Value::Object, RVX_ERR_SERIALIZATION, "expected a JSON object");
+        auto l = std::make_unique<rvx_layer>();
+        l->w_msg = linear_from(root.get("w_msg"), "w_msg");
+        l->w_agg = linear_from(root.get("w_agg"), "w_agg");
+        const json::Value* up = root.get("w_update");
+        RVX_REQUIRE(up, RVX_ERR_SERIALIZATION, "missing w_update");
+        l->w_z = linear_from(up->get("w_z"), "w_z"); l->u_z = linear_from(up->get("u_z"), "u_z");
+        l->w_r = linear_from(up->get("w_r"), "w_r"); l->u_r = linear_from(up->get("u_r"), "u_r");
+        l->w_h = linear_from(up->get("w_h"), "w_h"); l->u_h = linear_from(up->get("u_h"), "u_h");
+        const json::Value* at = root.get("attention");
+        RVX_REQUIRE(at && at->get("num_heads") && at->get("head_dim"), RVX_ERR_SERIALIZATION, "missing attention");
+        l->heads = (int)at->get("num_heads")->num;
+        l->hd = (int)at->get("head_dim")->num;
+        l->q = linear_from(at->get("q_linear"), "q_linear"); l->k = linear_from(at->get("k_linear"), "k_linear");
+        l->v = linear_from(at->get("v_linear"), "v_linear"); l->o = linear_from(at->get("out_linear"), "out_linear");
+        const json::Value* nm = root.get("norm");
+        RVX_REQUIRE(nm && nm->get("eps"), RVX_ERR_SERIALIZATION, "missing norm");
+        std::vector<int64_t> dg, db;
+        l->gamma = arr_data(nm->get("gamma"), dg);
+        l->beta = arr_data(nm->get("beta"), db);
+        l->eps = (float)nm->get("eps")->num;
+        const json::Value* dr = root.get("dropout");
+        RVX_REQUIRE(dr && dr->kind == json::Value::Number, RVX_ERR_SERIALIZATION, "missing dropout");
+        l->dropout = (float)dr->num;
+        l->in = l->w_msg.in;
+        l->H = l->w_msg.out;
+        RVX_REQUIRE(l->heads * l->hd == l->H, RVX_ERR_SERIALIZATION, "num_heads*head_dim != hidden_dim");
+        validate(l.get());
+        upload_layer(l.get());
+        *out = l.release();
+    });
+}
+
+rvx_status rvx_gnn_layer_to_json(const rvx_layer* l, char* buf, size_t* len) {
+    return guard([&] {
+        RVX_REQUIRE(l && len, RVX_ERR_INVALID_PARAMETER, "null argument");
+        std::string s;
+        s.reserve((size_t)(12 * (int64_t)l->H * l->H + l->H * l->in) * 12);
+        s += "{\"w_msg\":"; put_linear(s, l->w_msg);
+        s += ",\"w_agg\":"; put_linear(s, l->w_agg);
+        s += ",\"w_update\":{\"w_z\":"; put_linear(s, l->w_z);
+        s += ",\"u_z\":"; put_linear(s, l->u_z);
+        s += ",\"w_r\":"; put_linear(s, l->w_r);
+        s += ",\"u_r\":"; put_linear(s, l->u_r);
+        s += ",\"w_h\":"; put_linear(s, l->w_h);
+        s += ",\"u_h\":"; put_linear(s, l->u_h);
+        s += "},\"attention\":{\"num_heads\":" + std::to_string(l->heads) + ",\"head_dim\":" + std::to_string(l->hd);
+        s += ",\"q_linear\":"; put_linear(s, l->q);
+        s += ",\"k_linear\":"; put_linear(s, l->k);
+        s += ",\"v_linear\":"; put_linear(s, l->v);
+        s += ",\"out_linear\":"; put_linear(s, l->o);
+        s += "},\"norm\":{\"gamma\":"; put_arr(s, l->gamma, {l->H});
+        s += ",\"beta\":"; put_arr(s, l->beta, {l->H});
+        s += ",\"eps\":"; json::put_f32(s, l->eps);
+        s += "},\"dropout\":"; json::put_f32(s, l->dropout);
+        s += "}";
+        const size_t need = s.size() + 1;
+        const size_t have = *len;
+        *len = need;
+        if (buf && have >= need) std::memcpy(buf, s.c_str(), need);
+        else RVX_REQUIRE(buf == nullptr, RVX_ERR_INVALID_PARAMETER, "buffer too small");
+    });
+}
+
+rvx_status rvx_gnn_layer_dims(const rvx_layer* l, int32_t* in, int32_t* hidden, int32_t* heads, float* dropout) {
+    return guard([&] {
+        RVX_REQUIRE(l, RVX_ERR_INVALID_PARAMETER, "null layer");
+        if (in) *in = l->in;
+        if (hidden) *hidden = l->H;
+        if (heads) *heads = l->heads;
+        if (dropout) *dropout = l->dropout;
+    });
+}
+
+rvx_status rvx_gnn_layer_destroy(rvx_layer* l) {
+    return guard([&] { delete l; });
+}
+
+rvx_status rvx_gnn_forward_one(const rvx_layer* l, const float* node, const float* nbrs, int32_t deg, const float* w,
+                               int32_t nw, float* out) {
+    return guard([&] {
+        RVX_REQUIRE(l && node && out && deg >= 0 && nw >= 0, RVX_ERR_INVALID_PARAMETER, "bad arguments");
+        RVX_REQUIRE(deg == 0 || nbrs, RVX_ERR_INVALID_PARAMETER, "null neighbours");
+        RVX_REQUIRE(nw == 0 || w, RVX_ERR_INVALID_PARAMETER, "null weights");
+        ComputeLock cl;
+        const int64_t n = 1 + (int64_t)deg;
+        // Row 0 = the node, its neighbours rows 1..deg; other rows are unused.
+        std::vector<int64_t> rp(n + 1, deg);
+        rp[0] = 0;
+        std::vector<int32_t> col(std::max(deg, 1));
+        for (int j = 0; j < deg; ++j) col[j] = j + 1;
+        // aggregate_messages weights (layer.rs:421-445): empty -> zeros; the sum
+        // runs over every given weight; zip() truncates to min(deg, nw).
+        std::vector<float> wn(std::max(deg, 1), 0.0f);
+        int wmode = 0;
+        if (nw > 0 && deg > 0) {
+            wmode = 2;
+            float sum = 0.0f;
+            for (int j = 0; j < nw; ++j) sum = sum + w[j];
+            for (int j = 0; j < std::min(deg, nw); ++j) wn[j] = sum > 0.0f ? w[j] / sum : 1.0f / (float)nw;
+        }
+        float* dx = scratch_f32("rvl1_x", n * l->in);
+        float* dy = scratch_f32("rvl1_y", n * l->H);
+        auto* drp = (int64_t*)scratch_bytes("rvl1_rp", (n + 1) * 8);
+        auto* dcol = (int32_t*)scratch_bytes("rvl1_col", (int64_t)col.size() * 4);
+        float* dw = scratch_f32("rvl1_w", (int64_t)wn.size());
+        RVX_HIP(hipMemcpyAsync(dx, node, (size_t)l->in * 4, hipMemcpyHostToDevice, stream()));
+        if (deg)
+            RVX_HIP(hipMemcpyAsync(dx + l->in, nbrs, (size_t)deg * l->in * 4, hipMemcpyHostToDevice, stream()));
+        RVX_HIP(hipMemcpyAsync(drp, rp.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, stream()));
+        RVX_HIP(hipMemcpyAsync(dcol, col.data(), col.size() * 4, hipMemcpyHostToDevice, stream()));
+        RVX_HIP(hipMemcpyAsync(dw, wn.data(), wn.size() * 4, hipMemcpyHostToDevice, stream()));
+        // rows 1..deg have no neighbours of their own: only row 0 is kept
+        forward_dev(l, n, drp, dcol, deg, dw, wmode, dx, dy);
+        RVX_HIP(hipMemcpyAsync(out, dy, (size_t)l->H * 4, hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
+rvx_status rvx_gnn_forward_graph_device(const rvx_layer* l, const rvx_graph* g, const rvx_buffer* x, rvx_buffer* y) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(l && x && y, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(x->mem.bytes >= g->n * l->in * 4, RVX_ERR_DIMENSION_MISMATCH, "x smaller than n*input_dim");
+        RVX_REQUIRE(y->mem.bytes >= g->n * l->H * 4, RVX_ERR_DIMENSION_MISMATCH, "y smaller than n*hidden_dim");
+        ComputeLock cl;
+        forward_dev(l, g->n, g->row_ptr, g->col, g->e, g->w, 1, x->mem.as<float>(), y->mem.as<float>());
+    });
+}
+
+rvx_status rvx_gnn_forward_graph(const rvx_layer* l, const rvx_graph* g, const float* x, int64_t n, float* y) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(l && x && y, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(n == g->n, RVX_ERR_DIMENSION_MISMATCH, "feature rows != graph nodes");
+        ComputeLock cl;
+        float* dx = scratch_f32("rvlg_x", n * l->in);
+        float* dy = scratch_f32("rvlg_y", n * l->H);
+        RVX_HIP(hipMemcpyAsync(dx, x, (size_t)(n * l->in * 4), hipMemcpyHostToDevice, stream()));
+        forward_dev(l, n, g->row_ptr, g->col, g->e, g->w, 1, dx, dy);
+        RVX_HIP(hipMemcpyAsync(y, dy, (size_t)(n * l->H * 4), hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,371 @@
+// api_graph.cpp — graph handles, scratch pool and the message-passing layers
+// of crates/ruvector-postgres/src/gnn (GraphSAGE, GCN, aggregators).
+#include <algorithm>
+#include <cmath>
+
+#include "graph.hpp"
+#include "kernels.hpp"
+
+namespace rvx {
+
+namespace {
+std::mutex g_scratch_mu;
+std::map<std::pair<int, std::string>, std::unique_ptr<DevMem>> g_scratch;
+std::map<int, std::unique_ptr<std::recursive_mutex>> g_compute_mu;
+}  // namespace
+
+void* scratch_bytes(const std::string& slot, int64_t bytes) {
+    const int dev = device().id;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    auto& m = g_scratch[{dev, slot}];
+    if (!m) m = std::make_unique<DevMem>();
+    if (m->bytes < bytes) m->reset(std::max<int64_t>(bytes, 256));
+    return m->p;
+}
+float* scratch_f32(const std::string& slot, int64_t count) { return (float*)scratch_bytes(slot, count * 4); }
+
+ComputeLock::ComputeLock() {
+    const int dev = device().id;
+    std::recursive_mutex* mu;
+    {
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        auto& p = g_compute_mu[dev];
+        if (!p) p = std::make_unique<std::recursive_mutex>();
+        mu = p.get();
+    }
+    lk = std::unique_lock<std::recursive_mutex>(*mu);
+}
+
+void check_graph(const rvx_graph* g) {
+    RVX_REQUIRE(g && g->row_ptr && (g->e == 0 || g->col), RVX_ERR_INVALID_PARAMETER, "null graph");
+}
+
+namespace {
+
+// Finish a graph once row_ptr/col are on the device and a host row_ptr is known.
+void finish_graph(rvx_graph* g, const std::vector<int64_t>& rp) {
+    std::vector<int32_t> iso;
+    int64_t maxd = 0;
+    for (int64_t i = 0; i < g->n; ++i) {
+        const int64_t d = rp[i + 1] - rp[i];
+        RVX_REQUIRE(d >= 0, RVX_ERR_INVALID_PARAMETER, "row_ptr must be non-decreasing");
+        maxd = std::max(maxd, d);
+        if (d == 0) iso.push_back((int32_t)i);
+    }
+    RVX_REQUIRE(maxd < ((int64_t)1 << 31), RVX_ERR_INVALID_SHAPE, "degree too large");
+    g->max_deg = (int32_t)maxd;
+    g->n_isolated = (int64_t)iso.size();
+    if (!iso.empty()) {
+        g->isolated_mem.reset((int64_t)iso.size() * 4);
+        g->isolated_mem.upload(iso.data(), (int64_t)iso.size() * 4);
+        g->isolated = g->isolated_mem.as<int32_t>();
+    }
+}
+
+void upload_csr(rvx_graph* g, const std::vector<int64_t>& rp, const int32_t* col, const float* w) {
+    g->row_ptr_mem.reset((g->n + 1) * 8);
+    g->row_ptr_mem.upload(rp.data(), (g->n + 1) * 8);
+    g->row_ptr = g->row_ptr_mem.as<int64_t>();
+    g->col_mem.reset(std::max<int64_t>(g->e, 1) * 4);
+    g->col_mem.upload(col, g->e * 4);
+    g->col = g->col_mem.as<int32_t>();
+    if (w) {
+        g->w_mem.reset(std::max<int64_t>(g->e, 1) * 4);
+        g->w_mem.upload(w, g->e * 4);
+        g->w = g->w_mem.as<float>();
+        g->host_w.assign(w, w + g->e);
+    }
+    finish_graph(g, rp);
+}
+
+// GraphSAGELayer::with_aggregator deterministic init (graphsage.rs:56-78) and
+// GCNLayer::new_with_normalize (gcn.rs:32-41): W[i][j] = (((i*out+j+off) as f32 * 0.01) % 1.0 - 0.5) * scale.
+std::vector<float> det_init(int in, int out, int offset) {
+    const float scale = std::sqrt(2.0f / (float)(in + out));
+    std::vector<float> w((size_t)in * out);
+    for (int64_t i = 0; i < in; ++i)
+        for (int64_t j = 0; j < out; ++j) {
+            const float val = std::fmod((float)(uint64_t)(i * out + j + offset) * 0.01f, 1.0f);
+            w[(size_t)(i * out + j)] = (val - 0.5f) * scale;
+        }
+    return w;
+}
+
+// Upload an [in][out] matrix as its transpose [out][in] (the GEMM's K-contiguous B).
+void upload_transposed(DevMem& dst, const std::vector<float>& w_in_out, int in, int out) {
+    std::vector<float> t((size_t)in * out);
+    for (int64_t i = 0; i < in; ++i)
+        for (int64_t j = 0; j < out; ++j) t[(size_t)(j * in + i)] = w_in_out[(size_t)(i * out + j)];
+    dst.reset((int64_t)t.size() * 4);
+    dst.upload(t.data(), (int64_t)t.size() * 4);
+}
+
+}  // namespace
+}  // namespace rvx
+
+using namespace rvx;
+
+struct rvx_sage_layer {
+    int in = 0, out = 0, num_samples = 0, aggregator = 0, normalize = 1;
+    std::vector<float> wn, ws;  // host [in][out]
+    DevMem wn_t, ws_t;          // device [out][in]
+};
+
+struct rvx_gcn_layer {
+    int in = 0, out = 0, normalize = 1;
+    std::vector<float> w, b;
+    DevMem w_t, bias;
+};
+
+namespace {
+
+// x: node table indexed by the CSR columns; rows [row_offset, row_offset+g->n)
+// of it are this graph's destination (self) rows.
+void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* x, float* y, int64_t row_offset = 0) {
+    RVX_REQUIRE(g->max_deg <= l->num_samples, RVX_ERR_UNSUPPORTED,
+                "GraphSAGE neighbour sampling (num_samples < max degree, graphsage.rs:92-102) is not supported; "
+                "set num_samples >= max degree");
+    const int64_t n = g->n;
+    float* agg = scratch_f32("sage_agg", n * (int64_t)l->in);
+    const int a = (l->aggregator == RVX_SAGE_MAXPOOL) ? AGG_MAX : AGG_MEAN;
+    aggregate_rows(g->row_ptr, g->col, nullptr, n, x, l->in, a, /*empty_fill zeros*/ 0, 0, agg, "sage_aggregate");
+    GemmOperand s0{agg, l->in, l->wn_t.as<float>(), l->in, l->in};
+    GemmOperand s1{x + row_offset * l->in, l->in, l->ws_t.as<float>(), l->in, l->in};
+    GemmEpilogue ep;
+    ep.epi = GEMM_EPI_RELU;
+    gemm_nt(n, l->out, s0, &s1, ep, y, l->out, "sage_gemm");
+    if (l->normalize) normalize_rows(y, n, l->out, true, "sage_normalize");
+}
+
+__global__ void k_gcn_isolated(const int32_t* iso, int64_t n_iso, const float* x, int dim, float* y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = n_iso * dim;
+    if (i >= total) return;
+    const int64_t r = iso[i / dim];
+    const int c = (int)(i % dim);
+    y[r * dim + c] = fmaxf(x[r * dim + c], 0.0f);
+}
+
+void gcn_forward_dev(const rvx_gcn_layer* l, const rvx_graph* g, bool use_w, const float* x, float* y) {
+    const int64_t n = g->n;
+    RVX_REQUIRE(g->n_isolated == 0 || l->in == l->out, RVX_ERR_INVALID_SHAPE,
+                "GCN passes isolated nodes through unchanged (message_passing.rs:75-78); needs in == out");
+    const float* w = use_w ? g->w : nullptr;
+    float* agg = scratch_f32("gcn_agg", n * (int64_t)l->in);
+    aggregate_rows(g->row_ptr, g->col, w, n, x, l->in, AGG_SUM, 0, l->normalize ? 1 : 0, agg, "gcn_aggregate");
+    GemmOperand s0{agg, l->in, l->w_t.as<float>(), l->in, l->in};
+    GemmEpilogue ep;
+    ep.epi = GEMM_EPI_RELU;
+    ep.bias0 = l->bias.as<float>();
+    gemm_nt(n, l->out, s0, nullptr, ep, y, l->out, "gcn_gemm");
+    if (g->n_isolated) {
+        const int64_t total = g->n_isolated * l->in;
+        hipLaunchKernelGGL(k_gcn_isolated, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream(), g->isolated,
+                           g->n_isolated, x, l->in, y);
+        RVX_HIP(hipGetLastError());
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+rvx_status rvx_graph_from_edges(int64_t n, const int64_t* src, const int64_t* dst, int64_t ne, const float* ew,
+                                rvx_graph** out) {
+    return guard([&] {
+        RVX_REQUIRE(out && n >= 0 && n < ((int64_t)1 << 31) && ne >= 0, RVX_ERR_INVALID_PARAMETER, "bad graph args");
+        RVX_REQUIRE(ne == 0 || (src && dst), RVX_ERR_INVALID_PARAMETER, "null edge arrays");
+        // Stable counting sort by destination, dropping out-of-range edges
+        // (build_adjacency_list, message_passing.rs:43-47).
+        std::vector<int64_t> rp(n + 1, 0);
+        for (int64_t e = 0; e < ne; ++e)
+            if (src[e] >= 0 && src[e] < n && dst[e] >= 0 && dst[e] < n) rp[dst[e] + 1]++;
+        for (int64_t i = 0; i < n; ++i) rp[i + 1] += rp[i];
+        const int64_t kept = rp[n];
+        std::vector<int32_t> col(std::max<int64_t>(kept, 1));
+        std::vector<float> w(ew ? std::max<int64_t>(kept, 1) : 0);
+        std::vector<int64_t> fill(rp.begin(), rp.end() - 1);
+        for (int64_t e = 0; e < ne; ++e) {
+            if (!(src[e] >= 0 && src[e] < n && dst[e] >= 0 && dst[e] < n)) continue;
+            const int64_t p = fill[dst[e]]++;
+            col[p] = (int32_t)src[e];
+            if (ew) w[p] = ew[e];
+        }
+        auto g = std::make_unique<rvx_graph>();
+        g->n = n;
+        g->e = kept;
+        upload_csr(g.get(), rp, col.data(), ew ? w.data() : nullptr);
+        *out = g.release();
+    });
+}
+
+rvx_status rvx_graph_from_csr(int64_t n, const int64_t* row_ptr, const int32_t* col, const float* ew, rvx_graph** out) {
+    return guard([&] {
+        RVX_REQUIRE(out && row_ptr && n >= 0 && n < ((int64_t)1 << 31), RVX_ERR_INVALID_PARAMETER, "bad CSR args");
+        RVX_REQUIRE(row_ptr[0] == 0, RVX_ERR_INVALID_PARAMETER, "row_ptr[0] must be 0");
+        std::vector<int64_t> rp(row_ptr, row_ptr + n + 1);
+        const int64_t e = rp[n];
+        for (int64_t i = 0; i < e; ++i)
+            RVX_REQUIRE(col[i] >= 0 && col[i] < n, RVX_ERR_INDEX, "column index out of range");
+        auto g = std::make_unique<rvx_graph>();
+        g->n = n;
+        g->e = e;
+        upload_csr(g.get(), rp, col, ew);
+        *out = g.release();
+    });
+}
+
+rvx_status rvx_graph_from_device_csr(int64_t n, int64_t e, rvx_buffer* rp, rvx_buffer* col, rvx_buffer* w,
+                                     rvx_graph** out) {
+    return guard([&] {
+        RVX_REQUIRE(out && rp && col && n >= 0, RVX_ERR_INVALID_PARAMETER, "bad device CSR args");
+        RVX_REQUIRE(rp->mem.bytes >= (n + 1) * 8 && col->mem.bytes >= e * 4, RVX_ERR_INVALID_PARAMETER,
+                    "CSR buffers too small");
+        auto g = std::make_unique<rvx_graph>();
+        g->n = n;
+        g->e = e;
+        g->row_ptr = rp->mem.as<int64_t>();
+        g->col = col->mem.as<int32_t>();
+        if (w) {
+            RVX_REQUIRE(w->mem.bytes >= e * 4, RVX_ERR_INVALID_PARAMETER, "weights too small");
+            g->w = w->mem.as<float>();
+            g->host_w.resize(e);
+            w->mem.download(g->host_w.data(), e * 4);
+        }
+        std::vector<int64_t> h(n + 1);
+        rp->mem.download(h.data(), (n + 1) * 8);
+        RVX_REQUIRE(h[0] == 0 && h[n] == e, RVX_ERR_INVALID_PARAMETER, "row_ptr inconsistent with num_edges");
+        finish_graph(g.get(), h);
+        *out = g.release();
+    });
+}
+
+rvx_status rvx_graph_info(const rvx_graph* g, int64_t* n, int64_t* e, int32_t* max_deg) {
+    return guard([&] {
+        check_graph(g);
+        if (n) *n = g->n;
+        if (e) *e = g->e;
+        if (max_deg) *max_deg = g->max_deg;
+    });
+}
+
+rvx_status rvx_graph_destroy(rvx_graph* g) {
+    return guard([&] { delete g; });
+}
+
+rvx_status rvx_aggregate_device(const rvx_graph* g, int32_t agg, int32_t use_w, int32_t keep_isolated,
+                                const rvx_buffer* x, int32_t dim, rvx_buffer* out) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(x && out && dim > 0, RVX_ERR_INVALID_PARAMETER, "null buffers");
+        RVX_REQUIRE(x->mem.bytes >= g->n * dim * 4 && out->mem.bytes >= g->n * dim * 4, RVX_ERR_DIMENSION_MISMATCH,
+                    "feature buffers smaller than n*dim");
+        RVX_REQUIRE(!use_w || g->w, RVX_ERR_INVALID_PARAMETER, "graph has no edge weights");
+        ComputeLock cl;
+        aggregate_rows(g->row_ptr, g->col, use_w ? g->w : nullptr, g->n, x->mem.as<float>(), dim, agg,
+                       keep_isolated ? 1 : 0, 0, out->mem.as<float>(), "aggregate");
+    });
+}
+
+rvx_status rvx_sage_layer_create(int32_t in, int32_t out_f, int32_t num_samples, int32_t aggregator, int32_t normalize,
+                                 const float* wn, const float* ws, rvx_sage_layer** out) {
+    return guard([&] {
+        RVX_REQUIRE(out && in > 0 && out_f > 0 && num_samples >= 0, RVX_ERR_LAYER_CONFIG, "bad GraphSAGE dims");
+        RVX_REQUIRE(aggregator >= 0 && aggregator <= 2, RVX_ERR_LAYER_CONFIG, "unknown aggregator");
+        RVX_REQUIRE((wn == nullptr) == (ws == nullptr), RVX_ERR_INVALID_PARAMETER, "give both weight matrices or none");
+        auto l = std::make_unique<rvx_sage_layer>();
+        l->in = in; l->out = out_f; l->num_samples = num_samples; l->aggregator = aggregator;
+        l->normalize = normalize ? 1 : 0;
+        if (wn) {
+            l->wn.assign(wn, wn + (size_t)in * out_f);
+            l->ws.assign(ws, ws + (size_t)in * out_f);
+        } else {
+            l->wn = det_init(in, out_f, 0);
+            l->ws = det_init(in, out_f, 1000);
+        }
+        upload_transposed(l->wn_t, l->wn, in, out_f);
+        upload_transposed(l->ws_t, l->ws, in, out_f);
+        *out = l.release();
+    });
+}
+
+rvx_status rvx_sage_layer_destroy(rvx_sage_layer* l) {
+    return guard([&] { delete l; });
+}
+
+rvx_status rvx_sage_forward_device(const rvx_sage_layer* l, const rvx_graph* g, const rvx_buffer* x, rvx_buffer* y) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(l && x && y, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(x->mem.bytes >= g->n * l->in * 4, RVX_ERR_DIMENSION_MISMATCH, "x smaller than n*in");
+        RVX_REQUIRE(y->mem.bytes >= g->n * l->out * 4, RVX_ERR_DIMENSION_MISMATCH, "y smaller than n*out");
+        ComputeLock cl;
+        sage_forward_dev(l, g, x->mem.as<float>(), y->mem.as<float>());
+    });
+}
+
+rvx_status rvx_sage_forward_shard_device(const rvx_sage_layer* l, const rvx_graph* g, const rvx_buffer* x_full,
+                                         int64_t row_offset, rvx_buffer* y) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(l && x_full && y && row_offset >= 0, RVX_ERR_INVALID_PARAMETER, "bad argument");
+        RVX_REQUIRE(x_full->mem.bytes >= (row_offset + g->n) * l->in * 4, RVX_ERR_DIMENSION_MISMATCH,
+                    "x_full does not cover the shard rows");
+        RVX_REQUIRE(y->mem.bytes >= g->n * l->out * 4, RVX_ERR_DIMENSION_MISMATCH, "y smaller than rows*out");
+        ComputeLock cl;
+        sage_forward_dev(l, g, x_full->mem.as<float>(), y->mem.as<float>(), row_offset);
+    });
+}
+
+rvx_status rvx_sage_forward(const rvx_sage_layer* l, const rvx_graph* g, const float* x, int64_t n, float* y) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(l && x && y, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(n == g->n, RVX_ERR_DIMENSION_MISMATCH, "feature rows != graph nodes");
+        ComputeLock cl;
+        float* dx = scratch_f32("sage_x", n * (int64_t)l->in);
+        float* dy = scratch_f32("sage_y", n * (int64_t)l->out);
+        RVX_HIP(hipMemcpyAsync(dx, x, (size_t)(n * l->in * 4), hipMemcpyHostToDevice, stream()));
+        sage_forward_dev(l, g, dx, dy);
+        RVX_HIP(hipMemcpyAsync(y, dy, (size_t)(n * l->out * 4), hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
+rvx_status rvx_gcn_layer_create(int32_t in, int32_t out_f, int32_t normalize, const float* w, const float* b,
+                                rvx_gcn_layer** out) {
+    return guard([&] {
+        RVX_REQUIRE(out && in > 0 && out_f > 0, RVX_ERR_LAYER_CONFIG, "bad GCN dims");
+        auto l = std::make_unique<rvx_gcn_layer>();
+        l->in = in; l->out = out_f; l->normalize = normalize ? 1 : 0;
+        l->w = w ? std::vector<float>(w, w + (size_t)in * out_f) : det_init(in, out_f, 0);
+        l->b = b ? std::vector<float>(b, b + out_f) : std::vector<float>(out_f, 0.0f);
+        upload_transposed(l->w_t, l->w, in, out_f);
+        l->bias.reset(out_f * 4);
+        l->bias.upload(l->b.data(), out_f * 4);
+        *out = l.release();
+    });
+}
+
+rvx_status rvx_gcn_layer_destroy(rvx_gcn_layer* l) {
+    return guard([&] { delete l; });
+}
+
+rvx_status rvx_gcn_forward(const rvx_gcn_layer* l, const rvx_graph* g, int32_t use_w, const float* x, int64_t n,
+                           float* y) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(l && x && y, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(n == g->n, RVX_ERR_DIMENSION_MISMATCH, "feature rows != graph nodes");
+        RVX_REQUIRE(!use_w || g->w, RVX_ERR_INVALID_PARAMETER, "graph has no edge weights");
+        ComputeLock cl;
+        float* dx = scratch_f32("gcn_x", n * (int64_t)l->in);
+        float* dy = scratch_f32("gcn_y", n * (int64_t)l->out);
+        RVX_HIP(hipMemcpyAsync(dx, x, (size_t)(n * l->in * 4), hipMemcpyHostToDevice, stream()));
+        gcn_forward_dev(l, g, use_w != 0, dx, dy);
+        RVX_HIP(hipMemcpyAsync(y, dy, (size_t)(n * l->out * 4), hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
+}  // extern "C"

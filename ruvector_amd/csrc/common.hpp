@@ -1,0 +1,105 @@
+// common.hpp — shared host-side plumbing of librvx: status/error handling,
+// the per-device stream, device buffers and the event-based kernel profiler.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "rvx/rvx.h"
+
+namespace rvx {
+
+// An exception carrying an rvx_status; every extern "C" entry point catches it
+// and turns it into (status, thread-local message).
+struct Error : std::runtime_error {
+    rvx_status code;
+    Error(rvx_status c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+[[noreturn]] void fail(rvx_status code, const std::string& msg);
+void set_last_error(const std::string& msg);
+
+#define RVX_HIP(expr)                                                                            \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            ::rvx::fail(e_ == hipErrorOutOfMemory ? RVX_ERR_OUT_OF_MEMORY : RVX_ERR_DEVICE,      \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                      \
+    } while (0)
+
+#define RVX_REQUIRE(cond, code, msg)                                                             \
+    do {                                                                                         \
+        if (!(cond)) ::rvx::fail((code), (msg));                                                 \
+    } while (0)
+
+// Wrap an API body: maps exceptions to status codes.
+template <class F>
+rvx_status guard(F&& f) {
+    try {
+        f();
+        return RVX_OK;
+    } catch (const Error& e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        set_last_error("host allocation failed");
+        return RVX_ERR_OUT_OF_MEMORY;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return RVX_ERR_INVALID_PARAMETER;
+    }
+}
+
+// ---------------------------------------------------------------- device
+struct Device {
+    int id = 0;
+    hipStream_t stream = nullptr;  // every kernel of this device runs here
+    int num_cus = 0;
+    int64_t hbm_bytes = 0;
+    std::string arch;
+};
+Device& device();          // current thread's device (lazily initialised)
+hipStream_t stream();      // shorthand for device().stream
+void sync();               // hipStreamSynchronize(stream())
+
+// RAII device allocation (256-B aligned by hipMalloc).
+struct DevMem {
+    void* p = nullptr;
+    int64_t bytes = 0;
+    int dev = 0;
+    DevMem() = default;
+    explicit DevMem(int64_t b);
+    ~DevMem();
+    DevMem(const DevMem&) = delete;
+    DevMem& operator=(const DevMem&) = delete;
+    DevMem(DevMem&& o) noexcept { *this = std::move(o); }
+    DevMem& operator=(DevMem&& o) noexcept;
+    void reset(int64_t b);
+    template <class T> T* as() const { return static_cast<T*>(p); }
+    void upload(const void* src, int64_t n, int64_t off = 0);
+    void download(void* dst, int64_t n, int64_t off = 0) const;
+};
+
+// ---------------------------------------------------------------- profiler
+// Records a start/stop hipEvent pair on the library stream around one launch
+// when profiling is on; rvx_profile_query sums the pairs per tag.
+struct ProfScope {
+    const char* name;
+    hipEvent_t a = nullptr, b = nullptr;
+    explicit ProfScope(const char* n);
+    ~ProfScope();
+};
+
+}  // namespace rvx
+
+struct rvx_buffer {
+    rvx::DevMem mem;
+};

@@ -1,0 +1,245 @@
+// gemm_f32.hip — FP32 MFMA GEMM for gfx950 with fused epilogues.
+//
+// The dense feature-times-weight contraction of every GNN layer on the path:
+//   Linear::forward        y = W x + b      (crates/ruvector-gnn/src/layer.rs:37-41)
+//   GraphSAGE linear_transform  x·W         (crates/ruvector-postgres/src/gnn/graphsage.rs:105-115)
+//   GCN linear_transform   x·W + b          (crates/ruvector-postgres/src/gnn/gcn.rs:64-81)
+// batched over all nodes of the graph: C[M][N] = A[M][K] · B[N][K]^T (+ A1·B1^T).
+// Both operands are K-contiguous ("NT"), which is the ndarray [out][in] weight
+// layout of Linear; GraphSAGE/GCN [in][out] weights are transposed once at upload.
+//
+// Numerics: v_mfma_f32_32x32x2_f32 is an exact f32 fma chain (one rounding per
+// product, cdna_hip_programming.md §3), so results differ from the reference's
+// mul-then-add order only by rounding; parity is 1e-5 relative (north star).
+//
+// Tiling (CDNA4): 128x128 block tile, BK=32, 256 threads = 4 waves in a 2x2 grid,
+// each wave a 64x64 tile of 2x2 MFMA 32x32 accumulators (64 AGPR/VGPR).
+// Operands are staged through LDS with a +4-float row pad (144-B stride), which
+// makes the per-lane ds_read_b128 fragment reads bank-conflict free. The K axis
+// is permuted inside a BK tile so every lane reads 16 contiguous k values
+// (lane half h owns k = 16h..16h+15); A and B use the same permutation, so the
+// product is unchanged. Double-buffered LDS, one barrier per K tile, register
+// prefetch of tile k+1 during the MFMAs of tile k, XCD-aware block swizzle so
+// the column tiles of one row block share an XCD's L2.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace rvx {
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 32, LDS_ROW = BK + 4;  // 36 floats = 144 B
+constexpr int TILE_FLOATS = 128 * LDS_ROW;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct GemmArgs {
+    const float* A0; const float* B0; int64_t lda0, ldb0; int K0;
+    const float* A1; const float* B1; int64_t lda1, ldb1; int K1;
+    const float* bias0; const float* bias1;
+    const float* addend; int64_t ld_add;
+    float* C; int64_t ldc;
+    int64_t M; int N;
+    int tiles_n; int64_t nblocks;
+    float alpha;  // scale applied to acc before bias (dropout scale etc.)
+};
+
+__device__ __forceinline__ float epi_apply(int epi, float v) {
+    if (epi == GEMM_EPI_RELU) return fmaxf(v, 0.0f);
+    if (epi == GEMM_EPI_SIGMOID) {  // GRUCell::sigmoid, layer.rs:278-285
+        if (v > 0.0f) return 1.0f / (1.0f + expf(-v));
+        float ex = expf(v);
+        return ex / (1.0f + ex);
+    }
+    if (epi == GEMM_EPI_TANH) return tanhf(v);
+    return v;
+}
+
+template <bool DUAL>
+__global__ __launch_bounds__(256, 2) void gemm_nt_mfma(GemmArgs g, int epi) {
+    __shared__ __attribute__((aligned(16))) float smem[2 * 2 * TILE_FLOATS];  // [stage][A|B]
+
+    // XCD-aware bijective swizzle (cdna_hip_programming.md §5, T1): blocks b and
+    // b+8 share an XCD; give each XCD a contiguous run of logical tiles so the
+    // tiles_n column tiles of one row block hit the same L2.
+    const int64_t nwg = g.nblocks;
+    const int64_t bid = blockIdx.x;
+    const int64_t xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    const int64_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    const int64_t tm = wgid / g.tiles_n;
+    const int tn = (int)(wgid % g.tiles_n);
+    const int64_t m0 = tm * BM;
+    const int n0 = tn * BN;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int lr = lane & 31, lh = lane >> 5;
+
+    const int nk0 = (g.K0 + BK - 1) / BK;
+    const int nk1 = DUAL ? (g.K1 + BK - 1) / BK : 0;
+    const int nk = nk0 + nk1;
+
+    // Global->register staging: 4 float4 of A and 4 of B per thread per K tile.
+    float4 ra[4], rb[4];
+    auto load_tile = [&](int kt) {
+        const float* A; const float* B; int64_t lda, ldb; int K, k0;
+        if (!DUAL || kt < nk0) { A = g.A0; B = g.B0; lda = g.lda0; ldb = g.ldb0; K = g.K0; k0 = kt * BK; }
+        else { A = g.A1; B = g.B1; lda = g.lda1; ldb = g.ldb1; K = g.K1; k0 = (kt - nk0) * BK; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int f = tid + 256 * i;
+            const int row = f >> 3, c = (f & 7) * 4;
+            const int k = k0 + c;
+            const int64_t am = m0 + row;
+            const int bn = n0 + row;
+            float4 za = make_float4(0.f, 0.f, 0.f, 0.f), zb = za;
+            if (am < g.M && k < K) za = *reinterpret_cast<const float4*>(A + am * lda + k);
+            if (bn < g.N && k < K) zb = *reinterpret_cast<const float4*>(B + (int64_t)bn * ldb + k);
+            ra[i] = za; rb[i] = zb;
+        }
+    };
+    auto store_tile = [&](int stage) {
+        float* As = smem + stage * 2 * TILE_FLOATS;
+        float* Bs = As + TILE_FLOATS;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int f = tid + 256 * i;
+            const int row = f >> 3, c = (f & 7) * 4;
+            *reinterpret_cast<float4*>(As + row * LDS_ROW + c) = ra[i];
+            *reinterpret_cast<float4*>(Bs + row * LDS_ROW + c) = rb[i];
+        }
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+
+    for (int kt = 0; kt < nk; ++kt) {
+        const int stage = kt & 1;
+        if (kt + 1 < nk) load_tile(kt + 1);
+        const float* As = smem + stage * 2 * TILE_FLOATS;
+        const float* Bs = As + TILE_FLOATS;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            float4 af[2][2], bf[2][2];
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) {
+                const float* p = As + (wm * 64 + mi * 32 + lr) * LDS_ROW + lh * 16 + half * 8;
+                af[mi][0] = *reinterpret_cast<const float4*>(p);
+                af[mi][1] = *reinterpret_cast<const float4*>(p + 4);
+            }
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const float* p = Bs + (wn * 64 + ni * 32 + lr) * LDS_ROW + lh * 16 + half * 8;
+                bf[ni][0] = *reinterpret_cast<const float4*>(p);
+                bf[ni][1] = *reinterpret_cast<const float4*>(p + 4);
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+#pragma unroll
+                for (int mi = 0; mi < 2; ++mi) {
+                    const float a = (s < 4) ? af[mi][0][s & 3] : af[mi][1][s & 3];
+#pragma unroll
+                    for (int ni = 0; ni < 2; ++ni) {
+                        const float b = (s < 4) ? bf[ni][0][s & 3] : bf[ni][1][s & 3];
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[mi][ni], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        if (kt + 1 < nk) store_tile(stage ^ 1);
+        __syncthreads();
+    }
+
+    // Epilogue. 32x32 C/D map: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+            const int col = n0 + wn * 64 + ni * 32 + lr;
+            if (col >= g.N) continue;
+            float b = 0.0f;
+            if (g.bias0) b = g.bias0[col];
+            if (g.bias1) b += g.bias1[col];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int64_t row = m0 + wm * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+                if (row < g.M) {
+                    float v = acc[mi][ni][e];
+                    if (g.alpha != 1.0f) v *= g.alpha;
+                    if (g.bias0 || g.bias1) v += b;
+                    if (g.addend) v += g.addend[row * g.ld_add + col];
+                    g.C[row * g.ldc + col] = epi_apply(epi, v);
+                }
+            }
+        }
+    }
+}
+
+// Correctness path for shapes the tiled kernel cannot take (K % 4 != 0 or
+// unaligned rows, e.g. the reference's 2-wide unit tests): one thread per
+// output, k-sequential fma chain.
+__global__ void gemm_nt_simple(GemmArgs g, int epi) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= g.M * (int64_t)g.N) return;
+    const int64_t m = idx / g.N;
+    const int n = (int)(idx % g.N);
+    float acc = 0.0f;
+    for (int k = 0; k < g.K0; ++k) acc = fmaf(g.A0[m * g.lda0 + k], g.B0[(int64_t)n * g.ldb0 + k], acc);
+    if (g.A1)
+        for (int k = 0; k < g.K1; ++k) acc = fmaf(g.A1[m * g.lda1 + k], g.B1[(int64_t)n * g.ldb1 + k], acc);
+    if (g.alpha != 1.0f) acc *= g.alpha;
+    if (g.bias0) acc += g.bias0[n] + (g.bias1 ? g.bias1[n] : 0.0f);
+    else if (g.bias1) acc += g.bias1[n];
+    if (g.addend) acc += g.addend[m * g.ld_add + n];
+    g.C[m * g.ldc + n] = epi_apply(epi, acc);
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, const GemmEpilogue& ep, float* C,
+             int64_t ldc, const char* tag) {
+    if (M <= 0 || N <= 0) return;
+    const float* bias0 = ep.bias0;
+    const float* bias1 = ep.bias1;
+    const float alpha = ep.alpha;
+    const int epi = ep.epi;
+    GemmArgs g{};
+    g.addend = ep.addend;
+    g.ld_add = ep.ld_addend;
+    g.A0 = s0.A; g.B0 = s0.B; g.lda0 = s0.lda; g.ldb0 = s0.ldb; g.K0 = s0.K;
+    if (s1) { g.A1 = s1->A; g.B1 = s1->B; g.lda1 = s1->lda; g.ldb1 = s1->ldb; g.K1 = s1->K; }
+    g.bias0 = bias0; g.bias1 = bias1; g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.alpha = alpha;
+
+    bool fast = (s0.K % 4 == 0) && (s0.lda % 4 == 0) && (s0.ldb % 4 == 0) && aligned16(s0.A) && aligned16(s0.B);
+    if (s1) fast = fast && (s1->K % 4 == 0) && (s1->lda % 4 == 0) && (s1->ldb % 4 == 0) && aligned16(s1->A) &&
+                   aligned16(s1->B);
+    ProfScope ps(tag ? tag : "gemm_nt");
+    if (fast) {
+        g.tiles_n = (N + BN - 1) / BN;
+        const int64_t tiles_m = (M + BM - 1) / BM;
+        g.nblocks = tiles_m * g.tiles_n;
+        RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
+        if (s1)
+            hipLaunchKernelGGL(gemm_nt_mfma<true>, dim3((unsigned)g.nblocks), dim3(256), 0, stream(), g, epi);
+        else
+            hipLaunchKernelGGL(gemm_nt_mfma<false>, dim3((unsigned)g.nblocks), dim3(256), 0, stream(), g, epi);
+    } else {
+        const int64_t total = M * (int64_t)N;
+        hipLaunchKernelGGL(gemm_nt_simple, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream(), g, epi);
+    }
+    RVX_HIP(hipGetLastError());
+}
+
+}  // namespace rvx

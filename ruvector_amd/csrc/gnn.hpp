@@ -1,0 +1,40 @@
+// gnn.hpp — launch arguments of the RuvectorLayer kernels (k_gnn.hip).
+#pragma once
+#include <cstdint>
+
+namespace rvx {
+
+struct EdgeArgs {
+    int64_t n = 0;
+    int H = 0, heads = 0, hd = 0, G = 0;  // G = lanes per head of the grouped kernel (0 = generic)
+    const int64_t* rp = nullptr;
+    const int32_t* col = nullptr;
+    const float* w = nullptr;  // per-edge weights (wmode 1: raw, 2: pre-normalised)
+    int wmode = 0;
+    const float* qkv = nullptr;  // [n][3H]  (q | k | v)
+    const float* m = nullptr;    // [n][H]   messages w_msg(x)
+    float* scores = nullptr;     // [E][heads] scratch
+    float* att = nullptr;        // [n][H]   concat of head outputs
+    float* wagg = nullptr;       // [n][H]   weighted message aggregate
+};
+
+struct FinishArgs {
+    int64_t n = 0;
+    int H = 0;
+    const int64_t* rp = nullptr;
+    const float* m = nullptr;   // [n][H]  (GRU hidden = node message)
+    const float* zr = nullptr;  // [n][2H] (z | r)
+    const float* ht = nullptr;  // [n][H]
+    const float* gamma = nullptr;
+    const float* beta = nullptr;
+    float eps = 1e-5f;
+    float keep = 1.0f;          // 1 - dropout
+    float* y = nullptr;         // [n][H]
+};
+
+void edge_attention(const EdgeArgs& a);
+int edge_group_lanes(int H, int heads);  // 0 when the grouped kernel does not apply
+void mul_rows(const float* r, int64_t ldr, const float* h, float* out, int64_t n, int H);
+void gru_finish(const FinishArgs& a);
+
+}  // namespace rvx

@@ -1,0 +1,31 @@
+// hnsw.hpp — device-side HNSW graph view and the search launcher (k_hnsw.hip).
+#pragma once
+#include <cstdint>
+
+namespace rvx {
+
+constexpr int HNSW_MAX_EF = 1024;
+constexpr int HNSW_MAX_LEVEL = 16;  // NB_LAYER_MAX (patches/hnsw_rs/src/hnsw.rs:41)
+
+// Layer 0 is a CSR over all n points; layer l>=1 is a CSR over the sorted ids
+// of the points whose level is >= l. Offsets index the packed upper arrays.
+struct HnswDev {
+    int64_t n = 0;
+    int max_level = 0;
+    int64_t entry = 0;
+    const int64_t* rp0 = nullptr;
+    const int* col0 = nullptr;
+    const int* up_ids = nullptr;
+    const int64_t* up_rp = nullptr;
+    const int* up_col = nullptr;
+    int64_t up_count[HNSW_MAX_LEVEL + 1] = {};
+    int64_t up_ids_off[HNSW_MAX_LEVEL + 1] = {};
+    int64_t up_rp_off[HNSW_MAX_LEVEL + 1] = {};
+    int64_t up_col_off[HNSW_MAX_LEVEL + 1] = {};
+};
+
+void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
+                 const float* qnorm, int64_t nq, int k, int ef, float* out_d, int64_t* out_i, int32_t* out_n,
+                 const char* tag);
+
+}  // namespace rvx

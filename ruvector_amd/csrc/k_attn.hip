@@ -1,0 +1,184 @@
+// k_attn.hip — graph-attention head (EdgeFeaturedAttention) and the batched
+// differentiable_search re-rank.
+//
+// EdgeFeaturedAttention::compute_with_edges
+// (crates/ruvector-attention/src/graph/edge_featured.rs:196-258), per destination
+// node with transformed rows T = X W_node^T precomputed by one MFMA GEMM:
+//   score_hj = LeakyReLU( sum_c  tq[c]*a_src[c] + tk_j[c]*a_dst[c] + te_j[c]*a_edge[c] )
+//     as ONE interleaved f32 chain over c (edge_featured.rs:177-183), te = W_edge e_ij
+//   w_h = stable_softmax(score_h) (crates/ruvector-attention/src/utils.rs:11-54)
+//   out_h[c] = sum_j w_hj tv_j[c] ; concat or mean over heads.
+// Scores: one lane per edge, sequential over (head, c) in the reference order.
+// Sums: lanes over output columns, sequential over neighbours.
+//
+// differentiable_search (crates/ruvector-gnn/src/search.rs:56-94): one wave per
+// query, one lane per candidate: f32 dot + f64 norms (search.rs:4-26), softmax
+// with temperature, stable descending sort, top-k.
+#include "attn.hpp"
+#include "common.hpp"
+
+namespace rvx {
+namespace {
+
+__global__ __launch_bounds__(256) void k_edge_feat_scores(EfaArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const int heads = a.heads, hd = a.hd, D = heads * hd, ed = a.edge_dim;
+    const float* tq = a.tq + i * (int64_t)a.ldq;
+    const int64_t beg = a.rp[i], end = a.rp[i + 1];
+    for (int64_t e = beg + lane; e < end; e += 64) {
+        const float* tk = a.tk + (int64_t)a.col[e] * a.ldk;
+        const float* ef = a.edges ? a.edges + e * (int64_t)ed : nullptr;
+        for (int h = 0; h < heads; ++h) {
+            float score = 0.0f;
+            for (int c = 0; c < hd; ++c) {
+                const int off = h * hd + c;
+                float te = 0.0f;  // transform_edge (edge_featured.rs:159-171), sequential over edge_dim
+                if (ef)
+                    for (int k = 0; k < ed; ++k) te = te + ef[k] * a.w_edge[(int64_t)off * ed + k];
+                score = score + tq[off] * a.a_src[off];
+                score = score + tk[off] * a.a_dst[off];
+                score = score + te * a.a_edge[off];
+            }
+            a.scores[e * heads + h] = score < 0.0f ? a.slope * score : score;
+        }
+    }
+    (void)D;
+}
+
+// stable_softmax per (node, head), in place over the score scratch.
+__global__ void k_edge_feat_softmax(EfaArgs a) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.n * a.heads) return;
+    const int64_t i = t / a.heads;
+    const int h = (int)(t % a.heads);
+    const int64_t beg = a.rp[i], end = a.rp[i + 1];
+    const int64_t cnt = end - beg;
+    if (cnt == 0) return;
+    float mx = -INFINITY;
+    for (int64_t e = beg; e < end; ++e) {
+        const float v = a.scores[e * a.heads + h];
+        if (isfinite(v)) mx = fmaxf(mx, v);
+    }
+    if (!isfinite(mx)) {
+        for (int64_t e = beg; e < end; ++e) a.scores[e * a.heads + h] = 1.0f / (float)cnt;
+        return;
+    }
+    float sum = 0.0f;
+    for (int64_t e = beg; e < end; ++e) {
+        const float v = a.scores[e * a.heads + h];
+        sum = sum + (isfinite(v) ? expf(v - mx) : 0.0f);
+    }
+    if (sum <= 1e-10f || !isfinite(sum)) {
+        for (int64_t e = beg; e < end; ++e) a.scores[e * a.heads + h] = 1.0f / (float)cnt;
+        return;
+    }
+    const float inv = 1.0f / sum;
+    for (int64_t e = beg; e < end; ++e) {
+        const float v = a.scores[e * a.heads + h];
+        a.scores[e * a.heads + h] = (isfinite(v) ? expf(v - mx) : 0.0f) * inv;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_edge_feat_out(EfaArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const int heads = a.heads, hd = a.hd, D = heads * hd;
+    const int64_t beg = a.rp[i], end = a.rp[i + 1];
+    if (a.concat) {
+        for (int c = lane; c < D; c += 64) {
+            const int h = c / hd;
+            float acc = 0.0f;
+            for (int64_t e = beg; e < end; ++e)
+                acc = acc + a.scores[e * heads + h] * a.tv[(int64_t)a.col[e] * a.ldv + c];
+            a.out[i * (int64_t)D + c] = acc;
+        }
+    } else {
+        for (int c = lane; c < hd; c += 64) {
+            float o = 0.0f;
+            for (int h = 0; h < heads; ++h) {
+                float acc = 0.0f;
+                for (int64_t e = beg; e < end; ++e)
+                    acc = acc + a.scores[e * heads + h] * a.tv[(int64_t)a.col[e] * a.ldv + h * hd + c];
+                o = o + acc / (float)heads;
+            }
+            a.out[i * (int64_t)hd + c] = o;
+        }
+    }
+}
+
+// ---- differentiable_search -------------------------------------------------
+__global__ __launch_bounds__(64) void k_diff_search(const float* q, int64_t nq, const float* cand, int C, int d, int k,
+                                                    float temperature, float* sims, int64_t* out_idx, float* out_w) {
+    const int lane = threadIdx.x;
+    const int64_t qi = blockIdx.x;
+    if (qi >= nq) return;
+    const float* qv = q + qi * d;
+    float* s = sims + qi * C;
+    double qn2 = 0.0;
+    for (int c = 0; c < d; ++c) qn2 = qn2 + (double)qv[c] * (double)qv[c];
+    const float na = (float)sqrt(qn2);
+    for (int j = lane; j < C; j += 64) {
+        const float* cv = cand + (qi * C + j) * (int64_t)d;
+        float dot = 0.0f;
+        double n2 = 0.0;
+        for (int c = 0; c < d; ++c) {
+            dot = dot + qv[c] * cv[c];
+            n2 = n2 + (double)cv[c] * (double)cv[c];
+        }
+        const float nb = (float)sqrt(n2);
+        s[j] = (na == 0.0f || nb == 0.0f) ? 0.0f : dot / (na * nb);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
+    if (lane != 0) return;
+    // softmax with temperature (search.rs:29-44)
+    float mx = -INFINITY;
+    for (int j = 0; j < C; ++j) mx = fmaxf(mx, s[j]);
+    float sum = 0.0f;
+    for (int j = 0; j < C; ++j) { const float e = expf((s[j] - mx) / temperature); s[j] = e; sum = sum + e; }
+    sum = fmaxf(sum, 1e-10f);
+    for (int j = 0; j < C; ++j) s[j] = s[j] / sum;
+    // stable sort by weight descending (ties keep index order), take k
+    const int kk = min(k, C);
+    for (int t = 0; t < k; ++t) {
+        if (t >= kk) { out_idx[qi * k + t] = -1; out_w[qi * k + t] = 0.0f; continue; }
+        int best = -1;
+        float bw = 0.0f;
+        for (int j = 0; j < C; ++j) {
+            if (s[j] != s[j] && best < 0) continue;  // NaN weights sort as equal; skip
+            const float w = s[j];
+            if (w == -INFINITY) continue;
+            if (best < 0 || w > bw) { best = j; bw = w; }
+        }
+        if (best < 0) { out_idx[qi * k + t] = -1; out_w[qi * k + t] = 0.0f; continue; }
+        out_idx[qi * k + t] = best;
+        out_w[qi * k + t] = bw;
+        s[best] = -INFINITY;  // consumed
+    }
+}
+
+}  // namespace
+
+void edge_feat_attention(const EfaArgs& a) {
+    if (a.n <= 0) return;
+    ProfScope ps("efa_edge");
+    hipLaunchKernelGGL(k_edge_feat_scores, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, stream(), a);
+    const int64_t t = a.n * a.heads;
+    hipLaunchKernelGGL(k_edge_feat_softmax, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, stream(), a);
+    hipLaunchKernelGGL(k_edge_feat_out, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, stream(), a);
+    RVX_HIP(hipGetLastError());
+}
+
+void differentiable_search(const float* q, int64_t nq, const float* cand, int C, int d, int k, float temperature,
+                           float* sims, int64_t* out_idx, float* out_w) {
+    if (nq <= 0) return;
+    ProfScope ps("differentiable_search");
+    hipLaunchKernelGGL(k_diff_search, dim3((unsigned)nq), dim3(64), 0, stream(), q, nq, cand, C, d, k, temperature, sims,
+                       out_idx, out_w);
+    RVX_HIP(hipGetLastError());
+}
+
+}  // namespace rvx

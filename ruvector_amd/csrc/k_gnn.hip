@@ -1,0 +1,250 @@
+// k_gnn.hip — the per-edge and per-node kernels of RuvectorLayer::forward,
+// batched over a whole graph (crates/ruvector-gnn/src/layer.rs:379-451).
+//
+// The dense Linear layers run as MFMA GEMMs (gemm_f32.hip). What is left is
+// per destination node i with CSR neighbours j (edge order):
+//   K5 edge kernel (one wave per node):
+//     score_hj = (q_ih · k_jh) / sqrt(head_dim)        (layer.rs:184-193)
+//     a_hj = exp(s - max) / max(sum exp, 1e-10)         (layer.rs:196-199)
+//     att_i[h] = sum_j a_hj v_jh                        (layer.rs:202-207)
+//     wagg_i = sum_j w^_j m_j, w^ = w/sum(w) or 1/len   (layer.rs:421-445)
+//   gate kernel  r ⊙ h                                  (layer.rs:265)
+//   finish kernel (1-z)⊙h + z⊙h~, ×(1-dropout), LayerNorm (layer.rs:270-274, 448-451, 68-81)
+// Every per-neighbour sum runs in CSR order, one sequential f32 chain per
+// output element, like the reference loops. The q·k dot uses a lane tree.
+//
+// Traffic per edge: 3*H floats (k_j, v_j, m_j rows) + 4 B index (+4 B weight).
+#include "common.hpp"
+#include "gnn.hpp"
+
+namespace rvx {
+namespace {
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// Weighted-aggregate normaliser for row [beg,end): mode 0 none, 1 raw weights,
+// 2 pre-normalised weights.
+__device__ __forceinline__ float row_weight_sum(const float* w, int64_t beg, int64_t end) {
+    float s = 0.0f;
+    for (int64_t e = beg; e < end; ++e) s = s + w[e];  // weights.iter().sum()
+    return s;
+}
+__device__ __forceinline__ float norm_weight(int mode, const float* w, int64_t e, float wsum, int deg) {
+    if (mode == 1) return wsum > 0.0f ? w[e] / wsum : 1.0f / (float)deg;
+    return w[e];
+}
+
+// Fast path: H = 64*CPL, lane owns columns [lane*CPL, lane*CPL+CPL), a head is
+// G = head_dim/CPL consecutive lanes (G a power of two).
+template <int CPL>
+__global__ __launch_bounds__(256) void k_edge_attn_grouped(EdgeArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const int H = a.H, G = a.G;
+    const int head = (lane * CPL) / a.hd;
+    const int64_t beg = a.rp[i], end = a.rp[i + 1];
+    const int deg = (int)(end - beg);
+    const int c0 = lane * CPL;
+    float att[CPL], agg[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) { att[c] = 0.0f; agg[c] = 0.0f; }
+    if (deg == 0) {
+#pragma unroll
+        for (int c = 0; c < CPL; c += 4) {
+            *reinterpret_cast<float4*>(a.att + i * H + c0 + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+            *reinterpret_cast<float4*>(a.wagg + i * H + c0 + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        return;
+    }
+    float q[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; c += 4) {
+        const float4 v = ld4(a.qkv + i * (3 * (int64_t)H) + c0 + c);
+        q[c] = v.x; q[c + 1] = v.y; q[c + 2] = v.z; q[c + 3] = v.w;
+    }
+    const float scale = sqrtf((float)a.hd);
+    float mx = -INFINITY;
+    // pass 1: scores
+    for (int64_t e = beg; e < end; ++e) {
+        const int j = a.col[e];
+        const float* kr = a.qkv + (int64_t)j * (3 * (int64_t)H) + H + c0;
+        float p = 0.0f;
+#pragma unroll
+        for (int c = 0; c < CPL; c += 4) {
+            const float4 v = ld4(kr + c);
+            p = p + q[c] * v.x; p = p + q[c + 1] * v.y; p = p + q[c + 2] * v.z; p = p + q[c + 3] * v.w;
+        }
+        for (int o = 1; o < G; o <<= 1) p += __shfl_xor(p, o);
+        const float s = p / scale;
+        mx = fmaxf(mx, s);
+        if ((lane & (G - 1)) == 0) a.scores[e * a.heads + head] = s;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
+    // pass 2: sum of exp in neighbour order
+    float sum = 0.0f;
+    for (int64_t e = beg; e < end; ++e) sum = sum + expf(a.scores[e * a.heads + head] - mx);
+    sum = fmaxf(sum, 1e-10f);
+    float wsum = 0.0f;
+    if (a.wmode == 1) wsum = row_weight_sum(a.w, beg, end);
+    // pass 3: weighted sums of values and messages
+    for (int64_t e = beg; e < end; ++e) {
+        const int j = a.col[e];
+        const float wt = expf(a.scores[e * a.heads + head] - mx) / sum;
+        const float* vr = a.qkv + (int64_t)j * (3 * (int64_t)H) + 2 * H + c0;
+#pragma unroll
+        for (int c = 0; c < CPL; c += 4) {
+            const float4 v = ld4(vr + c);
+            att[c] = att[c] + wt * v.x; att[c + 1] = att[c + 1] + wt * v.y;
+            att[c + 2] = att[c + 2] + wt * v.z; att[c + 3] = att[c + 3] + wt * v.w;
+        }
+        if (a.wmode != 0) {
+            const float ww = norm_weight(a.wmode, a.w, e, wsum, deg);
+            const float* mr = a.m + (int64_t)j * H + c0;
+#pragma unroll
+            for (int c = 0; c < CPL; c += 4) {
+                const float4 v = ld4(mr + c);
+                agg[c] = agg[c] + ww * v.x; agg[c + 1] = agg[c + 1] + ww * v.y;
+                agg[c + 2] = agg[c + 2] + ww * v.z; agg[c + 3] = agg[c + 3] + ww * v.w;
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < CPL; c += 4) {
+        *reinterpret_cast<float4*>(a.att + i * H + c0 + c) = make_float4(att[c], att[c + 1], att[c + 2], att[c + 3]);
+        *reinterpret_cast<float4*>(a.wagg + i * H + c0 + c) = make_float4(agg[c], agg[c + 1], agg[c + 2], agg[c + 3]);
+    }
+}
+
+// Any H / heads: one wave per node. Scores: one lane per neighbour, a fully
+// sequential dot over the head (the reference order); sums: lanes over columns.
+__global__ __launch_bounds__(256) void k_edge_attn_generic(EdgeArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const int H = a.H, hd = a.hd, heads = a.heads;
+    const int64_t beg = a.rp[i], end = a.rp[i + 1];
+    const int deg = (int)(end - beg);
+    const float* qi = a.qkv + i * (3 * (int64_t)H);
+    const float scale = sqrtf((float)hd);
+    for (int64_t e = beg + lane; e < end; e += 64) {
+        const float* kr = a.qkv + (int64_t)a.col[e] * (3 * (int64_t)H) + H;
+        for (int h = 0; h < heads; ++h) {
+            float p = 0.0f;
+            for (int c = 0; c < hd; ++c) p = p + qi[h * hd + c] * kr[h * hd + c];
+            a.scores[e * heads + h] = p / scale;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
+    float wsum = 0.0f;
+    if (a.wmode == 1 && deg > 0) wsum = row_weight_sum(a.w, beg, end);
+    for (int c = lane; c < H; c += 64) {
+        const int h = c / hd;
+        float mx = -INFINITY;
+        for (int64_t e = beg; e < end; ++e) mx = fmaxf(mx, a.scores[e * heads + h]);
+        float sum = 0.0f;
+        for (int64_t e = beg; e < end; ++e) sum = sum + expf(a.scores[e * heads + h] - mx);
+        sum = fmaxf(sum, 1e-10f);
+        float at = 0.0f, ag = 0.0f;
+        for (int64_t e = beg; e < end; ++e) {
+            const int j = a.col[e];
+            const float wt = expf(a.scores[e * heads + h] - mx) / sum;
+            at = at + wt * a.qkv[(int64_t)j * (3 * (int64_t)H) + 2 * H + c];
+            if (a.wmode != 0) ag = ag + norm_weight(a.wmode, a.w, e, wsum, deg) * a.m[(int64_t)j * H + c];
+        }
+        a.att[i * H + c] = at;
+        a.wagg[i * H + c] = ag;
+    }
+}
+
+__global__ void k_mul(const float* r, int64_t ldr, const float* h, float* out, int64_t n, int H) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n * H) return;
+    const int64_t i = idx / H;
+    const int c = (int)(idx % H);
+    out[idx] = r[i * ldr + c] * h[idx];
+}
+
+// (1-z)⊙h + z⊙h~, ×(1-dropout), LayerNorm; deg==0 rows: LayerNorm(m_i).
+__global__ __launch_bounds__(256) void k_gru_finish(FinishArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const int H = a.H;
+    const bool iso = a.rp[i + 1] == a.rp[i];
+    float* y = a.y + i * H;
+    float s = 0.0f;
+    for (int c = lane; c < H; c += 64) {
+        float v;
+        const float h = a.m[i * H + c];
+        if (iso) v = h;
+        else {
+            const float z = a.zr[i * 2 * (int64_t)H + c];
+            const float t1 = (1.0f - z) * h;
+            const float t2 = z * a.ht[i * H + c];
+            v = (t1 + t2) * a.keep;
+        }
+        y[c] = v;
+        s += v;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / (float)H;
+    float var = 0.0f;
+    for (int c = lane; c < H; c += 64) { const float d = y[c] - mean; var += d * d; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) var += __shfl_xor(var, o);
+    var = var / (float)H;
+    const float den = sqrtf(var + a.eps);
+    for (int c = lane; c < H; c += 64) y[c] = a.gamma[c] * ((y[c] - mean) / den) + a.beta[c];
+}
+
+}  // namespace
+
+void edge_attention(const EdgeArgs& a) {
+    if (a.n <= 0) return;
+    const dim3 grid((unsigned)((a.n + 3) / 4)), block(256);
+    ProfScope ps("gnn_edge_attention");
+    const bool aligned = (((uintptr_t)a.qkv | (uintptr_t)a.m | (uintptr_t)a.att | (uintptr_t)a.wagg) & 15) == 0;
+    if (aligned && a.H % 64 == 0 && a.G > 0) {
+        switch (a.H / 64) {
+            case 4: hipLaunchKernelGGL(k_edge_attn_grouped<4>, grid, block, 0, stream(), a); break;
+            case 8: hipLaunchKernelGGL(k_edge_attn_grouped<8>, grid, block, 0, stream(), a); break;
+            case 12: hipLaunchKernelGGL(k_edge_attn_grouped<12>, grid, block, 0, stream(), a); break;
+            case 16: hipLaunchKernelGGL(k_edge_attn_grouped<16>, grid, block, 0, stream(), a); break;
+            default: hipLaunchKernelGGL(k_edge_attn_generic, grid, block, 0, stream(), a); break;
+        }
+    } else {
+        hipLaunchKernelGGL(k_edge_attn_generic, grid, block, 0, stream(), a);
+    }
+    RVX_HIP(hipGetLastError());
+}
+
+int edge_group_lanes(int H, int heads) {
+    if (H % 64 != 0 || heads <= 0 || H % heads != 0) return 0;
+    const int cpl = H / 64, hd = H / heads;
+    if (cpl % 4 != 0 || hd % cpl != 0) return 0;
+    const int g = hd / cpl;
+    if (g > 64 || (g & (g - 1)) != 0) return 0;
+    if (cpl != 4 && cpl != 8 && cpl != 12 && cpl != 16) return 0;
+    return g;
+}
+
+void mul_rows(const float* r, int64_t ldr, const float* h, float* out, int64_t n, int H) {
+    const int64_t total = n * H;
+    if (total <= 0) return;
+    ProfScope ps("gnn_gate_mul");
+    hipLaunchKernelGGL(k_mul, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream(), r, ldr, h, out, n, H);
+    RVX_HIP(hipGetLastError());
+}
+
+void gru_finish(const FinishArgs& a) {
+    if (a.n <= 0) return;
+    ProfScope ps("gnn_finish");
+    hipLaunchKernelGGL(k_gru_finish, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, stream(), a);
+    RVX_HIP(hipGetLastError());
+}
+
+}  // namespace rvx

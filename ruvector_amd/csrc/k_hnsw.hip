@@ -1,0 +1,312 @@
+// k_hnsw.hip — batched HNSW search on a fixed graph (one wave per query).
+//
+// Semantics are those of hnsw_rs 0.3.3 as vendored in the reference:
+//   Hnsw::search -> search_filter  (patches/hnsw_rs/src/hnsw.rs:1475-1589)
+//     upper layers: ONE pass over the pivot's neighbour list per layer, the
+//     pivot moves to the first neighbour with the smallest distance below the
+//     running best (:1499-1517) — no iterated hill climb;
+//     layer 0: search_layer(ef = max(ef_arg, k)) (:1519-1523)
+//   search_layer (:913-1055): pop the nearest candidate c; stop when
+//     d(c) > d(farthest result); for each neighbour e of c in stored order that
+//     is not yet visited: mark visited, admit iff d(e) < d(farthest) or
+//     |R| < ef, push to candidates and results, pop the farthest when |R| > ef.
+//   into_sorted_vec + first min(k, ef, |R|) (:1532-1568).
+// Distances use the reference's scalar accumulation order (see k_scan.hip), so
+// on the same graph the returned ids and distances are bit-exact. The
+// reference orders heap ties by distance only (:272-296); here ties are
+// broken by node id in both heaps (a measure-zero difference on real data).
+//
+// Per query: result set R as an ascending sorted array (farthest last) and the
+// candidate set C as a descending sorted array (nearest last) in LDS, updated
+// with wave-parallel sorted inserts; the visited set is an open-addressing
+// hash in a per-wave global scratch slot (32K entries, CAS-claimed by all
+// lanes at once); neighbour distances are computed one row per lane.
+#include "common.hpp"
+#include "graph.hpp"
+#include "hnsw.hpp"
+
+namespace rvx {
+namespace {
+
+constexpr int VCAP = 32768;  // visited-set slots per query (power of two)
+constexpr int C_EXTRA = 128; // candidate capacity = ef + C_EXTRA
+
+template <int METRIC>
+__device__ __forceinline__ float row_dist(const float* __restrict__ qs, const float* __restrict__ x, int d, float qn,
+                                          float xn) {
+    float acc = 0.0f;
+    if ((d & 3) == 0) {
+        const float4* r = reinterpret_cast<const float4*>(x);
+        const float4* qq = reinterpret_cast<const float4*>(qs);
+        for (int k = 0; k < (d >> 2); ++k) {
+            const float4 v = r[k], q = qq[k];
+            if (METRIC == RVX_METRIC_L2) {
+                float t = q.x - v.x; acc = acc + t * t;
+                t = q.y - v.y; acc = acc + t * t;
+                t = q.z - v.z; acc = acc + t * t;
+                t = q.w - v.w; acc = acc + t * t;
+            } else if (METRIC == RVX_METRIC_L1) {
+                acc = acc + fabsf(q.x - v.x); acc = acc + fabsf(q.y - v.y);
+                acc = acc + fabsf(q.z - v.z); acc = acc + fabsf(q.w - v.w);
+            } else {
+                acc = acc + q.x * v.x; acc = acc + q.y * v.y; acc = acc + q.z * v.z; acc = acc + q.w * v.w;
+            }
+        }
+    } else {
+        for (int k = 0; k < d; ++k) {
+            const float q = qs[k], v = x[k];
+            if (METRIC == RVX_METRIC_L2) { const float t = q - v; acc = acc + t * t; }
+            else if (METRIC == RVX_METRIC_L1) acc = acc + fabsf(q - v);
+            else acc = acc + q * v;
+        }
+    }
+    if (METRIC == RVX_METRIC_L2) return sqrtf(acc);
+    if (METRIC == RVX_METRIC_DOT) return -acc;
+    if (METRIC == RVX_METRIC_COSINE) return (qn > 1e-8f && xn > 1e-8f) ? 1.0f - acc / (qn * xn) : 1.0f;
+    return acc;
+}
+
+// Claim `node` in a query's visited set: true if it was not visited yet.
+// Slots whose tag is another query's are free (the table is zeroed per launch).
+__device__ __forceinline__ bool visit_claim(unsigned long long* vis, unsigned long long qtag, int node) {
+    const unsigned long long key = qtag | (unsigned)(node + 1);
+    unsigned h = ((unsigned)node * 2654435761u) & (VCAP - 1);
+    unsigned long long cur = __hip_atomic_load(&vis[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int probe = 0; probe < 4 * VCAP; ++probe) {
+        if ((cur & 0xFFFFFFFF00000000ull) == qtag) {
+            if (cur == key) return false;
+            h = (h + 1) & (VCAP - 1);
+            cur = __hip_atomic_load(&vis[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        const unsigned long long prev = atomicCAS(&vis[h], cur, key);
+        if (prev == cur) return true;
+        cur = prev;
+    }
+    return false;  // table full: cannot happen below VCAP visited nodes
+}
+
+__device__ __forceinline__ bool lt(float d, int id, float bd, int bid) { return d < bd || (d == bd && id < bid); }
+
+struct SearchArgs {
+    HnswDev g;
+    const float* x; const float* xnorm; int d;
+    const float* q; const float* qnorm; int64_t nq;
+    int k, ef;
+    unsigned long long* visited;  // [nslots][VCAP] {query tag, node+1}, zeroed per launch
+    int nslots;
+    float* out_d; int64_t* out_i; int32_t* out_n;  // [nq][k]
+    int* status;       // set to 1 on candidate overflow
+};
+
+// wave-parallel insert of (d,id) into an array sorted ascending (asc=true) or
+// descending by (d,id); size must be < capacity. Returns new size.
+__device__ __forceinline__ int sorted_insert(float* ad, int* ai, int size, float d, int id, bool asc, int lane) {
+    // position = number of elements that stay in front of the new one
+    int cnt = 0;
+    for (int i = lane; i < size; i += 64) {
+        const bool before = asc ? lt(ad[i], ai[i], d, id) : lt(d, id, ad[i], ai[i]);
+        cnt += before ? 1 : 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    const int pos = cnt;
+    // shift [pos, size) right by one, walking chunks from the end so every
+    // read of a chunk happens before the writes that could overwrite it
+    for (int base = ((size - 1) / 64) * 64; base >= pos - 63 && base >= 0; base -= 64) {
+        const int i = base + lane;
+        float vd = 0.f; int vi = 0;
+        const bool mv = (i >= pos && i < size);
+        if (mv) { vd = ad[i]; vi = ai[i]; }
+        __builtin_amdgcn_wave_barrier();
+        if (mv) { ad[i + 1] = vd; ai[i + 1] = vi; }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0) { ad[pos] = d; ai[pos] = id; }
+    __builtin_amdgcn_wave_barrier();
+    return size + 1;
+}
+
+template <int METRIC>
+__global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    const int lane = threadIdx.x;
+    const int ef = a.ef;
+    const int ccap = ef + C_EXTRA;
+    float* qs = reinterpret_cast<float*>(lds_raw);             // [d rounded to 4]
+    const int dq = (a.d + 3) & ~3;
+    float* rd = qs + dq;                                        // R dist [ef+1]
+    int* ri = reinterpret_cast<int*>(rd + ef + 1);              // R id
+    float* cd = reinterpret_cast<float*>(ri + ef + 1);          // C dist [ccap]
+    int* ci = reinterpret_cast<int*>(cd + ccap);                // C id
+
+    unsigned long long* vis = a.visited + (int64_t)blockIdx.x * VCAP;
+
+    for (int64_t qi = blockIdx.x; qi < a.nq; qi += a.nslots) {
+        const unsigned long long qtag = (unsigned long long)(qi + 1) << 32;
+        for (int i = lane; i < dq; i += 64) qs[i] = (i < a.d) ? a.q[qi * a.d + i] : 0.0f;
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        const float qn = (METRIC == RVX_METRIC_COSINE) ? a.qnorm[qi] : 0.0f;
+        auto dist_of = [&](int node) {
+            return row_dist<METRIC>(qs, a.x + (int64_t)node * a.d, a.d,
+                                    qn, METRIC == RVX_METRIC_COSINE ? a.xnorm[node] : 0.0f);
+        };
+
+        // ---- upper layers: single pass per layer (search_filter :1499-1517)
+        int pivot = (int)a.g.entry;
+        float best = dist_of(pivot);
+        for (int l = a.g.max_level; l >= 1; --l) {
+            // locate pivot in layer l's sorted id list
+            const int* ids = a.g.up_ids + a.g.up_ids_off[l];
+            const int64_t cnt = a.g.up_count[l];
+            int64_t lo = 0, hi = cnt;
+            while (lo < hi) { const int64_t mid = (lo + hi) >> 1; if (ids[mid] < pivot) lo = mid + 1; else hi = mid; }
+            if (lo >= cnt || ids[lo] != pivot) continue;  // pivot not on this layer (cannot happen for a valid graph)
+            const int64_t* rp = a.g.up_rp + a.g.up_rp_off[l];
+            const int* col = a.g.up_col + a.g.up_col_off[l];
+            const int64_t b = rp[lo], e = rp[lo + 1];
+            int new_pivot = pivot;
+            float new_best = best;
+            for (int64_t c0 = b; c0 < e; c0 += 64) {
+                const int64_t p = c0 + lane;
+                float dd = INFINITY;
+                int pos = INT_MAX, nid = -1;
+                if (p < e) { nid = col[p]; dd = dist_of(nid); pos = (int)(p - b); }
+                // first position holding the minimum of this chunk
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    const float od = __shfl_xor(dd, o);
+                    const int op = __shfl_xor(pos, o), on = __shfl_xor(nid, o);
+                    if (od < dd || (od == dd && op < pos)) { dd = od; pos = op; nid = on; }
+                }
+                if (dd < new_best) { new_best = dd; new_pivot = nid; }
+            }
+            pivot = new_pivot;
+            best = new_best;
+        }
+
+        // ---- layer 0: search_layer (:913-1055)
+        int rs = 0, cs = 0;
+        bool overflow = false;
+        {
+            const float d0 = dist_of(pivot);
+            if (lane == 0) {
+                rd[0] = d0; ri[0] = pivot; cd[0] = d0; ci[0] = pivot;
+                visit_claim(vis, qtag, pivot);
+            }
+            rs = 1; cs = 1;
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
+        }
+        while (cs > 0 && !overflow) {
+            const float c_d = cd[cs - 1];
+            const int c_id = ci[cs - 1];
+            cs -= 1;
+            if (c_d > rd[rs - 1]) break;  // -(c.dist) > f.dist  -> return
+            const int64_t b = a.g.rp0[c_id], e = a.g.rp0[c_id + 1];
+            for (int64_t c0 = b; c0 < e; c0 += 64) {
+                const int64_t p = c0 + lane;
+                int nid = -1;
+                bool fresh = false;
+                if (p < e) {
+                    nid = a.g.col0[p];
+                    fresh = visit_claim(vis, qtag, nid);
+                }
+                float dd = INFINITY;
+                if (fresh) dd = dist_of(nid);
+                // sequential admission in neighbour order (hnsw.rs:1004-1046)
+                unsigned long long todo = __ballot(fresh);
+                while (todo) {
+                    const int src = __ffsll((long long)todo) - 1;
+                    todo &= todo - 1;
+                    const float ed = __shfl(dd, src);
+                    const int eid = __shfl(nid, src);
+                    const float fd = rd[rs - 1];
+                    if (ed < fd || rs < ef) {
+                        if (cs >= ccap) {  // drop a candidate that can only terminate the search
+                            if (cd[0] > fd) {
+                                // compact: remove element 0 (the farthest)
+                                for (int base = 0; base < cs - 1; base += 64) {
+                                    const int i = base + lane;
+                                    float vd = 0.f; int vi = 0;
+                                    const bool mv = i + 1 < cs;
+                                    if (mv) { vd = cd[i + 1]; vi = ci[i + 1]; }
+                                    __builtin_amdgcn_wave_barrier();
+                                    if (mv) { cd[i] = vd; ci[i] = vi; }
+                                    __builtin_amdgcn_wave_barrier();
+                                }
+                                cs -= 1;
+                            } else {
+                                overflow = true;
+                                break;
+                            }
+                        }
+                        cs = sorted_insert(cd, ci, cs, ed, eid, /*asc=*/false, lane);
+                        rs = sorted_insert(rd, ri, rs, ed, eid, /*asc=*/true, lane);
+                        if (rs > ef) rs -= 1;  // pop farthest
+                    }
+                }
+                if (overflow) break;
+            }
+        }
+        if (overflow && lane == 0) atomicExch(a.status, 1);
+
+        // ---- output: ascending, first min(k, ef, |R|)
+        const int take = min(a.k, rs);
+        for (int s = lane; s < a.k; s += 64) {
+            a.out_d[qi * a.k + s] = s < take ? rd[s] : INFINITY;
+            a.out_i[qi * a.k + s] = s < take ? (int64_t)ri[s] : (int64_t)-1;
+        }
+        if (lane == 0) a.out_n[qi] = take;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+}  // namespace
+
+size_t hnsw_search_lds(int d, int ef) {
+    const int dq = (d + 3) & ~3;
+    return (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)(ef + C_EXTRA) * 8;
+}
+
+void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
+                 const float* qnorm, int64_t nq, int k, int ef, float* out_d, int64_t* out_i, int32_t* out_n,
+                 const char* tag) {
+    if (nq <= 0) return;
+    RVX_REQUIRE(ef >= 1 && ef <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER,
+                "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
+    const int nslots = (int)std::min<int64_t>(nq, 8192);
+    auto* vis = (unsigned long long*)scratch_bytes("hnsw_visited", (int64_t)nslots * VCAP * 8);
+    int* status = (int*)scratch_bytes("hnsw_status", 256);
+    RVX_HIP(hipMemsetAsync(vis, 0, (size_t)nslots * VCAP * 8, stream()));
+    RVX_HIP(hipMemsetAsync(status, 0, 4, stream()));
+    SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, nslots, out_d, out_i, out_n, status};
+    const size_t lds = hnsw_search_lds(d, ef);
+    RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    {
+        ProfScope ps(tag ? tag : "hnsw_search");
+        switch (metric) {
+            case RVX_METRIC_L2: hipLaunchKernelGGL(k_hnsw_search<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, stream(), a); break;
+            case RVX_METRIC_COSINE: hipLaunchKernelGGL(k_hnsw_search<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, stream(), a); break;
+            case RVX_METRIC_DOT: hipLaunchKernelGGL(k_hnsw_search<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, stream(), a); break;
+            case RVX_METRIC_L1: hipLaunchKernelGGL(k_hnsw_search<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, stream(), a); break;
+            default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by HNSW search");
+        }
+        RVX_HIP(hipGetLastError());
+    }
+    int st = 0;
+    RVX_HIP(hipMemcpyAsync(&st, status, 4, hipMemcpyDeviceToHost, stream()));
+    sync();
+    RVX_REQUIRE(st == 0, RVX_ERR_INDEX, "HNSW candidate list overflow (pathological distance ties)");
+}
+
+}  // namespace rvx

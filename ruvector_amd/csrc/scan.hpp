@@ -1,0 +1,26 @@
+// scan.hpp — exact distance scan / top-k launchers (k_scan.hip).
+#pragma once
+#include <cstdint>
+
+namespace rvx {
+
+constexpr int SCAN_MAX_K = 128;
+
+// Sequential-order row norms sqrt(sum x*x) (distance.rs:56-57), one per row.
+void row_norms(const float* x, int64_t n, int d, float* out);
+// Top-k (ascending (distance, id)) of every query against rows [0, n) of x.
+// Output ids are row + id_offset; rows with deleted[row] != 0 are skipped.
+void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
+               const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
+               const char* tag);
+// out[i][j] = distance(q_i, x_j) in the reference scalar order.
+void distance_matrix(int metric, const float* q, const float* qn, int64_t nq, const float* x, const float* xn, int64_t n,
+                     int d, float* out);
+
+// out[p] = distance(x[owner(p)], x[col[p]]) for every CSR edge p (wave per row).
+void edge_distances(int metric, const float* x, const float* xnorm, const int64_t* rp, const int32_t* col, int64_t n,
+                    int d, float* out);
+// Poincaré ball distance matrix (poincare.rs:227-255), curvature c.
+void poincare_matrix(const float* q, int64_t nq, const float* x, int64_t n, int d, float c, float* out);
+
+}  // namespace rvx

@@ -1,0 +1,101 @@
+"""Node-range sharding across GPUs of one node.
+
+One process per GPU. Rank r owns destination rows [r*n_local, (r+1)*n_local)
+and the CSR rows of those nodes (global column ids). Per GNN layer the only
+exchange is an all-gather of the node table (the halo is effectively the
+whole graph for HNSW-like topologies); HNSW shards merge per-shard top-k.
+
+The exchange is pluggable so the same driver runs over RCCL on MI355X
+(RcclComm, device buffers, librvx) and over torch.distributed gloo in the
+CPU tests (tests/test_shard_gloo.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Callable, List, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+from .device import Buffer
+
+
+@dataclass(frozen=True)
+class ShardPlan:
+    num_nodes: int
+    world: int
+
+    def rows(self, rank: int) -> Tuple[int, int]:
+        """[begin, end) of the rows owned by `rank` (contiguous, as even as possible)."""
+        base, extra = divmod(self.num_nodes, self.world)
+        begin = rank * base + min(rank, extra)
+        return begin, begin + base + (1 if rank < extra else 0)
+
+    def owner(self, node: int) -> int:
+        base, extra = divmod(self.num_nodes, self.world)
+        cut = extra * (base + 1)
+        return node // (base + 1) if node < cut else extra + (node - cut) // max(base, 1)
+
+    def equal(self) -> bool:
+        return self.num_nodes % self.world == 0
+
+
+class RcclComm:
+    """RCCL communicator of librvx (one per process/GPU)."""
+
+    def __init__(self, world: int, rank: int, unique_id: bytes):
+        arr = (C.c_uint8 * L.COMM_ID_BYTES).from_buffer_copy(unique_id)
+        h = C.c_void_p()
+        L.call("rvx_comm_init", arr, int(world), int(rank), C.byref(h))
+        self._h, self.world, self.rank = h, world, rank
+
+    @staticmethod
+    def unique_id() -> bytes:
+        arr = (C.c_uint8 * L.COMM_ID_BYTES)()
+        L.call("rvx_comm_unique_id", arr)
+        return bytes(arr)
+
+    def allgather(self, send: Buffer, count: int, recv: Buffer) -> None:
+        L.call("rvx_comm_allgather_f32", self._h, send.handle, int(count), recv.handle)
+
+    def max(self, value: float) -> float:
+        v = C.c_double(value)
+        L.call("rvx_comm_allreduce_max_f64", self._h, C.byref(v))
+        return v.value
+
+    def __del__(self):
+        try:
+            if self._h:
+                L.call("rvx_comm_destroy", self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+def merge_topk(parts: Sequence[Tuple[np.ndarray, np.ndarray]], k: int) -> Tuple[np.ndarray, np.ndarray]:
+    """ShardedHyperbolicHnsw::search merge (crates/ruvector-hyperbolic-hnsw/src/shard.rs:354-373):
+    concatenate per-shard (global id, distance) lists, sort by distance (ties by id), truncate k."""
+    ids = np.concatenate([p[0] for p in parts], axis=1)
+    d = np.concatenate([p[1] for p in parts], axis=1)
+    out_i = np.empty((ids.shape[0], k), ids.dtype)
+    out_d = np.empty((ids.shape[0], k), d.dtype)
+    for q in range(ids.shape[0]):
+        order = np.lexsort((ids[q], d[q]))[:k]
+        out_i[q], out_d[q] = ids[q][order], d[q][order]
+    return out_i, out_d
+
+
+def sharded_layers(x_local, layers: Sequence, plan: ShardPlan, rank: int,
+                   allgather: Callable, forward_rows: Callable):
+    """Run `layers` over a node-range-sharded graph.
+
+    allgather(local) -> full table; forward_rows(layer, full_table, row_begin, row_end) -> owned rows.
+    Returns this rank's rows of the last layer's output.
+    """
+    h = x_local
+    b, e = plan.rows(rank)
+    for layer in layers:
+        full = allgather(h)
+        h = forward_rows(layer, full, b, e)
+    return h

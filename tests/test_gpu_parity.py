@@ -1,0 +1,371 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar (north star): bit-exact for integer/index work and top-k ids; within
+1e-5 relative on f32 embeddings. "Relative" here is max|gpu - ref| divided by
+max|ref| over the compared row block (TOL below), i.e. error measured against
+the embedding's scale, plus an element-wise check with an absolute floor.
+Kernels that restate the reference's scalar arithmetic (distances,
+aggregation, generators, differentiable_search) are required to be bit-exact.
+"""
+import json
+import math
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+rv = pytest.importorskip("ruvector_amd")
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-30))
+
+
+def assert_close(a, b, tol=TOL):
+    assert a.shape == b.shape
+    assert np.all(np.isfinite(a)) == np.all(np.isfinite(b))
+    e = rel_err(a, b)
+    assert e <= tol, f"relative error {e:.3e} > {tol}"
+
+
+# ------------------------------------------------------------------ generators
+def test_fill_uniform_bit_exact():
+    b = rv.Buffer(4 * 100003)
+    b.fill_uniform(100003, 77, -1.0, 1.0)
+    assert np.array_equal(b.download(np.float32, 100003), O.fill_uniform(100003, 77))
+
+
+def test_random_csr_bit_exact():
+    g = rv.Graph.random(5000, 7, 11)
+    rp, col = O.random_csr(5000, 7, 11)
+    assert g.num_edges == len(col) and g.max_degree == 7
+    rp_d = g._keep[0].download(np.int64, 5001)
+    col_d = g._keep[1].download(np.int32, len(col))
+    assert np.array_equal(rp_d, rp) and np.array_equal(col_d, col)
+
+
+# ------------------------------------------------------------------ aggregation
+@pytest.mark.parametrize("dim", [3, 16, 128, 256, 768, 1000, 1100])
+@pytest.mark.parametrize("method", ["sum", "mean", "max"])
+def test_aggregate_bit_exact(dim, method):
+    n = 300
+    x = O.fill_uniform(n * dim, dim).reshape(n, dim)
+    edges = [(int(s), int(t)) for s, t in np.random.default_rng(dim).integers(0, n - 20, (2000, 2))]
+    rp, col, _ = O.build_csr(n, edges)  # the last 20 nodes stay isolated
+    g = rv.Graph.from_csr(rp, col)
+    xb, ob = rv.Buffer.from_numpy(x), rv.Buffer(x.nbytes)
+    rv.aggregate(xb, g, dim, method, ob)
+    got = ob.download(np.float32, x.shape)
+    ref = O.aggregate(x, rp, col, method)
+    assert np.array_equal(got, ref)
+
+
+def test_aggregate_weighted_keep_isolated_bit_exact():
+    n, dim = 200, 64
+    x = O.fill_uniform(n * dim, 5).reshape(n, dim)
+    edges = [(int(s), int(t)) for s, t in np.random.default_rng(1).integers(0, 150, (900, 2))]
+    w = O.fill_uniform(len(edges), 6, 0.0, 2.0)
+    rp, col, wc = O.build_csr(n, edges, w)
+    g = rv.Graph.from_csr(rp, col, wc)
+    xb, ob = rv.Buffer.from_numpy(x), rv.Buffer(x.nbytes)
+    rv.aggregate(xb, g, dim, "sum", ob, weighted=True, keep_isolated=True)
+    assert np.array_equal(ob.download(np.float32, x.shape), O.aggregate(x, rp, col, "sum", wc, keep_isolated=True))
+
+
+def test_graph_from_edges_matches_build_adjacency_list():
+    edges = [(0, 1), (1, 2), (2, 0), (5, 0), (1, 0)]
+    g = rv.Graph.from_edges(3, edges)
+    assert g.num_edges == 4 and g.max_degree == 2  # (5,0) dropped
+
+
+# ------------------------------------------------------------------ distances
+@pytest.mark.parametrize("metric,name", [(rv.DistanceMetric.Euclidean, "l2"), (rv.DistanceMetric.Cosine, "cosine"),
+                                         (rv.DistanceMetric.DotProduct, "dot"), (rv.DistanceMetric.Manhattan, "l1")])
+@pytest.mark.parametrize("d", [3, 128, 131])
+def test_distance_matrix_bit_exact(metric, name, d):
+    q = O.fill_uniform(17 * d, 1).reshape(17, d)
+    x = O.fill_uniform(301 * d, 2).reshape(301, d)
+    assert np.array_equal(rv.distance_matrix(q, x, metric), O.distance_matrix(q, x, name))
+
+
+def test_reference_distance_unit_cases():
+    assert abs(rv.distance([1, 2, 3], [4, 5, 6], rv.DistanceMetric.Euclidean) - 5.196) < 0.01
+    assert abs(rv.distance([1, 2, 3], [4, 5, 6], rv.DistanceMetric.DotProduct) + 32.0) < 0.01
+    assert abs(rv.distance([1, 2, 3], [4, 5, 6], rv.DistanceMetric.Manhattan) - 9.0) < 0.01
+    assert rv.distance([1, 0, 0], [-1, 0, 0], rv.DistanceMetric.Cosine) > 1.5
+    with pytest.raises(rv.RuvectorError):
+        rv.distance([1, 2], [1, 2, 3], rv.DistanceMetric.Euclidean)
+
+
+# ------------------------------------------------------------------ flat index
+@pytest.mark.parametrize("metric,name", [(rv.DistanceMetric.Euclidean, "l2"), (rv.DistanceMetric.Cosine, "cosine"),
+                                         (rv.DistanceMetric.DotProduct, "dot"), (rv.DistanceMetric.Manhattan, "l1")])
+@pytest.mark.parametrize("k", [1, 10, 100])
+def test_flat_search_bit_exact(metric, name, k):
+    n, d = 5003, 64
+    x = O.fill_uniform(n * d, 21).reshape(n, d)
+    q = O.fill_uniform(70 * d, 22).reshape(70, d)
+    idx = rv.FlatIndex(d, metric)
+    idx.add_array(x, np.arange(n, dtype=np.uint64))
+    ids, dist, _ = idx.search_array(q, k)
+    rids, rd = O.flat_search(x, q, k, name)
+    assert np.array_equal(ids.astype(np.int64), rids)
+    assert np.array_equal(dist, rd)
+
+
+def test_flat_search_remove_and_string_ids():
+    d = 8
+    idx = rv.FlatIndex(d, rv.DistanceMetric.Euclidean)
+    x = O.fill_uniform(50 * d, 3).reshape(50, d)
+    idx.add_batch([(f"vec_{i}", x[i]) for i in range(50)])
+    assert len(idx) == 50
+    r = idx.search(x[7], 3)
+    assert r[0].id == "vec_7" and r[0].score == 0.0
+    assert idx.remove("vec_7") and not idx.remove("vec_7")
+    assert len(idx) == 49
+    r = idx.search(x[7], 3)
+    assert "vec_7" not in [s.id for s in r] and len(r) == 3
+    deleted = np.zeros(50, np.uint8)
+    deleted[7] = 1
+    rids, _ = O.flat_search(x, x[7:8], 3, "l2", deleted=deleted)
+    assert [s.id for s in r] == [f"vec_{i}" for i in rids[0]]
+    with pytest.raises(rv.RuvectorError):
+        idx.add_batch([("bad", [1.0, 2.0])])
+
+
+def test_brute_force_large_k_and_ragged_tail():
+    n, d = 1000, 32
+    x = O.fill_uniform(n * d, 31).reshape(n, d)
+    idx = rv.FlatIndex(d, rv.DistanceMetric.Euclidean)
+    idx.add_array(x[:n], np.arange(n, dtype=np.uint64))
+    ids, dist = idx.brute_force_array(x[:5], 128)
+    rids, rd = O.flat_search(x, x[:5], 128, "l2")
+    assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd)
+
+
+# ------------------------------------------------------------------ HNSW search on a fixed graph
+def _hnsw_pair(n, d, metric, m, efc, seed):
+    x = O.fill_uniform(n * d, seed).reshape(n, d)
+    if metric == "cosine":
+        x = (x / np.sqrt(np.sum(x * x, 1, dtype=np.float32))[:, None]).astype(np.float32)
+    h = O.Hnsw(d, metric, m=m, ef_construction=efc, seed=seed)
+    h.insert(x, threads=8)
+    g = h.export()
+    idx = rv.HnswIndex(d, rv.DistanceMetric.Euclidean if metric == "l2" else rv.DistanceMetric.Cosine,
+                       rv.HnswConfig(m=m, ef_construction=efc, ef_search=100))
+    idx.add_array(x, np.arange(n, dtype=np.uint64))
+    idx.load_graph(g)
+    return x, h, g, idx
+
+
+@pytest.mark.parametrize("metric", ["l2", "cosine"])
+def test_hnsw_search_bit_exact_on_same_graph(metric):
+    x, h, g, idx = _hnsw_pair(4000, 48, metric, 16, 100, 5)
+    q = O.fill_uniform(200 * 48, 6).reshape(200, 48)
+    for k, ef in ((10, 10), (10, 50), (1, 100), (32, 200)):
+        ids, dist, cnt = idx.search_array(q, k, ef)
+        rids, rd, rc = h.search(q, k, ef)
+        assert np.array_equal(cnt, rc)
+        assert np.array_equal(ids.astype(np.int64)[:, :k], rids)
+        assert np.array_equal(dist, rd)
+
+
+def test_hnsw_layer0_export_matches_graph():
+    x, h, g, idx = _hnsw_pair(500, 16, "l2", 8, 40, 9)
+    rp, col, dist = idx.layer0()
+    assert np.array_equal(rp, g["row_ptr0"]) and np.array_equal(col, g["col0"])
+    assert np.array_equal(dist, g["dist0"])  # stored neighbour distances, reference order
+
+
+def test_hnsw_recall_reference_threshold():
+    # hnsw_integration_test.rs:122-185: 1000 unit vectors, M=32, ef_c=200, ef_s=200 -> recall >= 0.95
+    x, h, g, idx = _hnsw_pair(1000, 128, "cosine", 32, 200, 42)
+    q = x[::50]
+    ids, _, _ = idx.search_array(q, 10, 200)
+    gt, _ = idx.brute_force_array(q, 10)
+    rec = np.mean([len(set(a.tolist()) & set(b.tolist())) / 10 for a, b in zip(gt, ids)])
+    assert rec >= 0.95
+
+
+# ------------------------------------------------------------------ GraphSAGE / GCN
+@pytest.mark.parametrize("in_f,out_f,n,deg", [(2, 2, 3, 1), (16, 32, 257, 5), (128, 128, 1000, 16),
+                                              (768, 768, 600, 32)])
+def test_graphsage_matches_oracle(in_f, out_f, n, deg):
+    x = O.fill_uniform(n * in_f, in_f + n).reshape(n, in_f)
+    rp, col = O.random_csr(n, deg, 99)
+    rp = rp.copy()
+    # make two nodes isolated (empty neighbourhood -> zeros aggregate)
+    rp2 = np.concatenate([[0], np.cumsum([0 if i in (1, n - 1) else deg for i in range(n)])]).astype(np.int64)
+    col2 = np.concatenate([col[i * deg:(i + 1) * deg] for i in range(n) if i not in (1, n - 1)]).astype(np.int32)
+    g = rv.Graph.from_csr(rp2, col2)
+    for agg, a_id in (("mean", 0), ("maxpool", 1)):
+        layer = rv.GraphSAGELayer(in_f, out_f, num_samples=deg, aggregator=agg)
+        y = layer.forward_graph(x, g)
+        ref = O.sage_forward(x, rp2, col2, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), a_id)
+        assert_close(y, ref)
+
+
+def test_graphsage_reference_unit_cases():
+    layer = rv.GraphSAGELayer(2, 2, 2)
+    y = layer.forward([[1.0, 2.0], [3.0, 4.0], [5.0, 6.0]], [(0, 1), (1, 2), (2, 0)])
+    assert y.shape == (3, 2)
+    y = layer.forward([[1.0, 2.0], [3.0, 4.0]], [(0, 1)])
+    for row in y:
+        nrm = float(np.sqrt(np.sum(row.astype(np.float64) ** 2)))
+        assert abs(nrm - 1.0) < 1e-5 or nrm == 0.0
+
+
+def test_graphsage_sampling_rejected():
+    layer = rv.GraphSAGELayer(4, 4, num_samples=1)
+    with pytest.raises(rv.GnnError) as e:
+        layer.forward(np.ones((3, 4), np.float32), [(0, 1), (2, 1)])
+    assert e.value.kind == "Unsupported"
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_gcn_matches_oracle(weighted):
+    n, f = 400, 64
+    x = O.fill_uniform(n * f, 8).reshape(n, f)
+    edges = [(int(s), int(t)) for s, t in np.random.default_rng(3).integers(0, n - 10, (3000, 2))]
+    ew = O.fill_uniform(len(edges), 9, 0.0, 1.0) if weighted else None
+    layer = rv.GCNLayer(f, f)
+    y = layer.forward(x, edges, ew)
+    rp, col, wc = O.build_csr(n, edges, ew)
+    ref = O.gcn_forward(x, rp, col, O.sage_init(f, f, 0), np.zeros(f, np.float32), wc)
+    assert_close(y, ref)
+    assert np.array_equal(y[-5:], np.maximum(x[-5:], 0))  # isolated rows pass through
+
+
+# ------------------------------------------------------------------ RuvectorLayer
+def _layer_and_weights(in_dim, hidden, heads, dropout, seed=1):
+    layer = rv.RuvectorLayer(in_dim, hidden, heads, dropout, seed=seed)
+    js = json.loads(layer.to_json())
+    return layer, O.RvlWeights(js), js
+
+
+def test_ruvector_layer_errors():
+    with pytest.raises(rv.GnnError) as e:
+        rv.RuvectorLayer(4, 8, 2, 1.5)
+    assert e.value.kind == "LayerConfig"
+    with pytest.raises(rv.GnnError) as e:
+        rv.RuvectorLayer(4, 7, 3, 0.1)
+    assert "divisible" in str(e.value)
+
+
+@pytest.mark.parametrize("in_dim,hidden,heads,deg", [(4, 8, 2, 2), (4, 8, 2, 0), (32, 64, 4, 5), (128, 256, 8, 12),
+                                                     (768, 768, 8, 32)])
+def test_ruvector_forward_one_matches_oracle(in_dim, hidden, heads, deg):
+    layer, W, _ = _layer_and_weights(in_dim, hidden, heads, 0.1)
+    node = O.fill_uniform(in_dim, 1)
+    nbrs = O.fill_uniform(deg * in_dim, 2).reshape(deg, in_dim)
+    w = O.fill_uniform(deg, 3, 0.0, 1.0)
+    got = layer.forward(node, list(nbrs), w)
+    ref = O.rvl_forward_one(W, node, nbrs, w)
+    assert_close(got, ref)
+
+
+def test_ruvector_forward_one_weight_edge_cases():
+    layer, W, _ = _layer_and_weights(16, 32, 4, 0.0)
+    node = O.fill_uniform(16, 5)
+    nbrs = O.fill_uniform(3 * 16, 6).reshape(3, 16)
+    for w in ([], [0.0, 0.0, 0.0], [-1.0, 0.5, 0.2], [0.4, 0.6], [1.0, 2.0, 3.0, 4.0]):
+        assert_close(layer.forward(node, list(nbrs), w), O.rvl_forward_one(W, node, nbrs, w))
+
+
+def test_ruvector_json_roundtrip_is_exact():
+    layer, W, js = _layer_and_weights(8, 16, 2, 0.25, seed=3)
+    again = rv.RuvectorLayer.from_json(layer.to_json())
+    node = O.fill_uniform(8, 1)
+    nbrs = list(O.fill_uniform(3 * 8, 2).reshape(3, 8))
+    assert np.array_equal(layer.forward(node, nbrs, [0.3, 0.3, 0.4]), again.forward(node, nbrs, [0.3, 0.3, 0.4]))
+    assert json.loads(again.to_json()) == js
+    with pytest.raises(rv.GnnError):
+        rv.RuvectorLayer.from_json('{"w_msg": 1}')
+
+
+@pytest.mark.parametrize("hidden,heads", [(64, 4), (768, 8)])
+def test_ruvector_forward_graph_matches_oracle(hidden, heads):
+    n, deg = 300, 12
+    layer, W, _ = _layer_and_weights(hidden, hidden, heads, 0.1, seed=7)
+    x = O.fill_uniform(n * hidden, 4).reshape(n, hidden)
+    rp, col = O.random_csr(n, deg, 5)
+    ew = O.fill_uniform(n * deg, 6, 0.0, 1.0)
+    g = rv.Graph.from_csr(rp, col, ew)
+    y = layer.forward_graph(x, g)
+    ref = O.rvl_forward_graph(W, x, rp, col, ew)
+    assert_close(y, ref)
+
+
+def test_differentiable_search_bit_exact():
+    nq, c, d = 16, 50, 96
+    q = O.fill_uniform(nq * d, 1).reshape(nq, d)
+    cand = O.fill_uniform(nq * c * d, 2).reshape(nq, c, d)
+    for temp in (1.0, 0.1, 10.0):
+        idx, w = rv.differentiable_search_batch(q, cand, 10, temp)
+        for i in range(nq):
+            ri, rw = O.differentiable_search(q[i], cand[i], 10, temp)
+            assert np.array_equal(idx[i], ri) and np.array_equal(w[i], rw)
+    i, w = rv.differentiable_search([1, 0, 0], [[1, 0, 0], [0.9, 0.1, 0], [0, 1, 0]], 2, 1.0)
+    assert i[0] == 0 and len(w) == 2
+
+
+def test_hierarchical_forward_shape():
+    layer = rv.RuvectorLayer(2, 2, 1, 0.0)
+    out = rv.hierarchical_forward([1.0, 0.0], [[[1.0, 0.0], [0.0, 1.0]]], [layer])
+    assert out.shape == (2,)
+
+
+# ------------------------------------------------------------------ graph attention
+@pytest.mark.parametrize("node_dim,edge_dim,heads,n,concat", [(64, 16, 4, 10, True), (32, 8, 2, 5, False),
+                                                             (768, 1, 8, 24, True)])
+def test_edge_featured_attention_matches_oracle(node_dim, edge_dim, heads, n, concat):
+    cfg = rv.EdgeFeaturedConfig(node_dim=node_dim, edge_dim=edge_dim, num_heads=heads, concat_heads=concat)
+    att = rv.EdgeFeaturedAttention(cfg)
+    q = O.fill_uniform(node_dim, 1)
+    k = O.fill_uniform(n * node_dim, 2).reshape(n, node_dim)
+    v = O.fill_uniform(n * node_dim, 3).reshape(n, node_dim)
+    e = O.fill_uniform(n * edge_dim, 4).reshape(n, edge_dim)
+    got = att.compute_with_edges(q, list(k), list(v), list(e))
+    ref = O.efa_compute(node_dim, edge_dim, heads, q, k, v, e, concat=concat)
+    assert_close(got, ref)
+    got0 = att.compute(q, list(k), list(v))
+    ref0 = O.efa_compute(node_dim, edge_dim, heads, q, k, v, None, concat=concat)
+    assert_close(got0, ref0)
+    with pytest.raises(rv.RvxError):
+        att.compute(q, [], [])
+
+
+def test_edge_attention_graph_matches_per_node():
+    node_dim, heads, n, deg = 64, 4, 50, 6
+    cfg = rv.EdgeFeaturedConfig(node_dim=node_dim, edge_dim=1, num_heads=heads)
+    att = rv.EdgeFeaturedAttention(cfg)
+    x = O.fill_uniform(n * node_dim, 8).reshape(n, node_dim)
+    rp, col = O.random_csr(n, deg, 9)
+    ef = O.fill_uniform(n * deg, 10, 0.0, 1.0)
+    g = rv.Graph.from_csr(rp, col)
+    xb, eb, yb = rv.Buffer.from_numpy(x), rv.Buffer.from_numpy(ef), rv.Buffer(x.nbytes)
+    att.forward_graph_device(xb, g, eb, yb)
+    y = yb.download(np.float32, x.shape)
+    for i in range(0, n, 7):
+        nb = col[rp[i]:rp[i + 1]]
+        ref = O.efa_compute(node_dim, 1, heads, x[i], x[nb], x[nb], ef[rp[i]:rp[i + 1]].reshape(-1, 1))
+        assert_close(y[i], ref)
+
+
+# ------------------------------------------------------------------ Poincaré
+def test_poincare_distance_matrix():
+    d = 32
+    r = np.random.default_rng(0)
+    u = (r.standard_normal((20, d)) * 0.05).astype(np.float32)
+    v = (r.standard_normal((30, d)) * 0.05).astype(np.float32)
+    import ctypes
+    from ruvector_amd import _lib as L
+    out = np.empty((20, 30), np.float32)
+    L.call("rvx_distance_matrix", L.METRIC_POINCARE, L.fptr(u), 20, L.fptr(v), 30, d, 1.0, L.fptr(out))
+    ref = np.array([[O.poincare_distance(a, b) for b in v] for a in u], np.float32)
+    assert_close(out, ref, 1e-5)
