@@ -138,6 +138,7 @@ def main():
     if comm is not None and "rccl_allgather" in kern:
         rls["rccl_allgather"] = rl("rccl_allgather", "GB/s", (world - 1) * n_loc * d * 4, 7 * 153.0, "xgmi")
     dom = max((k for k in rls if rls[k]), key=lambda k: kern[k]["total_ms"])
+    attach_pmc_traffic(rls, {"nodes_per_gpu": n_loc, "dim": d, "degree": deg, "layers": layers})
 
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": a.steps,
@@ -160,6 +161,31 @@ def main():
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def attach_pmc_traffic(rls, cfg):
+    """HBM bytes per launch from the committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE
+    passes of this same workload (profiles/pmc_traffic_latest.json, gfx950 FETCH
+    correction applied by scripts/pmc_traffic.py); left null when the profile was
+    taken on a different configuration."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic_latest.json")
+    if not os.path.exists(path):
+        return
+    try:
+        pmc = json.load(open(path))
+    except ValueError:
+        return
+    pc = pmc.get("config") or {}
+    if any(pc.get(k) != v for k, v in cfg.items()):
+        return
+    for tag, r in rls.items():
+        ent = pmc.get("kernels", {}).get(tag)
+        if r is not None and ent and r["unit"] == "GB/s":
+            r["traffic"] = round(ent["hbm_bytes_per_launch"], 0)
+            r["traffic_source"] = "rocprofv3 --pmc FETCH_SIZE(x2, gfx950) + WRITE_SIZE, profiles/pmc_traffic_latest.json"
+        elif r is not None and ent:
+            r["traffic"] = round(ent["hbm_bytes_per_launch"], 0)
+            r["traffic_source"] = "rocprofv3 --pmc (HBM bytes per launch; MFMA-bound kernel)"
 
 
 def cpu_baseline(a, x_buf, g, h1_buf, sage, n, d, deg):

@@ -1,6 +1,7 @@
 // common.hpp — shared host-side plumbing of librvx: status/error handling,
 // the per-device stream, device buffers and the event-based kernel profiler.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -98,7 +99,25 @@ struct ProfScope {
     ~ProfScope();
 };
 
+// Event pair stamped by the dispatch packet itself (hipExtLaunchKernelGGL), so
+// the measured interval is exactly the kernel's execution; null when profiling
+// is off.
+struct KernelTimer {
+    const char* name;
+    hipEvent_t a = nullptr, b = nullptr;
+    explicit KernelTimer(const char* n);
+    ~KernelTimer();
+};
+
 }  // namespace rvx
+
+// Launch on the library stream, timed per kernel when profiling is enabled.
+#define RVX_LAUNCH(TAG, KERNEL, GRID, BLOCK, SHMEM, ...)                                                  \
+    do {                                                                                                   \
+        ::rvx::KernelTimer kt_(TAG);                                                                       \
+        hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, SHMEM, ::rvx::stream(), kt_.a, kt_.b, 0, __VA_ARGS__); \
+        RVX_HIP(hipGetLastError());                                                                        \
+    } while (0)
 
 struct rvx_buffer {
     rvx::DevMem mem;

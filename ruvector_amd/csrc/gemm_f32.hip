@@ -225,21 +225,20 @@ void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, con
     bool fast = (s0.K % 4 == 0) && (s0.lda % 4 == 0) && (s0.ldb % 4 == 0) && aligned16(s0.A) && aligned16(s0.B);
     if (s1) fast = fast && (s1->K % 4 == 0) && (s1->lda % 4 == 0) && (s1->ldb % 4 == 0) && aligned16(s1->A) &&
                    aligned16(s1->B);
-    ProfScope ps(tag ? tag : "gemm_nt");
+    const char* t = tag ? tag : "gemm_nt";
     if (fast) {
         g.tiles_n = (N + BN - 1) / BN;
         const int64_t tiles_m = (M + BM - 1) / BM;
         g.nblocks = tiles_m * g.tiles_n;
         RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
         if (s1)
-            hipLaunchKernelGGL(gemm_nt_mfma<true>, dim3((unsigned)g.nblocks), dim3(256), 0, stream(), g, epi);
+            RVX_LAUNCH(t, gemm_nt_mfma<true>, dim3((unsigned)g.nblocks), dim3(256), 0, g, epi);
         else
-            hipLaunchKernelGGL(gemm_nt_mfma<false>, dim3((unsigned)g.nblocks), dim3(256), 0, stream(), g, epi);
+            RVX_LAUNCH(t, gemm_nt_mfma<false>, dim3((unsigned)g.nblocks), dim3(256), 0, g, epi);
     } else {
         const int64_t total = M * (int64_t)N;
-        hipLaunchKernelGGL(gemm_nt_simple, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream(), g, epi);
+        RVX_LAUNCH(t, gemm_nt_simple, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, g, epi);
     }
-    RVX_HIP(hipGetLastError());
 }
 
 }  // namespace rvx

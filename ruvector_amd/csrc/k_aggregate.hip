@@ -140,20 +140,20 @@ __global__ __launch_bounds__(256) void k_aggregate_scalar(const int64_t* rp, con
 }
 
 template <int AGG, bool W>
-void launch_agg(const int64_t* rp, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
+void launch_agg(const char* t, const int64_t* rp, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
                 int empty_fill, int post_scale, float* out) {
     const dim3 grid((unsigned)((n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK)), block(256);
     const bool vec = (dim % 4 == 0) && (((uintptr_t)x & 15) == 0) && (((uintptr_t)out & 15) == 0);
     if (vec && dim <= 256)
-        hipLaunchKernelGGL((k_aggregate_vec<1, AGG, W>), grid, block, 0, stream(), rp, col, w, n, x, dim, empty_fill, post_scale, out);
+        RVX_LAUNCH(t, (k_aggregate_vec<1, AGG, W>), grid, block, 0, rp, col, w, n, x, dim, empty_fill, post_scale, out);
     else if (vec && dim <= 512)
-        hipLaunchKernelGGL((k_aggregate_vec<2, AGG, W>), grid, block, 0, stream(), rp, col, w, n, x, dim, empty_fill, post_scale, out);
+        RVX_LAUNCH(t, (k_aggregate_vec<2, AGG, W>), grid, block, 0, rp, col, w, n, x, dim, empty_fill, post_scale, out);
     else if (vec && dim <= 768)
-        hipLaunchKernelGGL((k_aggregate_vec<3, AGG, W>), grid, block, 0, stream(), rp, col, w, n, x, dim, empty_fill, post_scale, out);
+        RVX_LAUNCH(t, (k_aggregate_vec<3, AGG, W>), grid, block, 0, rp, col, w, n, x, dim, empty_fill, post_scale, out);
     else if (vec && dim <= 1024)
-        hipLaunchKernelGGL((k_aggregate_vec<4, AGG, W>), grid, block, 0, stream(), rp, col, w, n, x, dim, empty_fill, post_scale, out);
+        RVX_LAUNCH(t, (k_aggregate_vec<4, AGG, W>), grid, block, 0, rp, col, w, n, x, dim, empty_fill, post_scale, out);
     else
-        hipLaunchKernelGGL((k_aggregate_scalar<AGG, W>), grid, block, 0, stream(), rp, col, w, n, x, dim, empty_fill, post_scale, out);
+        RVX_LAUNCH(t, (k_aggregate_scalar<AGG, W>), grid, block, 0, rp, col, w, n, x, dim, empty_fill, post_scale, out);
 }
 
 }  // namespace
@@ -162,18 +162,17 @@ void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, 
                     int agg, int empty_fill, int post_scale, float* out, const char* tag) {
     if (n <= 0) return;
     RVX_REQUIRE(n / ROWS_PER_BLOCK < ((int64_t)1 << 31), RVX_ERR_INVALID_SHAPE, "graph too large for one launch");
-    ProfScope ps(tag ? tag : "aggregate");
+    const char* t = tag ? tag : "aggregate";
     const bool W = w != nullptr;
     switch (agg) {
-        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(row_ptr, col, w, n, x, dim, empty_fill, post_scale, out)
-                        : launch_agg<AGG_SUM, false>(row_ptr, col, w, n, x, dim, empty_fill, post_scale, out); break;
-        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(row_ptr, col, w, n, x, dim, empty_fill, post_scale, out)
-                         : launch_agg<AGG_MEAN, false>(row_ptr, col, w, n, x, dim, empty_fill, post_scale, out); break;
-        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(row_ptr, col, w, n, x, dim, empty_fill, post_scale, out)
-                        : launch_agg<AGG_MAX, false>(row_ptr, col, w, n, x, dim, empty_fill, post_scale, out); break;
+        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out)
+                        : launch_agg<AGG_SUM, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out); break;
+        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out)
+                         : launch_agg<AGG_MEAN, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out); break;
+        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out)
+                        : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out); break;
         default: fail(RVX_ERR_INVALID_PARAMETER, "unknown aggregator");
     }
-    RVX_HIP(hipGetLastError());
 }
 
 }  // namespace rvx

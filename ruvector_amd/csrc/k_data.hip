@@ -103,10 +103,8 @@ void fill_normal(float* p, int64_t n, uint64_t seed) {
 }
 void normalize_rows(float* p, int64_t rows, int dim, bool only_positive, const char* tag) {
     if (rows <= 0) return;
-    ProfScope ps(tag ? tag : "normalize_rows");
-    hipLaunchKernelGGL(k_normalize_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream(), p, rows, dim,
-                       only_positive ? 1 : 0);
-    RVX_HIP(hipGetLastError());
+    RVX_LAUNCH(tag ? tag : "normalize_rows", k_normalize_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, p, rows,
+               dim, only_positive ? 1 : 0);
 }
 void random_csr(int64_t n, int deg, uint64_t seed, int64_t* row_ptr, int32_t* col) {
     random_csr_shard(n, 0, n, deg, seed, row_ptr, col);

@@ -292,16 +292,13 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
-    {
-        ProfScope ps(tag ? tag : "hnsw_search");
-        switch (metric) {
-            case RVX_METRIC_L2: hipLaunchKernelGGL(k_hnsw_search<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, stream(), a); break;
-            case RVX_METRIC_COSINE: hipLaunchKernelGGL(k_hnsw_search<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, stream(), a); break;
-            case RVX_METRIC_DOT: hipLaunchKernelGGL(k_hnsw_search<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, stream(), a); break;
-            case RVX_METRIC_L1: hipLaunchKernelGGL(k_hnsw_search<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, stream(), a); break;
-            default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by HNSW search");
-        }
-        RVX_HIP(hipGetLastError());
+    const char* t = tag ? tag : "hnsw_search";
+    switch (metric) {
+        case RVX_METRIC_L2: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_DOT: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_L1: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
+        default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by HNSW search");
     }
     int st = 0;
     RVX_HIP(hipMemcpyAsync(&st, status, 4, hipMemcpyDeviceToHost, stream()));

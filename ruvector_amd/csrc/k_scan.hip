@@ -316,21 +316,16 @@ void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const
         attr_done = true;
     }
     const dim3 grid((unsigned)qtiles, (unsigned)nchunks);
-    {
-        ProfScope ps(tag ? tag : "scan_topk");
-        switch (metric) {
-            case RVX_METRIC_L2: hipLaunchKernelGGL(k_scan_topk<RVX_METRIC_L2>, grid, dim3(256), lds, stream(), a); break;
-            case RVX_METRIC_COSINE: hipLaunchKernelGGL(k_scan_topk<RVX_METRIC_COSINE>, grid, dim3(256), lds, stream(), a); break;
-            case RVX_METRIC_DOT: hipLaunchKernelGGL(k_scan_topk<RVX_METRIC_DOT>, grid, dim3(256), lds, stream(), a); break;
-            case RVX_METRIC_L1: hipLaunchKernelGGL(k_scan_topk<RVX_METRIC_L1>, grid, dim3(256), lds, stream(), a); break;
-            default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by the flat scan");
-        }
-        RVX_HIP(hipGetLastError());
+    const char* t = tag ? tag : "scan_topk";
+    switch (metric) {
+        case RVX_METRIC_L2: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_L2>, grid, dim3(256), lds, a); break;
+        case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_COSINE>, grid, dim3(256), lds, a); break;
+        case RVX_METRIC_DOT: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_DOT>, grid, dim3(256), lds, a); break;
+        case RVX_METRIC_L1: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_L1>, grid, dim3(256), lds, a); break;
+        default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by the flat scan");
     }
-    ProfScope ps2("scan_merge");
-    hipLaunchKernelGGL(k_merge_topk, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, stream(), part_d, part_i, nq,
-                       (int)nchunks, k, out_d, out_i);
-    RVX_HIP(hipGetLastError());
+    RVX_LAUNCH("scan_merge", k_merge_topk, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, part_d, part_i, nq,
+               (int)nchunks, k, out_d, out_i);
 }
 
 void edge_distances(int metric, const float* x, const float* xn, const int64_t* rp, const int32_t* col, int64_t n,

@@ -126,6 +126,17 @@ ProfScope::~ProfScope() {
     if (g_prof.pending.size() > 4096) g_prof.drain();
 }
 
+KernelTimer::KernelTimer(const char* n) : name(n) {
+    if (!g_prof.on) return;
+    if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) a = b = nullptr;
+}
+KernelTimer::~KernelTimer() {
+    if (!a) return;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    g_prof.pending.push_back({name, a, b});
+    if (g_prof.pending.size() > 4096) g_prof.drain();
+}
+
 }  // namespace rvx
 
 using namespace rvx;

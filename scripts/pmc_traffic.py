@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Turn rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs into per-kernel HBM bytes.
+
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 64 B per
+128-B request of a wide coalesced stream, i.e. half the bytes read, so the
+read side is doubled; WRITE_SIZE is exact for 16-B-per-lane stores. Both
+counters are in KiB. Usage:
+  pmc_traffic.py <fetch_dir> <write_dir> <out.json>
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+TAGS = {  # kernel symbol substring -> bench tag
+    "k_aggregate_vec": "sage_aggregate",
+    "gemm_nt_mfma": "sage_gemm",
+    "k_normalize_rows": "sage_normalize",
+    "k_scan_topk": "scan_topk",
+    "k_hnsw_search": "hnsw_search",
+    "k_edge_attn": "gnn_edge_attention",
+}
+
+
+def load(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    acc = defaultdict(lambda: [0.0, set()])
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                name = row.get("Kernel_Name", "")
+                disp = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                acc[name][0] += float(row["Counter_Value"])
+                acc[name][1].add(disp)
+    return {k: (v[0], len(v[1])) for k, v in acc.items()}
+
+
+def main():
+    fdir, wdir, out = sys.argv[1:4]
+    fetch = load(fdir, "FETCH_SIZE")
+    write = load(wdir, "WRITE_SIZE")
+    res = {}
+    for name in set(fetch) | set(write):
+        tag = next((t for s, t in TAGS.items() if s in name), None)
+        if tag is None:
+            continue
+        fk, fn = fetch.get(name, (0.0, 0))
+        wk, wn = write.get(name, (0.0, 0))
+        ent = res.setdefault(tag, {"kernels": [], "fetch_kib": 0.0, "write_kib": 0.0, "fetch_n": 0, "write_n": 0})
+        ent["kernels"].append(re.sub(r"\s+", " ", name)[:120])
+        ent["fetch_kib"] += fk
+        ent["write_kib"] += wk
+        ent["fetch_n"] += fn
+        ent["write_n"] += wn
+    for tag, e in res.items():
+        rd = 2.0 * e["fetch_kib"] * 1024 / max(e["fetch_n"], 1)
+        wr = e["write_kib"] * 1024 / max(e["write_n"], 1)
+        e["read_bytes_per_launch_corrected"] = rd
+        e["write_bytes_per_launch"] = wr
+        e["hbm_bytes_per_launch"] = rd + wr
+    # the bench configuration these counters belong to (bench JSON of the same command)
+    cfg = None
+    if len(sys.argv) > 4:
+        for line in open(sys.argv[4], errors="replace"):
+            if line.startswith("{") and '"metric"' in line:
+                cfg = json.loads(line).get("config")
+    json.dump({"config": cfg, "kernels": res}, open(out, "w"), indent=1)
+    print(json.dumps({k: round(v["hbm_bytes_per_launch"] / 1e9, 3) for k, v in res.items()}))
+
+
+if __name__ == "__main__":
+    main()
