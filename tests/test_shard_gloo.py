@@ -1,0 +1,109 @@
+"""Multi-process (world_size 2, gloo on CPU) test of the node-range sharding
+driver (ruvector_amd/shard.py): per-layer all-gather of the node table + each
+rank transforming its own rows must reproduce the single-process forward;
+per-shard top-k merged must equal the global top-k.
+
+The per-rank compute here is the oracle (test double for the HIP layer); the
+exchange is torch.distributed.all_gather over gloo — the same driver runs over
+RCCL with HBM buffers in bench.py.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    import oracle as O
+    from ruvector_amd.shard import ShardPlan, merge_topk, sharded_layers
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, d, deg = 203, 16, 5  # ragged: 203 rows over 2 ranks
+        plan = ShardPlan(n, world)
+        x = O.fill_uniform(n * d, 1).reshape(n, d)
+        rp, col = O.random_csr(n, deg, 2)
+        wn, ws = O.sage_init(d, d, 0), O.sage_init(d, d, 1000)
+        b, e = plan.rows(rank)
+
+        def allgather(local):
+            sizes = [plan.rows(r)[1] - plan.rows(r)[0] for r in range(world)]
+            bufs = [torch.zeros((s, d), dtype=torch.float32) for s in sizes]
+            t = torch.from_numpy(np.ascontiguousarray(local))
+            # gloo all_gather needs equal sizes: pad to the max
+            m = max(sizes)
+            pad = torch.zeros((m, d), dtype=torch.float32)
+            pad[:t.shape[0]] = t
+            outs = [torch.zeros((m, d), dtype=torch.float32) for _ in range(world)]
+            dist.all_gather(outs, pad)
+            return np.concatenate([o[:s].numpy() for o, s in zip(outs, sizes)])
+
+        def forward_rows(layer, full, rb, re):
+            return O.sage_forward(full, rp, col, wn, ws, rows=(rb, re - rb))
+
+        mine = sharded_layers(x[b:e], [0, 1], plan, rank, allgather, forward_rows)
+        ref = O.sage_forward(O.sage_forward(x, rp, col, wn, ws), rp, col, wn, ws)[b:e]
+        ok_gnn = bool(np.array_equal(mine, ref))
+
+        # HNSW/flat shard merge: each rank owns a row range of the corpus
+        base = O.fill_uniform(500 * 8, 3).reshape(500, 8)
+        qv = O.fill_uniform(12 * 8, 4).reshape(12, 8)
+        p2 = ShardPlan(500, world)
+        sb, se = p2.rows(rank)
+        li, ld = O.flat_search(base[sb:se], qv, 7, "l2")
+        li = li + sb
+        gi = [torch.zeros((12, 7), dtype=torch.int64) for _ in range(world)]
+        gd = [torch.zeros((12, 7), dtype=torch.float32) for _ in range(world)]
+        dist.all_gather(gi, torch.from_numpy(li))
+        dist.all_gather(gd, torch.from_numpy(ld))
+        mi, md = merge_topk([(a.numpy(), b_.numpy()) for a, b_ in zip(gi, gd)], 7)
+        fi, fd = O.flat_search(base, qv, 7, "l2")
+        ok_merge = bool(np.array_equal(mi, fi) and np.array_equal(md, fd))
+        q.put((rank, ok_gnn, ok_merge))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_node_range_shards_match_single_process():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    res = sorted(q.get(timeout=5) for _ in range(2))
+    assert res == [(0, True, True), (1, True, True)]
+
+
+def test_shard_plan_rows_cover_and_owner():
+    sys.path.insert(0, ROOT)
+    from ruvector_amd.shard import ShardPlan
+    for n, w in ((10, 3), (8, 8), (1000003, 8), (5, 8)):
+        p = ShardPlan(n, w)
+        spans = [p.rows(r) for r in range(w)]
+        assert spans[0][0] == 0 and spans[-1][1] == n
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+        for node in range(0, n, max(1, n // 97)):
+            r = p.owner(node)
+            assert spans[r][0] <= node < spans[r][1]
