@@ -275,6 +275,14 @@ typedef struct {
     const int32_t* const* upper_col;      /* per layer */
 } rvx_hnsw_graph;
 rvx_status rvx_index_load_graph(rvx_index* idx, const rvx_hnsw_graph* g);
+/* Export the searchable graph (built by add_batch on the GPU, or loaded) in the
+ * rvx_hnsw_graph layout: sizes first (upper_count/upper_edges [17]), then the
+ * arrays; upper layers are concatenated in layer order (1..max_level), each
+ * row_ptr block holding upper_count[l]+1 entries. */
+rvx_status rvx_index_graph_sizes(const rvx_index* idx, int64_t* n, int32_t* max_level, int64_t* entry_point,
+                                 int64_t* num_edges0, int64_t* upper_count, int64_t* upper_edges);
+rvx_status rvx_index_export_graph(const rvx_index* idx, uint8_t* levels, int64_t* row_ptr0, int32_t* col0,
+                                  int32_t* upper_ids, int64_t* upper_row_ptr, int32_t* upper_col);
 /* Layer-0 adjacency export for the GNN (edge weight = stored distance). */
 rvx_status rvx_index_layer0_size(const rvx_index* idx, int64_t* n, int64_t* num_edges);
 rvx_status rvx_index_export_layer0(const rvx_index* idx, int64_t* row_ptr, int32_t* col, float* dist);

@@ -123,6 +123,8 @@ SIGNATURES = {
     "rvx_index_brute_force": (None, [P, PF32, I64, I32, PU64, PF32]),
     "rvx_index_brute_force_device": (None, [P, P, I64, I32, P, P]),
     "rvx_index_load_graph": (None, [P, C.POINTER(HnswGraph)]),
+    "rvx_index_graph_sizes": (None, [P, PI64, PI32, PI64, PI64, PI64, PI64]),
+    "rvx_index_export_graph": (None, [P, C.POINTER(C.c_uint8), PI64, PI32, PI32, PI64, PI32]),
     "rvx_index_layer0_size": (None, [P, PI64, PI64]),
     "rvx_index_export_layer0": (None, [P, PI64, PI32, PF32]),
     "rvx_distance_matrix": (None, [I32, PF32, I64, PF32, I64, I32, F32, PF32]),

@@ -247,6 +247,34 @@ class HnswIndex(_Index):
                         upper_col=C.cast(col_arr, C.POINTER(P32)))
         _check("rvx_index_load_graph", self._h, C.byref(g))
 
+    def export_graph(self) -> dict:
+        """The searchable graph in the rvx_hnsw_graph layout (same dict as load_graph takes)."""
+        n, ml, ent, e0 = C.c_int64(), C.c_int32(), C.c_int64(), C.c_int64()
+        uc = np.zeros(17, np.int64)
+        ue = np.zeros(17, np.int64)
+        _check("rvx_index_graph_sizes", self._h, C.byref(n), C.byref(ml), C.byref(ent), C.byref(e0), L.i64ptr(uc),
+               L.i64ptr(ue))
+        N, Lm = n.value, ml.value
+        levels = np.empty(max(N, 1), np.uint8)
+        rp0 = np.empty(N + 1, np.int64)
+        col0 = np.empty(max(e0.value, 1), np.int32)
+        ids = np.empty(max(int(uc.sum()), 1), np.int32)
+        rps = np.empty(max(int((uc[1:Lm + 1] + 1).sum()), 1), np.int64)
+        cols = np.empty(max(int(ue.sum()), 1), np.int32)
+        _check("rvx_index_export_graph", self._h, levels.ctypes.data_as(C.POINTER(C.c_uint8)), L.i64ptr(rp0),
+               L.i32ptr(col0), L.i32ptr(ids), L.i64ptr(rps), L.i32ptr(cols))
+        g = {"n": N, "max_level": Lm, "entry": ent.value, "levels": levels[:N], "row_ptr0": rp0,
+             "col0": col0[:e0.value], "upper_ids": [], "upper_row_ptr": [], "upper_col": []}
+        oi = orp = oc = 0
+        for l in range(1, Lm + 1):
+            c = int(uc[l])
+            g["upper_ids"].append(ids[oi:oi + c].copy())
+            rp = rps[orp:orp + c + 1].copy()
+            g["upper_row_ptr"].append(rp)
+            g["upper_col"].append(cols[oc:oc + int(rp[-1])].copy())
+            oi, orp, oc = oi + c, orp + c + 1, oc + int(rp[-1])
+        return g
+
     def layer0(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Layer-0 adjacency (row_ptr, col, edge distance) for the GNN."""
         n, e = C.c_int64(), C.c_int64()

@@ -7,31 +7,11 @@
 
 #include "graph.hpp"
 #include "hnsw.hpp"
+#include "index.hpp"
 #include "kernels.hpp"
 #include "scan.hpp"
 
 using namespace rvx;
-
-struct rvx_index {
-    rvx_index_config cfg{};
-    int64_t n = 0, cap = 0;
-    DevMem vecs;       // [cap][dim]
-    DevMem norms;      // [cap] (cosine)
-    DevMem ids_dev;    // [cap] u64 user ids
-    DevMem deleted;    // [cap] u8 tombstones
-    std::vector<uint64_t> ids;
-    std::vector<uint8_t> deleted_h;
-    std::unordered_map<uint64_t, int64_t> id_to_row;
-    int64_t live = 0;
-    // HNSW graph (loaded or built)
-    bool has_graph = false;
-    int64_t graph_n = 0;
-    HnswDev g;
-    DevMem rp0, col0, up_ids, up_rp, up_col;
-    std::vector<int64_t> h_rp0;
-    std::vector<int32_t> h_col0;
-    mutable std::shared_mutex mu;
-};
 
 namespace {
 
@@ -107,7 +87,7 @@ void search_rows(const rvx_index* ix, const float* q, int64_t nq, int k, int ef,
         return;
     }
     RVX_REQUIRE(ix->has_graph && ix->graph_n == ix->n, RVX_ERR_INDEX,
-                "HNSW graph missing or stale: load one with rvx_index_load_graph after adding vectors");
+                "HNSW graph missing or stale");
     const int e = std::max(ef > 0 ? ef : ix->cfg.ef_search, k);  // ef = max(ef_arg, knbn) (hnsw.rs:1519)
     hnsw_search(ix->g, ix->cfg.metric, ix->vecs.as<float>(), ix->norms.as<float>(), d, q, qn, nq, k, e, dd, di, dn,
                 "hnsw_search");
@@ -160,7 +140,7 @@ rvx_status rvx_index_add_batch(rvx_index* ix, const float* vecs, const uint64_t*
         std::unique_lock<std::shared_mutex> lk(ix->mu);
         ComputeLock cl;
         append_rows(ix, vecs, ids, n, false);
-        if (ix->cfg.kind == RVX_INDEX_HNSW) ix->has_graph = false;
+        if (ix->cfg.kind == RVX_INDEX_HNSW) hnsw_insert_range(ix, ix->n - n, n);  // Hnsw::insert per vector
     });
 }
 
@@ -173,7 +153,7 @@ rvx_status rvx_index_add_batch_device(rvx_index* ix, const rvx_buffer* vecs, int
         std::vector<uint64_t> ids(n);
         for (int64_t i = 0; i < n; ++i) ids[i] = first_id + (uint64_t)i;
         append_rows(ix, vecs->mem.as<float>(), ids.data(), n, true);
-        if (ix->cfg.kind == RVX_INDEX_HNSW) ix->has_graph = false;
+        if (ix->cfg.kind == RVX_INDEX_HNSW) hnsw_insert_range(ix, ix->n - n, n);
     });
 }
 
@@ -295,49 +275,84 @@ rvx_status rvx_index_load_graph(rvx_index* ix, const rvx_hnsw_graph* hg) {
         RVX_REQUIRE(hg->max_level >= 0 && hg->max_level <= HNSW_MAX_LEVEL, RVX_ERR_INVALID_PARAMETER, "bad max_level");
         RVX_REQUIRE(hg->n == 0 || (hg->entry_point >= 0 && hg->entry_point < hg->n), RVX_ERR_INDEX, "bad entry point");
         const int64_t n = hg->n;
-        const int64_t e0 = hg->row_ptr0[n];
+        HostGraph h;
+        h.n = n;
+        h.max_level = hg->max_level;
+        h.entry = hg->entry_point;
+        h.levels.assign(hg->levels, hg->levels + n);
+        h.rp0.assign(hg->row_ptr0, hg->row_ptr0 + n + 1);
+        RVX_REQUIRE(h.rp0[0] == 0, RVX_ERR_INDEX, "row_ptr0[0] must be 0");
         // validate layer 0: ids in range, no duplicate inside a list
         std::vector<int64_t> mark(n, -1);
-        for (int64_t i = 0; i < n; ++i)
-            for (int64_t p = hg->row_ptr0[i]; p < hg->row_ptr0[i + 1]; ++p) {
+        for (int64_t i = 0; i < n; ++i) {
+            RVX_REQUIRE(h.rp0[i + 1] >= h.rp0[i], RVX_ERR_INDEX, "row_ptr0 must be non-decreasing");
+            for (int64_t p = h.rp0[i]; p < h.rp0[i + 1]; ++p) {
                 const int32_t c = hg->col0[p];
                 RVX_REQUIRE(c >= 0 && c < n, RVX_ERR_INDEX, "layer-0 neighbour out of range");
                 RVX_REQUIRE(mark[c] != i, RVX_ERR_INDEX, "duplicate neighbour in a layer-0 list");
                 mark[c] = i;
             }
-        ComputeLock cl;
-        HnswDev g;
-        g.n = n; g.max_level = hg->max_level; g.entry = hg->entry_point;
-        ix->h_rp0.assign(hg->row_ptr0, hg->row_ptr0 + n + 1);
-        ix->h_col0.assign(hg->col0, hg->col0 + e0);
-        ix->rp0.reset((n + 1) * 8); ix->rp0.upload(hg->row_ptr0, (n + 1) * 8);
-        ix->col0.reset(std::max<int64_t>(e0, 1) * 4); ix->col0.upload(hg->col0, e0 * 4);
-        g.rp0 = ix->rp0.as<int64_t>(); g.col0 = ix->col0.as<int>();
-        std::vector<int32_t> ids; std::vector<int64_t> rps; std::vector<int32_t> cols;
-        for (int l = 1; l <= hg->max_level; ++l) {
+        }
+        h.col0.assign(hg->col0, hg->col0 + h.rp0[n]);
+        h.up_ids.assign(h.max_level + 1, {});
+        h.up_rp.assign(h.max_level + 1, {});
+        h.up_col.assign(h.max_level + 1, {});
+        for (int l = 1; l <= h.max_level; ++l) {
             const int64_t cnt = hg->upper_count[l];
-            g.up_count[l] = cnt;
-            g.up_ids_off[l] = (int64_t)ids.size();
-            g.up_rp_off[l] = (int64_t)rps.size();
-            g.up_col_off[l] = (int64_t)cols.size();
             for (int64_t i = 0; i < cnt; ++i) {
-                ids.push_back(hg->upper_ids[l][i]);
                 RVX_REQUIRE(i == 0 || hg->upper_ids[l][i] > hg->upper_ids[l][i - 1], RVX_ERR_INDEX,
                             "upper-layer ids must be strictly increasing");
+                RVX_REQUIRE(hg->upper_ids[l][i] >= 0 && hg->upper_ids[l][i] < n, RVX_ERR_INDEX, "upper id out of range");
             }
-            for (int64_t i = 0; i <= cnt; ++i) rps.push_back(hg->upper_row_ptr[l][i]);
-            for (int64_t p = 0; p < hg->upper_row_ptr[l][cnt]; ++p) {
+            h.up_ids[l].assign(hg->upper_ids[l], hg->upper_ids[l] + cnt);
+            h.up_rp[l].assign(hg->upper_row_ptr[l], hg->upper_row_ptr[l] + cnt + 1);
+            const int64_t ec = h.up_rp[l][cnt];
+            for (int64_t p = 0; p < ec; ++p)
                 RVX_REQUIRE(hg->upper_col[l][p] >= 0 && hg->upper_col[l][p] < n, RVX_ERR_INDEX, "upper neighbour out of range");
-                cols.push_back(hg->upper_col[l][p]);
-            }
+            h.up_col[l].assign(hg->upper_col[l], hg->upper_col[l] + ec);
         }
-        ix->up_ids.reset(std::max<size_t>(ids.size(), 1) * 4); ix->up_ids.upload(ids.data(), ids.size() * 4);
-        ix->up_rp.reset(std::max<size_t>(rps.size(), 1) * 8); ix->up_rp.upload(rps.data(), rps.size() * 8);
-        ix->up_col.reset(std::max<size_t>(cols.size(), 1) * 4); ix->up_col.upload(cols.data(), cols.size() * 4);
-        g.up_ids = ix->up_ids.as<int>(); g.up_rp = ix->up_rp.as<int64_t>(); g.up_col = ix->up_col.as<int>();
-        ix->g = g;
-        ix->graph_n = n;
-        ix->has_graph = true;
+        ComputeLock cl;
+        ix->build_valid = false;
+        hnsw_install(ix, std::move(h));
+    });
+}
+
+rvx_status rvx_index_graph_sizes(const rvx_index* ix, int64_t* n, int32_t* max_level, int64_t* entry, int64_t* e0,
+                                 int64_t* upper_count, int64_t* upper_edges) {
+    return guard([&] {
+        RVX_REQUIRE(ix && ix->has_graph, RVX_ERR_INDEX, "no HNSW graph");
+        std::shared_lock<std::shared_mutex> lk(ix->mu);
+        const HostGraph& h = ix->hg;
+        if (n) *n = h.n;
+        if (max_level) *max_level = h.max_level;
+        if (entry) *entry = h.entry;
+        if (e0) *e0 = h.rp0.empty() ? 0 : h.rp0.back();
+        for (int l = 0; l <= HNSW_MAX_LEVEL; ++l) {
+            const bool has = l >= 1 && l <= h.max_level;
+            if (upper_count) upper_count[l] = has ? (int64_t)h.up_ids[l].size() : 0;
+            if (upper_edges) upper_edges[l] = has ? (int64_t)h.up_col[l].size() : 0;
+        }
+    });
+}
+
+rvx_status rvx_index_export_graph(const rvx_index* ix, uint8_t* levels, int64_t* row_ptr0, int32_t* col0,
+                                  int32_t* up_ids, int64_t* up_row_ptr, int32_t* up_col) {
+    return guard([&] {
+        RVX_REQUIRE(ix && ix->has_graph, RVX_ERR_INDEX, "no HNSW graph");
+        std::shared_lock<std::shared_mutex> lk(ix->mu);
+        const HostGraph& h = ix->hg;
+        if (levels) std::copy(h.levels.begin(), h.levels.end(), levels);
+        if (row_ptr0) std::copy(h.rp0.begin(), h.rp0.end(), row_ptr0);
+        if (col0) std::copy(h.col0.begin(), h.col0.end(), col0);
+        int64_t oi = 0, orp = 0, oc = 0;
+        for (int l = 1; l <= h.max_level; ++l) {
+            if (up_ids) std::copy(h.up_ids[l].begin(), h.up_ids[l].end(), up_ids + oi);
+            if (up_row_ptr) std::copy(h.up_rp[l].begin(), h.up_rp[l].end(), up_row_ptr + orp);
+            if (up_col) std::copy(h.up_col[l].begin(), h.up_col[l].end(), up_col + oc);
+            oi += (int64_t)h.up_ids[l].size();
+            orp += (int64_t)h.up_rp[l].size();
+            oc += (int64_t)h.up_col[l].size();
+        }
     });
 }
 
@@ -346,7 +361,7 @@ rvx_status rvx_index_layer0_size(const rvx_index* ix, int64_t* n, int64_t* e) {
         RVX_REQUIRE(ix && ix->has_graph, RVX_ERR_INDEX, "no HNSW graph");
         std::shared_lock<std::shared_mutex> lk(ix->mu);
         if (n) *n = ix->graph_n;
-        if (e) *e = ix->h_rp0.empty() ? 0 : ix->h_rp0.back();
+        if (e) *e = ix->hg.rp0.empty() ? 0 : ix->hg.rp0.back();
     });
 }
 
@@ -355,9 +370,9 @@ rvx_status rvx_index_export_layer0(const rvx_index* ix, int64_t* row_ptr, int32_
         RVX_REQUIRE(ix && ix->has_graph, RVX_ERR_INDEX, "no HNSW graph");
         std::shared_lock<std::shared_mutex> lk(ix->mu);
         ComputeLock cl;
-        const int64_t n = ix->graph_n, e = ix->h_rp0.back();
-        if (row_ptr) std::copy(ix->h_rp0.begin(), ix->h_rp0.end(), row_ptr);
-        if (col) std::copy(ix->h_col0.begin(), ix->h_col0.end(), col);
+        const int64_t n = ix->graph_n, e = ix->hg.rp0.back();
+        if (row_ptr) std::copy(ix->hg.rp0.begin(), ix->hg.rp0.end(), row_ptr);
+        if (col) std::copy(ix->hg.col0.begin(), ix->hg.col0.end(), col);
         if (dist && e > 0) {
             // edge weight = distance(owner, neighbour) in the reference order
             float* dv = scratch_f32("export_dist", e);

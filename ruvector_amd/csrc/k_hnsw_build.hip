@@ -1,0 +1,358 @@
+// k_hnsw_build.hip — batched HNSW construction on the GPU (K3).
+//
+// Follows hnsw_rs 0.3.3 insert_slice (patches/hnsw_rs/src/hnsw.rs:1068-1206) per
+// point, run for a batch of points at once against the graph as it stood
+// before the batch (what Hnsw::parallel_insert does with concurrent inserters,
+// :1212-1218, made deterministic):
+//   1. greedy descent with search_layer(ef = 1) on layers above the point's
+//      level (:1105-1146), from the current entry point;
+//   2. for l = level .. 0: search_layer(ef_construction) -> select_neighbours
+//      (:1287-1409: keep e unless some already selected s has d(e,s) <= d(e,q);
+//      2M at layer 0, M above) -> the point's list at l, sorted ascending;
+//   3. reverse_update_neighborhood_simple (:1229-1277): the new point is added
+//      to every selected neighbour's list AT THE NEW POINT'S OWN LEVEL (l_n),
+//      kept sorted and truncated to the capacity (M, 2M at layer 0). With all
+//      reverse edges of a batch known, the list becomes the best `cap` of
+//      (old list ∪ new entries) — the same set the reference's push/sort/pop
+//      sequence leaves. Reverse edges into a list that only exists above the
+//      neighbour's own level (never traversed by search) are dropped.
+// Batches grow geometrically (size ~ inserted/16) so batch-mates that cannot
+// see each other stay a small fraction. Build parity is recall vs the
+// oracle's CPU build.
+//
+// Storage (fixed capacity): layer 0 lists [n][2M] ids + distances + count;
+// upper lists compacted per point (up_base[p] + l - 1) of capacity M.
+// Distances are the reference scalar order (hnsw_dev.hpp), so a list's order
+// matches hnsw_rs's sort_unstable by distance (ties by id here).
+#include "common.hpp"
+#include "graph.hpp"
+#include "hnsw.hpp"
+#include "hnsw_build.hpp"
+#include "hnsw_dev.hpp"
+
+namespace rvx {
+namespace {
+using namespace hnswdev;
+
+struct BuildArgs {
+    BuildGraph G;
+    const float* x; const float* xnorm; int d;
+    int64_t batch_begin; int batch_n;
+    int entry; int entry_level;
+    unsigned nonempty_mask;  // bit l: some inserted point has level exactly l (points_by_layer[l])
+    int ef_c;
+    unsigned long long* visited; int nslots;
+    int* rev_head; int* rev_next; int* rev_key; float* rev_d; int* rev_src;  // reverse-edge chains
+    int rev_cap;  // records per batch point
+    int* status;
+};
+
+__device__ __forceinline__ int list_get(const BuildGraph& G, int p, int l, const int** ids, const float** ds) {
+    if (l == 0) {
+        *ids = G.nb0 + (int64_t)p * G.C0;
+        *ds = G.nbd0 + (int64_t)p * G.C0;
+        return G.cnt0[p];
+    }
+    if ((int)G.level[p] < l) return 0;
+    const int64_t li = G.up_base[p] + (l - 1);
+    *ids = G.nbu + li * G.M;
+    *ds = G.nbud + li * G.M;
+    return G.cntu[li];
+}
+__device__ __forceinline__ int list_key(const BuildGraph& G, int p, int l) {  // -1: no live list
+    if (l == 0) return p;
+    if ((int)G.level[p] < l) return -1;
+    return (int)(G.n_cap + G.up_base[p] + (l - 1));
+}
+
+// search_layer (hnsw.rs:913-1055) at layer l from ep; R left ascending in (rd, ri), returns |R|.
+template <int METRIC>
+__device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn, int ep, float d_ep, int ef, int l,
+                                  unsigned long long* vis, unsigned long long tag, float* rd, int* ri, float* cd,
+                                  int* ci, int ccap, int lane, bool& overflow) {
+    if (!((a.nonempty_mask >> l) & 1u)) return 0;  // points_by_layer[layer].is_empty()
+    int rs = 1, cs = 1;
+    if (lane == 0) {
+        rd[0] = d_ep; ri[0] = ep; cd[0] = d_ep; ci[0] = ep;
+        visit_claim(vis, tag, ep);
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    while (cs > 0 && !overflow) {
+        const float c_d = cd[cs - 1];
+        const int c_id = ci[cs - 1];
+        cs -= 1;
+        if (c_d > rd[rs - 1]) break;
+        const int* nbi;
+        const float* nbd;
+        const int cnt = list_get(a.G, c_id, l, &nbi, &nbd);
+        for (int c0 = 0; c0 < cnt; c0 += 64) {
+            const int p = c0 + lane;
+            int nid = -1;
+            bool fresh = false;
+            if (p < cnt) {
+                nid = nbi[p];
+                fresh = visit_claim(vis, tag, nid);
+            }
+            float dd = INFINITY;
+            if (fresh)
+                dd = row_dist<METRIC>(qs, a.x + (int64_t)nid * a.d, a.d, qn,
+                                      METRIC == RVX_METRIC_COSINE ? a.xnorm[nid] : 0.0f);
+            unsigned long long todo = __ballot(fresh);
+            while (todo) {
+                const int src = __ffsll((long long)todo) - 1;
+                todo &= todo - 1;
+                const float ed = __shfl(dd, src);
+                const int eid = __shfl(nid, src);
+                const float fd = rd[rs - 1];
+                if (ed < fd || rs < ef) {
+                    if (cs >= ccap) {
+                        if (cd[0] > fd) {
+                            for (int base = 0; base < cs - 1; base += 64) {
+                                const int i = base + lane;
+                                float vd = 0.f; int vi = 0;
+                                const bool mv = i + 1 < cs;
+                                if (mv) { vd = cd[i + 1]; vi = ci[i + 1]; }
+                                __builtin_amdgcn_wave_barrier();
+                                if (mv) { cd[i] = vd; ci[i] = vi; }
+                                __builtin_amdgcn_wave_barrier();
+                            }
+                            cs -= 1;
+                        } else {
+                            overflow = true;
+                            break;
+                        }
+                    }
+                    cs = sorted_insert(cd, ci, cs, ed, eid, false, lane);
+                    rs = sorted_insert(rd, ri, rs, ed, eid, true, lane);
+                    if (rs > ef) rs -= 1;
+                }
+            }
+            if (overflow) break;
+        }
+    }
+    return rs;
+}
+
+template <int METRIC>
+__global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    const int lane = threadIdx.x;
+    const int ef = a.ef_c;
+    const int ccap = ef + C_EXTRA;
+    const int dq = (a.d + 3) & ~3;
+    float* qs = reinterpret_cast<float*>(lds_raw);
+    float* rd = qs + dq;
+    int* ri = reinterpret_cast<int*>(rd + ef + 1);
+    float* cd = reinterpret_cast<float*>(ri + ef + 1);
+    int* ci = reinterpret_cast<int*>(cd + ccap);
+    float* sd = reinterpret_cast<float*>(ci + ccap);  // selected [64]
+    int* si = reinterpret_cast<int*>(sd + 64);
+    unsigned long long* vis = a.visited + (int64_t)blockIdx.x * VCAP;
+    unsigned epoch = 0;
+    bool overflow = false;
+
+    for (int b = blockIdx.x; b < a.batch_n; b += a.nslots) {
+        const int p = (int)(a.batch_begin + b);
+        for (int i = lane; i < dq; i += 64) qs[i] = (i < a.d) ? a.x[(int64_t)p * a.d + i] : 0.0f;
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        const float qn = (METRIC == RVX_METRIC_COSINE) ? a.xnorm[p] : 0.0f;
+        const int lev = a.G.level[p];
+        int rec = 0;  // reverse-edge records emitted for this point
+        const int rbase = b * a.rev_cap;
+
+        int ep = a.entry;
+        float d_ep = row_dist<METRIC>(qs, a.x + (int64_t)ep * a.d, a.d, qn,
+                                      METRIC == RVX_METRIC_COSINE ? a.xnorm[ep] : 0.0f);
+        // 1. greedy descent, ef = 1 (hnsw.rs:1105-1146)
+        for (int l = a.entry_level; l >= lev + 1; --l) {
+            const unsigned long long tag = (unsigned long long)(++epoch) << 32;
+            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, 1, l, vis, tag, rd, ri, cd, ci, ccap, lane,
+                                                      overflow);
+            if (rs > 0 && rd[0] < d_ep) { ep = ri[0]; d_ep = rd[0]; }
+        }
+        // 2. layers lev .. 0 (hnsw.rs:1149-1196)
+        for (int l = lev; l >= 0; --l) {
+            const unsigned long long tag = (unsigned long long)(++epoch) << 32;
+            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, ef, l, vis, tag, rd, ri, cd, ci, ccap, lane,
+                                                      overflow);
+            if (rs == 0) continue;
+            const int nb_conn = l == 0 ? 2 * a.G.M : a.G.M;
+            int ss = 0;
+            if (rs <= nb_conn) {
+                for (int i = lane; i < rs; i += 64) { sd[i] = rd[i]; si[i] = ri[i]; }
+                ss = rs;
+            } else {
+                // select_neighbours heuristic (hnsw.rs:1350-1380), one lane per selected point
+                for (int t = 0; t < rs && ss < nb_conn; ++t) {
+                    const int e = ri[t];
+                    const float de = rd[t];
+                    bool bad = false;
+                    if (lane < ss) {
+                        const int s = si[lane];
+                        const float dse = row_dist<METRIC>(a.x + (int64_t)e * a.d, a.x + (int64_t)s * a.d, a.d,
+                                                           METRIC == RVX_METRIC_COSINE ? a.xnorm[e] : 0.0f,
+                                                           METRIC == RVX_METRIC_COSINE ? a.xnorm[s] : 0.0f);
+                        bad = dse <= de;
+                    }
+                    if (__ballot(bad) == 0ull) {
+                        if (lane == 0) { sd[ss] = de; si[ss] = e; }
+                        ss += 1;
+                        __threadfence_block();
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                }
+            }
+            __threadfence_block();
+            __builtin_amdgcn_wave_barrier();
+            // the point's own list at layer l (sorted: R ascending, S is a subsequence)
+            int* oid;
+            float* od;
+            int* ocnt;
+            if (l == 0) {
+                oid = a.G.nb0 + (int64_t)p * a.G.C0;
+                od = a.G.nbd0 + (int64_t)p * a.G.C0;
+                ocnt = a.G.cnt0 + p;
+            } else {
+                const int64_t li = a.G.up_base[p] + (l - 1);
+                oid = a.G.nbu + li * a.G.M;
+                od = a.G.nbud + li * a.G.M;
+                ocnt = a.G.cntu + li;
+            }
+            for (int i = lane; i < ss; i += 64) { oid[i] = si[i]; od[i] = sd[i]; }
+            if (lane == 0) *ocnt = ss;
+            // reverse-edge records: p into s's list at p's own level
+            for (int i = lane; i < ss; i += 64) {
+                const int s = si[i];
+                const int key = (s == p) ? -1 : list_key(a.G, s, lev);
+                const int r = rbase + rec + i;
+                a.rev_key[r] = key;
+                a.rev_d[r] = sd[i];
+                a.rev_src[r] = p;
+                if (key >= 0) a.rev_next[r] = atomicExch(&a.rev_head[key], r);
+            }
+            rec += ss;
+            ep = si[0];
+            d_ep = sd[0];
+            __builtin_amdgcn_wave_barrier();
+        }
+        for (int i = rec + lane; i < a.rev_cap; i += 64) a.rev_key[rbase + i] = -1;
+    }
+    if (overflow && lane == 0) atomicExch(a.status, 1);
+}
+
+// One wave per list that received reverse edges (the record that found the
+// chain head empty owns it): merge old list ∪ new entries, keep the best cap.
+__global__ __launch_bounds__(256) void k_build_merge(BuildArgs a, int nrec) {
+    const int lane = threadIdx.x & 63;
+    const int wave = (blockIdx.x * 4) + (threadIdx.x >> 6);
+    const int r0 = wave * 64;
+    if (r0 >= nrec) return;
+    const int r = r0 + lane;
+    // owner = the record at the END of its chain (rev_next == -1), i.e. the first pushed
+    bool own = false;
+    if (r < nrec && a.rev_key[r] >= 0) own = (a.rev_next[r] == -1);
+    unsigned long long owners = __ballot(own);
+    while (owners) {
+        const int src = __ffsll((long long)owners) - 1;
+        owners &= owners - 1;
+        const int key = __shfl(a.rev_key[r < nrec ? r : r0], src);
+        int* ids;
+        float* ds;
+        int* cntp;
+        int cap;
+        if (key < a.G.n_cap) {
+            ids = a.G.nb0 + (int64_t)key * a.G.C0;
+            ds = a.G.nbd0 + (int64_t)key * a.G.C0;
+            cntp = a.G.cnt0 + key;
+            cap = a.G.C0;
+        } else {
+            const int64_t li = key - a.G.n_cap;
+            ids = a.G.nbu + li * a.G.M;
+            ds = a.G.nbud + li * a.G.M;
+            cntp = a.G.cntu + li;
+            cap = a.G.M;
+        }
+        int cnt = *cntp;
+        // lane j holds element j of the sorted list (cap <= 64)
+        float md = lane < cnt ? ds[lane] : INFINITY;
+        int mi = lane < cnt ? ids[lane] : INT_MAX;
+        int steps = 0;
+        for (int h = a.rev_head[key]; h >= 0 && h < nrec && steps < nrec; h = a.rev_next[h], ++steps) {
+            const float d = a.rev_d[h];
+            const int id = a.rev_src[h];
+            if (__ballot(mi == id) != 0ull) continue;  // already present
+            if (cnt == cap) {
+                const float ld = __shfl(md, cap - 1);
+                const int li2 = __shfl(mi, cap - 1);
+                if (!lt(d, id, ld, li2)) continue;
+            }
+            const bool before = lane < cnt && lt(md, mi, d, id);
+            const int pos = __popcll(__ballot(before));
+            const float upd = __shfl_up(md, 1);
+            const int upi = __shfl_up(mi, 1);
+            if (lane > pos) { md = upd; mi = upi; }
+            if (lane == pos) { md = d; mi = id; }
+            cnt = min(cnt + 1, cap);
+        }
+        if (lane < cnt) { ds[lane] = md; ids[lane] = mi; }
+        if (lane == 0) { *cntp = cnt; a.rev_head[key] = -1; }
+    }
+}
+
+}  // namespace
+
+size_t build_lds_bytes(int d, int ef) {
+    const int dq = (d + 3) & ~3;
+    return (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)(ef + C_EXTRA) * 8 + 64 * 8;
+}
+
+void build_insert_batch(const BuildGraph& G, int metric, const float* x, const float* xnorm, int d,
+                        int64_t batch_begin, int batch_n, int entry, int entry_level, unsigned nonempty_mask, int ef_c,
+                        BuildScratch& s) {
+    if (batch_n <= 0) return;
+    RVX_REQUIRE(G.C0 <= 64 && G.M <= 32, RVX_ERR_UNSUPPORTED, "GPU HNSW build supports m <= 32");
+    RVX_REQUIRE(ef_c >= 1 && ef_c <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER, "ef_construction out of range");
+    const int nslots = std::min(batch_n, 8192);
+    const int rev_cap = G.C0 + G.M * G.max_layer;
+    BuildArgs a{};
+    a.G = G; a.x = x; a.xnorm = xnorm; a.d = d;
+    a.batch_begin = batch_begin; a.batch_n = batch_n; a.entry = entry; a.entry_level = entry_level;
+    a.nonempty_mask = nonempty_mask; a.ef_c = ef_c;
+    a.visited = (unsigned long long*)scratch_bytes("build_visited", (int64_t)nslots * VCAP * 8);
+    const int64_t nrec = (int64_t)batch_n * rev_cap;
+    a.rev_next = (int*)scratch_bytes("build_rev_next", nrec * 4);
+    a.rev_key = (int*)scratch_bytes("build_rev_key", nrec * 4);
+    a.rev_d = (float*)scratch_bytes("build_rev_d", nrec * 4);
+    a.rev_src = (int*)scratch_bytes("build_rev_src", nrec * 4);
+    a.rev_head = s.rev_head;
+    a.rev_cap = rev_cap;
+    a.nslots = nslots;
+    a.status = (int*)scratch_bytes("build_status", 256);
+    RVX_HIP(hipMemsetAsync(a.visited, 0, (size_t)nslots * VCAP * 8, stream()));
+    RVX_HIP(hipMemsetAsync(a.status, 0, 4, stream()));
+    const size_t lds = build_lds_bytes(d, ef_c);
+    RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr = true;
+    }
+    switch (metric) {
+        case RVX_METRIC_L2: RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_COSINE: RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_L1: RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
+        default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by the GPU HNSW build");
+    }
+    const int waves = (int)((nrec + 63) / 64);
+    RVX_LAUNCH("hnsw_build_merge", k_build_merge, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, a, (int)nrec);
+    int st = 0;
+    RVX_HIP(hipMemcpyAsync(&st, a.status, 4, hipMemcpyDeviceToHost, stream()));
+    sync();
+    RVX_REQUIRE(st == 0, RVX_ERR_INDEX, "HNSW build candidate list overflow (pathological distance ties)");
+}
+
+}  // namespace rvx

@@ -1,0 +1,99 @@
+"""GPU HNSW construction (k_hnsw_build.hip) — parity by graph invariants,
+recall vs the oracle's CPU build, and bit-exact search on
+the GPU-built graph (GPU search vs the oracle's search of the same graph)."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+rv = pytest.importorskip("ruvector_amd")
+pytestmark = pytest.mark.gpu
+
+
+def unit(n, d, seed):
+    v = O.fill_uniform(n * d, seed).reshape(n, d)
+    return (v / np.sqrt(np.sum(v * v, 1, dtype=np.float32))[:, None]).astype(np.float32)
+
+
+def recall(gt, got):
+    return float(np.mean([len(set(a.tolist()) & set(b.tolist())) / len(a) for a, b in zip(gt, got)]))
+
+
+def build_gpu(x, metric, m, efc, seed, chunks=1):
+    idx = rv.HnswIndex(x.shape[1], rv.DistanceMetric.Euclidean if metric == "l2" else rv.DistanceMetric.Cosine,
+                       rv.HnswConfig(m=m, ef_construction=efc, ef_search=100), seed=seed)
+    for part in np.array_split(np.arange(len(x)), chunks):
+        idx.add_array(x[part], part.astype(np.uint64))
+    return idx
+
+
+def test_graph_invariants_and_levels():
+    n, d, m = 3000, 32, 16
+    x = O.fill_uniform(n * d, 3).reshape(n, d)
+    idx = build_gpu(x, "l2", m, 64, seed=9)
+    g = idx.export_graph()
+    # levels follow the same seeded LayerGenerator as the oracle
+    ref = O.Hnsw(d, "l2", m=m, ef_construction=64, seed=9)
+    ref.insert(x[:1], threads=1)
+    h = O.Hnsw(d, "l2", m=m, ef_construction=64, seed=9)
+    h.insert(x, threads=8)
+    assert np.array_equal(g["levels"], h.export()["levels"])
+    rp, col = g["row_ptr0"], g["col0"]
+    assert rp[0] == 0 and rp[-1] == len(col)
+    dm = O.distance_matrix(x, x, "l2")
+    for i in range(n):
+        nb = col[rp[i]:rp[i + 1]]
+        assert len(nb) <= 2 * m
+        assert i not in nb.tolist() and len(set(nb.tolist())) == len(nb)
+        dd = dm[i, nb]
+        assert np.all(np.diff(dd) >= 0)  # sorted by distance to the owner
+    assert g["entry"] == int(np.argmax(g["levels"]))  # first point of the highest level
+
+
+@pytest.mark.parametrize("metric", ["l2", "cosine"])
+def test_search_bit_exact_on_gpu_built_graph(metric):
+    n, d = 4000, 48
+    x = unit(n, d, 5) if metric == "cosine" else O.fill_uniform(n * d, 5).reshape(n, d)
+    idx = build_gpu(x, metric, 16, 100, seed=2, chunks=3)
+    h = O.Hnsw.from_graph(x, idx.export_graph(), metric)
+    q = O.fill_uniform(150 * d, 6).reshape(150, d)
+    for k, ef in ((10, 10), (10, 64), (20, 200)):
+        ids, dist, cnt = idx.search_array(q, k, ef)
+        rids, rd, rc = h.search(q, k, ef)
+        assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd) and np.array_equal(cnt, rc)
+
+
+def test_recall_matches_cpu_build():
+    n, d, m, efc = 20000, 64, 16, 100
+    x = O.fill_uniform(n * d, 7).reshape(n, d)
+    q = O.fill_uniform(300 * d, 8).reshape(300, d)
+    gt, _ = O.flat_search(x, q, 10, "l2")
+    idx = build_gpu(x, "l2", m, efc, seed=4)
+    h = O.Hnsw(d, "l2", m=m, ef_construction=efc, seed=4)
+    h.insert(x, threads=16)
+    for ef in (32, 100):
+        r_gpu = recall(gt, idx.search_array(q, 10, ef)[0].astype(np.int64))
+        r_cpu = recall(gt, h.search(q, 10, ef)[0])
+        assert r_gpu >= r_cpu - 0.02, (ef, r_gpu, r_cpu)
+
+
+def test_reference_recall_thresholds():
+    # hnsw_integration_test.rs:57-118 (100 vectors, m16 ef_c100 ef_s200, >= 0.90) and :122-185 (1k, >= 0.95)
+    for n, m, efc, thr in ((100, 16, 100, 0.90), (1000, 32, 200, 0.95)):
+        x = unit(n, 128, 42 + n)
+        idx = build_gpu(x, "cosine", m, efc, seed=1)
+        qq = x[::n // 10] if n == 100 else x[::50]
+        ids, _, _ = idx.search_array(qq, 10, 200)
+        gt, _ = O.flat_search(x, qq, 10, "cosine")
+        assert recall(gt, ids.astype(np.int64)) >= thr
+
+
+def test_remove_filters_hnsw_results():
+    x = O.fill_uniform(500 * 16, 9).reshape(500, 16)
+    idx = rv.HnswIndex(16, rv.DistanceMetric.Euclidean, rv.HnswConfig(m=8, ef_construction=50, ef_search=50))
+    idx.add_batch([(f"v{i}", x[i]) for i in range(500)])
+    top = idx.search(x[10], 5)
+    assert top[0].id == "v10"
+    assert idx.remove("v10")
+    after = idx.search(x[10], 5)
+    assert "v10" not in [r.id for r in after] and len(after) == 4  # filter_map drops it (index/hnsw.rs:250-258)
