@@ -1,20 +1,26 @@
 #!/usr/bin/env python3
-"""Headline benchmark: GNN-layer edges/s of the MI355X GNN-learned-index path.
+"""Headline benchmark: GNN-layer edges/s (+ HNSW queries/s@recall95) of the
+MI355X GNN-learned-index path.
 
-Workload (BASELINE.json configs[1], per GPU): 1M x 768 node table, uniform
-random out-degree-32 CSR, 2-layer ruvector-gnn GraphSAGE-mean forward
+Workload (BASELINE.json metric "10M x 768, 1/2/4/8 MI355X"; the configs[1]
+layer stack at configs[2]/[3] scale): a 10M x 768 node table, uniform random
+out-degree-32 CSR, 2-layer ruvector-gnn GraphSAGE-mean forward
 (crates/ruvector-postgres/src/gnn/graphsage.rs:118-187) with the reference's
 deterministic weights. A step = one full 2-layer forward over every node.
-Multi-GPU (one process per GPU, torch.distributed.run): node-range shards of
-1M rows per GPU (weak scaling); before each layer the node table is
-all-gathered over RCCL/xGMI (the halo of a random graph is the whole graph).
 
-value = (edges x layers over all ranks) / max-over-ranks wall time of K steps,
-inputs resident in HBM. Per-kernel device time comes from HIP events on the
-library stream (rvx profiler); the CPU baseline is the oracle (the reference
-algorithm restated in C++) timed on a bounded sample of rows on rank 0.
+Multi-GPU (one process per GPU, torch.distributed.run): the 10M nodes are
+split into contiguous node-id ranges (strong scaling). The input node table is
+resident on every GPU; each layer writes its owned rows of the next table and
+ships them to every peer over RCCL p2p (xGMI) chunk by chunk while the
+remaining chunks compute (rvx_sage_forward_exchange); the last layer's rows
+stay local. value = (edges x layers) / max-over-ranks wall time of K steps.
+
+Per-kernel device time comes from HIP events stamped by the dispatch packets
+(rvx profiler); the CPU baseline is the oracle (the reference algorithm
+restated in C++) timed on a bounded sample of rows on rank 0.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -25,9 +31,11 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-METRIC = "GNN-layer edges/sec + HNSW queries/sec@recall95, 10M×768, 1/2/4/8 MI355X"
+METRIC = "GNN-layer edges/sec + HNSW queries/sec@recall95, 10M\u00d7768, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_MFMA_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (dense spec)
+XGMI_PEAK_GBS = 7 * 153.0    # 7 xGMI links x ~153 GB/s per direction per GPU
+PIPELINE = "row chunks x8 (>=131072 rows), gather on aux stream overlapping GEMM+normalize"
 
 
 def parse():
@@ -35,12 +43,13 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--nodes", type=int, default=1_000_000, help="nodes per GPU")
+    p.add_argument("--nodes", type=int, default=10_000_000, help="total nodes (split over GPUs)")
     p.add_argument("--dim", type=int, default=768)
     p.add_argument("--degree", type=int, default=32)
     p.add_argument("--layers", type=int, default=2)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-hnsw", action="store_true", help="skip the HNSW queries/s@recall95 leg")
     return p.parse_args()
 
 
@@ -58,10 +67,12 @@ def main():
     from ruvector_amd.shard import RcclComm, ShardPlan
 
     rv.set_device(local)
-    n_loc, d, deg, layers = a.nodes, a.dim, a.degree, a.layers
-    n_tot = n_loc * world
+    n_tot, d, deg, layers = a.nodes, a.dim, a.degree, a.layers
     plan = ShardPlan(n_tot, world)
     r0, r1 = plan.rows(rank)
+    n_loc = r1 - r0
+    offsets = np.array([plan.rows(p)[0] for p in range(world)] + [n_tot], dtype=np.int64)
+    off_ptr = offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
 
     comm = None
     if world > 1:
@@ -69,28 +80,22 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         comm = RcclComm(world, rank, uid[0])
 
-    # ---- inputs resident in HBM
-    x_loc = rv.Buffer(n_loc * d * 4)
-    x_loc.fill_normal(n_loc * d, 3 + rank)
-    x_full = rv.Buffer(n_tot * d * 4) if world > 1 else x_loc
-    h_loc = [rv.Buffer(n_loc * d * 4) for _ in range(2)]
-    h_full = rv.Buffer(n_tot * d * 4) if world > 1 else None
+    # ---- inputs resident in HBM: the node table (same on every GPU), this
+    # rank's CSR rows (global column ids), two full tables for layer outputs
+    x = rv.Buffer(n_tot * d * 4)
+    x.fill_normal(n_tot * d, 3)
+    tables = [rv.Buffer(n_tot * d * 4) for _ in range(min(layers, 2))]
     g = rv.Graph.random_shard(n_tot, r0, n_loc, deg, 4)
     sage = [rv.GraphSAGELayer(d, d, num_samples=deg) for _ in range(layers)]
     rv.synchronize()
 
     def step():
-        src_full, src_loc = x_full, x_loc
+        src = x
         for li, layer in enumerate(sage):
-            if world > 1:
-                comm.allgather(src_loc, n_loc * d, src_full)
-                tbl, off = src_full, r0
-            else:
-                tbl, off = src_loc, 0
-            out = h_loc[li % 2]
-            rv._lib.call("rvx_sage_forward_shard_device", layer._h, g.handle, tbl.handle, off, out.handle)
-            src_loc = out
-            src_full = h_full
+            dst = tables[li % 2]
+            rv._lib.call("rvx_sage_forward_exchange", layer._h, g.handle, src.handle, dst.handle, off_ptr,
+                         comm._h if comm else None, int(li < layers - 1))
+            src = dst
 
     def barrier():
         rv.synchronize()
@@ -120,47 +125,88 @@ def main():
     edges_per_step = n_tot * deg * layers
     value = edges_per_step * a.steps / elapsed
 
-    # ---- roofline of the kernels on the path (HIP events, same stream)
-    def rl(name, unit, work_per_launch, peak, bound):
+    # ---- roofline of the kernels on the path. Layers run as a row-chunked
+    # two-stream pipeline (gather of chunk c+1 overlaps the GEMM of chunk c),
+    # so a kernel launches several times per layer; work per launch = work per
+    # step x steps / launches (this rank's rows).
+    def rl(name, unit, work_per_step, peak, bound):
         if name not in kern or kern[name]["launches"] == 0:
             return None
+        work_per_launch = work_per_step * a.steps / kern[name]["launches"]
         avg_s = kern[name]["total_ms"] / kern[name]["launches"] / 1e3
         ach = work_per_launch / avg_s / (1e9 if unit == "GB/s" else 1e12)
         return {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
                 "traffic": None, "avg_ms": round(avg_s * 1e3, 4), "launches": kern[name]["launches"],
                 "work_per_launch": work_per_launch}
 
-    agg_bytes = n_loc * deg * (4 * d + 4) + n_loc * (8 + 4 * d)
+    agg_bytes = n_loc * deg * (4 * d + 4) + n_loc * (8 + 4 * d)   # per layer
     gemm_flops = 2.0 * n_loc * d * (2 * d)
-    rls = {"sage_aggregate": rl("sage_aggregate", "GB/s", agg_bytes, HBM_PEAK_GBS, "hbm"),
-           "sage_gemm": rl("sage_gemm", "TFLOP/s", gemm_flops, FP32_MFMA_PEAK_TFS, "mfma"),
-           "sage_normalize": rl("sage_normalize", "GB/s", 2 * n_loc * d * 4, HBM_PEAK_GBS, "hbm")}
-    if comm is not None and "rccl_allgather" in kern:
-        rls["rccl_allgather"] = rl("rccl_allgather", "GB/s", (world - 1) * n_loc * d * 4, 7 * 153.0, "xgmi")
-    dom = max((k for k in rls if rls[k]), key=lambda k: kern[k]["total_ms"])
-    attach_pmc_traffic(rls, {"nodes_per_gpu": n_loc, "dim": d, "degree": deg, "layers": layers})
+    norm_bytes = 2 * n_loc * d * 4
+    rls = {"sage_aggregate": rl("sage_aggregate", "GB/s", agg_bytes * layers, HBM_PEAK_GBS, "hbm"),
+           "sage_gemm": rl("sage_gemm", "TFLOP/s", gemm_flops * layers, FP32_MFMA_PEAK_TFS, "mfma"),
+           "sage_normalize": rl("sage_normalize", "GB/s", norm_bytes * layers, HBM_PEAK_GBS, "hbm")}
+    if comm is not None:
+        rls["halo_exchange"] = rl("halo_exchange", "GB/s", (n_tot - n_loc) * d * 4 * (layers - 1), XGMI_PEAK_GBS,
+                                  "xgmi")
+    dom = max((k for k in rls if rls[k] and k != "halo_exchange"), key=lambda k: kern[k]["total_ms"])
+    attach_pmc_traffic(rls, {"nodes_total": n_tot, "dim": d, "degree": deg, "layers": layers,
+                             "parallelism": f"node-range x{world}", "pipeline": PIPELINE})
+    # whole-layer floor: HBM and MFMA work overlap, so a layer cannot beat the
+    # larger of the two floors
+    layer_ms = elapsed / a.steps / layers * 1e3
+    hbm_floor = (agg_bytes + norm_bytes) / (HBM_PEAK_GBS * 1e9) * 1e3
+    mfma_floor = gemm_flops / (FP32_MFMA_PEAK_TFS * 1e12) * 1e3
+    layer_rl = {"layer_ms": round(layer_ms, 3), "hbm_floor_ms": round(hbm_floor, 3),
+                "mfma_floor_ms": round(mfma_floor, 3), "frac": round(max(hbm_floor, mfma_floor) / layer_ms, 4)}
 
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic: X ~ N(0,1) Box-Muller on device (seed 3+rank); uniform random out-degree CSR (seed 4); "
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: X ~ N(0,1) Box-Muller on device (seed 3); uniform random out-degree CSR (seed 4); "
                 "GraphSAGE deterministic init (graphsage.rs:56-78)",
-        "config": {"workload": "configs[1]: 1M x 768 2-layer ruvector-gnn GraphSAGE-mean forward per GPU; "
-                               "node-range shards + RCCL all-gather halo for N>1",
-                   "nodes_per_gpu": n_loc, "nodes_total": n_tot, "dim": d, "degree": deg, "layers": layers,
-                   "edges_per_step": edges_per_step, "parallelism": f"node-range x{world}"},
+        "config": {"workload": "10M x 768 2-layer ruvector-gnn GraphSAGE-mean forward (configs[1] layers at the "
+                               "metric's 10M scale); node-range shards + chunked RCCL p2p halo exchange for N>1",
+                   "nodes_total": n_tot, "nodes_per_gpu": n_loc, "dim": d, "degree": deg, "layers": layers,
+                   "edges_per_step": edges_per_step, "parallelism": f"node-range x{world}",
+                   "pipeline": PIPELINE},
         "roofline": dict(rls[dom], kernel=dom),
         "roofline_kernels": {k: v for k, v in rls.items() if v},
+        "roofline_layer": layer_rl,
         "kernel_ms": {k: round(v["total_ms"] / max(v["launches"], 1), 4) for k, v in kern.items()},
     }
 
     if rank == 0 and world == 1 and not a.no_cpu:
-        line["cpu_baseline"], line["parity"] = cpu_baseline(a, x_loc, g, h_loc[0], sage, n_loc, d, deg)
+        line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, tables[0], n_tot, d, deg)
+    if not a.no_hnsw:
+        del x, tables, g
+        line["hnsw"] = hnsw_leg(a, rank, world, dist)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def hnsw_leg(a, rank, world, dist):
+    """Second half of the metric: HNSW queries/s at recall@10 >= 0.95 on
+    BASELINE configs[0] (C1: 100k x 128, M=32, ef_c=200, 10k queries). The index
+    is a replica per GPU (search does not shard), built on the GPU; each rank
+    answers its own 10k queries, so the job rate is the sum over ranks."""
+    import bench_hnsw
+    res = bench_hnsw.run(100_000, 128, 10_000, 32, 200, [300, 400, 600, 800], 10, "l2",
+                         cpu=(rank == 0 and world == 1 and not a.no_cpu), log=lambda s: None)
+    qps = res["qps_at_recall95"] or 0.0
+    if dist is not None:
+        import torch
+        t = torch.tensor([qps, res["build_s"]], dtype=torch.float64)
+        lo = t.clone()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        res["per_gpu_min_qps"] = float(lo[0])
+        qps = float(t[0])
+    res["value"] = round(qps, 1)
+    res["unit"] = "queries/s (recall@10 >= 0.95, replicas summed over GPUs)"
+    return res
 
 
 def attach_pmc_traffic(rls, cfg):
@@ -188,18 +234,16 @@ def attach_pmc_traffic(rls, cfg):
             r["traffic_source"] = "rocprofv3 --pmc (HBM bytes per launch; MFMA-bound kernel)"
 
 
-def cpu_baseline(a, x_buf, g, h1_buf, sage, n, d, deg):
-    """Oracle (reference algorithm, C++) on a bounded sample of layer-1 rows."""
+def cpu_baseline(a, x_buf, g, h1_buf, n, d, deg):
+    """Oracle (reference algorithm, C++) on a bounded sample of layer-1 rows;
+    h1_buf holds the GPU's layer-1 output of the last timed step."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
-    import ruvector_amd as rv
 
     threads = min(16, os.cpu_count() or 1)
     x = x_buf.download(np.float32, (n, d))
     rp, col = O.random_csr(n, deg, 4)
     wn, ws = O.sage_init(d, d, 0), O.sage_init(d, d, 1000)
-    # layer-1 GPU output for the whole graph (single forward, outside the timed region)
-    rv._lib.call("rvx_sage_forward_shard_device", sage[0]._h, g.handle, x_buf.handle, 0, h1_buf.handle)
     rows = 2048
     t0 = time.perf_counter()
     O.sage_forward(x, rp, col, wn, ws, rows=(0, rows), threads=threads)
@@ -212,7 +256,7 @@ def cpu_baseline(a, x_buf, g, h1_buf, sage, n, d, deg):
     err = float(np.max(np.abs(got.astype(np.float64) - ref)) / max(float(np.max(np.abs(ref))), 1e-30))
     cpu = {"value": round(rows * deg / dt, 1), "unit": "edges/s", "cores": threads, "kind": "port",
            "sample": f"oracle GraphSAGE-mean layer 1 (graphsage.rs:118-187 restated, AVX2, {threads} threads) on "
-                     f"rows 0..{rows} of the same 1M x 768 graph, {dt:.1f} s"}
+                     f"rows 0..{rows} of the same {n} x {d} graph, {dt:.1f} s"}
     parity = {"rows": rows, "max_rel_err": err, "tol": 1e-5, "ok": err <= 1e-5}
     return cpu, parity
 

@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""HNSW half of the headline metric: queries/s at recall@10 >= 0.95.
+
+Config C1 (BASELINE.json configs[0]): 100k x 128 uniform[-1,1)
+base (seed 1), 10k queries (seed 2), HnswConfig default M=32, ef_c=200, L2, k=10.
+The graph is built on the GPU (hnsw_rs insert semantics, batched); ground truth
+is the exact GPU scan (bit-exact with the reference distance order). Searches
+sweep ef; the reported QPS is the fastest ef whose recall@10 >= 0.95.
+Optionally times the oracle's CPU search on the same graph (--cpu).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def run(n, d, nq, m, efc, efs, k, metric_name, seed_base=1, cpu=False, cpu_seconds=10.0, cpu_build=False, log=print):
+    import ruvector_amd as rv
+    metric = {"l2": rv.DistanceMetric.Euclidean, "cosine": rv.DistanceMetric.Cosine}[metric_name]
+    xb = rv.Buffer(n * d * 4)
+    xb.fill_uniform(n * d, seed_base, -1.0, 1.0)
+    qb = rv.Buffer(nq * d * 4)
+    qb.fill_uniform(nq * d, seed_base + 1, -1.0, 1.0)
+    if metric_name == "cosine":
+        xb.normalize_rows(n, d)
+        qb.normalize_rows(nq, d)
+    idx = rv.HnswIndex(d, metric, rv.HnswConfig(m=m, ef_construction=efc, ef_search=100), seed=seed_base)
+    rv.synchronize()
+    t0 = time.perf_counter()
+    rv._lib.call("rvx_index_add_batch_device", idx.handle, xb.handle, n, 0)
+    rv.synchronize()
+    build_s = time.perf_counter() - t0
+    log(f"build {n}x{d} M={m} ef_c={efc}: {build_s:.2f} s")
+
+    ids_b = rv.Buffer(nq * k * 8)
+    dist_b = rv.Buffer(nq * k * 4)
+    t0 = time.perf_counter()
+    rv._lib.call("rvx_index_brute_force_device", idx.handle, qb.handle, nq, k, ids_b.handle, dist_b.handle)
+    rv.synchronize()
+    gt_s = time.perf_counter() - t0
+    gt = ids_b.download(np.uint64, (nq, k))
+    log(f"exact ground truth {nq} queries: {gt_s:.2f} s")
+
+    sweep = []
+    prof = rv.Profiler()
+    for ef in efs:
+        rv._lib.call("rvx_index_search_device", idx.handle, qb.handle, nq, k, ef, ids_b.handle, dist_b.handle)
+        rv.synchronize()
+        with prof:
+            t0 = time.perf_counter()
+            rv._lib.call("rvx_index_search_device", idx.handle, qb.handle, nq, k, ef, ids_b.handle, dist_b.handle)
+            rv.synchronize()
+            dt = time.perf_counter() - t0
+        ker_ms, _ = prof.query("hnsw_search")
+        got = ids_b.download(np.uint64, (nq, k))
+        rec = float(np.mean([len(set(a.tolist()) & set(b.tolist())) / k for a, b in zip(gt, got)]))
+        sweep.append({"ef": ef, "recall": round(rec, 4), "qps": round(nq / dt, 1), "kernel_ms": round(ker_ms, 3)})
+        log(f"ef={ef}: recall@{k}={rec:.4f} qps={nq / dt:.0f} (kernel {ker_ms:.2f} ms)")
+    ok = [s for s in sweep if s["recall"] >= 0.95]
+    best = max(ok, key=lambda s: s["qps"]) if ok else None
+    out = {"config": f"{n}x{d} uniform, {nq} queries, M={m}, ef_c={efc}, k={k}, {metric_name}",
+           "build_s": round(build_s, 3), "sweep": sweep, "qps_at_recall95": best["qps"] if best else None,
+           "ef_at_recall95": best["ef"] if best else None}
+    if cpu_build:
+        # recall of the oracle's CPU build (hnsw_rs parallel_insert semantics) on the same data
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle as O
+        x = xb.download(np.float32, (n, d))
+        q = qb.download(np.float32, (nq, d))
+        h = O.Hnsw(d, metric_name, m=m, ef_construction=efc, seed=seed_base)
+        t0 = time.perf_counter()
+        h.insert(x, threads=min(16, os.cpu_count() or 1))
+        cb = time.perf_counter() - t0
+        cs = []
+        for ef in efs:
+            cids, _, _ = h.search(q[:2000], k, ef, threads=min(16, os.cpu_count() or 1))
+            rec = float(np.mean([len(set(a.tolist()) & set(b.tolist())) / k for a, b in zip(gt[:2000].astype(np.int64), cids)]))
+            cs.append({"ef": ef, "recall": round(rec, 4)})
+        out["cpu_build"] = {"build_s": round(cb, 2), "threads": min(16, os.cpu_count() or 1), "sweep_2k_queries": cs}
+        log(f"cpu build {cb:.1f} s; recall {cs}")
+    if cpu and best:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle as O
+        x = xb.download(np.float32, (n, d))
+        q = qb.download(np.float32, (nq, d))
+        h = O.Hnsw.from_graph(x, idx.export_graph(), metric_name)
+        threads = min(16, os.cpu_count() or 1)
+        sample = min(nq, 500)
+        t0 = time.perf_counter()
+        h.search(q[:sample], k, best["ef"], threads=threads)
+        dt = time.perf_counter() - t0
+        sample = int(min(nq, max(sample, sample * cpu_seconds / max(dt, 1e-3))))
+        t0 = time.perf_counter()
+        cids, _, _ = h.search(q[:sample], k, best["ef"], threads=threads)
+        dt = time.perf_counter() - t0
+        gpu_ids = idx.search_array(q[:sample], k, best["ef"])[0].astype(np.int64)
+        out["cpu_baseline"] = {"value": round(sample / dt, 1), "unit": "queries/s", "cores": threads, "kind": "port",
+                               "sample": f"oracle hnsw_rs search_filter on the same graph, {sample} queries, ef={best['ef']}"}
+        out["cpu_gpu_ids_equal"] = bool(np.array_equal(cids, gpu_ids))
+    return out
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--n", type=int, default=100_000)
+    p.add_argument("--dim", type=int, default=128)
+    p.add_argument("--queries", type=int, default=10_000)
+    p.add_argument("--m", type=int, default=32)
+    p.add_argument("--ef-construction", type=int, default=200)
+    p.add_argument("--ef", type=str, default="16,32,64,100,200,300,400,600,800,1000")
+    p.add_argument("--k", type=int, default=10)
+    p.add_argument("--metric", default="l2")
+    p.add_argument("--cpu", action="store_true")
+    p.add_argument("--cpu-build", action="store_true")
+    a = p.parse_args()
+    out = run(a.n, a.dim, a.queries, a.m, a.ef_construction, [int(e) for e in a.ef.split(",")], a.k, a.metric,
+              cpu=a.cpu, cpu_build=a.cpu_build, log=lambda s: print(s, file=sys.stderr, flush=True))
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -130,6 +130,7 @@ rvx_status rvx_aggregate_device(const rvx_graph* g, int32_t agg, int32_t use_edg
 /* GraphSAGE (crates/ruvector-postgres/src/gnn/graphsage.rs:25-196)    */
 /* ------------------------------------------------------------------ */
 typedef struct rvx_sage_layer rvx_sage_layer;
+typedef struct rvx_comm rvx_comm; /* RCCL communicator, see Multi-GPU below */
 enum { RVX_SAGE_MEAN = 0, RVX_SAGE_MAXPOOL = 1, RVX_SAGE_LSTM = 2 /* = mean, graphsage.rs:159 */ };
 /* w_neighbor/w_self: [in][out] row-major as GraphSAGELayer stores them; NULL
  * for both selects the deterministic init of graphsage.rs:56-78.
@@ -150,6 +151,19 @@ rvx_status rvx_sage_forward_device(const rvx_sage_layer* l, const rvx_graph* g, 
  * all-gathered node table; y [g.n][out] receives the owned rows. */
 rvx_status rvx_sage_forward_shard_device(const rvx_sage_layer* l, const rvx_graph* g, const rvx_buffer* x_full,
                                          int64_t row_offset, rvx_buffer* y);
+/* One layer of a node-range-sharded stack with the halo exchange fused in
+ * (replaces the per-node loop of
+ * GraphSAGELayer::forward, graphsage.rs:190-196, over the shard). Rank r
+ * (of comm; NULL = single GPU) owns rows [offsets[r], offsets[r+1]) and g
+ * holds those CSR rows with GLOBAL column ids. Reads x_full [N][in]; writes the
+ * owned rows of y_full [N][out] and, when `exchange` != 0, receives every
+ * peer's rows of y_full over RCCL point-to-point as they are produced, so the
+ * next layer can read the whole table. The exchange of chunk c overlaps the
+ * compute of chunk c+1; the call returns with all of it queued on the library
+ * stream. x_full and y_full must differ. offsets has comm_size+1 entries. */
+rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g, const rvx_buffer* x_full,
+                                     rvx_buffer* y_full, const int64_t* offsets, rvx_comm* comm, int32_t exchange);
+
 
 /* ------------------------------------------------------------------ */
 /* GCN (crates/ruvector-postgres/src/gnn/gcn.rs:12-149)                */
@@ -309,7 +323,6 @@ rvx_status rvx_profile_names(char* buf, size_t len);
 /* ------------------------------------------------------------------ */
 /* Multi-GPU: node-range sharding with RCCL over xGMI   */
 /* ------------------------------------------------------------------ */
-typedef struct rvx_comm rvx_comm;
 #define RVX_COMM_ID_BYTES 128
 rvx_status rvx_comm_unique_id(uint8_t id[RVX_COMM_ID_BYTES]);
 rvx_status rvx_comm_init(const uint8_t id[RVX_COMM_ID_BYTES], int32_t nranks, int32_t rank, rvx_comm** out);

@@ -4,6 +4,7 @@
 // node tables (GNN halo); HNSW shards merge per-shard top-k.
 #include <rccl/rccl.h>
 
+#include "comm.hpp"
 #include "graph.hpp"
 
 using namespace rvx;
@@ -20,6 +21,29 @@ struct rvx_comm {
     } while (0)
 
 static_assert(sizeof(ncclUniqueId) == RVX_COMM_ID_BYTES, "ncclUniqueId size");
+
+namespace rvx {
+
+int comm_rank(const rvx_comm* c) { return c ? c->rank : 0; }
+int comm_size(const rvx_comm* c) { return c ? c->nranks : 1; }
+
+void comm_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int64_t* r0, const int64_t* rows,
+                        hipStream_t s) {
+    if (!c || c->nranks <= 1) return;
+    const int me = c->rank;
+    RVX_NCCL(ncclGroupStart());
+    for (int k = 1; k < c->nranks; ++k) {
+        // peers in rotated order so every rank starts on a different link
+        const int p = (me + k) % c->nranks;
+        if (rows[me] > 0)
+            RVX_NCCL(ncclSend(table + r0[me] * row_elems, (size_t)(rows[me] * row_elems), ncclFloat32, p, c->comm, s));
+        if (rows[p] > 0)
+            RVX_NCCL(ncclRecv(table + r0[p] * row_elems, (size_t)(rows[p] * row_elems), ncclFloat32, p, c->comm, s));
+    }
+    RVX_NCCL(ncclGroupEnd());
+}
+
+}  // namespace rvx
 
 extern "C" {
 

@@ -3,6 +3,9 @@
 #include <algorithm>
 #include <cmath>
 
+#include <functional>
+
+#include "comm.hpp"
 #include "graph.hpp"
 #include "kernels.hpp"
 
@@ -119,22 +122,61 @@ struct rvx_gcn_layer {
 
 namespace {
 
+// Row chunking of the layer pipeline (same on every rank for a given chunk count).
+int sage_chunks_for(int64_t n) {
+    static const int pipe_chunks = std::max(1, env_int("RVX_SAGE_CHUNKS", 8));
+    return n >= (int64_t)pipe_chunks * 16384 ? pipe_chunks : 1;
+}
+int64_t chunk_step(int64_t n, int chunks) { return ((n + chunks - 1) / chunks + 127) / 128 * 128; }
+
+// Called on the host after chunk c's launches are queued (rows [r0, r0+rows)
+// of y, possibly empty); the chunk's output is complete at that point of the
+// library stream.
+using ChunkHook = std::function<void(int c, int64_t r0, int64_t rows)>;
+
 // x: node table indexed by the CSR columns; rows [row_offset, row_offset+g->n)
 // of it are this graph's destination (self) rows.
-void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* x, float* y, int64_t row_offset = 0) {
+void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* x, float* y, int64_t row_offset = 0,
+                      int chunks = 0, const ChunkHook& hook = nullptr) {
     RVX_REQUIRE(g->max_deg <= l->num_samples, RVX_ERR_UNSUPPORTED,
                 "GraphSAGE neighbour sampling (num_samples < max degree, graphsage.rs:92-102) is not supported; "
                 "set num_samples >= max degree");
     const int64_t n = g->n;
     float* agg = scratch_f32("sage_agg", n * (int64_t)l->in);
     const int a = (l->aggregator == RVX_SAGE_MAXPOOL) ? AGG_MAX : AGG_MEAN;
-    aggregate_rows(g->row_ptr, g->col, nullptr, n, x, l->in, a, /*empty_fill zeros*/ 0, 0, agg, "sage_aggregate");
-    GemmOperand s0{agg, l->in, l->wn_t.as<float>(), l->in, l->in};
-    GemmOperand s1{x + row_offset * l->in, l->in, l->ws_t.as<float>(), l->in, l->in};
     GemmEpilogue ep;
     ep.epi = GEMM_EPI_RELU;
-    gemm_nt(n, l->out, s0, &s1, ep, y, l->out, "sage_gemm");
-    if (l->normalize) normalize_rows(y, n, l->out, true, "sage_normalize");
+    // Rows are independent, so the layer runs as a two-stage pipeline over
+    // row chunks: the HBM-bound gather of chunk c+1 (aux stream) overlaps the
+    // MFMA-bound GEMM + normalisation of chunk c (library stream). Every row
+    // sees the same arithmetic as the unchunked layer.
+    if (chunks <= 0) chunks = sage_chunks_for(n);
+    const int64_t step = chunk_step(n, chunks);
+    Device& d = device();
+    hipEvent_t* ev = pipeline_events(chunks + 1);
+    if (chunks > 1) {
+        RVX_HIP(hipEventRecord(ev[chunks], d.stream));  // aux may not overwrite agg before earlier work is done
+        RVX_HIP(hipStreamWaitEvent(d.aux, ev[chunks], 0));
+    }
+    int c = 0;
+    for (int64_t r0 = 0; r0 < n; r0 += step, ++c) {
+        const int64_t rows = std::min(step, n - r0);
+        if (chunks > 1) {
+            StreamScope on_aux(d.aux);
+            aggregate_rows(g->row_ptr + r0, g->col, nullptr, rows, x, l->in, a, /*empty_fill zeros*/ 0, 0,
+                           agg + r0 * l->in, "sage_aggregate", /*overlapped*/ true);
+            RVX_HIP(hipEventRecord(ev[c], d.aux));
+            RVX_HIP(hipStreamWaitEvent(d.stream, ev[c], 0));
+        } else {
+            aggregate_rows(g->row_ptr, g->col, nullptr, n, x, l->in, a, 0, 0, agg, "sage_aggregate");
+        }
+        GemmOperand s0{agg + r0 * l->in, l->in, l->wn_t.as<float>(), l->in, l->in};
+        GemmOperand s1{x + (row_offset + r0) * l->in, l->in, l->ws_t.as<float>(), l->in, l->in};
+        gemm_nt(rows, l->out, s0, &s1, ep, y + r0 * l->out, l->out, "sage_gemm");
+        if (l->normalize) normalize_rows(y + r0 * l->out, rows, l->out, true, "sage_normalize");
+        if (hook) hook(c, r0, rows);
+    }
+    for (; hook && c < chunks; ++c) hook(c, n, 0);
 }
 
 __global__ void k_gcn_isolated(const int32_t* iso, int64_t n_iso, const float* x, int dim, float* y) {
@@ -314,6 +356,56 @@ rvx_status rvx_sage_forward_shard_device(const rvx_sage_layer* l, const rvx_grap
         RVX_REQUIRE(y->mem.bytes >= g->n * l->out * 4, RVX_ERR_DIMENSION_MISMATCH, "y smaller than rows*out");
         ComputeLock cl;
         sage_forward_dev(l, g, x_full->mem.as<float>(), y->mem.as<float>(), row_offset);
+    });
+}
+
+rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g, const rvx_buffer* x_full,
+                                     rvx_buffer* y_full, const int64_t* offsets, rvx_comm* comm, int32_t exchange) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(l && x_full && y_full && offsets, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(x_full != y_full, RVX_ERR_INVALID_PARAMETER, "x_full and y_full must be different buffers");
+        const int world = comm_size(comm), me = comm_rank(comm);
+        for (int p = 0; p < world; ++p)
+            RVX_REQUIRE(offsets[p] >= 0 && offsets[p] <= offsets[p + 1], RVX_ERR_INVALID_PARAMETER,
+                        "offsets must be non-decreasing");
+        RVX_REQUIRE(offsets[me + 1] - offsets[me] == g->n, RVX_ERR_DIMENSION_MISMATCH,
+                    "graph rows differ from this rank's shard");
+        const int64_t N = offsets[world];
+        RVX_REQUIRE(x_full->mem.bytes >= N * l->in * 4, RVX_ERR_DIMENSION_MISMATCH, "x_full smaller than N*in");
+        RVX_REQUIRE(y_full->mem.bytes >= N * l->out * 4, RVX_ERR_DIMENSION_MISMATCH, "y_full smaller than N*out");
+        ComputeLock cl;
+        float* y = y_full->mem.as<float>();
+        const float* x = x_full->mem.as<float>();
+        if (!exchange || world == 1) {
+            sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me]);
+            return;
+        }
+        // every rank uses the chunk count of the largest shard, so the p2p
+        // rounds pair up (a shard with fewer real chunks sends empty ones)
+        int64_t maxn = 0;
+        for (int p = 0; p < world; ++p) maxn = std::max(maxn, offsets[p + 1] - offsets[p]);
+        const int chunks = sage_chunks_for(maxn);
+        Device& d = device();
+        hipEvent_t* ev = pipeline_events(2 * chunks + 2) + chunks + 1;
+        std::vector<int64_t> r0(world), rows(world);
+        auto hook = [&](int c, int64_t, int64_t) {
+            for (int p = 0; p < world; ++p) {
+                const int64_t np = offsets[p + 1] - offsets[p];
+                const int64_t st = chunk_step(np, chunks);
+                const int64_t b = std::min(np, (int64_t)c * st);
+                r0[p] = offsets[p] + b;
+                rows[p] = std::min(st, np - b);
+            }
+            RVX_HIP(hipEventRecord(ev[c], d.stream));
+            RVX_HIP(hipStreamWaitEvent(d.xfer, ev[c], 0));
+            StreamScope on_xfer(d.xfer);
+            ProfScope ps("halo_exchange");
+            comm_exchange_rows(comm, y, l->out, r0.data(), rows.data(), d.xfer);
+        };
+        sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], chunks, hook);
+        RVX_HIP(hipEventRecord(ev[chunks], d.xfer));
+        RVX_HIP(hipStreamWaitEvent(d.stream, ev[chunks], 0));
     });
 }
 

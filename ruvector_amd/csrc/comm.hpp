@@ -1,0 +1,20 @@
+// comm.hpp — internal RCCL helpers shared by the layer drivers.
+#pragma once
+#include "common.hpp"
+
+struct rvx_comm;
+
+namespace rvx {
+
+int comm_rank(const rvx_comm* c);
+int comm_size(const rvx_comm* c);
+
+// One grouped point-to-point round on stream `s`: this rank sends its rows
+// [r0[me], r0[me]+rows[me]) of `table` to every peer and receives each peer
+// p's rows [r0[p], r0[p]+rows[p]) into the same rows of its own `table`
+// (row = row_elems floats). On xGMI every pair has its own link, so the
+// round moves all peers' chunks concurrently.
+void comm_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int64_t* r0, const int64_t* rows,
+                        hipStream_t s);
+
+}  // namespace rvx

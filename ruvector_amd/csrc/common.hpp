@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -62,14 +63,33 @@ rvx_status guard(F&& f) {
 // ---------------------------------------------------------------- device
 struct Device {
     int id = 0;
-    hipStream_t stream = nullptr;  // every kernel of this device runs here
+    hipStream_t stream = nullptr;  // every kernel of this device runs here ...
+    hipStream_t aux = nullptr;     // ... except pipelined stages overlapped on this one
+    hipStream_t xfer = nullptr;    // RCCL halo exchange overlapped with compute
+    std::vector<hipEvent_t> pipe_events;  // timing-free events for stream hand-offs
     int num_cus = 0;
     int64_t hbm_bytes = 0;
     std::string arch;
 };
 Device& device();          // current thread's device (lazily initialised)
-hipStream_t stream();      // shorthand for device().stream
-void sync();               // hipStreamSynchronize(stream())
+hipStream_t stream();      // the stream launches go to (device().stream unless a StreamScope is active)
+void sync();               // hipStreamSynchronize(device().stream)
+// At least `count` reusable hand-off events of the current device (callers
+// hold the device's ComputeLock).
+hipEvent_t* pipeline_events(int count);
+
+// Integer tuning knob from the environment (read once by the caller).
+inline int env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// Route this thread's launches to `s` for the scope's lifetime (pipelining).
+struct StreamScope {
+    hipStream_t prev;
+    explicit StreamScope(hipStream_t s);
+    ~StreamScope();
+};
 
 // RAII device allocation (256-B aligned by hipMalloc).
 struct DevMem {

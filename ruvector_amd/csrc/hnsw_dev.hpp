@@ -9,7 +9,7 @@
 namespace rvx {
 namespace hnswdev {
 
-constexpr int VCAP = 32768;  // visited-set slots per query (power of two)
+constexpr int VCAP_MIN = 32768;  // visited-set slots per query (power of two), grown with ef
 constexpr int C_EXTRA = 128; // candidate capacity = ef + C_EXTRA
 
 template <int METRIC>
@@ -49,14 +49,14 @@ __device__ __forceinline__ float row_dist(const float* __restrict__ qs, const fl
 
 // Claim `node` in a query's visited set: true if it was not visited yet.
 // Slots whose tag is another query's are free (the table is zeroed per launch).
-__device__ __forceinline__ bool visit_claim(unsigned long long* vis, unsigned long long qtag, int node) {
+__device__ __forceinline__ bool visit_claim(unsigned long long* vis, unsigned vmask, unsigned long long qtag, int node) {
     const unsigned long long key = qtag | (unsigned)(node + 1);
-    unsigned h = ((unsigned)node * 2654435761u) & (VCAP - 1);
+    unsigned h = ((unsigned)node * 2654435761u) & vmask;
     unsigned long long cur = __hip_atomic_load(&vis[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int probe = 0; probe < 4 * VCAP; ++probe) {
+    for (unsigned probe = 0; probe <= vmask; ++probe) {
         if ((cur & 0xFFFFFFFF00000000ull) == qtag) {
             if (cur == key) return false;
-            h = (h + 1) & (VCAP - 1);
+            h = (h + 1) & vmask;
             cur = __hip_atomic_load(&vis[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             continue;
         }
@@ -64,7 +64,14 @@ __device__ __forceinline__ bool visit_claim(unsigned long long* vis, unsigned lo
         if (prev == cur) return true;
         cur = prev;
     }
-    return false;  // table full: cannot happen below VCAP visited nodes
+    return false;  // table full: cannot happen below vmask+1 visited nodes
+}
+
+// visited-table size for a search of width ef (load factor well below 1/2)
+inline unsigned visited_capacity(int ef) {
+    unsigned v = VCAP_MIN;
+    while (v < (unsigned)ef * 128u && v < (1u << 22)) v <<= 1;
+    return v;
 }
 
 __device__ __forceinline__ bool lt(float d, int id, float bd, int bid) { return d < bd || (d == bd && id < bid); }

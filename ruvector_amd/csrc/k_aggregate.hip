@@ -31,15 +31,18 @@ __device__ __forceinline__ float4 agg_op(float4 a, float4 v) {
 }
 __device__ __forceinline__ float4 scale4(float4 v, float w) { return make_float4(v.x * w, v.y * w, v.z * w, v.w * w); }
 
-// NV = float4 slots per lane (dim <= 256*NV; dim % 4 == 0).
-template <int NV, int AGG, bool W>
+// NV = float4 slots per lane (dim <= 256*NV; dim % 4 == 0); U = neighbour
+// rows in flight per wave (more when the grid is capped to few waves per CU).
+template <int NV, int AGG, bool W, int U = 4>
 __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
                                                       const float* __restrict__ wts, int64_t n,
                                                       const float* __restrict__ x, int dim, int empty_fill,
                                                       int post_scale, float* __restrict__ out) {
     const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
-    if (row >= n) return;
+    // grid-stride over rows: the grid may be capped (persistent) so the gather
+    // leaves CU slots to a concurrently running GEMM
+    for (int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6); row < n;
+         row += (int64_t)gridDim.x * ROWS_PER_BLOCK) {
     const int64_t beg = rp[row], end = rp[row + 1];
     const int cnt_total = (int)(end - beg);
 
@@ -56,10 +59,10 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
         const int my_c = lane < cnt ? col[e0 + lane] : 0;
         const float my_w = (W && lane < cnt) ? wts[e0 + lane] : 1.0f;
         int t = 0;
-        for (; t + 4 <= cnt; t += 4) {
-            float4 v[4][NV];
+        for (; t + U <= cnt; t += U) {
+            float4 v[U][NV];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < U; ++u) {
                 const int c = __builtin_amdgcn_readlane(my_c, t + u);
                 const float* src = x + (int64_t)c * dim + 4 * lane;
 #pragma unroll
@@ -67,7 +70,7 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
                     v[u][j] = active[j] ? *reinterpret_cast<const float4*>(src + 256 * j) : make_float4(0, 0, 0, 0);
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < U; ++u) {
                 float wu = 1.0f;
                 if (W) wu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), t + u));
 #pragma unroll
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
             if (active[j])
                 *reinterpret_cast<float4*>(dst + 256 * j) =
                     empty_fill == 1 ? *reinterpret_cast<const float4*>(self + 256 * j) : make_float4(0, 0, 0, 0);
-        return;
+        continue;
     }
     if (AGG == AGG_MEAN) {
         const float cntf = (float)cnt_total;  // mean_aggregate: x / count (aggregators.rs:64-67)
@@ -111,6 +114,7 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
 #pragma unroll
     for (int j = 0; j < NV; ++j)
         if (active[j]) *reinterpret_cast<float4*>(dst + 256 * j) = acc[j];
+    }
 }
 
 // Any dim: one wave per row, scalar columns; same sequential order.
@@ -141,36 +145,53 @@ __global__ __launch_bounds__(256) void k_aggregate_scalar(const int64_t* rp, con
 
 template <int AGG, bool W>
 void launch_agg(const char* t, const int64_t* rp, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
-                int empty_fill, int post_scale, float* out) {
-    const dim3 grid((unsigned)((n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK)), block(256);
+                int empty_fill, int post_scale, float* out, int cap_per_cu, bool deep) {
+    int64_t blocks = (n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
+    if (cap_per_cu > 0) blocks = std::min<int64_t>(blocks, (int64_t)cap_per_cu * device().num_cus);
+    const dim3 grid((unsigned)blocks), block(256);
     const bool vec = (dim % 4 == 0) && (((uintptr_t)x & 15) == 0) && (((uintptr_t)out & 15) == 0);
-    if (vec && dim <= 256)
-        RVX_LAUNCH(t, (k_aggregate_vec<1, AGG, W>), grid, block, 0, rp, col, w, n, x, dim, empty_fill, post_scale, out);
-    else if (vec && dim <= 512)
-        RVX_LAUNCH(t, (k_aggregate_vec<2, AGG, W>), grid, block, 0, rp, col, w, n, x, dim, empty_fill, post_scale, out);
-    else if (vec && dim <= 768)
-        RVX_LAUNCH(t, (k_aggregate_vec<3, AGG, W>), grid, block, 0, rp, col, w, n, x, dim, empty_fill, post_scale, out);
-    else if (vec && dim <= 1024)
-        RVX_LAUNCH(t, (k_aggregate_vec<4, AGG, W>), grid, block, 0, rp, col, w, n, x, dim, empty_fill, post_scale, out);
+#define RVX_AGG_VEC(NV)                                                                                          \
+    do {                                                                                                         \
+        if (deep)                                                                                                \
+            RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 8>), grid, block, 0, rp, col, w, n, x, dim, empty_fill,   \
+                       post_scale, out);                                                                         \
+        else                                                                                                     \
+            RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 4>), grid, block, 0, rp, col, w, n, x, dim, empty_fill,   \
+                       post_scale, out);                                                                         \
+    } while (0)
+    if (vec && dim <= 256) RVX_AGG_VEC(1);
+    else if (vec && dim <= 512) RVX_AGG_VEC(2);
+    else if (vec && dim <= 768) RVX_AGG_VEC(3);
+    else if (vec && dim <= 1024) RVX_AGG_VEC(4);
     else
         RVX_LAUNCH(t, (k_aggregate_scalar<AGG, W>), grid, block, 0, rp, col, w, n, x, dim, empty_fill, post_scale, out);
+#undef RVX_AGG_VEC
 }
 
 }  // namespace
 
+// Overlapped launches (beside a GEMM) run a capped persistent grid with deeper
+// per-wave load queues: measured on the 1M x 768 layer, 1 block (4 waves) per
+// CU with 8 rows in flight gave the shortest layer (65.3 ms vs 75.3 ms for the
+// full grid, scripts/exp_pipeline.sh); a standalone gather uses the full grid.
+int g_agg_overlap_cap = env_int("RVX_AGG_BLOCKS_PER_CU", 1);
+int g_agg_overlap_unroll = env_int("RVX_AGG_UNROLL", 8);
+
 void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
-                    int agg, int empty_fill, int post_scale, float* out, const char* tag) {
+                    int agg, int empty_fill, int post_scale, float* out, const char* tag, bool overlapped) {
     if (n <= 0) return;
+    const int cap = overlapped ? g_agg_overlap_cap : 0;
+    const bool deep = overlapped && g_agg_overlap_unroll >= 8;
     RVX_REQUIRE(n / ROWS_PER_BLOCK < ((int64_t)1 << 31), RVX_ERR_INVALID_SHAPE, "graph too large for one launch");
     const char* t = tag ? tag : "aggregate";
     const bool W = w != nullptr;
     switch (agg) {
-        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out)
-                        : launch_agg<AGG_SUM, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out); break;
-        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out)
-                         : launch_agg<AGG_MEAN, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out); break;
-        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out)
-                        : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out); break;
+        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep)
+                        : launch_agg<AGG_SUM, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep); break;
+        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep)
+                         : launch_agg<AGG_MEAN, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep); break;
+        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep)
+                        : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep); break;
         default: fail(RVX_ERR_INVALID_PARAMETER, "unknown aggregator");
     }
 }

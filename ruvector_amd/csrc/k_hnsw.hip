@@ -35,8 +35,9 @@ struct SearchArgs {
     const float* x; const float* xnorm; int d;
     const float* q; const float* qnorm; int64_t nq;
     int k, ef;
-    unsigned long long* visited;  // [nslots][VCAP] {query tag, node+1}, zeroed per launch
+    unsigned long long* visited;  // [nslots][vcap] {query tag, node+1}, zeroed per launch
     int nslots;
+    unsigned vcap;
     float* out_d; int64_t* out_i; int32_t* out_n;  // [nq][k]
     int* status;       // set to 1 on candidate overflow
 };
@@ -54,7 +55,8 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
     float* cd = reinterpret_cast<float*>(ri + ef + 1);          // C dist [ccap]
     int* ci = reinterpret_cast<int*>(cd + ccap);                // C id
 
-    unsigned long long* vis = a.visited + (int64_t)blockIdx.x * VCAP;
+    unsigned long long* vis = a.visited + (int64_t)blockIdx.x * a.vcap;
+    const unsigned vmask = a.vcap - 1;
 
     for (int64_t qi = blockIdx.x; qi < a.nq; qi += a.nslots) {
         const unsigned long long qtag = (unsigned long long)(qi + 1) << 32;
@@ -107,7 +109,7 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
             const float d0 = dist_of(pivot);
             if (lane == 0) {
                 rd[0] = d0; ri[0] = pivot; cd[0] = d0; ci[0] = pivot;
-                visit_claim(vis, qtag, pivot);
+                visit_claim(vis, vmask, qtag, pivot);
             }
             rs = 1; cs = 1;
             __threadfence_block();
@@ -125,7 +127,7 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
                 bool fresh = false;
                 if (p < e) {
                     nid = a.g.col0[p];
-                    fresh = visit_claim(vis, qtag, nid);
+                    fresh = visit_claim(vis, vmask, qtag, nid);
                 }
                 float dd = INFINITY;
                 if (fresh) dd = dist_of(nid);
@@ -190,12 +192,14 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     if (nq <= 0) return;
     RVX_REQUIRE(ef >= 1 && ef <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER,
                 "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
-    const int nslots = (int)std::min<int64_t>(nq, 8192);
-    auto* vis = (unsigned long long*)scratch_bytes("hnsw_visited", (int64_t)nslots * VCAP * 8);
+    const unsigned vcap = visited_capacity(ef);
+    const int64_t mem_slots = std::max<int64_t>(1024, ((int64_t)4 << 30) / ((int64_t)vcap * 8));
+    const int nslots = (int)std::min<int64_t>(std::min<int64_t>(nq, 8192), mem_slots);
+    auto* vis = (unsigned long long*)scratch_bytes("hnsw_visited", (int64_t)nslots * vcap * 8);
     int* status = (int*)scratch_bytes("hnsw_status", 256);
-    RVX_HIP(hipMemsetAsync(vis, 0, (size_t)nslots * VCAP * 8, stream()));
+    RVX_HIP(hipMemsetAsync(vis, 0, (size_t)nslots * vcap * 8, stream()));
     RVX_HIP(hipMemsetAsync(status, 0, 4, stream()));
-    SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, nslots, out_d, out_i, out_n, status};
+    SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, nslots, vcap, out_d, out_i, out_n, status};
     const size_t lds = hnsw_search_lds(d, ef);
     RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");
     static bool attr = false;

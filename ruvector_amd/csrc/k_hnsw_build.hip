@@ -41,7 +41,7 @@ struct BuildArgs {
     int entry; int entry_level;
     unsigned nonempty_mask;  // bit l: some inserted point has level exactly l (points_by_layer[l])
     int ef_c;
-    unsigned long long* visited; int nslots;
+    unsigned long long* visited; int nslots; unsigned vcap;
     int* rev_head; int* rev_next; int* rev_key; float* rev_d; int* rev_src;  // reverse-edge chains
     int rev_cap;  // records per batch point
     int* status;
@@ -68,13 +68,13 @@ __device__ __forceinline__ int list_key(const BuildGraph& G, int p, int l) {  //
 // search_layer (hnsw.rs:913-1055) at layer l from ep; R left ascending in (rd, ri), returns |R|.
 template <int METRIC>
 __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn, int ep, float d_ep, int ef, int l,
-                                  unsigned long long* vis, unsigned long long tag, float* rd, int* ri, float* cd,
+                                  unsigned long long* vis, unsigned vmask, unsigned long long tag, float* rd, int* ri, float* cd,
                                   int* ci, int ccap, int lane, bool& overflow) {
     if (!((a.nonempty_mask >> l) & 1u)) return 0;  // points_by_layer[layer].is_empty()
     int rs = 1, cs = 1;
     if (lane == 0) {
         rd[0] = d_ep; ri[0] = ep; cd[0] = d_ep; ci[0] = ep;
-        visit_claim(vis, tag, ep);
+        visit_claim(vis, vmask, tag, ep);
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
@@ -92,7 +92,7 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
             bool fresh = false;
             if (p < cnt) {
                 nid = nbi[p];
-                fresh = visit_claim(vis, tag, nid);
+                fresh = visit_claim(vis, vmask, tag, nid);
             }
             float dd = INFINITY;
             if (fresh)
@@ -148,7 +148,8 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
     int* ci = reinterpret_cast<int*>(cd + ccap);
     float* sd = reinterpret_cast<float*>(ci + ccap);  // selected [64]
     int* si = reinterpret_cast<int*>(sd + 64);
-    unsigned long long* vis = a.visited + (int64_t)blockIdx.x * VCAP;
+    unsigned long long* vis = a.visited + (int64_t)blockIdx.x * a.vcap;
+    const unsigned vmask = a.vcap - 1;
     unsigned epoch = 0;
     bool overflow = false;
 
@@ -168,14 +169,14 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
         // 1. greedy descent, ef = 1 (hnsw.rs:1105-1146)
         for (int l = a.entry_level; l >= lev + 1; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
-            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, 1, l, vis, tag, rd, ri, cd, ci, ccap, lane,
+            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, 1, l, vis, vmask, tag, rd, ri, cd, ci, ccap, lane,
                                                       overflow);
             if (rs > 0 && rd[0] < d_ep) { ep = ri[0]; d_ep = rd[0]; }
         }
         // 2. layers lev .. 0 (hnsw.rs:1149-1196)
         for (int l = lev; l >= 0; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
-            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, ef, l, vis, tag, rd, ri, cd, ci, ccap, lane,
+            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, ef, l, vis, vmask, tag, rd, ri, cd, ci, ccap, lane,
                                                       overflow);
             if (rs == 0) continue;
             const int nb_conn = l == 0 ? 2 * a.G.M : a.G.M;
@@ -314,13 +315,16 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     if (batch_n <= 0) return;
     RVX_REQUIRE(G.C0 <= 64 && G.M <= 32, RVX_ERR_UNSUPPORTED, "GPU HNSW build supports m <= 32");
     RVX_REQUIRE(ef_c >= 1 && ef_c <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER, "ef_construction out of range");
-    const int nslots = std::min(batch_n, 8192);
+    const unsigned vcap = visited_capacity(ef_c);
+    const int nslots = (int)std::min<int64_t>(std::min(batch_n, 8192),
+                                              std::max<int64_t>(1024, ((int64_t)4 << 30) / ((int64_t)vcap * 8)));
     const int rev_cap = G.C0 + G.M * G.max_layer;
     BuildArgs a{};
     a.G = G; a.x = x; a.xnorm = xnorm; a.d = d;
     a.batch_begin = batch_begin; a.batch_n = batch_n; a.entry = entry; a.entry_level = entry_level;
     a.nonempty_mask = nonempty_mask; a.ef_c = ef_c;
-    a.visited = (unsigned long long*)scratch_bytes("build_visited", (int64_t)nslots * VCAP * 8);
+    a.vcap = vcap;
+    a.visited = (unsigned long long*)scratch_bytes("build_visited", (int64_t)nslots * vcap * 8);
     const int64_t nrec = (int64_t)batch_n * rev_cap;
     a.rev_next = (int*)scratch_bytes("build_rev_next", nrec * 4);
     a.rev_key = (int*)scratch_bytes("build_rev_key", nrec * 4);
@@ -330,7 +334,7 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     a.rev_cap = rev_cap;
     a.nslots = nslots;
     a.status = (int*)scratch_bytes("build_status", 256);
-    RVX_HIP(hipMemsetAsync(a.visited, 0, (size_t)nslots * VCAP * 8, stream()));
+    RVX_HIP(hipMemsetAsync(a.visited, 0, (size_t)nslots * vcap * 8, stream()));
     RVX_HIP(hipMemsetAsync(a.status, 0, 4, stream()));
     const size_t lds = build_lds_bytes(d, ef_c);
     RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");

@@ -39,6 +39,7 @@ enum { AGG_SUM = 0, AGG_MEAN = 1, AGG_MAX = 2 };
 // out[i] = agg over CSR row i of (w_e * x[col_e]) ; empty row -> `empty_fill`
 // (0 = zeros, 1 = copy x[i], 2 = -inf for max). post_scale: 0 none, 1 = ×1/sqrt(deg) (GCN).
 void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, int64_t n, const float* x,
-                    int dim, int agg, int empty_fill, int post_scale, float* out, const char* tag);
+                    int dim, int agg, int empty_fill, int post_scale, float* out, const char* tag,
+                    bool overlapped = false);  // true: runs beside a GEMM (capped grid)
 
 }  // namespace rvx

@@ -28,6 +28,8 @@ static Device& device_for(int id) {
     auto d = std::make_unique<Device>();
     d->id = id;
     RVX_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    RVX_HIP(hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking));
+    RVX_HIP(hipStreamCreateWithFlags(&d->xfer, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     RVX_HIP(hipGetDeviceProperties(&prop, id));
     d->num_cus = prop.multiProcessorCount;
@@ -45,8 +47,23 @@ Device& device() {
     if (hipGetDevice(&cur) != hipSuccess || cur != d.id) RVX_HIP(hipSetDevice(d.id));
     return d;
 }
-hipStream_t stream() { return device().stream; }
-void sync() { RVX_HIP(hipStreamSynchronize(stream())); }
+static thread_local hipStream_t g_stream_override = nullptr;
+hipStream_t stream() {
+    Device& d = device();
+    return g_stream_override ? g_stream_override : d.stream;
+}
+void sync() { RVX_HIP(hipStreamSynchronize(device().stream)); }
+hipEvent_t* pipeline_events(int count) {
+    Device& d = device();
+    while ((int)d.pipe_events.size() < count) {
+        hipEvent_t e;
+        RVX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        d.pipe_events.push_back(e);
+    }
+    return d.pipe_events.data();
+}
+StreamScope::StreamScope(hipStream_t s) : prev(g_stream_override) { g_stream_override = s; }
+StreamScope::~StreamScope() { g_stream_override = prev; }
 
 DevMem::DevMem(int64_t b) { reset(b); }
 DevMem::~DevMem() {

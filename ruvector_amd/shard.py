@@ -73,6 +73,38 @@ class RcclComm:
             pass
 
 
+PIPE_CHUNKS = 8          # RVX_SAGE_CHUNKS default (api_graph.cpp sage_chunks_for)
+PIPE_MIN_ROWS = 16384    # rows per chunk below which a layer is not chunked
+
+
+def chunk_count(n_rows: int, chunks: int = PIPE_CHUNKS) -> int:
+    """Row chunks of one layer pipeline (mirror of sage_chunks_for)."""
+    return chunks if n_rows >= chunks * PIPE_MIN_ROWS else 1
+
+
+def chunk_step(n_rows: int, chunks: int) -> int:
+    """Rows per chunk, a multiple of the GEMM's 128-row tile (mirror of chunk_step)."""
+    return (-(-n_rows // chunks) + 127) // 128 * 128
+
+
+def exchange_rounds(offsets: Sequence[int]) -> List[List[Tuple[int, int]]]:
+    """The p2p rounds of rvx_sage_forward_exchange: every rank uses the chunk
+    count of the largest shard, and in round c rank p ships its rows
+    [r0, r0+rows) (possibly empty) to every peer. Returns rounds[c][p]."""
+    world = len(offsets) - 1
+    sizes = [offsets[p + 1] - offsets[p] for p in range(world)]
+    chunks = chunk_count(max(sizes))
+    rounds = []
+    for c in range(chunks):
+        rr = []
+        for p in range(world):
+            st = chunk_step(sizes[p], chunks)
+            b = min(sizes[p], c * st)
+            rr.append((offsets[p] + b, min(st, sizes[p] - b)))
+        rounds.append(rr)
+    return rounds
+
+
 def merge_topk(parts: Sequence[Tuple[np.ndarray, np.ndarray]], k: int) -> Tuple[np.ndarray, np.ndarray]:
     """ShardedHyperbolicHnsw::search merge (crates/ruvector-hyperbolic-hnsw/src/shard.rs:354-373):
     concatenate per-shard (global id, distance) lists, sort by distance (ties by id), truncate k."""

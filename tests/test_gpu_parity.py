@@ -210,6 +210,34 @@ def test_graphsage_matches_oracle(in_f, out_f, n, deg):
         assert_close(y, ref)
 
 
+def test_graphsage_chunked_pipeline_and_exchange_entry():
+    """n >= 8*16384 rows runs the two-stream row-chunk pipeline (api_graph.cpp
+    sage_forward_dev); rvx_sage_forward_exchange at world 1 writes the same rows."""
+    import ctypes
+    n, d, deg = 140_000, 64, 8
+    x = rv.Buffer(n * d * 4)
+    x.fill_uniform(n * d, 21, -1.0, 1.0)
+    g = rv.Graph.random(n, deg, 22)
+    layer = rv.GraphSAGELayer(d, d, num_samples=deg)
+    y = rv.Buffer(n * d * 4)
+    layer.forward_device(x, g, y)
+    y_full = rv.Buffer(n * d * 4)
+    off = np.array([0, n], np.int64)
+    rv._lib.call("rvx_sage_forward_exchange", layer._h, g.handle, x.handle, y_full.handle,
+                 off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None, 1)
+    got = y.download(np.float32, (n, d))
+    assert np.array_equal(got, y_full.download(np.float32, (n, d)))
+    xs = x.download(np.float32, (n, d))
+    rp, col = O.random_csr(n, deg, 22)
+    wn, ws = O.sage_init(d, d, 0), O.sage_init(d, d, 1000)
+    for r0 in (0, 17_536 - 1500, n - 3000):  # first chunk, across the chunk-0/1 seam, the ragged tail
+        ref = O.sage_forward(xs, rp, col, wn, ws, rows=(r0, 3000))
+        assert_close(got[r0:r0 + 3000], ref)
+    with pytest.raises(rv.RvxError):  # x and y may not alias
+        rv._lib.call("rvx_sage_forward_exchange", layer._h, g.handle, x.handle, x.handle,
+                     off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None, 1)
+
+
 def test_graphsage_reference_unit_cases():
     layer = rv.GraphSAGELayer(2, 2, 2)
     y = layer.forward([[1.0, 2.0], [3.0, 4.0], [5.0, 6.0]], [(0, 1), (1, 2), (2, 0)])

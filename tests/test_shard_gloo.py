@@ -96,6 +96,68 @@ def test_node_range_shards_match_single_process():
     assert res == [(0, True, True), (1, True, True)]
 
 
+def _exchange_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    from ruvector_amd.shard import exchange_rounds
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # ragged shards, one far below the pipelining threshold
+        sizes = [200_000, 150_001, 5_000][:world]
+        offsets = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        n, d = int(offsets[-1]), 3
+        full = np.arange(n * d, dtype=np.float32).reshape(n, d)
+        table = np.zeros_like(full)
+        b, e = offsets[rank], offsets[rank + 1]
+        rounds = exchange_rounds(offsets)
+        mine = []
+        for rr in rounds:
+            r0, rows = rr[rank]
+            mine.append((r0, rows))
+            table[r0:r0 + rows] = full[r0:r0 + rows]  # "compute" of this chunk
+            reqs = []
+            for k in range(1, world):  # same rotated peer order as comm_exchange_rows
+                p = (rank + k) % world
+                if rows > 0:
+                    reqs.append(dist.isend(torch.from_numpy(table[r0:r0 + rows].copy()), p))
+                pr0, prows = rr[p]
+                if prows > 0:
+                    buf = torch.zeros((prows, d), dtype=torch.float32)
+                    reqs.append((dist.irecv(buf, p), pr0, buf))
+            for r in reqs:
+                if isinstance(r, tuple):
+                    r[0].wait()
+                    table[r[1]:r[1] + r[2].shape[0]] = r[2].numpy()
+                else:
+                    r.wait()
+        covered = sum(rows for _, rows in mine) == e - b and mine[0][0] == b and all(
+            mine[i][0] + mine[i][1] == mine[i + 1][0] for i in range(len(mine) - 1) if mine[i + 1][1] > 0)
+        q.put((rank, bool(np.array_equal(table, full)), bool(covered), len(rounds)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_chunked_halo_exchange_protocol(world):
+    """rvx_sage_forward_exchange's round plan (mirrored by shard.exchange_rounds)
+    reconstructs the full table on every rank with ragged shards."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    assert res == [(r, True, True, 8) for r in range(world)]
+
+
 def test_shard_plan_rows_cover_and_owner():
     sys.path.insert(0, ROOT)
     from ruvector_amd.shard import ShardPlan
