@@ -112,6 +112,7 @@ struct rvx_sage_layer {
     int in = 0, out = 0, num_samples = 0, aggregator = 0, normalize = 1;
     std::vector<float> wn, ws;  // host [in][out]
     DevMem wn_t, ws_t;          // device [out][in]
+    DevMem wn_x3, ws_x3;        // exact 3-way bf16 splits of wn_t / ws_t (split-bf16 MFMA GEMM)
 };
 
 struct rvx_gcn_layer {
@@ -170,8 +171,10 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         } else {
             aggregate_rows(g->row_ptr, g->col, nullptr, n, x, l->in, a, 0, 0, agg, "sage_aggregate");
         }
-        GemmOperand s0{agg + r0 * l->in, l->in, l->wn_t.as<float>(), l->in, l->in};
-        GemmOperand s1{x + (row_offset + r0) * l->in, l->in, l->ws_t.as<float>(), l->in, l->in};
+        const int64_t plane = (int64_t)l->in * l->out;
+        GemmOperand s0{agg + r0 * l->in, l->in, l->wn_t.as<float>(), l->in, l->in, l->wn_x3.as<uint16_t>(), plane};
+        GemmOperand s1{x + (row_offset + r0) * l->in, l->in, l->ws_t.as<float>(), l->in, l->in,
+                       l->ws_x3.as<uint16_t>(), plane};
         gemm_nt(rows, l->out, s0, &s1, ep, y + r0 * l->out, l->out, "sage_gemm");
         if (l->normalize) normalize_rows(y + r0 * l->out, rows, l->out, true, "sage_normalize");
         if (hook) hook(c, r0, rows);
@@ -327,6 +330,11 @@ rvx_status rvx_sage_layer_create(int32_t in, int32_t out_f, int32_t num_samples,
         }
         upload_transposed(l->wn_t, l->wn, in, out_f);
         upload_transposed(l->ws_t, l->ws, in, out_f);
+        l->wn_x3.reset((int64_t)in * out_f * 6);
+        l->ws_x3.reset((int64_t)in * out_f * 6);
+        split_x3(l->wn_t.as<float>(), (int64_t)in * out_f, l->wn_x3.as<uint16_t>());
+        split_x3(l->ws_t.as<float>(), (int64_t)in * out_f, l->ws_x3.as<uint16_t>());
+        sync();
         *out = l.release();
     });
 }

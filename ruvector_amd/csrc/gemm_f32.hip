@@ -36,6 +36,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 struct GemmArgs {
     const float* A0; const float* B0; int64_t lda0, ldb0; int K0;
     const float* A1; const float* B1; int64_t lda1, ldb1; int K1;
+    const uint16_t* B0x3; const uint16_t* B1x3; int64_t B0x3_plane, B1x3_plane;  // split-bf16 weight planes
     const float* bias0; const float* bias1;
     const float* addend; int64_t ld_add;
     float* C; int64_t ldc;
@@ -55,7 +56,7 @@ __device__ __forceinline__ float epi_apply(int epi, float v) {
     return v;
 }
 
-template <bool DUAL>
+template <bool DUAL, int DEPTH>
 __global__ __launch_bounds__(256, 2) void gemm_nt_mfma(GemmArgs g, int epi) {
     __shared__ __attribute__((aligned(16))) float smem[2 * 2 * TILE_FLOATS];  // [stage][A|B]
 
@@ -80,9 +81,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_mfma(GemmArgs g, int epi) {
     const int nk1 = DUAL ? (g.K1 + BK - 1) / BK : 0;
     const int nk = nk0 + nk1;
 
-    // Global->register staging: 4 float4 of A and 4 of B per thread per K tile.
-    float4 ra[4], rb[4];
-    auto load_tile = [&](int kt) {
+    // Global->register staging: 4 float4 of A and 4 of B per thread per K tile,
+    // DEPTH register sets: tile kt+DEPTH is requested while tile kt is in the
+    // MFMAs, so a load has DEPTH-1 full K tiles of compute (plus the current
+    // one) to land — what keeps the GEMM fed when a concurrent gather has
+    // HBM latency high.
+    float4 ra[DEPTH][4], rb[DEPTH][4];
+    auto load_tile = [&](int kt, float4 (&xa)[4], float4 (&xb)[4]) {
         const float* A; const float* B; int64_t lda, ldb; int K, k0;
         if (!DUAL || kt < nk0) { A = g.A0; B = g.B0; lda = g.lda0; ldb = g.ldb0; K = g.K0; k0 = kt * BK; }
         else { A = g.A1; B = g.B1; lda = g.lda1; ldb = g.ldb1; K = g.K1; k0 = (kt - nk0) * BK; }
@@ -96,18 +101,18 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_mfma(GemmArgs g, int epi) {
             float4 za = make_float4(0.f, 0.f, 0.f, 0.f), zb = za;
             if (am < g.M && k < K) za = *reinterpret_cast<const float4*>(A + am * lda + k);
             if (bn < g.N && k < K) zb = *reinterpret_cast<const float4*>(B + (int64_t)bn * ldb + k);
-            ra[i] = za; rb[i] = zb;
+            xa[i] = za; xb[i] = zb;
         }
     };
-    auto store_tile = [&](int stage) {
+    auto store_tile = [&](int stage, const float4 (&xa)[4], const float4 (&xb)[4]) {
         float* As = smem + stage * 2 * TILE_FLOATS;
         float* Bs = As + TILE_FLOATS;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int f = tid + 256 * i;
             const int row = f >> 3, c = (f & 7) * 4;
-            *reinterpret_cast<float4*>(As + row * LDS_ROW + c) = ra[i];
-            *reinterpret_cast<float4*>(Bs + row * LDS_ROW + c) = rb[i];
+            *reinterpret_cast<float4*>(As + row * LDS_ROW + c) = xa[i];
+            *reinterpret_cast<float4*>(Bs + row * LDS_ROW + c) = xb[i];
         }
     };
 
@@ -119,13 +124,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_mfma(GemmArgs g, int epi) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
-    load_tile(0);
-    store_tile(0);
-    __syncthreads();
-
-    for (int kt = 0; kt < nk; ++kt) {
-        const int stage = kt & 1;
-        if (kt + 1 < nk) load_tile(kt + 1);
+    auto compute = [&](int stage) {
         const float* As = smem + stage * 2 * TILE_FLOATS;
         const float* Bs = As + TILE_FLOATS;
 #pragma unroll
@@ -156,8 +155,38 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_mfma(GemmArgs g, int epi) {
                 }
             }
         }
-        if (kt + 1 < nk) store_tile(stage ^ 1);
+    };
+
+    if (DEPTH == 1) {
+        load_tile(0, ra[0], rb[0]);
+        store_tile(0, ra[0], rb[0]);
         __syncthreads();
+        for (int kt = 0; kt < nk; ++kt) {
+            const int stage = kt & 1;
+            if (kt + 1 < nk) load_tile(kt + 1, ra[0], rb[0]);
+            compute(stage);
+            if (kt + 1 < nk) store_tile(stage ^ 1, ra[0], rb[0]);
+            __syncthreads();
+        }
+    } else {
+        // two register sets, loop unrolled by two so the set index is static
+        load_tile(0, ra[0], rb[0]);
+        store_tile(0, ra[0], rb[0]);
+        if (nk > 1) load_tile(1, ra[1 % DEPTH], rb[1 % DEPTH]);
+        __syncthreads();
+        for (int kt = 0; kt < nk; kt += 2) {
+            // even tile kt: compute stage 0; request tile kt+2 into set 0; publish tile kt+1 (set 1)
+            if (kt + 2 < nk) load_tile(kt + 2, ra[0], rb[0]);
+            compute(0);
+            if (kt + 1 < nk) store_tile(1, ra[1 % DEPTH], rb[1 % DEPTH]);
+            __syncthreads();
+            if (kt + 1 >= nk) break;
+            // odd tile kt+1: compute stage 1; request tile kt+3 into set 1; publish tile kt+2 (set 0)
+            if (kt + 3 < nk) load_tile(kt + 3, ra[1 % DEPTH], rb[1 % DEPTH]);
+            compute(1);
+            if (kt + 2 < nk) store_tile(0, ra[0], rb[0]);
+            __syncthreads();
+        }
     }
 
     // Epilogue. 32x32 C/D map: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
@@ -183,6 +212,211 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_mfma(GemmArgs g, int epi) {
             }
         }
     }
+}
+
+
+// ---------------------------------------------------------------------------
+// Split-bf16 MFMA GEMM ("x3"). Every f32 operand is split exactly into three
+// bf16 parts, a = a1 + a2 + a3 (truncation: a1 keeps the top 8 significand
+// bits, a2 the next 8 of the exact remainder, a3 the rest; the sum is exact),
+// and the six partial products whose weight is >= 2^-16 —
+// a1b1, a1b2, a2b1, a1b3, a3b1, a2b2 — run on v_mfma_f32_32x32x16_bf16 with
+// f32 accumulation. Each bf16 x bf16 product is exact in f32; the dropped
+// terms (a2b3, a3b2, a3b3) are below 2^-23 |a b|, i.e. f32 rounding level, so
+// the result is an f32 GEMM to within reordering error, at 6/16 of the
+// FP32-MFMA cycle cost (bf16 MFMA is 16x the f32 rate on gfx950).
+//
+// Tile 128x128x32, 256 threads = 4 waves as 2(M) x 2(N), each wave 64x64 =
+// 2x2 32x32 accumulators, two blocks per CU (8 waves). A is staged as f32
+// and split into its three bf16 parts per fragment read (VALU work that
+// issues in the MFMAs' shadow); B comes pre-split from HBM (weights are split
+// once at upload). No row padding: 16-B chunks are XOR-swizzled so the
+// per-lane 16-B fragment reads of 16 consecutive rows hit 16 distinct bank
+// groups (A rows 128 B: chunk ^ (row>>1)&7; B plane rows 64 B: chunk ^
+// (row>>2)&3). Double-buffered, 2 x 40 KB, register prefetch of tile k+1.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int XBM = 128, XBN = 128;
+constexpr int XA_TILE = XBM * 128;                  // f32 A tile bytes
+constexpr int XB_PLANE = XBN * 64;                  // one bf16 B plane tile bytes
+constexpr int X_STAGE = XA_TILE + 3 * XB_PLANE;     // 40,960 B
+constexpr int X_LDS = 2 * X_STAGE;                  // 81,920 B -> 2 blocks / CU
+
+__device__ __forceinline__ int xa_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int xb_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+// exact three-way bf16 split of 8 floats into packed bf16x8 parts
+__device__ __forceinline__ void split8(const float4& lo, const float4& hi, bf16x8& p1, bf16x8& p2, bf16x8& p3) {
+    const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    u32x4 w1, w2, w3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float a0 = v[2 * j], a1 = v[2 * j + 1];
+        const unsigned h0 = __float_as_uint(a0) & 0xFFFF0000u, h1 = __float_as_uint(a1) & 0xFFFF0000u;
+        const float r0 = a0 - __uint_as_float(h0), r1 = a1 - __uint_as_float(h1);
+        const unsigned m0 = __float_as_uint(r0) & 0xFFFF0000u, m1 = __float_as_uint(r1) & 0xFFFF0000u;
+        // the remainder r - m has at most 8 significant bits: its top half is exact
+        const unsigned l0 = __float_as_uint(r0 - __uint_as_float(m0)), l1 = __float_as_uint(r1 - __uint_as_float(m1));
+        w1[j] = __builtin_amdgcn_perm(h1, h0, 0x07060302u);
+        w2[j] = __builtin_amdgcn_perm(m1, m0, 0x07060302u);
+        w3[j] = __builtin_amdgcn_perm(l1, l0, 0x07060302u);
+    }
+    p1 = __builtin_bit_cast(bf16x8, w1);
+    p2 = __builtin_bit_cast(bf16x8, w2);
+    p3 = __builtin_bit_cast(bf16x8, w3);
+}
+
+template <bool DUAL>
+__global__ __launch_bounds__(256, 2) void gemm_nt_x3(GemmArgs g, int epi) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
+
+    const int64_t nwg = g.nblocks;
+    const int64_t bid = blockIdx.x;
+    const int64_t xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    const int64_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    const int64_t tm = wgid / g.tiles_n;
+    const int tn = (int)(wgid % g.tiles_n);
+    const int64_t m0 = tm * XBM;
+    const int n0 = tn * XBN;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int lr = lane & 31, lh = lane >> 5;
+
+    const int nk0 = (g.K0 + 31) / 32;
+    const int nk1 = DUAL ? (g.K1 + 31) / 32 : 0;
+    const int nk = nk0 + nk1;
+
+    float4 ra[4];
+    u32x4 rb[3][2];
+    auto load_tile = [&](int kt) {
+        const float* A; const uint16_t* B; int64_t lda, ldb, bpl; int K, k0;
+        if (!DUAL || kt < nk0) { A = g.A0; B = g.B0x3; lda = g.lda0; ldb = g.ldb0; bpl = g.B0x3_plane; K = g.K0; k0 = kt * 32; }
+        else { A = g.A1; B = g.B1x3; lda = g.lda1; ldb = g.ldb1; bpl = g.B1x3_plane; K = g.K1; k0 = (kt - nk0) * 32; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int f = tid + 256 * i;
+            const int row = f >> 3, k = k0 + (f & 7) * 4;
+            const int64_t am = m0 + row;
+            ra[i] = (am < g.M && k < K) ? *reinterpret_cast<const float4*>(A + am * lda + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int f = tid + 256 * i;
+            const int brow = f >> 2, bk = k0 + (f & 3) * 8;
+            const bool bin = (n0 + brow < g.N) && (bk < K);
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                rb[p][i] = bin ? *reinterpret_cast<const u32x4*>(B + p * bpl + (int64_t)(n0 + brow) * ldb + bk)
+                               : u32x4{0, 0, 0, 0};
+        }
+    };
+    auto store_tile = [&](int stage) {
+        unsigned char* base = xsm + stage * X_STAGE;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int f = tid + 256 * i;
+            *reinterpret_cast<float4*>(base + xa_off(f >> 3, f & 7)) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int f = tid + 256 * i;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                *reinterpret_cast<u32x4*>(base + XA_TILE + p * XB_PLANE + xb_off(f >> 2, f & 3)) = rb[p][i];
+        }
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int stage = kt & 1;
+        if (kt + 1 < nk) load_tile(kt + 1);
+        const unsigned char* base = xsm + stage * X_STAGE;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8 af[2][3], bf[2][3];
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int off = xb_off(wn * 64 + ni * 32 + lr, 2 * s + lh);
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    bf[ni][p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(base + XA_TILE + p * XB_PLANE + off));
+            }
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) {
+                const int row = wm * 64 + mi * 32 + lr;
+                const int c = 4 * s + 2 * lh;  // k = 16s + 8lh .. +7 = chunks c, c+1
+                const float4 lo = *reinterpret_cast<const float4*>(base + xa_off(row, c));
+                const float4 hi = *reinterpret_cast<const float4*>(base + xa_off(row, c + 1));
+                split8(lo, hi, af[mi][0], af[mi][1], af[mi][2]);
+            }
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni) {
+                    f32x16 c = acc[mi][ni];
+                    // small terms first
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi][1], bf[ni][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi][2], bf[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi][0], bf[ni][2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi][1], bf[ni][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi][0], bf[ni][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mi][0], bf[ni][0], c, 0, 0, 0);
+                    acc[mi][ni] = c;
+                }
+        }
+        if (kt + 1 < nk) store_tile(stage ^ 1);
+        __syncthreads();
+    }
+
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+            const int col = n0 + wn * 64 + ni * 32 + lr;
+            if (col >= g.N) continue;
+            float b = 0.0f;
+            if (g.bias0) b = g.bias0[col];
+            if (g.bias1) b += g.bias1[col];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int64_t row = m0 + wm * 64 + mi * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+                if (row < g.M) {
+                    float v = acc[mi][ni][e];
+                    if (g.alpha != 1.0f) v *= g.alpha;
+                    if (g.bias0 || g.bias1) v += b;
+                    if (g.addend) v += g.addend[row * g.ld_add + col];
+                    g.C[row * g.ldc + col] = epi_apply(epi, v);
+                }
+            }
+        }
+    }
+}
+
+// Split a [rows][cols] f32 matrix into three bf16 planes (plane stride rows*cols).
+__global__ void k_split_x3(const float* __restrict__ src, int64_t n, uint16_t* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float a = src[i];
+    const unsigned h = __float_as_uint(a) & 0xFFFF0000u;
+    const float r = a - __uint_as_float(h);
+    const unsigned m = __float_as_uint(r) & 0xFFFF0000u;
+    const float s = r - __uint_as_float(m);
+    dst[i] = (uint16_t)(h >> 16);
+    dst[n + i] = (uint16_t)(m >> 16);
+    dst[2 * n + i] = (uint16_t)(__float_as_uint(s) >> 16);
 }
 
 // Correctness path for shapes the tiled kernel cannot take (K % 4 != 0 or
@@ -226,19 +460,49 @@ void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, con
     if (s1) fast = fast && (s1->K % 4 == 0) && (s1->lda % 4 == 0) && (s1->ldb % 4 == 0) && aligned16(s1->A) &&
                    aligned16(s1->B);
     const char* t = tag ? tag : "gemm_nt";
+    static const int x3_mode = env_int("RVX_GEMM_X3", 1);
+    bool x3 = fast && x3_mode && s0.Bx3 && (s0.K % 8 == 0) && (s0.ldb % 8 == 0);
+    if (s1) x3 = x3 && s1->Bx3 && (s1->K % 8 == 0) && (s1->ldb % 8 == 0);
+    if (x3) {
+        g.B0x3 = s0.Bx3; g.B0x3_plane = s0.Bx3_plane;
+        if (s1) { g.B1x3 = s1->Bx3; g.B1x3_plane = s1->Bx3_plane; }
+        g.tiles_n = (N + XBN - 1) / XBN;
+        const int64_t tiles_m = (M + XBM - 1) / XBM;
+        g.nblocks = tiles_m * g.tiles_n;
+        RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
+        static bool attr = false;
+        if (!attr) {
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3<true>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3<false>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
+            attr = true;
+        }
+        const dim3 grid((unsigned)g.nblocks), block(256);
+        if (s1) RVX_LAUNCH(t, gemm_nt_x3<true>, grid, block, X_LDS, g, epi);
+        else RVX_LAUNCH(t, gemm_nt_x3<false>, grid, block, X_LDS, g, epi);
+        return;
+    }
     if (fast) {
         g.tiles_n = (N + BN - 1) / BN;
         const int64_t tiles_m = (M + BM - 1) / BM;
         g.nblocks = tiles_m * g.tiles_n;
         RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
-        if (s1)
-            RVX_LAUNCH(t, gemm_nt_mfma<true>, dim3((unsigned)g.nblocks), dim3(256), 0, g, epi);
-        else
-            RVX_LAUNCH(t, gemm_nt_mfma<false>, dim3((unsigned)g.nblocks), dim3(256), 0, g, epi);
+        static const int depth = env_int("RVX_GEMM_DEPTH", 1);
+        const dim3 grid((unsigned)g.nblocks), block(256);
+        if (s1 && depth >= 2) RVX_LAUNCH(t, (gemm_nt_mfma<true, 2>), grid, block, 0, g, epi);
+        else if (s1) RVX_LAUNCH(t, (gemm_nt_mfma<true, 1>), grid, block, 0, g, epi);
+        else if (depth >= 2) RVX_LAUNCH(t, (gemm_nt_mfma<false, 2>), grid, block, 0, g, epi);
+        else RVX_LAUNCH(t, (gemm_nt_mfma<false, 1>), grid, block, 0, g, epi);
     } else {
         const int64_t total = M * (int64_t)N;
         RVX_LAUNCH(t, gemm_nt_simple, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, g, epi);
     }
 }
 
+}  // namespace rvx
+
+namespace rvx {
+void split_x3(const float* src, int64_t n, uint16_t* dst) {
+    if (n <= 0) return;
+    RVX_LAUNCH("split_x3", k_split_x3, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, src, n, dst);
+}
 }  // namespace rvx

@@ -31,9 +31,22 @@ __device__ __forceinline__ float4 agg_op(float4 a, float4 v) {
 }
 __device__ __forceinline__ float4 scale4(float4 v, float w) { return make_float4(v.x * w, v.y * w, v.z * w, v.w * w); }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+// Gathered rows are touched once per edge at random, so they never hit in L2
+// on a large table; NT loads keep them from evicting the working set of a
+// GEMM running beside the gather.
+template <bool NT>
+__device__ __forceinline__ float4 ld_row4(const float* p) {
+    if (NT) {
+        const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    }
+    return *reinterpret_cast<const float4*>(p);
+}
+
 // NV = float4 slots per lane (dim <= 256*NV; dim % 4 == 0); U = neighbour
 // rows in flight per wave (more when the grid is capped to few waves per CU).
-template <int NV, int AGG, bool W, int U = 4>
+template <int NV, int AGG, bool W, int U = 4, bool NT = false>
 __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
                                                       const float* __restrict__ wts, int64_t n,
                                                       const float* __restrict__ x, int dim, int empty_fill,
@@ -67,7 +80,7 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
                 const float* src = x + (int64_t)c * dim + 4 * lane;
 #pragma unroll
                 for (int j = 0; j < NV; ++j)
-                    v[u][j] = active[j] ? *reinterpret_cast<const float4*>(src + 256 * j) : make_float4(0, 0, 0, 0);
+                    v[u][j] = active[j] ? ld_row4<NT>(src + 256 * j) : make_float4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -84,7 +97,7 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
             if (W) wu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), t));
 #pragma unroll
             for (int j = 0; j < NV; ++j) {
-                float4 v = active[j] ? *reinterpret_cast<const float4*>(src + 256 * j) : make_float4(0, 0, 0, 0);
+                float4 v = active[j] ? ld_row4<NT>(src + 256 * j) : make_float4(0, 0, 0, 0);
                 acc[j] = agg_op<AGG>(acc[j], W ? scale4(v, wu) : v);
             }
         }
@@ -145,14 +158,17 @@ __global__ __launch_bounds__(256) void k_aggregate_scalar(const int64_t* rp, con
 
 template <int AGG, bool W>
 void launch_agg(const char* t, const int64_t* rp, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
-                int empty_fill, int post_scale, float* out, int cap_per_cu, bool deep) {
+                int empty_fill, int post_scale, float* out, int cap_per_cu, bool deep, bool nt) {
     int64_t blocks = (n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
     if (cap_per_cu > 0) blocks = std::min<int64_t>(blocks, (int64_t)cap_per_cu * device().num_cus);
     const dim3 grid((unsigned)blocks), block(256);
     const bool vec = (dim % 4 == 0) && (((uintptr_t)x & 15) == 0) && (((uintptr_t)out & 15) == 0);
 #define RVX_AGG_VEC(NV)                                                                                          \
     do {                                                                                                         \
-        if (deep)                                                                                                \
+        if (deep && nt)                                                                                        \
+            RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 8, true>), grid, block, 0, rp, col, w, n, x, dim,         \
+                       empty_fill, post_scale, out);                                                             \
+        else if (deep)                                                                                           \
             RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 8>), grid, block, 0, rp, col, w, n, x, dim, empty_fill,   \
                        post_scale, out);                                                                         \
         else                                                                                                     \
@@ -176,22 +192,24 @@ void launch_agg(const char* t, const int64_t* rp, const int32_t* col, const floa
 // full grid, scripts/exp_pipeline.sh); a standalone gather uses the full grid.
 int g_agg_overlap_cap = env_int("RVX_AGG_BLOCKS_PER_CU", 1);
 int g_agg_overlap_unroll = env_int("RVX_AGG_UNROLL", 8);
+int g_agg_nt = env_int("RVX_AGG_NT", 1);
 
 void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
                     int agg, int empty_fill, int post_scale, float* out, const char* tag, bool overlapped) {
     if (n <= 0) return;
     const int cap = overlapped ? g_agg_overlap_cap : 0;
     const bool deep = overlapped && g_agg_overlap_unroll >= 8;
+    const bool nt = overlapped && g_agg_nt;
     RVX_REQUIRE(n / ROWS_PER_BLOCK < ((int64_t)1 << 31), RVX_ERR_INVALID_SHAPE, "graph too large for one launch");
     const char* t = tag ? tag : "aggregate";
     const bool W = w != nullptr;
     switch (agg) {
-        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep)
-                        : launch_agg<AGG_SUM, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep); break;
-        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep)
-                         : launch_agg<AGG_MEAN, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep); break;
-        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep)
-                        : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep); break;
+        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt)
+                        : launch_agg<AGG_SUM, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt); break;
+        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt)
+                         : launch_agg<AGG_MEAN, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt); break;
+        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt)
+                        : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt); break;
         default: fail(RVX_ERR_INVALID_PARAMETER, "unknown aggregator");
     }
 }

@@ -11,6 +11,10 @@ struct GemmOperand {
     const float* A; int64_t lda;  // A [M][K]
     const float* B; int64_t ldb;  // B [N][K]  (C = A · B^T)
     int K;
+    // optional exact 3-way bf16 split of B (split_x3): planes of [N][ldb]
+    // uint16 at Bx3 + p*Bx3_plane; selects the split-bf16 MFMA kernel
+    const uint16_t* Bx3 = nullptr;
+    int64_t Bx3_plane = 0;
 };
 // Epilogue: C = epi(alpha * acc + bias0 + bias1 + addend[row][col])
 struct GemmEpilogue {
@@ -24,6 +28,9 @@ struct GemmEpilogue {
 // C[M][N] = epilogue(A0·B0^T [+ A1·B1^T])
 void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, const GemmEpilogue& ep, float* C,
              int64_t ldc, const char* tag);
+
+// dst[p*n + i] = bf16 part p of src[i] (exact split src = p0 + p1 + p2)
+void split_x3(const float* src, int64_t n, uint16_t* dst);
 
 // ---- data generators (k_data.hip) ---------------------------------------
 void fill_uniform(float* p, int64_t n, uint64_t seed, float lo, float hi);
