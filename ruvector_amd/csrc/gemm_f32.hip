@@ -405,6 +405,140 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x3(GemmArgs g, int epi) {
     }
 }
 
+// Same tile and MFMA schedule as gemm_nt_x3, but the stage fill is LDS-DMA
+// (global_load_lds_dwordx4): no register staging and no ds_write pass. One
+// wave-instruction writes 1 KiB lane-linear, so the XOR swizzle goes on the
+// per-lane SOURCE address: LDS slot p of row r receives global chunk
+// p ^ swz(r). Waves are 4(M) x 1(N) — each owns 32 rows x all 128 columns —
+// so every A fragment is split by exactly one wave. Requires K % 32 == 0 (no
+// tail tile: the DMA has no zero fill); rows past M / N are clamped to a
+// valid row and never stored.
+template <bool DUAL>
+__global__ __launch_bounds__(256, 2) void gemm_nt_x3g(GemmArgs g, int epi) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
+
+    const int64_t nwg = g.nblocks;
+    const int64_t bid = blockIdx.x;
+    const int64_t xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    const int64_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    const int64_t tm = wgid / g.tiles_n;
+    const int tn = (int)(wgid % g.tiles_n);
+    const int64_t m0 = tm * XBM;
+    const int n0 = tn * XBN;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 31, lh = lane >> 5;
+
+    const int nk0 = g.K0 / 32;
+    const int nk1 = DUAL ? g.K1 / 32 : 0;
+    const int nk = nk0 + nk1;
+
+    // per-lane source rows/chunks of this wave's DMA pieces (fixed over k)
+    // A: pieces 4*wave .. 4*wave+3, each 8 rows x 8 chunks of 16 B
+    int64_t a_row_off[4];
+    int a_chunk[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = 8 * (4 * wave + j) + (lane >> 3);
+        a_chunk[j] = (lane & 7) ^ ((row >> 1) & 7);
+        a_row_off[j] = std::min<int64_t>(m0 + row, g.M - 1);
+    }
+    // B: pieces 6*wave .. 6*wave+5 over 3 planes x 8 pieces, each 16 rows x 4 chunks
+    int b_plane[6], b_chunk[6];
+    int64_t b_row[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const int piece = 6 * wave + j;
+        const int row = 16 * (piece & 7) + (lane >> 2);
+        b_plane[j] = piece >> 3;
+        b_chunk[j] = (lane & 3) ^ ((row >> 2) & 3);
+        b_row[j] = std::min<int64_t>(n0 + row, (int64_t)g.N - 1);
+    }
+
+    auto fill = [&](int kt, int stage) {
+        const float* A; const uint16_t* B; int64_t lda, ldb, bpl; int k0;
+        if (!DUAL || kt < nk0) { A = g.A0; B = g.B0x3; lda = g.lda0; ldb = g.ldb0; bpl = g.B0x3_plane; k0 = kt * 32; }
+        else { A = g.A1; B = g.B1x3; lda = g.lda1; ldb = g.ldb1; bpl = g.B1x3_plane; k0 = (kt - nk0) * 32; }
+        unsigned char* base = xsm + stage * X_STAGE;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(A + a_row_off[j] * lda + k0 + 4 * a_chunk[j]),
+                                             (__attribute__((address_space(3))) void*)(base + (4 * wave + j) * 1024),
+                                             16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const int piece = 6 * wave + j;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(B + b_plane[j] * bpl + b_row[j] * ldb + k0 + 8 * b_chunk[j]),
+                (__attribute__((address_space(3))) void*)(base + XA_TILE + (piece >> 3) * XB_PLANE + (piece & 7) * 1024),
+                16, 0, 0);
+        }
+    };
+
+    f32x16 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.0f;
+
+    fill(0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int stage = kt & 1;
+        if (kt + 1 < nk) fill(kt + 1, stage ^ 1);
+        const unsigned char* base = xsm + stage * X_STAGE;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8 af[3];
+            {
+                const int row = wave * 32 + lr;
+                const int c = 4 * s + 2 * lh;
+                const float4 lo = *reinterpret_cast<const float4*>(base + xa_off(row, c));
+                const float4 hi = *reinterpret_cast<const float4*>(base + xa_off(row, c + 1));
+                split8(lo, hi, af[0], af[1], af[2]);
+            }
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int off = xb_off(ni * 32 + lr, 2 * s + lh);
+                bf16x8 bf[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    bf[p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(base + XA_TILE + p * XB_PLANE + off));
+                f32x16 c = acc[ni];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bf[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bf[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bf[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[0], c, 0, 0, 0);
+                acc[ni] = c;
+            }
+        }
+        __syncthreads();  // retires the DMA of tile kt+1 and frees stage for tile kt+2
+    }
+
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+        const int col = n0 + ni * 32 + lr;
+        if (col >= g.N) continue;
+        float b = 0.0f;
+        if (g.bias0) b = g.bias0[col];
+        if (g.bias1) b += g.bias1[col];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int64_t row = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+            if (row < g.M) {
+                float v = acc[ni][e];
+                if (g.alpha != 1.0f) v *= g.alpha;
+                if (g.bias0 || g.bias1) v += b;
+                if (g.addend) v += g.addend[row * g.ld_add + col];
+                g.C[row * g.ldc + col] = epi_apply(epi, v);
+            }
+        }
+    }
+}
+
 // Split a [rows][cols] f32 matrix into three bf16 planes (plane stride rows*cols).
 __global__ void k_split_x3(const float* __restrict__ src, int64_t n, uint16_t* __restrict__ dst) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -474,10 +608,16 @@ void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, con
         if (!attr) {
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3<true>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3<false>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<true>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<false>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
             attr = true;
         }
         const dim3 grid((unsigned)g.nblocks), block(256);
-        if (s1) RVX_LAUNCH(t, gemm_nt_x3<true>, grid, block, X_LDS, g, epi);
+        static const int use_dma = env_int("RVX_GEMM_DMA", 1);
+        const bool dma = use_dma && s0.K % 32 == 0 && (!s1 || s1->K % 32 == 0);
+        if (dma && s1) RVX_LAUNCH(t, gemm_nt_x3g<true>, grid, block, X_LDS, g, epi);
+        else if (dma) RVX_LAUNCH(t, gemm_nt_x3g<false>, grid, block, X_LDS, g, epi);
+        else if (s1) RVX_LAUNCH(t, gemm_nt_x3<true>, grid, block, X_LDS, g, epi);
         else RVX_LAUNCH(t, gemm_nt_x3<false>, grid, block, X_LDS, g, epi);
         return;
     }

@@ -12,7 +12,7 @@ for cfg in "${LIST[@]}"; do
   tag="c$1_cap$2_u$3_d$4"
   tag="${tag}_nt${RVX_AGG_NT:-1}_x3${RVX_GEMM_X3:-1}"
   RVX_SAGE_CHUNKS=$1 RVX_AGG_BLOCKS_PER_CU=$2 RVX_AGG_UNROLL=$3 RVX_GEMM_DEPTH=$4 \
-    timeout -k 10 180 python bench.py --nodes 1000000 --no-cpu --no-hnsw --steps 5 > gpurun_out/exp_$tag.log 2>&1
+    timeout -k 10 300 python bench.py --nodes ${NODES:-1000000} --no-cpu --no-hnsw --steps 5 > gpurun_out/exp_$tag.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "$tag failed rc=$rc"; tail -5 gpurun_out/exp_$tag.log; exit $rc; fi
   python3 - "$tag" gpurun_out/exp_$tag.log <<'PY'
