@@ -42,7 +42,7 @@ BF16_MFMA_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (spe
 GEMM_X3 = os.environ.get("RVX_GEMM_X3", "1") != "0"
 GEMM_PEAK_TFS = BF16_MFMA_PEAK_TFS / 6 if GEMM_X3 else FP32_MFMA_PEAK_TFS
 XGMI_PEAK_GBS = 7 * 153.0    # 7 xGMI links x ~153 GB/s per direction per GPU
-PIPELINE = "row chunks x8 (>=131072 rows), gather on aux stream overlapping GEMM+normalize"
+PIPELINE = "row chunks x16 (>=262144 rows), gather on aux stream overlapping GEMM+normalize"
 
 
 def parse():

@@ -125,7 +125,7 @@ namespace {
 
 // Row chunking of the layer pipeline (same on every rank for a given chunk count).
 int sage_chunks_for(int64_t n) {
-    static const int pipe_chunks = std::max(1, env_int("RVX_SAGE_CHUNKS", 8));
+    static const int pipe_chunks = std::max(1, env_int("RVX_SAGE_CHUNKS", 16));
     return n >= (int64_t)pipe_chunks * 16384 ? pipe_chunks : 1;
 }
 int64_t chunk_step(int64_t n, int chunks) { return ((n + chunks - 1) / chunks + 127) / 128 * 128; }

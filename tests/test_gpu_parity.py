@@ -211,10 +211,10 @@ def test_graphsage_matches_oracle(in_f, out_f, n, deg):
 
 
 def test_graphsage_chunked_pipeline_and_exchange_entry():
-    """n >= 8*16384 rows runs the two-stream row-chunk pipeline (api_graph.cpp
+    """n >= 16*16384 rows runs the two-stream row-chunk pipeline (api_graph.cpp
     sage_forward_dev); rvx_sage_forward_exchange at world 1 writes the same rows."""
     import ctypes
-    n, d, deg = 140_000, 64, 8
+    n, d, deg = 280_000, 64, 8
     x = rv.Buffer(n * d * 4)
     x.fill_uniform(n * d, 21, -1.0, 1.0)
     g = rv.Graph.random(n, deg, 22)
@@ -230,7 +230,7 @@ def test_graphsage_chunked_pipeline_and_exchange_entry():
     xs = x.download(np.float32, (n, d))
     rp, col = O.random_csr(n, deg, 22)
     wn, ws = O.sage_init(d, d, 0), O.sage_init(d, d, 1000)
-    for r0 in (0, 17_536 - 1500, n - 3000):  # first chunk, across the chunk-0/1 seam, the ragged tail
+    for r0 in (0, 17_536 - 1500, n - 3000):  # first chunk, across the chunk-0/1 seam (16 chunks of 17,536), the tail
         ref = O.sage_forward(xs, rp, col, wn, ws, rows=(r0, 3000))
         assert_close(got[r0:r0 + 3000], ref)
     with pytest.raises(rv.RvxError):  # x and y may not alias
