@@ -13,6 +13,7 @@ struct rvx_edge_attention {
     int hd = 0, D = 0;
     std::vector<float> w_node, w_edge, a_src, a_dst, a_edge;
     DevMem d_wnode, d_wedge, d_asrc, d_adst, d_aedge;
+    DevMem d_wnode_x3;  // exact 3-way bf16 split of W_node (split-bf16 MFMA GEMM)
 };
 
 namespace {
@@ -24,7 +25,7 @@ void upload_vec(DevMem& d, const std::vector<float>& v) {
 
 // One destination row per query row q of `tq`, neighbours given by rp/col.
 void run_efa(const rvx_edge_attention* a, int64_t n, const int64_t* rp, const int32_t* col, int64_t E, const float* tq,
-             const float* tk, const float* tv, const float* edges, float* out) {
+             int64_t nk, const float* tk, const float* tv, const float* edges, float* out) {
     EfaArgs ea;
     ea.n = n; ea.heads = a->cfg.num_heads; ea.hd = a->hd; ea.edge_dim = a->cfg.edge_dim;
     ea.concat = a->cfg.concat_heads ? 1 : 0; ea.slope = a->cfg.negative_slope;
@@ -35,12 +36,18 @@ void run_efa(const rvx_edge_attention* a, int64_t n, const int64_t* rp, const in
     ea.a_src = a->d_asrc.as<float>(); ea.a_dst = a->d_adst.as<float>(); ea.a_edge = a->d_aedge.as<float>();
     ea.scores = scratch_f32("efa_scores", std::max<int64_t>(E, 1) * a->cfg.num_heads);
     ea.out = out;
+    ea.nk = nk;
+    ea.sq = scratch_f32("efa_sq", std::max<int64_t>(n, 1) * a->cfg.num_heads);
+    ea.sk = scratch_f32("efa_sk", std::max<int64_t>(nk, 1) * a->cfg.num_heads);
+    ea.u = scratch_f32("efa_u", (int64_t)a->cfg.num_heads * std::max(a->cfg.edge_dim, 1));
     edge_feat_attention(ea);
 }
 
 void transform(const rvx_edge_attention* a, const float* x, int64_t rows, float* t, const char* tag) {
     // transform_node for every head at once: T = X W_node^T, W_node [heads*hd][node_dim]
-    gemm_nt(rows, a->D, GemmOperand{x, a->cfg.node_dim, a->d_wnode.as<float>(), a->cfg.node_dim, a->cfg.node_dim},
+    gemm_nt(rows, a->D,
+            GemmOperand{x, a->cfg.node_dim, a->d_wnode.as<float>(), a->cfg.node_dim, a->cfg.node_dim,
+                        a->d_wnode_x3.as<uint16_t>(), (int64_t)a->D * a->cfg.node_dim},
             nullptr, GemmEpilogue(), t, a->D, tag);
 }
 
@@ -80,6 +87,9 @@ rvx_status rvx_edge_attention_create(const rvx_edge_attention_config* cfg, rvx_e
         a->a_edge.resize(H * hd);
         for (auto& v : a->a_edge) v = rnd() * 2.0f * attn_scale;
         upload_vec(a->d_wnode, a->w_node);
+        a->d_wnode_x3.reset(std::max<int64_t>((int64_t)a->w_node.size(), 1) * 6);
+        split_x3(a->d_wnode.as<float>(), (int64_t)a->w_node.size(), a->d_wnode_x3.as<uint16_t>());
+        sync();
         upload_vec(a->d_wedge, a->w_edge);
         upload_vec(a->d_asrc, a->a_src);
         upload_vec(a->d_adst, a->a_dst);
@@ -136,7 +146,7 @@ rvx_status rvx_edge_attention_compute(const rvx_edge_attention* a, const float* 
             transform(a, dk, n, tk, "efa_transform");
             transform(a, dv, n, tv, "efa_transform");
         }
-        run_efa(a, 1, rp, col, n, tq, tk, tv, (edges && a->cfg.edge_dim > 0) ? de : nullptr, dout);
+        run_efa(a, 1, rp, col, n, tq, n, tk, tv, (edges && a->cfg.edge_dim > 0) ? de : nullptr, dout);
         const int od = a->cfg.concat_heads ? D : a->hd;
         RVX_HIP(hipMemcpyAsync(out, dout, (size_t)od * 4, hipMemcpyDeviceToHost, stream()));
         sync();
@@ -157,7 +167,7 @@ rvx_status rvx_edge_attention_forward_graph_device(const rvx_edge_attention* a, 
         ComputeLock cl;
         float* t = scratch_f32("efa_t", g->n * (int64_t)a->D);
         transform(a, x->mem.as<float>(), g->n, t, "efa_transform");
-        run_efa(a, g->n, g->row_ptr, g->col, g->e, t, t, t, ef ? ef->mem.as<float>() : nullptr, y->mem.as<float>());
+        run_efa(a, g->n, g->row_ptr, g->col, g->e, t, g->n, t, t, ef ? ef->mem.as<float>() : nullptr, y->mem.as<float>());
     });
 }
 

@@ -58,15 +58,36 @@ HostLinear make_linear(int in, int out, uint64_t seed) {
 
 }  // namespace
 
+namespace rvx {
+// A [rows][cols] weight on the device: f32 and its split_x3 planes.
+struct DevWeight {
+    DevMem w, x3;
+    int64_t rows = 0, cols = 0;
+    void upload(const std::vector<float>& v, int64_t r, int64_t c) {
+        rows = r; cols = c;
+        w.reset(std::max<int64_t>(r * c, 1) * 4);
+        w.upload(v.data(), r * c * 4);
+        x3.reset(std::max<int64_t>(r * c, 1) * 6);
+        split_x3(w.as<float>(), r * c, x3.as<uint16_t>());
+    }
+    // operand C = A · W[row_off : row_off+n]^T with A [M][cols] (lda)
+    GemmOperand op(const float* A, int64_t lda, int64_t row_off = 0) const {
+        return GemmOperand{A, lda, w.as<float>() + row_off * cols, cols, (int)cols,
+                           x3.as<uint16_t>() + row_off * cols, rows * cols};
+    }
+};
+}  // namespace rvx
+
 struct rvx_layer {
     int in = 0, H = 0, heads = 0, hd = 0;
     float dropout = 0.0f;
     HostLinear w_msg, w_agg, w_z, u_z, w_r, u_r, w_h, u_h, q, k, v, o;
     std::vector<float> gamma, beta;
     float eps = 1e-5f;
-    // device
-    DevMem d_wmsg, d_bmsg, d_wqkv, d_bqkv, d_wo, d_bo, d_wagg, d_bagg, d_wzr, d_uzr, d_bwzr, d_buzr, d_wh, d_uh, d_bwh,
-        d_buh, d_gamma, d_beta;
+    // device: weights [out][in] (the GEMM's K-contiguous B) with their exact
+    // 3-way bf16 splits for the split-bf16 MFMA GEMM; biases and norm f32
+    DevWeight d_wmsg, d_wqkv, d_wo, d_wagg, d_wzr, d_uzr, d_wh, d_uh;
+    DevMem d_bmsg, d_bqkv, d_bo, d_bagg, d_bwzr, d_buzr, d_bwh, d_buh, d_gamma, d_beta;
 };
 
 namespace {
@@ -97,14 +118,17 @@ void validate(const rvx_layer* l) {
 }
 
 void upload_layer(rvx_layer* l) {
-    upload(l->d_wmsg, l->w_msg.w); upload(l->d_bmsg, l->w_msg.b);
-    upload(l->d_wqkv, cat({&l->q.w, &l->k.w, &l->v.w})); upload(l->d_bqkv, cat({&l->q.b, &l->k.b, &l->v.b}));
-    upload(l->d_wo, l->o.w); upload(l->d_bo, l->o.b);
-    upload(l->d_wagg, l->w_agg.w); upload(l->d_bagg, l->w_agg.b);
-    upload(l->d_wzr, cat({&l->w_z.w, &l->w_r.w})); upload(l->d_uzr, cat({&l->u_z.w, &l->u_r.w}));
+    const int64_t H = l->H;
+    l->d_wmsg.upload(l->w_msg.w, H, l->in); upload(l->d_bmsg, l->w_msg.b);
+    l->d_wqkv.upload(cat({&l->q.w, &l->k.w, &l->v.w}), 3 * H, H); upload(l->d_bqkv, cat({&l->q.b, &l->k.b, &l->v.b}));
+    l->d_wo.upload(l->o.w, H, H); upload(l->d_bo, l->o.b);
+    l->d_wagg.upload(l->w_agg.w, H, H); upload(l->d_bagg, l->w_agg.b);
+    l->d_wzr.upload(cat({&l->w_z.w, &l->w_r.w}), 2 * H, H); l->d_uzr.upload(cat({&l->u_z.w, &l->u_r.w}), 2 * H, H);
     upload(l->d_bwzr, cat({&l->w_z.b, &l->w_r.b})); upload(l->d_buzr, cat({&l->u_z.b, &l->u_r.b}));
-    upload(l->d_wh, l->w_h.w); upload(l->d_uh, l->u_h.w); upload(l->d_bwh, l->w_h.b); upload(l->d_buh, l->u_h.b);
+    l->d_wh.upload(l->w_h.w, H, H); l->d_uh.upload(l->u_h.w, H, H);
+    upload(l->d_bwh, l->w_h.b); upload(l->d_buh, l->u_h.b);
     upload(l->d_gamma, l->gamma); upload(l->d_beta, l->beta);
+    sync();
 }
 
 // ---- serde JSON ------------------------------------------------------------
@@ -149,52 +173,74 @@ void put_linear(std::string& s, const HostLinear& l) {
 
 // ---- batched forward ---------------------------------------------------------
 // wmode: 0 no weights, 1 raw per-edge weights (graph), 2 pre-normalised.
-void forward_dev(const rvx_layer* l, int64_t n, const int64_t* rp, const int32_t* col, int64_t E, const float* w,
-                 int wmode, const float* x, float* y) {
-    const int H = l->H;
+// rp/col/w: the CSR of destination rows 0..n-1 (global edge indices); x/y
+// [n][in] / [n][H]; max_deg bounds the per-chunk edge count.
+//
+// Phase 1 (whole table, neighbours read it): M = w_msg(x) [n][H] and
+// K|V = M·[W_k;W_v]^T [n][2H]. Phase 2 (row chunks of CHUNK rows, everything
+// row-local): Q, edge attention + weighted message aggregate, COMB = out(att)
+// + wagg, AGG = w_agg(COMB), z|r, r⊙h, h~, GRU blend + dropout + LayerNorm.
+// Peak scratch = 3 n H + CHUNK (6 H + max_deg heads) floats — a 10M x 768
+// layer fits beside its input and output in HBM.
+void forward_dev(const rvx_layer* l, int64_t n, const int64_t* rp, const int32_t* col, int64_t max_deg,
+                 const float* w, int wmode, const float* x, float* y) {
+    const int64_t H = l->H;
+    const int64_t CHUNK = std::max<int64_t>(4096, env_int("RVX_GNN_CHUNK_ROWS", 1 << 20));  // read per call
+    const int64_t chunk = std::min<int64_t>(n, CHUNK);
     float* M = scratch_f32("rvl_m", n * H);
-    float* S1 = scratch_f32("rvl_s1", n * 3 * (int64_t)H);
-    float* S2 = scratch_f32("rvl_s2", n * H);
-    float* S3 = scratch_f32("rvl_s3", n * H);
-    float* S4 = scratch_f32("rvl_s4", n * H);
-    float* scores = scratch_f32("rvl_scores", std::max<int64_t>(E, 1) * l->heads);
+    float* KV = scratch_f32("rvl_kv", n * 2 * H);
+    float* Q = scratch_f32("rvl_q", chunk * H);
+    float* S1 = scratch_f32("rvl_s1", chunk * 2 * H);
+    float* S2 = scratch_f32("rvl_s2", chunk * H);
+    float* S3 = scratch_f32("rvl_s3", chunk * H);
+    float* S4 = scratch_f32("rvl_s4", chunk * H);
+    float* scores = scratch_f32("rvl_scores", std::max<int64_t>(chunk * max_deg, 1) * l->heads);
 
     GemmEpilogue ep;
     ep.bias0 = l->d_bmsg.as<float>();
-    gemm_nt(n, H, GemmOperand{x, l->in, l->d_wmsg.as<float>(), l->in, l->in}, nullptr, ep, M, H, "gnn_gemm_msg");
+    gemm_nt(n, (int)H, l->d_wmsg.op(x, l->in), nullptr, ep, M, H, "gnn_gemm_msg");
     ep = GemmEpilogue();
-    ep.bias0 = l->d_bqkv.as<float>();
-    gemm_nt(n, 3 * H, GemmOperand{M, H, l->d_wqkv.as<float>(), H, H}, nullptr, ep, S1, 3 * H, "gnn_gemm_qkv");
+    ep.bias0 = l->d_bqkv.as<float>() + H;
+    gemm_nt(n, (int)(2 * H), l->d_wqkv.op(M, H, H), nullptr, ep, KV, 2 * H, "gnn_gemm_kv");
 
-    EdgeArgs ea;
-    ea.n = n; ea.H = H; ea.heads = l->heads; ea.hd = l->hd; ea.G = edge_group_lanes(H, l->heads);
-    ea.rp = rp; ea.col = col; ea.w = w; ea.wmode = w ? wmode : 0;
-    ea.qkv = S1; ea.m = M; ea.scores = scores; ea.att = S2; ea.wagg = S3;
-    edge_attention(ea);
+    for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+        const int64_t rows = std::min(chunk, n - r0);
+        const float* Mc = M + r0 * H;
+        ep = GemmEpilogue();
+        ep.bias0 = l->d_bqkv.as<float>();
+        gemm_nt(rows, (int)H, l->d_wqkv.op(Mc, H, 0), nullptr, ep, Q, H, "gnn_gemm_q");
 
-    ep = GemmEpilogue();
-    ep.bias0 = l->d_bo.as<float>();
-    ep.addend = S3; ep.ld_addend = H;
-    gemm_nt(n, H, GemmOperand{S2, H, l->d_wo.as<float>(), H, H}, nullptr, ep, S4, H, "gnn_gemm_out");  // COMB
-    ep = GemmEpilogue();
-    ep.bias0 = l->d_bagg.as<float>();
-    gemm_nt(n, H, GemmOperand{S4, H, l->d_wagg.as<float>(), H, H}, nullptr, ep, S2, H, "gnn_gemm_agg");  // AGG
-    ep = GemmEpilogue();
-    ep.epi = GEMM_EPI_SIGMOID; ep.bias0 = l->d_bwzr.as<float>(); ep.bias1 = l->d_buzr.as<float>();
-    GemmOperand zr_b{M, H, l->d_uzr.as<float>(), H, H};
-    gemm_nt(n, 2 * H, GemmOperand{S2, H, l->d_wzr.as<float>(), H, H}, &zr_b, ep, S1, 2 * H, "gnn_gemm_zr");
-    mul_rows(S1 + H, 2 * (int64_t)H, M, S3, n, H);  // RH = r ⊙ h
-    ep = GemmEpilogue();
-    ep.epi = GEMM_EPI_TANH; ep.bias0 = l->d_bwh.as<float>(); ep.bias1 = l->d_buh.as<float>();
-    GemmOperand h_b{S3, H, l->d_uh.as<float>(), H, H};
-    gemm_nt(n, H, GemmOperand{S2, H, l->d_wh.as<float>(), H, H}, &h_b, ep, S4, H, "gnn_gemm_h");  // HT
+        EdgeArgs ea;
+        ea.n = rows; ea.H = (int)H; ea.heads = l->heads; ea.hd = l->hd; ea.G = edge_group_lanes((int)H, l->heads);
+        ea.rp = rp + r0; ea.col = col; ea.w = w; ea.wmode = w ? wmode : 0;
+        ea.q = Q; ea.ldq = H; ea.k = KV; ea.v = KV + H; ea.ldkv = 2 * H; ea.m = M;
+        ea.scores = scores; ea.att = S2; ea.wagg = S3;
+        edge_attention(ea);
 
-    FinishArgs fa;
-    fa.n = n; fa.H = H; fa.rp = rp; fa.m = M; fa.zr = S1; fa.ht = S4;
-    fa.gamma = l->d_gamma.as<float>(); fa.beta = l->d_beta.as<float>(); fa.eps = l->eps;
-    fa.keep = 1.0f - l->dropout;
-    fa.y = y;
-    gru_finish(fa);
+        ep = GemmEpilogue();
+        ep.bias0 = l->d_bo.as<float>();
+        ep.addend = S3; ep.ld_addend = H;
+        gemm_nt(rows, (int)H, l->d_wo.op(S2, H), nullptr, ep, S4, H, "gnn_gemm_out");  // COMB
+        ep = GemmEpilogue();
+        ep.bias0 = l->d_bagg.as<float>();
+        gemm_nt(rows, (int)H, l->d_wagg.op(S4, H), nullptr, ep, S2, H, "gnn_gemm_agg");  // AGG
+        ep = GemmEpilogue();
+        ep.epi = GEMM_EPI_SIGMOID; ep.bias0 = l->d_bwzr.as<float>(); ep.bias1 = l->d_buzr.as<float>();
+        const GemmOperand zr_b = l->d_uzr.op(Mc, H);
+        gemm_nt(rows, (int)(2 * H), l->d_wzr.op(S2, H), &zr_b, ep, S1, 2 * H, "gnn_gemm_zr");
+        mul_rows(S1 + H, 2 * H, Mc, S3, rows, (int)H);  // RH = r ⊙ h
+        ep = GemmEpilogue();
+        ep.epi = GEMM_EPI_TANH; ep.bias0 = l->d_bwh.as<float>(); ep.bias1 = l->d_buh.as<float>();
+        const GemmOperand h_b = l->d_uh.op(S3, H);
+        gemm_nt(rows, (int)H, l->d_wh.op(S2, H), &h_b, ep, S4, H, "gnn_gemm_h");  // HT
+
+        FinishArgs fa;
+        fa.n = rows; fa.H = (int)H; fa.rp = rp + r0; fa.m = Mc; fa.zr = S1; fa.ht = S4;
+        fa.gamma = l->d_gamma.as<float>(); fa.beta = l->d_beta.as<float>(); fa.eps = l->eps;
+        fa.keep = 1.0f - l->dropout;
+        fa.y = y + r0 * H;
+        gru_finish(fa);
+    }
 }
 
 }  // namespace
@@ -359,7 +405,7 @@ rvx_status rvx_gnn_forward_graph_device(const rvx_layer* l, const rvx_graph* g, 
         RVX_REQUIRE(x->mem.bytes >= g->n * l->in * 4, RVX_ERR_DIMENSION_MISMATCH, "x smaller than n*input_dim");
         RVX_REQUIRE(y->mem.bytes >= g->n * l->H * 4, RVX_ERR_DIMENSION_MISMATCH, "y smaller than n*hidden_dim");
         ComputeLock cl;
-        forward_dev(l, g->n, g->row_ptr, g->col, g->e, g->w, 1, x->mem.as<float>(), y->mem.as<float>());
+        forward_dev(l, g->n, g->row_ptr, g->col, g->max_deg, g->w, 1, x->mem.as<float>(), y->mem.as<float>());
     });
 }
 
@@ -372,7 +418,7 @@ rvx_status rvx_gnn_forward_graph(const rvx_layer* l, const rvx_graph* g, const f
         float* dx = scratch_f32("rvlg_x", n * l->in);
         float* dy = scratch_f32("rvlg_y", n * l->H);
         RVX_HIP(hipMemcpyAsync(dx, x, (size_t)(n * l->in * 4), hipMemcpyHostToDevice, stream()));
-        forward_dev(l, n, g->row_ptr, g->col, g->e, g->w, 1, dx, dy);
+        forward_dev(l, n, g->row_ptr, g->col, g->max_deg, g->w, 1, dx, dy);
         RVX_HIP(hipMemcpyAsync(y, dy, (size_t)(n * l->H * 4), hipMemcpyDeviceToHost, stream()));
         sync();
     });

@@ -21,6 +21,10 @@ struct EfaArgs {
     const float* a_edge = nullptr;               // [heads*hd]
     float* scores = nullptr;                     // [E][heads] scratch
     float* out = nullptr;                        // [n][concat ? heads*hd : hd]
+    int64_t nk = 0;                              // rows of tk
+    float* sq = nullptr;                         // [n][heads]  scratch: tq . a_src per head
+    float* sk = nullptr;                         // [nk][heads] scratch: tk . a_dst per head
+    float* u = nullptr;                          // [heads][edge_dim] scratch: W_edge^T a_edge per head
 };
 
 void edge_feat_attention(const EfaArgs& a);

@@ -4,6 +4,10 @@
 
 namespace rvx {
 
+// Destination rows i = 0..n-1 of a row chunk: rp points at the chunk's first
+// row_ptr entry (edge indices stay global, so col / w are the whole graph's);
+// q, att, wagg are chunk-local; k, v, m are whole node tables indexed by the
+// global neighbour id. scores holds the chunk's edges from rp[0] on.
 struct EdgeArgs {
     int64_t n = 0;
     int H = 0, heads = 0, hd = 0, G = 0;  // G = lanes per head of the grouped kernel (0 = generic)
@@ -11,9 +15,12 @@ struct EdgeArgs {
     const int32_t* col = nullptr;
     const float* w = nullptr;  // per-edge weights (wmode 1: raw, 2: pre-normalised)
     int wmode = 0;
-    const float* qkv = nullptr;  // [n][3H]  (q | k | v)
-    const float* m = nullptr;    // [n][H]   messages w_msg(x)
-    float* scores = nullptr;     // [E][heads] scratch
+    const float* q = nullptr; int64_t ldq = 0;   // [n][ldq]
+    const float* k = nullptr;                    // [N][ldkv]
+    const float* v = nullptr;                    // [N][ldkv]
+    int64_t ldkv = 0;
+    const float* m = nullptr;    // [N][H]   messages w_msg(x)
+    float* scores = nullptr;     // [chunk edges][heads] scratch
     float* att = nullptr;        // [n][H]   concat of head outputs
     float* wagg = nullptr;       // [n][H]   weighted message aggregate
 };

@@ -20,31 +20,54 @@
 namespace rvx {
 namespace {
 
+// The score of edge (i, j) in head h is LeakyReLU of
+//   sum_c tq_i[c] a_src[c] + tk_j[c] a_dst[c] + te_ij[c] a_edge[c],  c over the head,
+// which the reference accumulates as one interleaved chain (edge_featured.rs:177-183).
+// It is evaluated here as three separately summed parts: per-node head dots
+// sq_i[h] = tq_i . a_src and sk_j[h] = tk_j . a_dst (one pass over T), and the
+// edge term sum_k e_ij[k] u[h][k] with u = W_edge^T a_edge folded once per call
+// — O(E heads) instead of O(E heads hd), reassociating one f32 sum (the 1e-5
+// bar of the north star covers it; tests/test_gpu_parity.py).
+__global__ void k_efa_row_dots(const float* __restrict__ t, int64_t ld, int64_t rows, int heads, int hd,
+                               const float* __restrict__ av, float* __restrict__ out) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= rows * heads) return;
+    const int64_t r = idx / heads;
+    const int h = (int)(idx % heads);
+    const float* tr = t + r * ld + (int64_t)h * hd;
+    const float* ar = av + (int64_t)h * hd;
+    float s = 0.0f;
+    for (int c = 0; c < hd; ++c) s = s + tr[c] * ar[c];
+    out[idx] = s;
+}
+
+__global__ void k_efa_edge_u(const float* __restrict__ w_edge, const float* __restrict__ a_edge, int heads, int hd,
+                             int ed, float* __restrict__ u) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= heads * ed) return;
+    const int h = idx / ed, kk = idx % ed;
+    float s = 0.0f;
+    for (int c = 0; c < hd; ++c) s = s + w_edge[(int64_t)(h * hd + c) * ed + kk] * a_edge[h * hd + c];
+    u[idx] = s;
+}
+
 __global__ __launch_bounds__(256) void k_edge_feat_scores(EfaArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= a.n) return;
-    const int heads = a.heads, hd = a.hd, D = heads * hd, ed = a.edge_dim;
-    const float* tq = a.tq + i * (int64_t)a.ldq;
+    const int heads = a.heads, ed = a.edge_dim;
     const int64_t beg = a.rp[i], end = a.rp[i + 1];
     for (int64_t e = beg + lane; e < end; e += 64) {
-        const float* tk = a.tk + (int64_t)a.col[e] * a.ldk;
+        const int64_t j = a.col[e];
         const float* ef = a.edges ? a.edges + e * (int64_t)ed : nullptr;
         for (int h = 0; h < heads; ++h) {
-            float score = 0.0f;
-            for (int c = 0; c < hd; ++c) {
-                const int off = h * hd + c;
-                float te = 0.0f;  // transform_edge (edge_featured.rs:159-171), sequential over edge_dim
-                if (ef)
-                    for (int k = 0; k < ed; ++k) te = te + ef[k] * a.w_edge[(int64_t)off * ed + k];
-                score = score + tq[off] * a.a_src[off];
-                score = score + tk[off] * a.a_dst[off];
-                score = score + te * a.a_edge[off];
-            }
+            float te = 0.0f;
+            if (ef)
+                for (int kk = 0; kk < ed; ++kk) te = te + ef[kk] * a.u[h * ed + kk];
+            const float score = (a.sq[i * heads + h] + a.sk[j * heads + h]) + te;
             a.scores[e * heads + h] = score < 0.0f ? a.slope * score : score;
         }
     }
-    (void)D;
 }
 
 // stable_softmax per (node, head), in place over the score scratch.
@@ -164,12 +187,20 @@ __global__ __launch_bounds__(64) void k_diff_search(const float* q, int64_t nq, 
 
 void edge_feat_attention(const EfaArgs& a) {
     if (a.n <= 0) return;
-    ProfScope ps("efa_edge");
-    hipLaunchKernelGGL(k_edge_feat_scores, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, stream(), a);
-    const int64_t t = a.n * a.heads;
-    hipLaunchKernelGGL(k_edge_feat_softmax, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, stream(), a);
-    hipLaunchKernelGGL(k_edge_feat_out, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, stream(), a);
-    RVX_HIP(hipGetLastError());
+    const int64_t nq = a.n * a.heads, nkh = a.nk * a.heads;
+    RVX_LAUNCH("efa_node_dots", k_efa_row_dots, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, a.tq, a.ldq, a.n,
+               a.heads, a.hd, a.a_src, a.sq);
+    if (nkh > 0)
+        RVX_LAUNCH("efa_node_dots", k_efa_row_dots, dim3((unsigned)((nkh + 255) / 256)), dim3(256), 0, a.tk, a.ldk,
+                   a.nk, a.heads, a.hd, a.a_dst, a.sk);
+    if (a.edges && a.edge_dim > 0) {
+        const int nu = a.heads * a.edge_dim;
+        RVX_LAUNCH("efa_node_dots", k_efa_edge_u, dim3((unsigned)((nu + 255) / 256)), dim3(256), 0, a.w_edge, a.a_edge,
+                   a.heads, a.hd, a.edge_dim, a.u);
+    }
+    RVX_LAUNCH("efa_scores", k_edge_feat_scores, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, a);
+    RVX_LAUNCH("efa_softmax", k_edge_feat_softmax, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, a);
+    RVX_LAUNCH("efa_out", k_edge_feat_out, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, a);
 }
 
 void differentiable_search(const float* q, int64_t nq, const float* cand, int C, int d, int k, float temperature,

@@ -45,6 +45,7 @@ __global__ __launch_bounds__(256) void k_edge_attn_grouped(EdgeArgs a) {
     const int head = (lane * CPL) / a.hd;
     const int64_t beg = a.rp[i], end = a.rp[i + 1];
     const int deg = (int)(end - beg);
+    float* scores = a.scores - a.rp[0] * a.heads;  // chunk-relative edge slots
     const int c0 = lane * CPL;
     float att[CPL], agg[CPL];
 #pragma unroll
@@ -60,7 +61,7 @@ __global__ __launch_bounds__(256) void k_edge_attn_grouped(EdgeArgs a) {
     float q[CPL];
 #pragma unroll
     for (int c = 0; c < CPL; c += 4) {
-        const float4 v = ld4(a.qkv + i * (3 * (int64_t)H) + c0 + c);
+        const float4 v = ld4(a.q + i * a.ldq + c0 + c);
         q[c] = v.x; q[c + 1] = v.y; q[c + 2] = v.z; q[c + 3] = v.w;
     }
     const float scale = sqrtf((float)a.hd);
@@ -68,7 +69,7 @@ __global__ __launch_bounds__(256) void k_edge_attn_grouped(EdgeArgs a) {
     // pass 1: scores
     for (int64_t e = beg; e < end; ++e) {
         const int j = a.col[e];
-        const float* kr = a.qkv + (int64_t)j * (3 * (int64_t)H) + H + c0;
+        const float* kr = a.k + (int64_t)j * a.ldkv + c0;
         float p = 0.0f;
 #pragma unroll
         for (int c = 0; c < CPL; c += 4) {
@@ -78,21 +79,21 @@ __global__ __launch_bounds__(256) void k_edge_attn_grouped(EdgeArgs a) {
         for (int o = 1; o < G; o <<= 1) p += __shfl_xor(p, o);
         const float s = p / scale;
         mx = fmaxf(mx, s);
-        if ((lane & (G - 1)) == 0) a.scores[e * a.heads + head] = s;
+        if ((lane & (G - 1)) == 0) scores[e * a.heads + head] = s;
     }
     __builtin_amdgcn_wave_barrier();
     __threadfence_block();
     // pass 2: sum of exp in neighbour order
     float sum = 0.0f;
-    for (int64_t e = beg; e < end; ++e) sum = sum + expf(a.scores[e * a.heads + head] - mx);
+    for (int64_t e = beg; e < end; ++e) sum = sum + expf(scores[e * a.heads + head] - mx);
     sum = fmaxf(sum, 1e-10f);
     float wsum = 0.0f;
     if (a.wmode == 1) wsum = row_weight_sum(a.w, beg, end);
     // pass 3: weighted sums of values and messages
     for (int64_t e = beg; e < end; ++e) {
         const int j = a.col[e];
-        const float wt = expf(a.scores[e * a.heads + head] - mx) / sum;
-        const float* vr = a.qkv + (int64_t)j * (3 * (int64_t)H) + 2 * H + c0;
+        const float wt = expf(scores[e * a.heads + head] - mx) / sum;
+        const float* vr = a.v + (int64_t)j * a.ldkv + c0;
 #pragma unroll
         for (int c = 0; c < CPL; c += 4) {
             const float4 v = ld4(vr + c);
@@ -126,14 +127,15 @@ __global__ __launch_bounds__(256) void k_edge_attn_generic(EdgeArgs a) {
     const int H = a.H, hd = a.hd, heads = a.heads;
     const int64_t beg = a.rp[i], end = a.rp[i + 1];
     const int deg = (int)(end - beg);
-    const float* qi = a.qkv + i * (3 * (int64_t)H);
+    float* scores = a.scores - a.rp[0] * heads;  // chunk-relative edge slots
+    const float* qi = a.q + i * a.ldq;
     const float scale = sqrtf((float)hd);
     for (int64_t e = beg + lane; e < end; e += 64) {
-        const float* kr = a.qkv + (int64_t)a.col[e] * (3 * (int64_t)H) + H;
+        const float* kr = a.k + (int64_t)a.col[e] * a.ldkv;
         for (int h = 0; h < heads; ++h) {
             float p = 0.0f;
             for (int c = 0; c < hd; ++c) p = p + qi[h * hd + c] * kr[h * hd + c];
-            a.scores[e * heads + h] = p / scale;
+            scores[e * heads + h] = p / scale;
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -143,15 +145,15 @@ __global__ __launch_bounds__(256) void k_edge_attn_generic(EdgeArgs a) {
     for (int c = lane; c < H; c += 64) {
         const int h = c / hd;
         float mx = -INFINITY;
-        for (int64_t e = beg; e < end; ++e) mx = fmaxf(mx, a.scores[e * heads + h]);
+        for (int64_t e = beg; e < end; ++e) mx = fmaxf(mx, scores[e * heads + h]);
         float sum = 0.0f;
-        for (int64_t e = beg; e < end; ++e) sum = sum + expf(a.scores[e * heads + h] - mx);
+        for (int64_t e = beg; e < end; ++e) sum = sum + expf(scores[e * heads + h] - mx);
         sum = fmaxf(sum, 1e-10f);
         float at = 0.0f, ag = 0.0f;
         for (int64_t e = beg; e < end; ++e) {
             const int j = a.col[e];
-            const float wt = expf(a.scores[e * heads + h] - mx) / sum;
-            at = at + wt * a.qkv[(int64_t)j * (3 * (int64_t)H) + 2 * H + c];
+            const float wt = expf(scores[e * heads + h] - mx) / sum;
+            at = at + wt * a.v[(int64_t)j * a.ldkv + c];
             if (a.wmode != 0) ag = ag + norm_weight(a.wmode, a.w, e, wsum, deg) * a.m[(int64_t)j * H + c];
         }
         a.att[i * H + c] = at;
@@ -206,20 +208,14 @@ __global__ __launch_bounds__(256) void k_gru_finish(FinishArgs a) {
 void edge_attention(const EdgeArgs& a) {
     if (a.n <= 0) return;
     const dim3 grid((unsigned)((a.n + 3) / 4)), block(256);
-    ProfScope ps("gnn_edge_attention");
-    const bool aligned = (((uintptr_t)a.qkv | (uintptr_t)a.m | (uintptr_t)a.att | (uintptr_t)a.wagg) & 15) == 0;
-    if (aligned && a.H % 64 == 0 && a.G > 0) {
-        switch (a.H / 64) {
-            case 4: hipLaunchKernelGGL(k_edge_attn_grouped<4>, grid, block, 0, stream(), a); break;
-            case 8: hipLaunchKernelGGL(k_edge_attn_grouped<8>, grid, block, 0, stream(), a); break;
-            case 12: hipLaunchKernelGGL(k_edge_attn_grouped<12>, grid, block, 0, stream(), a); break;
-            case 16: hipLaunchKernelGGL(k_edge_attn_grouped<16>, grid, block, 0, stream(), a); break;
-            default: hipLaunchKernelGGL(k_edge_attn_generic, grid, block, 0, stream(), a); break;
-        }
-    } else {
-        hipLaunchKernelGGL(k_edge_attn_generic, grid, block, 0, stream(), a);
-    }
-    RVX_HIP(hipGetLastError());
+    const char* t = "gnn_edge_attention";
+    const bool aligned = (((uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v | (uintptr_t)a.m | (uintptr_t)a.att |
+                           (uintptr_t)a.wagg) & 15) == 0 && a.ldq % 4 == 0 && a.ldkv % 4 == 0;
+    if (aligned && a.H % 64 == 0 && a.G > 0 && a.H / 64 == 4) RVX_LAUNCH(t, k_edge_attn_grouped<4>, grid, block, 0, a);
+    else if (aligned && a.H % 64 == 0 && a.G > 0 && a.H / 64 == 8) RVX_LAUNCH(t, k_edge_attn_grouped<8>, grid, block, 0, a);
+    else if (aligned && a.H % 64 == 0 && a.G > 0 && a.H / 64 == 12) RVX_LAUNCH(t, k_edge_attn_grouped<12>, grid, block, 0, a);
+    else if (aligned && a.H % 64 == 0 && a.G > 0 && a.H / 64 == 16) RVX_LAUNCH(t, k_edge_attn_grouped<16>, grid, block, 0, a);
+    else RVX_LAUNCH(t, k_edge_attn_generic, grid, block, 0, a);
 }
 
 int edge_group_lanes(int H, int heads) {
@@ -235,16 +231,12 @@ int edge_group_lanes(int H, int heads) {
 void mul_rows(const float* r, int64_t ldr, const float* h, float* out, int64_t n, int H) {
     const int64_t total = n * H;
     if (total <= 0) return;
-    ProfScope ps("gnn_gate_mul");
-    hipLaunchKernelGGL(k_mul, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream(), r, ldr, h, out, n, H);
-    RVX_HIP(hipGetLastError());
+    RVX_LAUNCH("gnn_gate_mul", k_mul, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, r, ldr, h, out, n, H);
 }
 
 void gru_finish(const FinishArgs& a) {
     if (a.n <= 0) return;
-    ProfScope ps("gnn_finish");
-    hipLaunchKernelGGL(k_gru_finish, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, stream(), a);
-    RVX_HIP(hipGetLastError());
+    RVX_LAUNCH("gnn_finish", k_gru_finish, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, a);
 }
 
 }  // namespace rvx

@@ -51,15 +51,20 @@ class Graph:
         return cls(h)
 
     @classmethod
-    def random(cls, num_nodes: int, degree: int, seed: int) -> "Graph":
-        """Uniform random out-degree CSR generated on the device."""
+    def random(cls, num_nodes: int, degree: int, seed: int, weight_seed: Optional[int] = None) -> "Graph":
+        """Uniform random out-degree CSR generated on the device (SURVEY §8d C2);
+        with weight_seed, edge weights uniform [0, 1) from the same generator."""
         rp = Buffer((num_nodes + 1) * 8)
         col = Buffer(max(num_nodes * degree * 4, 4))
         L.call("rvx_random_csr", int(num_nodes), int(degree), int(seed), rp.handle, col.handle)
+        w = None
+        if weight_seed is not None:
+            w = Buffer(max(num_nodes * degree * 4, 4))
+            w.fill_uniform(num_nodes * degree, weight_seed, 0.0, 1.0)
         h = C.c_void_p()
-        L.call("rvx_graph_from_device_csr", int(num_nodes), int(num_nodes * degree), rp.handle, col.handle, None,
-               C.byref(h))
-        return cls(h, keep=(rp, col))
+        L.call("rvx_graph_from_device_csr", int(num_nodes), int(num_nodes * degree), rp.handle, col.handle,
+               w.handle if w is not None else None, C.byref(h))
+        return cls(h, keep=(rp, col) if w is None else (rp, col, w))
 
     @classmethod
     def random_shard(cls, num_nodes_total: int, row_begin: int, num_rows: int, degree: int, seed: int) -> "Graph":

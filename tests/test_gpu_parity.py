@@ -329,6 +329,29 @@ def test_ruvector_forward_graph_matches_oracle(hidden, heads):
     assert_close(y, ref)
 
 
+def test_ruvector_forward_graph_row_chunks(monkeypatch):
+    """Phase 2 of the batched layer runs in row chunks (api_gnn.cpp forward_dev):
+    chunk seams, the chunk-relative score slots and isolated rows in a later
+    chunk must not change the result."""
+    n, deg, hidden, heads = 10_000, 9, 64, 4
+    layer, W, _ = _layer_and_weights(hidden, hidden, heads, 0.0, seed=11)
+    x = O.fill_uniform(n * hidden, 14).reshape(n, hidden)
+    rp, col = O.random_csr(n, deg, 15)
+    keep = np.ones(n, bool)
+    keep[[5, 4100, 9999]] = False  # isolated rows in chunks 0, 1 and 2
+    rp2 = np.concatenate([[0], np.cumsum(np.where(keep, deg, 0))]).astype(np.int64)
+    col2 = np.concatenate([col[i * deg:(i + 1) * deg] for i in range(n) if keep[i]]).astype(np.int32)
+    ew = O.fill_uniform(len(col2), 16, 0.0, 1.0)
+    g = rv.Graph.from_csr(rp2, col2, ew)
+    monkeypatch.setenv("RVX_GNN_CHUNK_ROWS", "4096")
+    y = layer.forward_graph(x, g)
+    monkeypatch.delenv("RVX_GNN_CHUNK_ROWS")
+    assert np.array_equal(y, layer.forward_graph(x, g))  # one chunk: identical bits
+    for r0 in (0, 4000, 8100):
+        ref = O.rvl_forward_graph(W, x, rp2, col2, ew, rows=(r0, 200))
+        assert_close(y[r0:r0 + 200], ref)
+
+
 def test_differentiable_search_matches_oracle():
     # indices bit-exact; softmax weights within f32 tolerance (device expf vs
     # glibc expf differ by <= 1 ulp; cosine similarities are bit-exact)
