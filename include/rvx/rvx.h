@@ -310,6 +310,56 @@ rvx_status rvx_distance_matrix(int32_t metric, const float* q, int64_t nq, const
                                int32_t d, float curvature, float* out);
 
 /* ------------------------------------------------------------------ */
+/* HyperbolicHnsw: Poincaré-ball HNSW                                  */
+/* (crates/ruvector-hyperbolic-hnsw/src/hnsw.rs:127-528, tangent.rs)   */
+/* ------------------------------------------------------------------ */
+typedef struct rvx_hyperbolic rvx_hyperbolic;
+typedef struct {                 /* HyperbolicHnswConfig (hnsw.rs:36-72), metric Poincaré */
+    int32_t dim;
+    int32_t max_connections;     /* M, 16 */
+    int32_t max_connections_0;   /* M0 at layer 0, 32 (<= 64) */
+    int32_t ef_construction;     /* 200 */
+    int32_t ef_search;           /* 50 */
+    float   level_mult;          /* 1 / ln(16) */
+    float   curvature;           /* 1.0, > 0 */
+    int32_t prune_factor;        /* 10: search_with_pruning keeps k * prune_factor (<= 128) */
+    uint64_t seed;               /* level draws (the reference uses rand::random) */
+} rvx_hyperbolic_config;
+/* HyperbolicHnswConfig::default() with dim = 0 (set it). */
+void rvx_hyperbolic_default_config(rvx_hyperbolic_config* cfg);
+/* HyperbolicHnsw::new (hnsw.rs:142-150). curvature <= 0 -> RVX_ERR_INVALID_PARAMETER (InvalidCurvature). */
+rvx_status rvx_hyperbolic_create(const rvx_hyperbolic_config* cfg, rvx_hyperbolic** out);
+rvx_status rvx_hyperbolic_destroy(rvx_hyperbolic* h);
+/* The underlying graph index (borrowed; owned by h): rvx_index_graph_sizes /
+ * export_graph / load_graph / len work on it. */
+rvx_status rvx_hyperbolic_index(rvx_hyperbolic* h, rvx_index** out);
+/* insert / insert_batch (hnsw.rs:192-261): each vector is projected into the
+ * ball; ids are insertion order (first_id returns the first new id). Invalidates
+ * the tangent cache. */
+rvx_status rvx_hyperbolic_insert_batch(rvx_hyperbolic* h, const float* vecs, int64_t n, int64_t* first_id);
+rvx_status rvx_hyperbolic_insert_batch_device(rvx_hyperbolic* h, const rvx_buffer* vecs, int64_t n, int64_t* first_id);
+rvx_status rvx_hyperbolic_len(const rvx_hyperbolic* h, int64_t* len);
+/* search (hnsw.rs:400-423): ids [nq][k] (-1 past the end), distances ascending;
+ * ef = max(ef or ef_search when 0, k). */
+rvx_status rvx_hyperbolic_search(const rvx_hyperbolic* h, const float* q, int64_t nq, int32_t k, int32_t ef,
+                                 int64_t* ids, float* dist, int32_t* counts);
+/* search_with_pruning (hnsw.rs:425-483); without a tangent cache: search. */
+rvx_status rvx_hyperbolic_search_with_pruning(const rvx_hyperbolic* h, const float* q, int64_t nq, int32_t k,
+                                              int64_t* ids, float* dist, int32_t* counts);
+/* Exact scan by HyperbolicHnsw::distance (ground truth; k <= 16). */
+rvx_status rvx_hyperbolic_brute_force(const rvx_hyperbolic* h, const float* q, int64_t nq, int32_t k, int64_t* ids,
+                                      float* dist);
+/* HBM-resident queries/outputs; mode 0 search, 1 exact, 2 with pruning. */
+rvx_status rvx_hyperbolic_search_device(const rvx_hyperbolic* h, const rvx_buffer* q, int64_t nq, int32_t k, int32_t ef,
+                                        int32_t mode, rvx_buffer* ids_i64, rvx_buffer* dist);
+/* build_tangent_cache (hnsw.rs:485-497): Fréchet-mean centroid + log maps. */
+rvx_status rvx_hyperbolic_build_tangent_cache(rvx_hyperbolic* h);
+rvx_status rvx_hyperbolic_tangent_centroid(const rvx_hyperbolic* h, float* centroid);
+rvx_status rvx_hyperbolic_get_vector(const rvx_hyperbolic* h, int64_t id, float* out);
+/* set_curvature (hnsw.rs:505-528): reprojects all vectors, rebuilds an existing cache. */
+rvx_status rvx_hyperbolic_set_curvature(rvx_hyperbolic* h, float curvature);
+
+/* ------------------------------------------------------------------ */
 /* Profiling: per-kernel device time measured with HIP events on the   */
 /* stream the kernels run on.                                          */
 /* ------------------------------------------------------------------ */

@@ -16,12 +16,14 @@ from .core import (DistanceMetric, FlatIndex, HnswConfig, HnswIndex, RuvectorErr
 from .gnn import (GCNLayer, GnnError, GraphSAGELayer, RuvectorLayer, aggregate, differentiable_search,  # noqa: E402
                   differentiable_search_batch, hierarchical_forward)
 from .attention import EdgeFeaturedAttention, EdgeFeaturedConfig  # noqa: E402
+from .hyperbolic import (HyperbolicError, HyperbolicHnsw, HyperbolicHnswConfig,  # noqa: E402
+                         ShardedHyperbolicHnsw)
 
 __all__ = [
     "RvxError", "Buffer", "Profiler", "device_count", "device_info", "set_device", "synchronize", "Graph",
     "DistanceMetric", "FlatIndex", "HnswConfig", "HnswIndex", "RuvectorError", "SearchResult", "batch_distances",
     "distance", "distance_matrix", "GCNLayer", "GnnError", "GraphSAGELayer", "RuvectorLayer", "aggregate",
     "differentiable_search", "differentiable_search_batch", "hierarchical_forward", "EdgeFeaturedAttention",
-    "EdgeFeaturedConfig",
+    "EdgeFeaturedConfig", "HyperbolicError", "HyperbolicHnsw", "HyperbolicHnswConfig", "ShardedHyperbolicHnsw",
 ]
 __version__ = "0.1.0"

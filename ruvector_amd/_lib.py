@@ -50,6 +50,12 @@ class EdgeAttentionConfig(C.Structure):
                 ("concat_heads", C.c_int32), ("add_self_loops", C.c_int32), ("negative_slope", C.c_float)]
 
 
+class HyperbolicConfig(C.Structure):
+    _fields_ = [("dim", C.c_int32), ("max_connections", C.c_int32), ("max_connections_0", C.c_int32),
+                ("ef_construction", C.c_int32), ("ef_search", C.c_int32), ("level_mult", C.c_float),
+                ("curvature", C.c_float), ("prune_factor", C.c_int32), ("seed", C.c_uint64)]
+
+
 class HnswGraph(C.Structure):
     _fields_ = [("n", C.c_int64), ("max_level", C.c_int32), ("entry_point", C.c_int64),
                 ("levels", C.POINTER(C.c_uint8)), ("row_ptr0", C.POINTER(C.c_int64)),
@@ -124,6 +130,21 @@ SIGNATURES = {
     "rvx_index_brute_force": (None, [P, PF32, I64, I32, PU64, PF32]),
     "rvx_index_brute_force_device": (None, [P, P, I64, I32, P, P]),
     "rvx_index_load_graph": (None, [P, C.POINTER(HnswGraph)]),
+    "rvx_hyperbolic_default_config": (C.c_void_p, [C.POINTER(HyperbolicConfig)]),  # void
+    "rvx_hyperbolic_create": (None, [C.POINTER(HyperbolicConfig), PP]),
+    "rvx_hyperbolic_destroy": (None, [P]),
+    "rvx_hyperbolic_index": (None, [P, PP]),
+    "rvx_hyperbolic_insert_batch": (None, [P, PF32, I64, PI64]),
+    "rvx_hyperbolic_insert_batch_device": (None, [P, P, I64, PI64]),
+    "rvx_hyperbolic_len": (None, [P, PI64]),
+    "rvx_hyperbolic_search": (None, [P, PF32, I64, I32, I32, PI64, PF32, PI32]),
+    "rvx_hyperbolic_search_with_pruning": (None, [P, PF32, I64, I32, PI64, PF32, PI32]),
+    "rvx_hyperbolic_brute_force": (None, [P, PF32, I64, I32, PI64, PF32]),
+    "rvx_hyperbolic_search_device": (None, [P, P, I64, I32, I32, I32, P, P]),
+    "rvx_hyperbolic_build_tangent_cache": (None, [P]),
+    "rvx_hyperbolic_tangent_centroid": (None, [P, PF32]),
+    "rvx_hyperbolic_get_vector": (None, [P, I64, PF32]),
+    "rvx_hyperbolic_set_curvature": (None, [P, F32]),
     "rvx_index_graph_sizes": (None, [P, PI64, PI32, PI64, PI64, PI64, PI64]),
     "rvx_index_export_graph": (None, [P, C.POINTER(C.c_uint8), PI64, PI32, PI32, PI64, PI32]),
     "rvx_index_layer0_size": (None, [P, PI64, PI64]),

@@ -218,62 +218,11 @@ class HnswIndex(_Index):
 
     def load_graph(self, graph: dict) -> None:
         """Install a fixed HNSW graph (rvx_hnsw_graph layout; see oracle export)."""
-        n = int(graph["n"])
-        max_level = int(graph["max_level"])
-        levels = np.ascontiguousarray(graph["levels"], dtype=np.uint8)
-        rp0 = np.ascontiguousarray(graph["row_ptr0"], dtype=np.int64)
-        col0 = np.ascontiguousarray(graph["col0"], dtype=np.int32)
-        ucount = np.zeros(17, np.int64)
-        ids_l, rp_l, col_l = [], [], []
-        for l in range(1, max_level + 1):
-            ids_l.append(np.ascontiguousarray(graph["upper_ids"][l - 1], dtype=np.int32))
-            rp_l.append(np.ascontiguousarray(graph["upper_row_ptr"][l - 1], dtype=np.int64))
-            col_l.append(np.ascontiguousarray(graph["upper_col"][l - 1], dtype=np.int32))
-            ucount[l] = len(ids_l[-1])
-        dummy32 = np.zeros(1, np.int32)
-        dummy64 = np.zeros(1, np.int64)
-        P32 = C.POINTER(C.c_int32)
-        P64 = C.POINTER(C.c_int64)
-        ids_arr = (P32 * 17)(*([dummy32.ctypes.data_as(P32)] + [a.ctypes.data_as(P32) for a in ids_l] +
-                               [dummy32.ctypes.data_as(P32)] * (16 - max_level)))
-        rp_arr = (P64 * 17)(*([dummy64.ctypes.data_as(P64)] + [a.ctypes.data_as(P64) for a in rp_l] +
-                              [dummy64.ctypes.data_as(P64)] * (16 - max_level)))
-        col_arr = (P32 * 17)(*([dummy32.ctypes.data_as(P32)] + [a.ctypes.data_as(P32) for a in col_l] +
-                               [dummy32.ctypes.data_as(P32)] * (16 - max_level)))
-        g = L.HnswGraph(n=n, max_level=max_level, entry_point=int(graph["entry"]),
-                        levels=levels.ctypes.data_as(C.POINTER(C.c_uint8)), row_ptr0=L.i64ptr(rp0),
-                        col0=L.i32ptr(col0), upper_count=L.i64ptr(ucount),
-                        upper_ids=C.cast(ids_arr, C.POINTER(P32)), upper_row_ptr=C.cast(rp_arr, C.POINTER(P64)),
-                        upper_col=C.cast(col_arr, C.POINTER(P32)))
-        _check("rvx_index_load_graph", self._h, C.byref(g))
+        load_graph_handle(self._h, graph)
 
     def export_graph(self) -> dict:
         """The searchable graph in the rvx_hnsw_graph layout (same dict as load_graph takes)."""
-        n, ml, ent, e0 = C.c_int64(), C.c_int32(), C.c_int64(), C.c_int64()
-        uc = np.zeros(17, np.int64)
-        ue = np.zeros(17, np.int64)
-        _check("rvx_index_graph_sizes", self._h, C.byref(n), C.byref(ml), C.byref(ent), C.byref(e0), L.i64ptr(uc),
-               L.i64ptr(ue))
-        N, Lm = n.value, ml.value
-        levels = np.empty(max(N, 1), np.uint8)
-        rp0 = np.empty(N + 1, np.int64)
-        col0 = np.empty(max(e0.value, 1), np.int32)
-        ids = np.empty(max(int(uc.sum()), 1), np.int32)
-        rps = np.empty(max(int((uc[1:Lm + 1] + 1).sum()), 1), np.int64)
-        cols = np.empty(max(int(ue.sum()), 1), np.int32)
-        _check("rvx_index_export_graph", self._h, levels.ctypes.data_as(C.POINTER(C.c_uint8)), L.i64ptr(rp0),
-               L.i32ptr(col0), L.i32ptr(ids), L.i64ptr(rps), L.i32ptr(cols))
-        g = {"n": N, "max_level": Lm, "entry": ent.value, "levels": levels[:N], "row_ptr0": rp0,
-             "col0": col0[:e0.value], "upper_ids": [], "upper_row_ptr": [], "upper_col": []}
-        oi = orp = oc = 0
-        for l in range(1, Lm + 1):
-            c = int(uc[l])
-            g["upper_ids"].append(ids[oi:oi + c].copy())
-            rp = rps[orp:orp + c + 1].copy()
-            g["upper_row_ptr"].append(rp)
-            g["upper_col"].append(cols[oc:oc + int(rp[-1])].copy())
-            oi, orp, oc = oi + c, orp + c + 1, oc + int(rp[-1])
-        return g
+        return export_graph_handle(self._h)
 
     def layer0(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Layer-0 adjacency (row_ptr, col, edge distance) for the GNN."""
@@ -284,3 +233,63 @@ class HnswIndex(_Index):
         dist = np.empty(max(e.value, 1), np.float32)
         _check("rvx_index_export_layer0", self._h, L.i64ptr(rp), L.i32ptr(col), L.fptr(dist))
         return rp, col[:e.value], dist[:e.value]
+
+
+def load_graph_handle(handle, graph: dict) -> None:
+    """Install a fixed HNSW graph (rvx_hnsw_graph layout; see oracle export) on an rvx_index handle."""
+    n = int(graph["n"])
+    max_level = int(graph["max_level"])
+    levels = np.ascontiguousarray(graph["levels"], dtype=np.uint8)
+    rp0 = np.ascontiguousarray(graph["row_ptr0"], dtype=np.int64)
+    col0 = np.ascontiguousarray(graph["col0"], dtype=np.int32)
+    ucount = np.zeros(17, np.int64)
+    ids_l, rp_l, col_l = [], [], []
+    for l in range(1, max_level + 1):
+        ids_l.append(np.ascontiguousarray(graph["upper_ids"][l - 1], dtype=np.int32))
+        rp_l.append(np.ascontiguousarray(graph["upper_row_ptr"][l - 1], dtype=np.int64))
+        col_l.append(np.ascontiguousarray(graph["upper_col"][l - 1], dtype=np.int32))
+        ucount[l] = len(ids_l[-1])
+    dummy32 = np.zeros(1, np.int32)
+    dummy64 = np.zeros(1, np.int64)
+    P32 = C.POINTER(C.c_int32)
+    P64 = C.POINTER(C.c_int64)
+    ids_arr = (P32 * 17)(*([dummy32.ctypes.data_as(P32)] + [a.ctypes.data_as(P32) for a in ids_l] +
+                           [dummy32.ctypes.data_as(P32)] * (16 - max_level)))
+    rp_arr = (P64 * 17)(*([dummy64.ctypes.data_as(P64)] + [a.ctypes.data_as(P64) for a in rp_l] +
+                          [dummy64.ctypes.data_as(P64)] * (16 - max_level)))
+    col_arr = (P32 * 17)(*([dummy32.ctypes.data_as(P32)] + [a.ctypes.data_as(P32) for a in col_l] +
+                           [dummy32.ctypes.data_as(P32)] * (16 - max_level)))
+    g = L.HnswGraph(n=n, max_level=max_level, entry_point=int(graph["entry"]),
+                    levels=levels.ctypes.data_as(C.POINTER(C.c_uint8)), row_ptr0=L.i64ptr(rp0),
+                    col0=L.i32ptr(col0), upper_count=L.i64ptr(ucount),
+                    upper_ids=C.cast(ids_arr, C.POINTER(P32)), upper_row_ptr=C.cast(rp_arr, C.POINTER(P64)),
+                    upper_col=C.cast(col_arr, C.POINTER(P32)))
+    _check("rvx_index_load_graph", handle, C.byref(g))
+
+def export_graph_handle(handle) -> dict:
+    """The searchable graph of an rvx_index handle in the rvx_hnsw_graph layout."""
+    n, ml, ent, e0 = C.c_int64(), C.c_int32(), C.c_int64(), C.c_int64()
+    uc = np.zeros(17, np.int64)
+    ue = np.zeros(17, np.int64)
+    _check("rvx_index_graph_sizes", handle, C.byref(n), C.byref(ml), C.byref(ent), C.byref(e0), L.i64ptr(uc),
+           L.i64ptr(ue))
+    N, Lm = n.value, ml.value
+    levels = np.empty(max(N, 1), np.uint8)
+    rp0 = np.empty(N + 1, np.int64)
+    col0 = np.empty(max(e0.value, 1), np.int32)
+    ids = np.empty(max(int(uc.sum()), 1), np.int32)
+    rps = np.empty(max(int((uc[1:Lm + 1] + 1).sum()), 1), np.int64)
+    cols = np.empty(max(int(ue.sum()), 1), np.int32)
+    _check("rvx_index_export_graph", handle, levels.ctypes.data_as(C.POINTER(C.c_uint8)), L.i64ptr(rp0),
+           L.i32ptr(col0), L.i32ptr(ids), L.i64ptr(rps), L.i32ptr(cols))
+    g = {"n": N, "max_level": Lm, "entry": ent.value, "levels": levels[:N], "row_ptr0": rp0,
+         "col0": col0[:e0.value], "upper_ids": [], "upper_row_ptr": [], "upper_col": []}
+    oi = orp = oc = 0
+    for l in range(1, Lm + 1):
+        c = int(uc[l])
+        g["upper_ids"].append(ids[oi:oi + c].copy())
+        rp = rps[orp:orp + c + 1].copy()
+        g["upper_row_ptr"].append(rp)
+        g["upper_col"].append(cols[oc:oc + int(rp[-1])].copy())
+        oi, orp, oc = oi + c, orp + c + 1, oc + int(rp[-1])
+    return g

@@ -1,0 +1,343 @@
+// api_hyper.cpp — HyperbolicHnsw over HBM (crates/ruvector-hyperbolic-hnsw/src/hnsw.rs:127-504,
+// tangent.rs, poincare.rs). The graph lives in an rvx_index in hyperbolic mode:
+// the GPU builder and search kernels with the Poincaré metric and the
+// reference's insert/search rules (k_hnsw_build.hip / k_hnsw.hip, hyper = 1).
+#include <cmath>
+#include <shared_mutex>
+
+#include "graph.hpp"
+#include "hnsw.hpp"
+#include "hyper.hpp"
+#include "index.hpp"
+#include "kernels.hpp"
+#include "poincare_dev.hpp"
+#include "scan.hpp"
+
+using namespace rvx;
+
+struct rvx_hyperbolic {
+    rvx_hyperbolic_config cfg{};
+    rvx_index ix;
+};
+
+namespace {
+
+void invalidate_tangent(rvx_hyperbolic* h) { h->ix.tan_valid = false; }
+
+// HyperbolicHnsw::insert_batch (hnsw.rs:254-261): ids are insertion order
+void insert_rows(rvx_hyperbolic* h, const float* rows, int64_t n, bool on_device, int64_t* first_id) {
+    rvx_index* ix = &h->ix;
+    const int64_t n0 = ix->n;
+    if (first_id) *first_id = n0;
+    if (n <= 0) return;
+    std::vector<uint64_t> ids((size_t)n);
+    for (int64_t i = 0; i < n; ++i) ids[(size_t)i] = (uint64_t)(n0 + i);
+    index_append_rows(ix, rows, ids.data(), n, on_device);
+    // project_to_ball(&vector, curvature, EPS) before storing (hnsw.rs:195)
+    project_rows(ix->vecs.as<float>() + n0 * ix->cfg.dim, n, ix->cfg.dim, ix->curv);
+    hnsw_insert_range(ix, n0, n);
+    invalidate_tangent(h);
+}
+
+// queries projected into the ball (search / search_with_pruning, hnsw.rs:409, :449)
+float* projected_queries(const rvx_hyperbolic* h, const float* q, int64_t nq, bool on_device) {
+    const int d = h->ix.cfg.dim;
+    float* dq = scratch_f32("hyp_q", nq * d);
+    RVX_HIP(hipMemcpyAsync(dq, q, (size_t)(nq * d * 4), on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                           stream()));
+    project_rows(dq, nq, d, h->ix.curv);
+    return dq;
+}
+
+__global__ void k_rows_to_ids(const int64_t* rows, const float* dist, int64_t total, int64_t* ids, float* out_d) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int64_t r = rows[i];
+    const bool ok = r >= 0 && r != INT64_MAX;
+    ids[i] = ok ? r : -1;
+    out_d[i] = ok ? dist[i] : INFINITY;
+}
+
+void finish_ids(const int64_t* rows, const float* dist, int64_t nq, int k, int64_t* ids, float* out_d) {
+    const int64_t total = nq * k;
+    if (total <= 0) return;
+    hipLaunchKernelGGL(k_rows_to_ids, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream(), rows, dist, total,
+                       ids, out_d);
+    RVX_HIP(hipGetLastError());
+}
+
+// device search core; outputs on the device
+void search_dev(const rvx_hyperbolic* h, const float* dq, int64_t nq, int k, int ef, int64_t* ids, float* dist,
+                int32_t* counts, int mode /*0 graph, 1 exact, 2 pruned*/) {
+    const rvx_index* ix = &h->ix;
+    const int d = ix->cfg.dim;
+    auto* rows = (int64_t*)scratch_bytes("hyp_rows", nq * k * 8);
+    float* rd = scratch_f32("hyp_rd", nq * k);
+    if (ix->n == 0) {
+        RVX_HIP(hipMemsetAsync(rows, 0xFF, (size_t)(nq * k * 8), stream()));
+        if (counts) RVX_HIP(hipMemsetAsync(counts, 0, (size_t)(nq * 4), stream()));
+        finish_ids(rows, rd, nq, k, ids, dist);
+        return;
+    }
+    if (mode == 1) {
+        poincare_topk(dq, nq, ix->vecs.as<float>(), ix->n, d, ix->curv, k, rd, rows);
+        if (counts) {
+            std::vector<int32_t> c((size_t)nq, (int32_t)std::min<int64_t>(k, ix->n));
+            RVX_HIP(hipMemcpyAsync(counts, c.data(), (size_t)nq * 4, hipMemcpyHostToDevice, stream()));
+            sync();
+        }
+    } else if (mode == 2) {
+        // search_with_pruning (hnsw.rs:440-483): tangent-space L2 scan of every
+        // point, keep k * prune_factor, exact Poincaré re-rank
+        const int nc = (int)std::min<int64_t>((int64_t)k * h->cfg.prune_factor, ix->n);
+        RVX_REQUIRE(nc <= SCAN_MAX_K, RVX_ERR_UNSUPPORTED, "k * prune_factor must be <= 128");
+        float* qt = scratch_f32("hyp_qt", nq * d);
+        std::vector<float> cen((size_t)d);
+        ix->tan_centroid.download(cen.data(), (int64_t)d * 4);
+        log_map_rows(dq, nq, d, ix->tan_norms.as<float>(), pdev::norm_sq(cen.data(), d), ix->curv, qt);
+        float* cdist = scratch_f32("hyp_cand_d", nq * nc);
+        auto* cand = (int64_t*)scratch_bytes("hyp_cand_i", nq * nc * 8);
+        scan_topk(RVX_METRIC_L2, qt, nullptr, nq, ix->tan_coords.as<float>(), nullptr, nullptr, ix->n, d, nc, 0, cdist,
+                  cand, "hyp_tangent_scan");
+        rerank(dq, nq, ix->vecs.as<float>(), d, ix->curv, cand, nc, k, rd, rows, counts);
+    } else {
+        index_search_rows(ix, dq, nq, k, ef, rd, rows, counts, false);
+    }
+    finish_ids(rows, rd, nq, k, ids, dist);
+}
+
+// TangentCache::new (tangent.rs:47-73): centroid = frechet_mean (poincare.rs:463-538,
+// PoincareConfig defaults: max_iter 100, tol 1e-6, learning rate 0.1), then
+// log_centroid of every point. The gradient sums run on the GPU in a fixed
+// order (not the reference's point-major f32 order).
+void build_tangent(rvx_hyperbolic* h) {
+    rvx_index* ix = &h->ix;
+    const int64_t n = ix->n;
+    const int d = ix->cfg.dim;
+    RVX_REQUIRE(n > 0, RVX_ERR_INVALID_PARAMETER, "empty collection");
+    const float c = ix->curv;
+    const float w = 1.0f / (float)n;
+    const float* x = ix->vecs.as<float>();
+    float* dsum = scratch_f32("hyp_fm_sum", d);
+    std::vector<float> mean((size_t)d), grad((size_t)d), part((size_t)d), tmp((size_t)d), upd((size_t)d), negp((size_t)d);
+    col_sum(x, n, d, w, dsum);
+    RVX_HIP(hipMemcpyAsync(mean.data(), dsum, (size_t)d * 4, hipMemcpyDeviceToHost, stream()));
+    sync();
+    pdev::project_inplace(mean.data(), d, c, pdev::EPS);
+    const int64_t chunk = std::min<int64_t>(n, (int64_t)1 << 20);
+    float* logs = scratch_f32("hyp_fm_logs", chunk * d);
+    float* dnegp = scratch_f32("hyp_fm_negp", d);
+    for (int it = 0; it < 100; ++it) {
+        for (int i = 0; i < d; ++i) negp[(size_t)i] = -mean[(size_t)i];
+        RVX_HIP(hipMemcpyAsync(dnegp, negp.data(), (size_t)d * 4, hipMemcpyHostToDevice, stream()));
+        const float np_sq = pdev::norm_sq(mean.data(), d);
+        std::fill(grad.begin(), grad.end(), 0.0f);
+        for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+            const int64_t rows = std::min(chunk, n - r0);
+            log_map_rows(x + r0 * d, rows, d, dnegp, np_sq, c, logs);
+            col_sum(logs, rows, d, w, dsum);
+            RVX_HIP(hipMemcpyAsync(part.data(), dsum, (size_t)d * 4, hipMemcpyDeviceToHost, stream()));
+            sync();
+            for (int i = 0; i < d; ++i) grad[(size_t)i] = grad[(size_t)i] + part[(size_t)i];
+        }
+        if (std::sqrt(pdev::norm_sq(grad.data(), d)) < 1e-6f) break;
+        for (int i = 0; i < d; ++i) upd[(size_t)i] = 0.1f * grad[(size_t)i];
+        std::vector<float> next((size_t)d);
+        pdev::exp_map(upd.data(), mean.data(), d, c, next.data(), tmp.data());
+        mean.swap(next);
+    }
+    ix->tan_centroid.reset((int64_t)d * 4);
+    ix->tan_centroid.upload(mean.data(), (int64_t)d * 4);
+    for (int i = 0; i < d; ++i) negp[(size_t)i] = -mean[(size_t)i];
+    ix->tan_norms.reset((int64_t)d * 4);  // holds -centroid for the query log maps
+    ix->tan_norms.upload(negp.data(), (int64_t)d * 4);
+    ix->tan_coords.reset(std::max<int64_t>(n * d, 1) * 4);
+    log_map_rows(x, n, d, ix->tan_norms.as<float>(), pdev::norm_sq(mean.data(), d), c, ix->tan_coords.as<float>());
+    sync();
+    ix->tan_valid = true;
+}
+
+void check_cfg(const rvx_hyperbolic_config* c) {
+    RVX_REQUIRE(c->dim > 0, RVX_ERR_INVALID_PARAMETER, "dimension must be positive");
+    RVX_REQUIRE(c->max_connections >= 1 && c->max_connections <= 64 && c->max_connections_0 >= 1 &&
+                    c->max_connections_0 <= 64,
+                RVX_ERR_UNSUPPORTED, "max_connections / max_connections_0 must be in [1, 64]");
+    RVX_REQUIRE(c->ef_construction >= 1 && c->ef_construction <= HNSW_MAX_EF && c->ef_search >= 1,
+                RVX_ERR_INVALID_PARAMETER, "ef out of range");
+    RVX_REQUIRE(c->curvature > 0.0f, RVX_ERR_INVALID_PARAMETER, "invalid curvature (must be > 0)");
+    RVX_REQUIRE(c->level_mult > 0.0f && c->prune_factor >= 1, RVX_ERR_INVALID_PARAMETER, "bad level_mult / prune_factor");
+}
+
+}  // namespace
+
+extern "C" {
+
+void rvx_hyperbolic_default_config(rvx_hyperbolic_config* c) {
+    if (!c) return;
+    c->dim = 0;
+    c->max_connections = 16;
+    c->max_connections_0 = 32;
+    c->ef_construction = 200;
+    c->ef_search = 50;
+    c->level_mult = 1.0f / std::log(16.0f);
+    c->curvature = 1.0f;
+    c->prune_factor = 10;
+    c->seed = 0;
+}
+
+rvx_status rvx_hyperbolic_create(const rvx_hyperbolic_config* cfg, rvx_hyperbolic** out) {
+    return guard([&] {
+        RVX_REQUIRE(cfg && out, RVX_ERR_INVALID_PARAMETER, "null argument");
+        check_cfg(cfg);
+        auto h = std::make_unique<rvx_hyperbolic>();
+        h->cfg = *cfg;
+        rvx_index& ix = h->ix;
+        ix.cfg.kind = RVX_INDEX_HNSW;
+        ix.cfg.dim = cfg->dim;
+        ix.cfg.metric = RVX_METRIC_POINCARE;
+        ix.cfg.m = cfg->max_connections;
+        ix.cfg.ef_construction = cfg->ef_construction;
+        ix.cfg.ef_search = cfg->ef_search;
+        ix.cfg.seed = cfg->seed;
+        ix.cfg.curvature = cfg->curvature;
+        ix.hyper = true;
+        ix.m0 = cfg->max_connections_0;
+        ix.level_mult = cfg->level_mult;
+        ix.curv = cfg->curvature;
+        *out = h.release();
+    });
+}
+
+rvx_status rvx_hyperbolic_destroy(rvx_hyperbolic* h) {
+    return guard([&] { delete h; });
+}
+
+rvx_status rvx_hyperbolic_index(rvx_hyperbolic* h, rvx_index** out) {
+    return guard([&] {
+        RVX_REQUIRE(h && out, RVX_ERR_INVALID_PARAMETER, "null argument");
+        *out = &h->ix;
+    });
+}
+
+rvx_status rvx_hyperbolic_insert_batch(rvx_hyperbolic* h, const float* vecs, int64_t n, int64_t* first_id) {
+    return guard([&] {
+        RVX_REQUIRE(h && n >= 0 && (n == 0 || vecs), RVX_ERR_INVALID_PARAMETER, "bad arguments");
+        std::unique_lock<std::shared_mutex> lk(h->ix.mu);
+        ComputeLock cl;
+        insert_rows(h, vecs, n, false, first_id);
+    });
+}
+
+rvx_status rvx_hyperbolic_insert_batch_device(rvx_hyperbolic* h, const rvx_buffer* vecs, int64_t n, int64_t* first_id) {
+    return guard([&] {
+        RVX_REQUIRE(h && vecs && n >= 0, RVX_ERR_INVALID_PARAMETER, "bad arguments");
+        RVX_REQUIRE(vecs->mem.bytes >= n * h->cfg.dim * 4, RVX_ERR_DIMENSION_MISMATCH, "buffer smaller than n*dim");
+        std::unique_lock<std::shared_mutex> lk(h->ix.mu);
+        ComputeLock cl;
+        insert_rows(h, vecs->mem.as<float>(), n, true, first_id);
+    });
+}
+
+rvx_status rvx_hyperbolic_len(const rvx_hyperbolic* h, int64_t* len) {
+    return guard([&] {
+        RVX_REQUIRE(h && len, RVX_ERR_INVALID_PARAMETER, "null argument");
+        *len = h->ix.n;
+    });
+}
+
+static rvx_status hyp_search_host(const rvx_hyperbolic* h, const float* q, int64_t nq, int32_t k, int32_t ef,
+                                  int64_t* ids, float* dist, int32_t* counts, int mode) {
+    return guard([&] {
+        RVX_REQUIRE(h && nq >= 0 && k >= 1 && (nq == 0 || (q && ids && dist)), RVX_ERR_INVALID_PARAMETER,
+                    "bad search arguments");
+        if (nq == 0) return;
+        std::shared_lock<std::shared_mutex> lk(h->ix.mu);
+        ComputeLock cl;
+        const int m = (mode == 2 && !h->ix.tan_valid) ? 0 : mode;  // no cache -> regular search (hnsw.rs:441-444)
+        float* dq = projected_queries(h, q, nq, false);
+        auto* di = (int64_t*)scratch_bytes("hyp_out_i", nq * k * 8);
+        float* dd = scratch_f32("hyp_out_d", nq * k);
+        int32_t* dn = counts ? (int32_t*)scratch_bytes("hyp_out_n", nq * 4) : nullptr;
+        search_dev(h, dq, nq, k, ef, di, dd, dn, m);
+        RVX_HIP(hipMemcpyAsync(ids, di, (size_t)(nq * k * 8), hipMemcpyDeviceToHost, stream()));
+        RVX_HIP(hipMemcpyAsync(dist, dd, (size_t)(nq * k * 4), hipMemcpyDeviceToHost, stream()));
+        if (counts) RVX_HIP(hipMemcpyAsync(counts, dn, (size_t)(nq * 4), hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
+rvx_status rvx_hyperbolic_search(const rvx_hyperbolic* h, const float* q, int64_t nq, int32_t k, int32_t ef,
+                                 int64_t* ids, float* dist, int32_t* counts) {
+    return hyp_search_host(h, q, nq, k, ef, ids, dist, counts, 0);
+}
+
+rvx_status rvx_hyperbolic_search_with_pruning(const rvx_hyperbolic* h, const float* q, int64_t nq, int32_t k,
+                                              int64_t* ids, float* dist, int32_t* counts) {
+    return hyp_search_host(h, q, nq, k, 0, ids, dist, counts, 2);
+}
+
+rvx_status rvx_hyperbolic_brute_force(const rvx_hyperbolic* h, const float* q, int64_t nq, int32_t k, int64_t* ids,
+                                      float* dist) {
+    return hyp_search_host(h, q, nq, k, 0, ids, dist, nullptr, 1);
+}
+
+rvx_status rvx_hyperbolic_search_device(const rvx_hyperbolic* h, const rvx_buffer* q, int64_t nq, int32_t k, int32_t ef,
+                                        int32_t mode, rvx_buffer* ids, rvx_buffer* dist) {
+    return guard([&] {
+        RVX_REQUIRE(h && q && ids && dist && nq >= 0 && k >= 1 && mode >= 0 && mode <= 2, RVX_ERR_INVALID_PARAMETER,
+                    "bad search arguments");
+        RVX_REQUIRE(q->mem.bytes >= nq * h->cfg.dim * 4 && ids->mem.bytes >= nq * k * 8 && dist->mem.bytes >= nq * k * 4,
+                    RVX_ERR_DIMENSION_MISMATCH, "buffer too small");
+        if (nq == 0) return;
+        std::shared_lock<std::shared_mutex> lk(h->ix.mu);
+        ComputeLock cl;
+        const int m = (mode == 2 && !h->ix.tan_valid) ? 0 : mode;
+        float* dq = projected_queries(h, q->mem.as<float>(), nq, true);
+        search_dev(h, dq, nq, k, ef, ids->mem.as<int64_t>(), dist->mem.as<float>(), nullptr, m);
+    });
+}
+
+rvx_status rvx_hyperbolic_build_tangent_cache(rvx_hyperbolic* h) {
+    return guard([&] {
+        RVX_REQUIRE(h, RVX_ERR_INVALID_PARAMETER, "null argument");
+        std::unique_lock<std::shared_mutex> lk(h->ix.mu);
+        if (h->ix.n == 0) return;  // build_tangent_cache: Ok(()) on an empty index (hnsw.rs:487-489)
+        ComputeLock cl;
+        build_tangent(h);
+    });
+}
+
+rvx_status rvx_hyperbolic_tangent_centroid(const rvx_hyperbolic* h, float* centroid) {
+    return guard([&] {
+        RVX_REQUIRE(h && centroid, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(h->ix.tan_valid, RVX_ERR_NOT_FOUND, "no tangent cache");
+        h->ix.tan_centroid.download(centroid, (int64_t)h->cfg.dim * 4);
+    });
+}
+
+rvx_status rvx_hyperbolic_get_vector(const rvx_hyperbolic* h, int64_t id, float* out) {
+    return guard([&] {
+        RVX_REQUIRE(h && out, RVX_ERR_INVALID_PARAMETER, "null argument");
+        std::shared_lock<std::shared_mutex> lk(h->ix.mu);
+        RVX_REQUIRE(id >= 0 && id < h->ix.n, RVX_ERR_NOT_FOUND, "no such id");
+        h->ix.vecs.download(out, (int64_t)h->cfg.dim * 4, id * h->cfg.dim * 4);
+    });
+}
+
+rvx_status rvx_hyperbolic_set_curvature(rvx_hyperbolic* h, float curvature) {
+    return guard([&] {
+        RVX_REQUIRE(h, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(curvature > 0.0f, RVX_ERR_INVALID_PARAMETER, "invalid curvature (must be > 0)");
+        std::unique_lock<std::shared_mutex> lk(h->ix.mu);
+        ComputeLock cl;
+        // set_curvature (hnsw.rs:510-528): reproject every vector, rebuild an existing cache
+        h->cfg.curvature = curvature;
+        h->ix.curv = curvature;
+        h->ix.cfg.curvature = curvature;
+        project_rows(h->ix.vecs.as<float>(), h->ix.n, h->cfg.dim, curvature);
+        sync();
+        if (h->ix.tan_valid) build_tangent(h);
+    });
+}
+
+}  // extern "C"

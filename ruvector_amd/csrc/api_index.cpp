@@ -7,6 +7,7 @@
 
 #include "graph.hpp"
 #include "hnsw.hpp"
+#include "hyper.hpp"
 #include "index.hpp"
 #include "kernels.hpp"
 #include "scan.hpp"
@@ -80,6 +81,10 @@ void search_rows(const rvx_index* ix, const float* q, int64_t nq, int k, int ef,
         qn = scratch_f32("index_qnorm", nq);
         row_norms(q, nq, d, qn);
     }
+    if (exact && ix->cfg.metric == RVX_METRIC_POINCARE) {
+        poincare_topk(q, nq, ix->vecs.as<float>(), ix->n, d, ix->curv, k, dd, di);
+        return;
+    }
     if (exact || ix->cfg.kind == RVX_INDEX_FLAT) {
         scan_topk(ix->cfg.metric, q, qn, nq, ix->vecs.as<float>(), ix->norms.as<float>(),
                   ix->cfg.kind == RVX_INDEX_FLAT ? ix->deleted.as<uint8_t>() : nullptr, ix->n, d, k, 0, dd, di,
@@ -90,7 +95,7 @@ void search_rows(const rvx_index* ix, const float* q, int64_t nq, int k, int ef,
                 "HNSW graph missing or stale");
     const int e = std::max(ef > 0 ? ef : ix->cfg.ef_search, k);  // ef = max(ef_arg, knbn) (hnsw.rs:1519)
     hnsw_search(ix->g, ix->cfg.metric, ix->vecs.as<float>(), ix->norms.as<float>(), d, q, qn, nq, k, e, dd, di, dn,
-                "hnsw_search");
+                "hnsw_search", ix->curv, ix->hyper ? 1 : 0);
 }
 
 void map_out(const rvx_index* ix, const int64_t* di, const float* dd, int64_t nq, int k, uint64_t* oi, float* od,
@@ -106,6 +111,66 @@ void check_query_args(const rvx_index* ix, int64_t nq, int k) {
 }
 
 }  // namespace
+
+namespace rvx {
+
+void index_append_rows(rvx_index* ix, const float* rows, const uint64_t* ids, int64_t cnt, bool rows_on_device) {
+    append_rows(ix, rows, ids, cnt, rows_on_device);
+}
+
+void index_search_rows(const rvx_index* ix, const float* q, int64_t nq, int k, int ef, float* dd, int64_t* di,
+                       int32_t* dn, bool exact) {
+    search_rows(ix, q, nq, k, ef, dd, di, dn, exact);
+}
+
+// Validate a caller's graph and make it the searchable graph (caller holds ix->mu).
+void index_load_graph(rvx_index* ix, const rvx_hnsw_graph* hg) {
+    RVX_REQUIRE(hg->n == ix->n, RVX_ERR_DIMENSION_MISMATCH, "graph size != number of stored vectors");
+    RVX_REQUIRE(hg->max_level >= 0 && hg->max_level <= HNSW_MAX_LEVEL, RVX_ERR_INVALID_PARAMETER, "bad max_level");
+    RVX_REQUIRE(hg->n == 0 || (hg->entry_point >= 0 && hg->entry_point < hg->n), RVX_ERR_INDEX, "bad entry point");
+    const int64_t n = hg->n;
+    HostGraph h;
+    h.n = n;
+    h.max_level = hg->max_level;
+    h.entry = hg->entry_point;
+    h.levels.assign(hg->levels, hg->levels + n);
+    h.rp0.assign(hg->row_ptr0, hg->row_ptr0 + n + 1);
+    RVX_REQUIRE(h.rp0[0] == 0, RVX_ERR_INDEX, "row_ptr0[0] must be 0");
+    // validate layer 0: ids in range, no duplicate inside a list
+    std::vector<int64_t> mark(n, -1);
+    for (int64_t i = 0; i < n; ++i) {
+        RVX_REQUIRE(h.rp0[i + 1] >= h.rp0[i], RVX_ERR_INDEX, "row_ptr0 must be non-decreasing");
+        for (int64_t p = h.rp0[i]; p < h.rp0[i + 1]; ++p) {
+            const int32_t c = hg->col0[p];
+            RVX_REQUIRE(c >= 0 && c < n, RVX_ERR_INDEX, "layer-0 neighbour out of range");
+            RVX_REQUIRE(mark[c] != i, RVX_ERR_INDEX, "duplicate neighbour in a layer-0 list");
+            mark[c] = i;
+        }
+    }
+    h.col0.assign(hg->col0, hg->col0 + h.rp0[n]);
+    h.up_ids.assign(h.max_level + 1, {});
+    h.up_rp.assign(h.max_level + 1, {});
+    h.up_col.assign(h.max_level + 1, {});
+    for (int l = 1; l <= h.max_level; ++l) {
+        const int64_t cnt = hg->upper_count[l];
+        for (int64_t i = 0; i < cnt; ++i) {
+            RVX_REQUIRE(i == 0 || hg->upper_ids[l][i] > hg->upper_ids[l][i - 1], RVX_ERR_INDEX,
+                        "upper-layer ids must be strictly increasing");
+            RVX_REQUIRE(hg->upper_ids[l][i] >= 0 && hg->upper_ids[l][i] < n, RVX_ERR_INDEX, "upper id out of range");
+        }
+        h.up_ids[l].assign(hg->upper_ids[l], hg->upper_ids[l] + cnt);
+        h.up_rp[l].assign(hg->upper_row_ptr[l], hg->upper_row_ptr[l] + cnt + 1);
+        const int64_t ec = h.up_rp[l][cnt];
+        for (int64_t p = 0; p < ec; ++p)
+            RVX_REQUIRE(hg->upper_col[l][p] >= 0 && hg->upper_col[l][p] < n, RVX_ERR_INDEX, "upper neighbour out of range");
+        h.up_col[l].assign(hg->upper_col[l], hg->upper_col[l] + ec);
+    }
+    ComputeLock cl;
+    ix->build_valid = false;
+    hnsw_install(ix, std::move(h));
+}
+
+}  // namespace rvx
 
 extern "C" {
 
@@ -271,49 +336,7 @@ rvx_status rvx_index_load_graph(rvx_index* ix, const rvx_hnsw_graph* hg) {
         RVX_REQUIRE(ix && hg, RVX_ERR_INVALID_PARAMETER, "null argument");
         RVX_REQUIRE(ix->cfg.kind == RVX_INDEX_HNSW, RVX_ERR_INVALID_PARAMETER, "not an HNSW index");
         std::unique_lock<std::shared_mutex> lk(ix->mu);
-        RVX_REQUIRE(hg->n == ix->n, RVX_ERR_DIMENSION_MISMATCH, "graph size != number of stored vectors");
-        RVX_REQUIRE(hg->max_level >= 0 && hg->max_level <= HNSW_MAX_LEVEL, RVX_ERR_INVALID_PARAMETER, "bad max_level");
-        RVX_REQUIRE(hg->n == 0 || (hg->entry_point >= 0 && hg->entry_point < hg->n), RVX_ERR_INDEX, "bad entry point");
-        const int64_t n = hg->n;
-        HostGraph h;
-        h.n = n;
-        h.max_level = hg->max_level;
-        h.entry = hg->entry_point;
-        h.levels.assign(hg->levels, hg->levels + n);
-        h.rp0.assign(hg->row_ptr0, hg->row_ptr0 + n + 1);
-        RVX_REQUIRE(h.rp0[0] == 0, RVX_ERR_INDEX, "row_ptr0[0] must be 0");
-        // validate layer 0: ids in range, no duplicate inside a list
-        std::vector<int64_t> mark(n, -1);
-        for (int64_t i = 0; i < n; ++i) {
-            RVX_REQUIRE(h.rp0[i + 1] >= h.rp0[i], RVX_ERR_INDEX, "row_ptr0 must be non-decreasing");
-            for (int64_t p = h.rp0[i]; p < h.rp0[i + 1]; ++p) {
-                const int32_t c = hg->col0[p];
-                RVX_REQUIRE(c >= 0 && c < n, RVX_ERR_INDEX, "layer-0 neighbour out of range");
-                RVX_REQUIRE(mark[c] != i, RVX_ERR_INDEX, "duplicate neighbour in a layer-0 list");
-                mark[c] = i;
-            }
-        }
-        h.col0.assign(hg->col0, hg->col0 + h.rp0[n]);
-        h.up_ids.assign(h.max_level + 1, {});
-        h.up_rp.assign(h.max_level + 1, {});
-        h.up_col.assign(h.max_level + 1, {});
-        for (int l = 1; l <= h.max_level; ++l) {
-            const int64_t cnt = hg->upper_count[l];
-            for (int64_t i = 0; i < cnt; ++i) {
-                RVX_REQUIRE(i == 0 || hg->upper_ids[l][i] > hg->upper_ids[l][i - 1], RVX_ERR_INDEX,
-                            "upper-layer ids must be strictly increasing");
-                RVX_REQUIRE(hg->upper_ids[l][i] >= 0 && hg->upper_ids[l][i] < n, RVX_ERR_INDEX, "upper id out of range");
-            }
-            h.up_ids[l].assign(hg->upper_ids[l], hg->upper_ids[l] + cnt);
-            h.up_rp[l].assign(hg->upper_row_ptr[l], hg->upper_row_ptr[l] + cnt + 1);
-            const int64_t ec = h.up_rp[l][cnt];
-            for (int64_t p = 0; p < ec; ++p)
-                RVX_REQUIRE(hg->upper_col[l][p] >= 0 && hg->upper_col[l][p] < n, RVX_ERR_INDEX, "upper neighbour out of range");
-            h.up_col[l].assign(hg->upper_col[l], hg->upper_col[l] + ec);
-        }
-        ComputeLock cl;
-        ix->build_valid = false;
-        hnsw_install(ix, std::move(h));
+        index_load_graph(ix, hg);
     });
 }
 

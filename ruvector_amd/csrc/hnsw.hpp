@@ -24,8 +24,10 @@ struct HnswDev {
     int64_t up_col_off[HNSW_MAX_LEVEL + 1] = {};
 };
 
+// hyper != 0: HyperbolicHnsw::search semantics (iterated greedy upper descent,
+// layer-0 stop also needs |R| >= ef); curv: Poincaré curvature.
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
                  const float* qnorm, int64_t nq, int k, int ef, float* out_d, int64_t* out_i, int32_t* out_n,
-                 const char* tag);
+                 const char* tag, float curv = 1.0f, int hyper = 0);
 
 }  // namespace rvx

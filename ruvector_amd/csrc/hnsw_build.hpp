@@ -6,8 +6,8 @@ namespace rvx {
 
 struct BuildGraph {
     int64_t n_cap = 0;     // capacity of the layer-0 arrays; upper list keys start here
-    int M = 0, C0 = 0;     // capacity M above layer 0, 2M at layer 0
-    int max_layer = 0;     // min(16, dim) as ruvector-core wires it (index/hnsw.rs:102-108)
+    int M = 0, C0 = 0;     // capacity M above layer 0, C0 at layer 0 (2M for hnsw_rs, M0 for HyperbolicHnsw)
+    int max_layer = 0;     // min(16, dim) as ruvector-core wires it (index/hnsw.rs:102-108); 16 hyperbolic
     const uint8_t* level = nullptr;   // [n_cap]
     int* nb0 = nullptr;               // [n_cap][C0]
     float* nbd0 = nullptr;            // [n_cap][C0] distance to the owner
@@ -22,8 +22,11 @@ struct BuildScratch {
     int* rev_head = nullptr;  // [n_cap + U] chain heads of reverse edges, -1 when idle
 };
 
+// hyper != 0: HyperbolicHnsw::insert rules (hnsw.rs:192-251): the closest
+// max_conn of the ef_c search (no heuristic), reverse edge into the neighbour's
+// list at the CURRENT level, pruned to its max_conn closest.
 void build_insert_batch(const BuildGraph& G, int metric, const float* x, const float* xnorm, int d,
                         int64_t batch_begin, int batch_n, int entry, int entry_level, unsigned nonempty_mask, int ef_c,
-                        BuildScratch& s);
+                        BuildScratch& s, float curv = 1.0f, int hyper = 0);
 
 }  // namespace rvx

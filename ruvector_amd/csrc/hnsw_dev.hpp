@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "poincare_dev.hpp"
 #include "rvx/rvx.h"
 
 namespace rvx {
@@ -12,9 +13,12 @@ namespace hnswdev {
 constexpr int VCAP_MIN = 32768;  // visited-set slots per query (power of two), grown with ef
 constexpr int C_EXTRA = 128; // candidate capacity = ef + C_EXTRA
 
+// curv: the Poincaré curvature (RVX_METRIC_POINCARE only: HyperbolicHnsw::distance,
+// fused norms + poincare_distance_from_norms, hnsw.rs:173-180)
 template <int METRIC>
 __device__ __forceinline__ float row_dist(const float* __restrict__ qs, const float* __restrict__ x, int d, float qn,
-                                          float xn) {
+                                          float xn, float curv = 1.0f) {
+    if constexpr (METRIC == RVX_METRIC_POINCARE) return pdev::hyp_dist(qs, x, d, curv);
     float acc = 0.0f;
     if ((d & 3) == 0) {
         const float4* r = reinterpret_cast<const float4*>(x);
@@ -108,8 +112,8 @@ __device__ __forceinline__ int sorted_insert(float* ad, int* ai, int size, float
 // distance between two stored rows, reference scalar order (distance.rs)
 template <int METRIC>
 __device__ __forceinline__ float pair_dist(const float* __restrict__ a, const float* __restrict__ b, int d, float na,
-                                           float nb) {
-    return row_dist<METRIC>(a, b, d, na, nb);
+                                           float nb, float curv = 1.0f) {
+    return row_dist<METRIC>(a, b, d, na, nb, curv);
 }
 
 }  // namespace hnswdev

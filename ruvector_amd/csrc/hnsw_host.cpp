@@ -35,8 +35,8 @@ BuildGraph build_view(rvx_index* ix) {
     BuildGraph G;
     G.n_cap = ix->bn_cap;
     G.M = ix->cfg.m;
-    G.C0 = 2 * ix->cfg.m;
-    G.max_layer = std::min(16, ix->cfg.dim);
+    G.C0 = ix->hyper ? ix->m0 : 2 * ix->cfg.m;
+    G.max_layer = ix->hyper ? HNSW_MAX_LEVEL : std::min(16, ix->cfg.dim);
     G.level = ix->b_level.as<uint8_t>();
     G.nb0 = ix->b_nb0.as<int>();
     G.nbd0 = ix->b_nbd0.as<float>();
@@ -49,7 +49,7 @@ BuildGraph build_view(rvx_index* ix) {
 }
 
 HostGraph build_to_host(rvx_index* ix, int64_t n) {
-    const int M = ix->cfg.m, C0 = 2 * M;
+    const int M = ix->cfg.m, C0 = ix->hyper ? ix->m0 : 2 * M;
     HostGraph hg;
     hg.n = n;
     hg.max_level = std::max(0, ix->entry_level);
@@ -106,6 +106,14 @@ int hnsw_level(uint64_t seed, int m, int max_layer, int64_t i) {
     return (int)ul;
 }
 
+int hyper_level(uint64_t seed, float level_mult, int64_t i) {
+    // r in (0, 1]: rand::random::<f32>() is [0, 1); r = 0 would give an
+    // unbounded level, capped like every level at the storage limit
+    const float r = (float)((sm64(sm64(seed) + (uint64_t)i) >> 40) + 1) * (1.0f / 16777216.0f);
+    const float lev = -std::log(r) * level_mult;
+    return (int)std::min<float>(std::floor(lev), (float)(HNSW_MAX_LEVEL - 1));
+}
+
 void hnsw_install(rvx_index* ix, HostGraph&& hg) {
     const int64_t n = hg.n;
     HnswDev g;
@@ -147,14 +155,15 @@ void hnsw_install(rvx_index* ix, HostGraph&& hg) {
 void hnsw_insert_range(rvx_index* ix, int64_t first, int64_t count) {
     RVX_REQUIRE(ix->build_valid, RVX_ERR_UNSUPPORTED,
                 "adding vectors to an HNSW index whose graph was loaded with rvx_index_load_graph is not supported");
-    RVX_REQUIRE(ix->cfg.m <= 32, RVX_ERR_UNSUPPORTED, "GPU HNSW construction supports m <= 32");
+    RVX_REQUIRE(ix->hyper ? (ix->cfg.m <= 64 && ix->m0 <= 64) : ix->cfg.m <= 32, RVX_ERR_UNSUPPORTED,
+                "GPU HNSW construction supports lists of <= 64 neighbours");
     RVX_REQUIRE(ix->cfg.metric != RVX_METRIC_DOT, RVX_ERR_INVALID_PARAMETER, "DotProduct cannot be used with HNSW");
     if (count <= 0) return;
-    const int M = ix->cfg.m, C0 = 2 * M, max_layer = std::min(16, ix->cfg.dim);
+    const int M = ix->cfg.m, C0 = ix->hyper ? ix->m0 : 2 * M, max_layer = std::min(16, ix->cfg.dim);
     const int64_t end = first + count;
     RVX_REQUIRE(end < ((int64_t)1 << 31) - 1, RVX_ERR_INVALID_SHAPE, "too many points");
     for (int64_t i = first; i < end; ++i) {
-        const int lev = hnsw_level(ix->cfg.seed, M, max_layer, i);
+        const int lev = ix->hyper ? hyper_level(ix->cfg.seed, ix->level_mult, i) : hnsw_level(ix->cfg.seed, M, max_layer, i);
         ix->h_level.push_back((uint8_t)lev);
         if (lev > 0) {
             ix->h_up_base.push_back(ix->n_upper);
@@ -198,8 +207,12 @@ void hnsw_insert_range(rvx_index* ix, int64_t first, int64_t count) {
         b = std::min(b, end - i);
         unsigned mask = ix->level_mask;
         for (int64_t p = i; p < i + b; ++p) mask |= 1u << ix->h_level[p];
+        // HyperbolicHnsw::search_layer has no per-layer emptiness test: every
+        // layer up to max_level holds the entry point
+        const unsigned search_mask = ix->hyper ? 0xFFFFFFFFu : mask;
         build_insert_batch(G, ix->cfg.metric, ix->vecs.as<float>(), ix->norms.as<float>(), ix->cfg.dim, i, (int)b,
-                           ix->entry, ix->entry_level, mask, ix->cfg.ef_construction, S);
+                           ix->entry, ix->entry_level, search_mask, ix->cfg.ef_construction, S, ix->curv,
+                           ix->hyper ? 1 : 0);
         for (int64_t p = i; p < i + b; ++p)  // check_entry_point (hnsw.rs:529-552), first higher level wins
             if ((int)ix->h_level[p] > ix->entry_level) { ix->entry = (int)p; ix->entry_level = ix->h_level[p]; }
         ix->level_mask = mask;

@@ -1,0 +1,20 @@
+// hyper.hpp — launchers of the HyperbolicHnsw kernels (k_hyper.hip).
+#pragma once
+#include <cstdint>
+
+namespace rvx {
+
+// project_to_ball of every row of x [n][d] in place (eps = poincare EPS)
+void project_rows(float* x, int64_t n, int d, float c);
+// exact top-k (k <= 16) of every query by HyperbolicHnsw::distance, ascending (distance, row)
+void poincare_topk(const float* q, int64_t nq, const float* x, int64_t n, int d, float c, int k, float* out_d,
+                   int64_t* out_i);
+// out[r] = log_p(x[r]) given -p (device) and |p|^2
+void log_map_rows(const float* x, int64_t n, int d, const float* negp_dev, float np_sq, float c, float* out);
+// out[j] = sum_i w * rows[i][j] (deterministic order)
+void col_sum(const float* rows, int64_t n, int d, float w, float* out);
+// exact Poincaré re-rank of nc candidates per query (ids, -1 = none), first k ascending
+void rerank(const float* q, int64_t nq, const float* x, int d, float c, const int64_t* cand, int nc, int k,
+            float* out_d, int64_t* out_i, int32_t* out_n);
+
+}  // namespace rvx

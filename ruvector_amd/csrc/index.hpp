@@ -54,6 +54,15 @@ struct rvx_index {
     int entry = -1, entry_level = -1;
     unsigned level_mask = 0;
 
+    // HyperbolicHnsw mode (crates/ruvector-hyperbolic-hnsw/src/hnsw.rs): Poincaré
+    // metric with curvature `curv`, M0 lists at layer 0, level = floor(-ln r * level_mult)
+    bool hyper = false;
+    int m0 = 0;
+    float level_mult = 0.0f, curv = 1.0f;
+    // TangentCache (tangent.rs:24-40): Fréchet-mean centroid + log-map coordinates
+    bool tan_valid = false;
+    rvx::DevMem tan_centroid, tan_coords, tan_norms;
+
     mutable std::shared_mutex mu;
 };
 
@@ -64,4 +73,12 @@ void hnsw_insert_range(rvx_index* ix, int64_t first, int64_t count);
 void hnsw_install(rvx_index* ix, HostGraph&& hg);
 // hnsw_rs level of point i (seeded LayerGenerator::generate, hnsw.rs:358-369).
 int hnsw_level(uint64_t seed, int m, int max_layer, int64_t i);
+// HyperbolicHnsw::random_level (hyperbolic hnsw.rs:186-189) from the same seeded stream.
+int hyper_level(uint64_t seed, float level_mult, int64_t i);
+
+// index plumbing shared by the VectorIndex and HyperbolicHnsw entry points (api_index.cpp)
+void index_append_rows(rvx_index* ix, const float* rows, const uint64_t* ids, int64_t cnt, bool rows_on_device);
+void index_search_rows(const rvx_index* ix, const float* q, int64_t nq, int k, int ef, float* dd, int64_t* di,
+                       int32_t* dn, bool exact);
+void index_load_graph(rvx_index* ix, const rvx_hnsw_graph* hg);
 }  // namespace rvx

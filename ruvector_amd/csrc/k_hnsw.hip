@@ -40,6 +40,8 @@ struct SearchArgs {
     unsigned vcap;
     float* out_d; int64_t* out_i; int32_t* out_n;  // [nq][k]
     int* status;       // set to 1 on candidate overflow
+    float curv;        // Poincaré curvature
+    int hyper;         // HyperbolicHnsw::search semantics (see below)
 };
 
 template <int METRIC>
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
         const float qn = (METRIC == RVX_METRIC_COSINE) ? a.qnorm[qi] : 0.0f;
         auto dist_of = [&](int node) {
             return row_dist<METRIC>(qs, a.x + (int64_t)node * a.d, a.d,
-                                    qn, METRIC == RVX_METRIC_COSINE ? a.xnorm[node] : 0.0f);
+                                    qn, METRIC == RVX_METRIC_COSINE ? a.xnorm[node] : 0.0f, a.curv);
         };
 
         // ---- upper layers: single pass per layer (search_filter :1499-1517)
@@ -81,25 +83,36 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
             if (lo >= cnt || ids[lo] != pivot) continue;  // pivot not on this layer (cannot happen for a valid graph)
             const int64_t* rp = a.g.up_rp + a.g.up_rp_off[l];
             const int* col = a.g.up_col + a.g.up_col_off[l];
-            const int64_t b = rp[lo], e = rp[lo + 1];
-            int new_pivot = pivot;
-            float new_best = best;
-            for (int64_t c0 = b; c0 < e; c0 += 64) {
-                const int64_t p = c0 + lane;
-                float dd = INFINITY;
-                int pos = INT_MAX, nid = -1;
-                if (p < e) { nid = col[p]; dd = dist_of(nid); pos = (int)(p - b); }
-                // first position holding the minimum of this chunk
+            bool moved;
+            do {
+                const int64_t b = rp[lo], e = rp[lo + 1];
+                int new_pivot = pivot;
+                float new_best = best;
+                for (int64_t c0 = b; c0 < e; c0 += 64) {
+                    const int64_t p = c0 + lane;
+                    float dd = INFINITY;
+                    int pos = INT_MAX, nid = -1;
+                    if (p < e) { nid = col[p]; dd = dist_of(nid); pos = (int)(p - b); }
+                    // first position holding the minimum of this chunk
 #pragma unroll
-                for (int o = 32; o > 0; o >>= 1) {
-                    const float od = __shfl_xor(dd, o);
-                    const int op = __shfl_xor(pos, o), on = __shfl_xor(nid, o);
-                    if (od < dd || (od == dd && op < pos)) { dd = od; pos = op; nid = on; }
+                    for (int o = 32; o > 0; o >>= 1) {
+                        const float od = __shfl_xor(dd, o);
+                        const int op = __shfl_xor(pos, o), on = __shfl_xor(nid, o);
+                        if (od < dd || (od == dd && op < pos)) { dd = od; pos = op; nid = on; }
+                    }
+                    if (dd < new_best) { new_best = dd; new_pivot = nid; }
                 }
-                if (dd < new_best) { new_best = dd; new_pivot = nid; }
-            }
-            pivot = new_pivot;
-            best = new_best;
+                moved = new_pivot != pivot;
+                pivot = new_pivot;
+                best = new_best;
+                // HyperbolicHnsw::search_layer_single (hnsw.rs:305-329) repeats the
+                // pass from the new pivot until nothing improves
+                if (moved && a.hyper) {
+                    lo = 0; hi = cnt;
+                    while (lo < hi) { const int64_t mid = (lo + hi) >> 1; if (ids[mid] < pivot) lo = mid + 1; else hi = mid; }
+                    if (lo >= cnt || ids[lo] != pivot) break;
+                }
+            } while (moved && a.hyper);
         }
 
         // ---- layer 0: search_layer (:913-1055)
@@ -119,7 +132,8 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
             const float c_d = cd[cs - 1];
             const int c_id = ci[cs - 1];
             cs -= 1;
-            if (c_d > rd[rs - 1]) break;  // -(c.dist) > f.dist  -> return
+            // -(c.dist) > f.dist -> return; HyperbolicHnsw also needs |R| >= ef (hnsw.rs:357-361)
+            if (c_d > rd[rs - 1] && (!a.hyper || rs >= ef)) break;
             const int64_t b = a.g.rp0[c_id], e = a.g.rp0[c_id + 1];
             for (int64_t c0 = b; c0 < e; c0 += 64) {
                 const int64_t p = c0 + lane;
@@ -188,7 +202,7 @@ size_t hnsw_search_lds(int d, int ef) {
 
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
                  const float* qnorm, int64_t nq, int k, int ef, float* out_d, int64_t* out_i, int32_t* out_n,
-                 const char* tag) {
+                 const char* tag, float curv, int hyper) {
     if (nq <= 0) return;
     RVX_REQUIRE(ef >= 1 && ef <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER,
                 "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
@@ -199,7 +213,7 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     int* status = (int*)scratch_bytes("hnsw_status", 256);
     RVX_HIP(hipMemsetAsync(vis, 0, (size_t)nslots * vcap * 8, stream()));
     RVX_HIP(hipMemsetAsync(status, 0, 4, stream()));
-    SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, nslots, vcap, out_d, out_i, out_n, status};
+    SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, nslots, vcap, out_d, out_i, out_n, status, curv, hyper};
     const size_t lds = hnsw_search_lds(d, ef);
     RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");
     static bool attr = false;
@@ -208,6 +222,7 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     const char* t = tag ? tag : "hnsw_search";
@@ -216,6 +231,7 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
         case RVX_METRIC_DOT: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, a); break;
         case RVX_METRIC_L1: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_POINCARE: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_POINCARE>, dim3(nslots), dim3(64), lds, a); break;
         default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by HNSW search");
     }
     int st = 0;

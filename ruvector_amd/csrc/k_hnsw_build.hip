@@ -45,6 +45,8 @@ struct BuildArgs {
     int* rev_head; int* rev_next; int* rev_key; float* rev_d; int* rev_src;  // reverse-edge chains
     int rev_cap;  // records per batch point
     int* status;
+    float curv;  // Poincaré curvature
+    int hyper;   // HyperbolicHnsw::insert rules
 };
 
 __device__ __forceinline__ int list_get(const BuildGraph& G, int p, int l, const int** ids, const float** ds) {
@@ -97,7 +99,7 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
             float dd = INFINITY;
             if (fresh)
                 dd = row_dist<METRIC>(qs, a.x + (int64_t)nid * a.d, a.d, qn,
-                                      METRIC == RVX_METRIC_COSINE ? a.xnorm[nid] : 0.0f);
+                                      METRIC == RVX_METRIC_COSINE ? a.xnorm[nid] : 0.0f, a.curv);
             unsigned long long todo = __ballot(fresh);
             while (todo) {
                 const int src = __ffsll((long long)todo) - 1;
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
 
         int ep = a.entry;
         float d_ep = row_dist<METRIC>(qs, a.x + (int64_t)ep * a.d, a.d, qn,
-                                      METRIC == RVX_METRIC_COSINE ? a.xnorm[ep] : 0.0f);
+                                      METRIC == RVX_METRIC_COSINE ? a.xnorm[ep] : 0.0f, a.curv);
         // 1. greedy descent, ef = 1 (hnsw.rs:1105-1146)
         for (int l = a.entry_level; l >= lev + 1; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
@@ -173,17 +175,20 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
                                                       overflow);
             if (rs > 0 && rd[0] < d_ep) { ep = ri[0]; d_ep = rd[0]; }
         }
-        // 2. layers lev .. 0 (hnsw.rs:1149-1196)
-        for (int l = lev; l >= 0; --l) {
+        // 2. layers lev .. 0 (hnsw.rs:1149-1196); HyperbolicHnsw inserts at
+        //    min(level, max_level) .. 0 (hyperbolic hnsw.rs:213)
+        const int ltop = a.hyper ? min(lev, a.entry_level) : lev;
+        for (int l = ltop; l >= 0; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
             const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, ef, l, vis, vmask, tag, rd, ri, cd, ci, ccap, lane,
                                                       overflow);
             if (rs == 0) continue;
-            const int nb_conn = l == 0 ? 2 * a.G.M : a.G.M;
+            const int nb_conn = l == 0 ? a.G.C0 : a.G.M;
             int ss = 0;
-            if (rs <= nb_conn) {
-                for (int i = lane; i < rs; i += 64) { sd[i] = rd[i]; si[i] = ri[i]; }
-                ss = rs;
+            if (rs <= nb_conn || a.hyper) {
+                // all of R, or (HyperbolicHnsw, hnsw.rs:225) its closest nb_conn
+                ss = min(rs, nb_conn);
+                for (int i = lane; i < ss; i += 64) { sd[i] = rd[i]; si[i] = ri[i]; }
             } else {
                 // select_neighbours heuristic (hnsw.rs:1350-1380), one lane per selected point
                 for (int t = 0; t < rs && ss < nb_conn; ++t) {
@@ -194,7 +199,7 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
                         const int s = si[lane];
                         const float dse = row_dist<METRIC>(a.x + (int64_t)e * a.d, a.x + (int64_t)s * a.d, a.d,
                                                            METRIC == RVX_METRIC_COSINE ? a.xnorm[e] : 0.0f,
-                                                           METRIC == RVX_METRIC_COSINE ? a.xnorm[s] : 0.0f);
+                                                           METRIC == RVX_METRIC_COSINE ? a.xnorm[s] : 0.0f, a.curv);
                         bad = dse <= de;
                     }
                     if (__ballot(bad) == 0ull) {
@@ -223,10 +228,11 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
             }
             for (int i = lane; i < ss; i += 64) { oid[i] = si[i]; od[i] = sd[i]; }
             if (lane == 0) *ocnt = ss;
-            // reverse-edge records: p into s's list at p's own level
+            // reverse-edge records: p into s's list at p's own level (hnsw_rs quirk),
+            // or at the current level l (HyperbolicHnsw, hnsw.rs:232-239)
             for (int i = lane; i < ss; i += 64) {
                 const int s = si[i];
-                const int key = (s == p) ? -1 : list_key(a.G, s, lev);
+                const int key = (s == p) ? -1 : list_key(a.G, s, a.hyper ? l : lev);
                 const int r = rbase + rec + i;
                 a.rev_key[r] = key;
                 a.rev_d[r] = sd[i];
@@ -311,9 +317,9 @@ size_t build_lds_bytes(int d, int ef) {
 
 void build_insert_batch(const BuildGraph& G, int metric, const float* x, const float* xnorm, int d,
                         int64_t batch_begin, int batch_n, int entry, int entry_level, unsigned nonempty_mask, int ef_c,
-                        BuildScratch& s) {
+                        BuildScratch& s, float curv, int hyper) {
     if (batch_n <= 0) return;
-    RVX_REQUIRE(G.C0 <= 64 && G.M <= 32, RVX_ERR_UNSUPPORTED, "GPU HNSW build supports m <= 32");
+    RVX_REQUIRE(G.C0 <= 64 && G.M <= 64, RVX_ERR_UNSUPPORTED, "GPU HNSW build supports lists of <= 64 neighbours");
     RVX_REQUIRE(ef_c >= 1 && ef_c <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER, "ef_construction out of range");
     const unsigned vcap = visited_capacity(ef_c);
     const int nslots = (int)std::min<int64_t>(std::min(batch_n, 8192),
@@ -323,6 +329,7 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     a.G = G; a.x = x; a.xnorm = xnorm; a.d = d;
     a.batch_begin = batch_begin; a.batch_n = batch_n; a.entry = entry; a.entry_level = entry_level;
     a.nonempty_mask = nonempty_mask; a.ef_c = ef_c;
+    a.curv = curv; a.hyper = hyper;
     a.vcap = vcap;
     a.visited = (unsigned long long*)scratch_bytes("build_visited", (int64_t)nslots * vcap * 8);
     const int64_t nrec = (int64_t)batch_n * rev_cap;
@@ -343,12 +350,16 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
         hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     switch (metric) {
         case RVX_METRIC_L2: RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
         case RVX_METRIC_COSINE: RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
         case RVX_METRIC_L1: RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_POINCARE:
+            RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_POINCARE>, dim3(nslots), dim3(64), lds, a);
+            break;
         default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by the GPU HNSW build");
     }
     const int waves = (int)((nrec + 63) / 64);

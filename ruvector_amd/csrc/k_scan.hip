@@ -328,6 +328,13 @@ void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const
                (int)nchunks, k, out_d, out_i);
 }
 
+void merge_topk(const float* part_d, const int64_t* part_i, int64_t nq, int nchunks, int k, float* out_d,
+                int64_t* out_i) {
+    if (nq <= 0) return;
+    RVX_LAUNCH("scan_merge", k_merge_topk, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, part_d, part_i, nq, nchunks, k,
+               out_d, out_i);
+}
+
 void edge_distances(int metric, const float* x, const float* xn, const int64_t* rp, const int32_t* col, int64_t n,
                     int d, float* out) {
     if (n <= 0) return;

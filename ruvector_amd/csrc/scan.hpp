@@ -20,6 +20,9 @@ void distance_matrix(int metric, const float* q, const float* qn, int64_t nq, co
 // out[p] = distance(x[owner(p)], x[col[p]]) for every CSR edge p (wave per row).
 void edge_distances(int metric, const float* x, const float* xnorm, const int64_t* rp, const int32_t* col, int64_t n,
                     int d, float* out);
+// Merge per-chunk ascending top-k lists part_[d|i] [nq][nchunks*k] into out [nq][k].
+void merge_topk(const float* part_d, const int64_t* part_i, int64_t nq, int nchunks, int k, float* out_d,
+                int64_t* out_i);
 // Poincaré ball distance matrix (poincare.rs:227-255), curvature c.
 void poincare_matrix(const float* q, int64_t nq, const float* x, int64_t n, int d, float c, float* out);
 

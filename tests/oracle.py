@@ -54,6 +54,21 @@ _SIG = {
     "orc_efa_init": (None, [I32, I32, I32, PF, PF, PF, PF, PF]),
     "orc_efa_compute": (I32, [I32, I32, I32, I32, F32, PF, PF, PF, PF, PF, PF, PF, PF, PF, I32, PF]),
     "orc_poincare_distance": (F32, [PF, PF, I64, F32]),
+    "orc_hyp_new": (P, [I32, I32, I32, I32, I32, F32, F32, I32, U64]),
+    "orc_hyp_free": (None, [P]),
+    "orc_hyp_len": (I64, [P]),
+    "orc_hyp_insert": (None, [P, PF, I64]),
+    "orc_hyp_get_vector": (None, [P, I64, PF]),
+    "orc_hyp_search": (None, [P, PF, I64, I32, I32, PI64, PF, PI32, I32]),
+    "orc_hyp_brute_force": (None, [P, PF, I64, I32, PI64, PF, I32]),
+    "orc_hyp_build_tangent": (None, [P]),
+    "orc_hyp_centroid": (None, [P, PF]),
+    "orc_hyp_search_pruning": (None, [P, PF, I64, I32, PI64, PF, I32]),
+    "orc_hyp_set_curvature": (None, [P, F32]),
+    "orc_hyp_export_sizes": (None, [P, PI64, PI32, PI64, PI64, PI64, PI64]),
+    "orc_hyp_export": (None, [P, PU8, PI64, PI32, PI32, PI64, PI32]),
+    "orc_hyp_from_graph": (P, [PF, I64, I32, I32, I32, I32, F32, I32, PU8, I64, I32, PI64, PI32, PI64, PI32, PI64,
+                               PI32]),
 }
 
 _lib = None
@@ -348,3 +363,109 @@ def efa_compute(node_dim, edge_dim, heads, query, keys, values, edges=None, conc
 def poincare_distance(u, v, c=1.0):
     u, v = f32(u), f32(v)
     return lib().orc_poincare_distance(fp(u), fp(v), u.size, c)
+
+
+class Hyp:
+    """HyperbolicHnsw restated (oracle/hyperbolic.cpp; crates/ruvector-hyperbolic-hnsw/src/hnsw.rs)."""
+
+    def __init__(self, dim, m=16, m0=32, ef_construction=200, ef_search=50, level_mult=None, curvature=1.0,
+                 prune_factor=10, seed=0, _h=None):
+        import math
+        self.dim = dim
+        lm = 1.0 / math.log(16.0) if level_mult is None else level_mult
+        self._h = _h or lib().orc_hyp_new(dim, m, m0, ef_construction, ef_search, lm, curvature, prune_factor, seed)
+
+    def __len__(self):
+        return lib().orc_hyp_len(self._h)
+
+    def insert(self, vecs):
+        v = f32(vecs).reshape(-1, self.dim)
+        lib().orc_hyp_insert(self._h, fp(v), v.shape[0])
+
+    def get_vector(self, i):
+        out = np.empty(self.dim, np.float32)
+        lib().orc_hyp_get_vector(self._h, int(i), fp(out))
+        return out
+
+    def _q(self, q, k):
+        q = f32(q).reshape(-1, self.dim)
+        return q, np.empty((q.shape[0], k), np.int64), np.empty((q.shape[0], k), np.float32)
+
+    def search(self, q, k, ef=0, threads=8):
+        q, ids, d = self._q(q, k)
+        cnt = np.empty(q.shape[0], np.int32)
+        lib().orc_hyp_search(self._h, fp(q), q.shape[0], k, ef, ip64(ids), fp(d), ip32(cnt), threads)
+        return ids, d, cnt
+
+    def brute_force(self, q, k, threads=8):
+        q, ids, d = self._q(q, k)
+        lib().orc_hyp_brute_force(self._h, fp(q), q.shape[0], k, ip64(ids), fp(d), threads)
+        return ids, d
+
+    def build_tangent_cache(self):
+        lib().orc_hyp_build_tangent(self._h)
+
+    def centroid(self):
+        out = np.empty(self.dim, np.float32)
+        lib().orc_hyp_centroid(self._h, fp(out))
+        return out
+
+    def search_with_pruning(self, q, k, threads=8):
+        q, ids, d = self._q(q, k)
+        lib().orc_hyp_search_pruning(self._h, fp(q), q.shape[0], k, ip64(ids), fp(d), threads)
+        return ids, d
+
+    def set_curvature(self, c):
+        lib().orc_hyp_set_curvature(self._h, float(c))
+
+    def export(self):
+        n, ml, ent, e0 = C.c_int64(), C.c_int32(), C.c_int64(), C.c_int64()
+        uc = np.zeros(17, np.int64)
+        ue = np.zeros(17, np.int64)
+        lib().orc_hyp_export_sizes(self._h, C.byref(n), C.byref(ml), C.byref(ent), C.byref(e0), ip64(uc), ip64(ue))
+        N, L = n.value, ml.value
+        levels = np.empty(max(N, 1), np.uint8)
+        rp0 = np.empty(N + 1, np.int64)
+        col0 = np.empty(max(e0.value, 1), np.int32)
+        up_ids = np.empty(max(int(uc[1:L + 1].sum()), 1), np.int32)
+        up_rp = np.empty(max(int((uc[1:L + 1] + 1).sum()), 1), np.int64)
+        up_col = np.empty(max(int(ue[1:L + 1].sum()), 1), np.int32)
+        lib().orc_hyp_export(self._h, levels.ctypes.data_as(PU8), ip64(rp0), ip32(col0), ip32(up_ids), ip64(up_rp),
+                             ip32(up_col))
+        g = {"n": N, "max_level": L, "entry": ent.value, "levels": levels[:N], "row_ptr0": rp0,
+             "col0": col0[:e0.value], "upper_ids": [], "upper_row_ptr": [], "upper_col": []}
+        oi = orp = oc = 0
+        for l in range(1, L + 1):
+            c = int(uc[l])
+            g["upper_ids"].append(up_ids[oi:oi + c].copy())
+            rp = up_rp[orp:orp + c + 1].copy()
+            g["upper_row_ptr"].append(rp)
+            g["upper_col"].append(up_col[oc:oc + int(rp[-1])].copy())
+            oi += c
+            orp += c + 1
+            oc += int(rp[-1])
+        return g
+
+    @classmethod
+    def from_graph(cls, vecs, g, m=16, m0=32, ef_search=50, curvature=1.0, prune_factor=10):
+        v = f32(vecs)
+        L = g["max_level"]
+        uc = np.zeros(17, np.int64)
+        for l in range(1, L + 1):
+            uc[l] = len(g["upper_ids"][l - 1])
+        cat32 = lambda xs: np.ascontiguousarray(np.concatenate(xs) if xs else np.zeros(1), np.int32)  # noqa: E731
+        cat64 = lambda xs: np.ascontiguousarray(np.concatenate(xs) if xs else np.zeros(1), np.int64)  # noqa: E731
+        ids, rps, cols = cat32(g["upper_ids"]), cat64(g["upper_row_ptr"]), cat32(g["upper_col"])
+        lv = np.ascontiguousarray(g["levels"], np.uint8)
+        h = lib().orc_hyp_from_graph(fp(v), v.shape[0], v.shape[1], m, m0, ef_search, curvature, prune_factor,
+                                     lv.ctypes.data_as(PU8), g["entry"], L, ip64(np.ascontiguousarray(g["row_ptr0"],
+                                                                                                       np.int64)),
+                                     ip32(np.ascontiguousarray(g["col0"], np.int32)), ip64(uc), ip32(ids), ip64(rps),
+                                     ip32(cols))
+        return cls(v.shape[1], _h=h)
+
+    def __del__(self):
+        try:
+            lib().orc_hyp_free(self._h)
+        except Exception:
+            pass

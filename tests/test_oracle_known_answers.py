@@ -244,3 +244,69 @@ def test_hnsw_results_sorted():  # property_tests.rs:308-331
     _, d, cnt = h.search(_unit_vectors(20, 16, 10), 10, 40)
     for row, c in zip(d, cnt):
         assert np.all(np.diff(row[:c]) >= 0)
+
+
+# ---------------------------------------------------------------- HyperbolicHnsw
+# crates/ruvector-hyperbolic-hnsw/tests/math_tests.rs, restated on the oracle
+def _grid20():
+    return [[0.1 * (i % 5), 0.05 * (i / 5)] for i in range(20)]
+
+
+def test_hyp_insert_and_search_sorted():  # math_tests.rs:308-331
+    h = O.Hyp(2)
+    h.insert(np.array(_grid20(), np.float32))
+    assert len(h) == 20
+    ids, d, cnt = h.search([0.25, 0.125], 5)
+    assert cnt[0] == 5 and np.all(np.diff(d[0]) >= 0)
+
+
+def test_hyp_nearest_is_origin():  # math_tests.rs:334-354
+    h = O.Hyp(2)
+    h.insert(np.array([[0.0, 0.0], [0.5, 0.0], [0.0, 0.5], [0.3, 0.3]], np.float32))
+    ids, _, _ = h.search([0.05, 0.05], 1)
+    assert ids[0, 0] == 0
+
+
+def test_hyp_edge_cases():  # math_tests.rs:357-375, 464-495
+    h = O.Hyp(2)
+    ids, _, cnt = h.search([0.1, 0.2], 5)
+    assert cnt[0] == 0 and np.all(ids == -1)
+    h.insert(np.array([[0.3, 0.2]], np.float32))
+    ids, _, cnt = h.search([0.1, 0.2], 5)
+    assert cnt[0] == 1 and ids[0, 0] == 0
+    h3 = O.Hyp(2)
+    h3.insert(np.array([[0.1 * i, 0.1] for i in range(3)], np.float32))
+    assert h3.search([0.15, 0.1], 10)[2][0] == 3
+    h2 = O.Hyp(2)
+    h2.insert(np.array([[0.1, 0.2], [0.3, 0.1]], np.float32))
+    h2.set_curvature(2.0)
+    assert h2.search([0.2, 0.15], 2)[2][0] == 2
+
+
+def test_hyp_search_performance_case():  # math_tests.rs:498-530
+    h = O.Hyp(2)
+    h.insert(np.array([[0.05 * (i % 10), 0.05 * (i // 10)] for i in range(100)], np.float32))
+    for _ in range(10):
+        assert h.search([0.25, 0.25], 10)[2][0] == 10
+
+
+def test_hyp_frechet_mean_and_tangent_cache():  # math_tests.rs:219-305
+    one = O.Hyp(2)
+    one.insert(np.array([[0.3, 0.2]], np.float32))
+    one.build_tangent_cache()
+    assert np.allclose(one.centroid(), [0.3, 0.2], atol=1e-4)
+    sym = O.Hyp(2)
+    sym.insert(np.array([[0.3, 0.0], [-0.3, 0.0]], np.float32))
+    sym.build_tangent_cache()
+    assert np.linalg.norm(sym.centroid()) < 0.1
+    tc = O.Hyp(3)
+    tc.insert(np.array([[0.1, 0.2, 0.1], [-0.1, 0.15, 0.05], [0.2, -0.1, 0.1]], np.float32))
+    tc.build_tangent_cache()
+    assert np.linalg.norm(tc.centroid()) < 1.0 - 1e-5
+    # tangent_distance_ordering: with one candidate kept, the tangent nearest is the hyperbolic nearest
+    to = O.Hyp(2, prune_factor=1)
+    to.insert(np.array([[0.1, 0.1], [0.2, 0.1], [0.5, 0.3]], np.float32))
+    to.build_tangent_cache()
+    ids, _ = to.search_with_pruning([0.12, 0.11], 1)
+    exact, _ = to.brute_force([0.12, 0.11], 1)
+    assert ids[0, 0] == exact[0, 0]
