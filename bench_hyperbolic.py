@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""C5 benchmark: hyperbolic HNSW (Poincaré ball, c = 1) on one
+GPU shard — the per-GPU unit of the 50M x 1024 / 8-GPU configuration.
+
+Data (C5 generator): direction ~ N(0,1) normalised, radius 0.9 * U[0,1)
+(seed 7 points, seed 8 queries), HyperbolicHnswConfig defaults (M=16, M0=32,
+ef_c=200, ef_s=50). Build: GPU batched insert from HBM-resident vectors.
+Ground truth: exact Poincaré scan (K8) on the GPU (bit-exact with the oracle's
+scan order). Reports build time, recall@10 / QPS over an ef sweep, QPS at
+recall >= 0.95, tangent-pruned search, and the oracle's CPU search on the same
+graph (bounded sample) with an id-equality check.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def ball(n, d, seed, chunk=1 << 18):
+    r = np.random.default_rng(seed)
+    out = np.empty((n, d), np.float32)
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        v = r.standard_normal((m, d), dtype=np.float32)
+        v /= np.linalg.norm(v, axis=1, keepdims=True)
+        out[s:s + m] = v * (0.9 * r.random((m, 1), dtype=np.float32))
+    return out
+
+
+def recall(gt, got):
+    k = gt.shape[1]
+    return float(np.mean([len(set(a.tolist()) & set(b.tolist())) / k for a, b in zip(gt, got)]))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--n", type=int, default=1_000_000)
+    p.add_argument("--dim", type=int, default=1024)
+    p.add_argument("--queries", type=int, default=10_000)
+    p.add_argument("--ef", default="50,100,200,400,800")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu", action="store_true")
+    a = p.parse_args()
+    import ruvector_amd as rv
+
+    log = lambda s: print(s, file=sys.stderr, flush=True)  # noqa: E731
+    n, d, nq, k = a.n, a.dim, a.queries, 10
+    x = ball(n, d, 7)
+    q = ball(nq, d, 8)
+    xb = rv.Buffer.from_numpy(x)
+    h = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=7))
+    rv.synchronize()
+    t0 = time.perf_counter()
+    h.insert_device(xb, n, d)
+    rv.synchronize()
+    build_s = time.perf_counter() - t0
+    log(f"build {n} x {d}: {build_s:.1f} s")
+    del xb
+
+    t0 = time.perf_counter()
+    gt, gtd, _ = h.brute_force(q, k)
+    gt_s = time.perf_counter() - t0
+    log(f"exact Poincaré ground truth, {nq} queries: {gt_s:.2f} s")
+
+    sweep = []
+    prof = rv.Profiler()
+    for ef in [int(e) for e in a.ef.split(",")]:
+        h.search_batch(q[:256], k, ef)
+        with prof:
+            t0 = time.perf_counter()
+            ids, dist, _ = h.search_batch(q, k, ef)
+            dt = time.perf_counter() - t0
+        ker, _ = prof.query("hnsw_search")
+        rec = recall(gt, ids)
+        sweep.append({"ef": ef, "recall": round(rec, 4), "qps": round(nq / dt, 1), "kernel_ms": round(ker, 2)})
+        log(f"ef={ef}: recall@10 {rec:.4f}, {nq / dt:.0f} QPS (kernel {ker:.1f} ms)")
+    ok = [s for s in sweep if s["recall"] >= 0.95]
+    best = max(ok, key=lambda s: s["qps"]) if ok else None
+
+    t0 = time.perf_counter()
+    h.build_tangent_cache()
+    rv.synchronize()
+    cache_s = time.perf_counter() - t0
+    h.search_with_pruning_batch(q[:256], k)
+    t0 = time.perf_counter()
+    pids, _, _ = h.search_with_pruning_batch(q, k)
+    pdt = time.perf_counter() - t0
+    pruned = {"tangent_cache_build_s": round(cache_s, 2), "recall": round(recall(gt, pids), 4),
+              "qps": round(nq / pdt, 1), "candidates": k * h.config.prune_factor}
+    log(f"pruned: {pruned}")
+
+    out = {"config": f"C5 shard: {n} x {d} Poincaré ball (c=1), {nq} queries, M=16 M0=32 ef_c=200, k=10",
+           "build_s": round(build_s, 2), "build_points_per_s": round(n / build_s, 1), "gt_s": round(gt_s, 2),
+           "sweep": sweep, "qps_at_recall95": best["qps"] if best else None,
+           "ef_at_recall95": best["ef"] if best else None, "search_with_pruning": pruned}
+
+    if not a.no_cpu and best:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle as O
+        g = h.export_graph()
+        xs = np.stack([h.get_vector(i) for i in range(n)]) if n <= 200_000 else x  # projected == x inside the ball
+        o = O.Hyp.from_graph(xs, g)
+        threads = min(16, os.cpu_count() or 1)
+        s = 64
+        t0 = time.perf_counter()
+        o.search(q[:s], k, best["ef"], threads=threads)
+        dt = time.perf_counter() - t0
+        s = int(min(nq, max(s, s * a.cpu_seconds / max(dt, 1e-3))))
+        t0 = time.perf_counter()
+        cids, _, _ = o.search(q[:s], k, best["ef"], threads=threads)
+        dt = time.perf_counter() - t0
+        gids, _, _ = h.search_batch(q[:s], k, best["ef"])
+        out["cpu_baseline"] = {"value": round(s / dt, 1), "unit": "queries/s", "cores": threads, "kind": "port",
+                               "sample": f"oracle HyperbolicHnsw::search on the same graph, {s} queries, ef={best['ef']}"}
+        out["cpu_gpu_ids_equal_frac"] = float(np.mean(np.all(cids == gids, axis=1)))
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

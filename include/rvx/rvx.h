@@ -346,7 +346,7 @@ rvx_status rvx_hyperbolic_search(const rvx_hyperbolic* h, const float* q, int64_
 /* search_with_pruning (hnsw.rs:425-483); without a tangent cache: search. */
 rvx_status rvx_hyperbolic_search_with_pruning(const rvx_hyperbolic* h, const float* q, int64_t nq, int32_t k,
                                               int64_t* ids, float* dist, int32_t* counts);
-/* Exact scan by HyperbolicHnsw::distance (ground truth; k <= 16). */
+/* Exact scan by HyperbolicHnsw::distance (ground truth; k <= 128, dim % 4 == 0). */
 rvx_status rvx_hyperbolic_brute_force(const rvx_hyperbolic* h, const float* q, int64_t nq, int32_t k, int64_t* ids,
                                       float* dist);
 /* HBM-resident queries/outputs; mode 0 search, 1 exact, 2 with pruning. */

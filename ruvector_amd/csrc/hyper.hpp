@@ -6,7 +6,7 @@ namespace rvx {
 
 // project_to_ball of every row of x [n][d] in place (eps = poincare EPS)
 void project_rows(float* x, int64_t n, int d, float c);
-// exact top-k (k <= 16) of every query by HyperbolicHnsw::distance, ascending (distance, row)
+// exact top-k (k <= 128) of every query by HyperbolicHnsw::distance, ascending (distance, row)
 void poincare_topk(const float* q, int64_t nq, const float* x, int64_t n, int d, float c, int k, float* out_d,
                    int64_t* out_i);
 // out[r] = log_p(x[r]) given -p (device) and |p|^2

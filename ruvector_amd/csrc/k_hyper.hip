@@ -1,7 +1,8 @@
 // k_hyper.hip — the Poincaré-ball kernels of HyperbolicHnsw beyond graph
 // search (crates/ruvector-hyperbolic-hnsw/src/{hnsw.rs,tangent.rs,poincare.rs}):
 //   project_rows      project_to_ball of inserted vectors / queries (hnsw.rs:195, :409)
-//   poincare_topk     exact top-k scan with HyperbolicHnsw::distance (ground truth, K8)
+//   poincare_topk     exact top-k with HyperbolicHnsw::distance (ground truth, K8) on
+//                     the tiled scan of k_scan.hip
 //   log_map_rows      TangentCache coordinates log_c(x) (tangent.rs:57-62)
 //   frechet_grad      sum_i w log_mean(p_i) for frechet_mean's gradient step (poincare.rs:463-538)
 //   rerank            search_with_pruning phase 2: exact distance of the tangent
@@ -19,69 +20,10 @@
 namespace rvx {
 namespace {
 
-constexpr int TOPK_MAX = 16;    // per-thread list length of poincare_topk (48 KB of LDS)
-constexpr int TOPK_SEG = 65536; // rows per block of poincare_topk
-
 __global__ void k_project_rows(float* x, int64_t n, int d, float c) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     pdev::project_inplace(x + r * d, d, c, pdev::EPS);
-}
-
-__device__ __forceinline__ bool before(float d, int64_t i, float bd, int64_t bi) { return d < bd || (d == bd && i < bi); }
-
-// One block = one query x one segment of rows; each thread keeps its own
-// ascending (dist, id) list in LDS, the block then merges the 256 lists.
-__global__ __launch_bounds__(256) void k_poincare_topk(const float* q, const float* x, int64_t n, int d, float c, int k,
-                                                      int nseg, float* part_d, int64_t* part_i) {
-    __shared__ float ld[256 * TOPK_MAX];
-    __shared__ int64_t li[256 * TOPK_MAX];
-    __shared__ float rd[256];
-    __shared__ int64_t ri[256];
-    __shared__ int rt[256];
-    const int t = threadIdx.x;
-    const int64_t qi = blockIdx.x / nseg;
-    const int seg = (int)(blockIdx.x % nseg);
-    const float* qv = q + qi * d;
-    float* myd = ld + t * TOPK_MAX;
-    int64_t* myi = li + t * TOPK_MAX;
-    int cnt = 0;
-    const int64_t r0 = (int64_t)seg * TOPK_SEG, r1 = min<int64_t>(n, r0 + TOPK_SEG);
-    for (int64_t r = r0 + t; r < r1; r += 256) {
-        const float dd = pdev::hyp_dist(qv, x + r * d, d, c);
-        if (cnt == k && !before(dd, r, myd[k - 1], myi[k - 1])) continue;
-        int pos = cnt == k ? k - 1 : cnt;
-        while (pos > 0 && before(dd, r, myd[pos - 1], myi[pos - 1])) {
-            myd[pos] = myd[pos - 1];
-            myi[pos] = myi[pos - 1];
-            --pos;
-        }
-        myd[pos] = dd;
-        myi[pos] = r;
-        if (cnt < k) ++cnt;
-    }
-    // block merge: k rounds of an argmin over the 256 list heads
-    int head = 0;
-    for (int s = 0; s < k; ++s) {
-        rd[t] = head < cnt ? myd[head] : INFINITY;
-        ri[t] = head < cnt ? myi[head] : INT64_MAX;
-        rt[t] = t;
-        __syncthreads();
-        for (int w = 128; w > 0; w >>= 1) {
-            if (t < w && before(rd[t + w], ri[t + w], rd[t], ri[t])) {
-                rd[t] = rd[t + w];
-                ri[t] = ri[t + w];
-                rt[t] = rt[t + w];
-            }
-            __syncthreads();
-        }
-        if (t == 0) {
-            part_d[(qi * nseg + seg) * k + s] = rd[0];
-            part_i[(qi * nseg + seg) * k + s] = ri[0];
-        }
-        if (rt[0] == t && head < cnt) ++head;
-        __syncthreads();
-    }
 }
 
 // out[r] = log_centroid(x[r]) with -centroid and |centroid|^2 precomputed.
@@ -167,14 +109,13 @@ void project_rows(float* x, int64_t n, int d, float c) {
 void poincare_topk(const float* q, int64_t nq, const float* x, int64_t n, int d, float c, int k, float* out_d,
                    int64_t* out_i) {
     if (nq <= 0) return;
-    RVX_REQUIRE(k >= 1 && k <= TOPK_MAX, RVX_ERR_UNSUPPORTED, "exact Poincaré top-k supports k <= 16");
-    const int nseg = (int)std::max<int64_t>(1, (n + TOPK_SEG - 1) / TOPK_SEG);
-    RVX_REQUIRE(nq * nseg < ((int64_t)1 << 31), RVX_ERR_INVALID_SHAPE, "too many queries x segments");
-    float* pd = scratch_f32("hyp_topk_pd", nq * nseg * k);
-    auto* pi = (int64_t*)scratch_bytes("hyp_topk_pi", nq * nseg * k * 8);
-    RVX_LAUNCH("hyp_brute_force", k_poincare_topk, dim3((unsigned)(nq * nseg)), dim3(256), 0, q, x, n, d, c, k, nseg,
-               pd, pi);
-    merge_topk(pd, pi, nq, nseg, k, out_d, out_i);
+    // the tiled exact scan (k_scan.hip) with the Poincaré metric: |q-x|^2 per
+    // pair in fused_norms' chunked order, squared norms precomputed per row
+    float* qn = scratch_f32("hyp_bf_qn", nq);
+    float* xn = scratch_f32("hyp_bf_xn", n);
+    row_norm_sq(q, nq, d, qn);
+    row_norm_sq(x, n, d, xn);
+    scan_topk(RVX_METRIC_POINCARE, q, qn, nq, x, xn, nullptr, n, d, k, 0, out_d, out_i, "hyp_brute_force", c);
 }
 
 void log_map_rows(const float* x, int64_t n, int d, const float* negp_dev, float np_sq, float c, float* out) {

@@ -24,6 +24,7 @@
 #include "common.hpp"
 #include "kernels.hpp"
 #include "graph.hpp"
+#include "poincare_dev.hpp"
 #include "scan.hpp"
 
 namespace rvx {
@@ -39,7 +40,10 @@ __device__ __forceinline__ float pair_step(float acc, float q, float x) {
 }
 
 template <int METRIC>
-__device__ __forceinline__ float pair_finish(float acc, float qn, float xn) {
+__device__ __forceinline__ float pair_finish(float acc, float qn, float xn, float curv = 1.0f) {
+    // Poincaré: acc = |q-x|^2 in fused_norms' chunked order, qn/xn = squared
+    // norms in the same order (norm_squared == fused_norms' own norm sums)
+    if (METRIC == RVX_METRIC_POINCARE) return pdev::from_norms(acc, qn, xn, curv);
     if (METRIC == RVX_METRIC_L2) return sqrtf(acc);
     if (METRIC == RVX_METRIC_DOT) return -acc;
     if (METRIC == RVX_METRIC_COSINE) return (qn > 1e-8f && xn > 1e-8f) ? 1.0f - acc / (qn * xn) : 1.0f;
@@ -57,6 +61,7 @@ struct ScanArgs {
     float* part_d; int64_t* part_i;  // [nq][nchunks][k]
     int64_t id_offset;               // added to row index
     const uint8_t* deleted;          // optional tombstones [n]
+    float curv;                      // Poincaré curvature
 };
 
 template <int METRIC>
@@ -87,7 +92,7 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int64_t qi = q0 + tq + 8 * i;
-        qn[i] = (METRIC == RVX_METRIC_COSINE && qi < a.nq) ? a.qnorm[qi] : 0.0f;
+        qn[i] = ((METRIC == RVX_METRIC_COSINE || METRIC == RVX_METRIC_POINCARE) && qi < a.nq) ? a.qnorm[qi] : 0.0f;
     }
     __syncthreads();
 
@@ -130,11 +135,37 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
                     for (int i = 0; i < 4; ++i)
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            acc[i][j] = pair_step<METRIC>(acc[i][j], qv[i].x, xv[j].x);
-                            acc[i][j] = pair_step<METRIC>(acc[i][j], qv[i].y, xv[j].y);
-                            acc[i][j] = pair_step<METRIC>(acc[i][j], qv[i].z, xv[j].z);
-                            acc[i][j] = pair_step<METRIC>(acc[i][j], qv[i].w, xv[j].w);
+                            if constexpr (METRIC == RVX_METRIC_POINCARE) {  // one 4-wide chunk of fused_norms
+                                const float d0 = qv[i].x - xv[j].x, d1 = qv[i].y - xv[j].y;
+                                const float d2 = qv[i].z - xv[j].z, d3 = qv[i].w - xv[j].w;
+                                acc[i][j] = acc[i][j] + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
+                            } else {
+                                acc[i][j] = pair_step<METRIC>(acc[i][j], qv[i].x, xv[j].x);
+                                acc[i][j] = pair_step<METRIC>(acc[i][j], qv[i].y, xv[j].y);
+                                acc[i][j] = pair_step<METRIC>(acc[i][j], qv[i].z, xv[j].z);
+                                acc[i][j] = pair_step<METRIC>(acc[i][j], qv[i].w, xv[j].w);
+                            }
                         }
+                }
+            } else if (METRIC == RVX_METRIC_POINCARE) {  // tail tile: whole chunks, then a sequential remainder
+                int kk = 0;
+                for (; kk + 4 <= kc; kk += 4) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const float* qp = qs + (tq + 8 * i) * ROWF + kk;
+                            const float* xp = xs + (tr + 32 * j) * ROWF + kk;
+                            const float d0 = qp[0] - xp[0], d1 = qp[1] - xp[1], d2 = qp[2] - xp[2], d3 = qp[3] - xp[3];
+                            acc[i][j] = acc[i][j] + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
+                        }
+                }
+                for (; kk < kc; ++kk) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            acc[i][j] = pair_step<RVX_METRIC_L2>(acc[i][j], qs[(tq + 8 * i) * ROWF + kk], xs[(tr + 32 * j) * ROWF + kk]);
                 }
             } else {
                 for (int kk = 0; kk < kc; ++kk) {
@@ -159,8 +190,8 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
                 const int64_t ri = rt + tr + 32 * j;
                 if (ri >= r_end) continue;
                 if (a.deleted && a.deleted[ri]) continue;
-                const float xn = (METRIC == RVX_METRIC_COSINE) ? a.xnorm[ri] : 0.0f;
-                const float dist = pair_finish<METRIC>(acc[i][j], qn[i], xn);
+                const float xn = (METRIC == RVX_METRIC_COSINE || METRIC == RVX_METRIC_POINCARE) ? a.xnorm[ri] : 0.0f;
+                const float dist = pair_finish<METRIC>(acc[i][j], qn[i], xn, a.curv);
                 if (dist <= t) {  // ties at the threshold are resolved by id in the merge
                     const int slot = atomicAdd(&cand_n[ql], 1);
                     cand_d[ql * TR + slot] = dist;
@@ -287,9 +318,19 @@ void row_norms(const float* x, int64_t n, int d, float* out) {
     RVX_HIP(hipGetLastError());
 }
 
+__global__ void k_row_norm_sq(const float* x, int64_t n, int d, float* out) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n) out[r] = pdev::norm_sq(x + r * d, d);
+}
+
+void row_norm_sq(const float* x, int64_t n, int d, float* out) {
+    if (n <= 0) return;
+    RVX_LAUNCH("row_norm_sq", k_row_norm_sq, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, x, n, d, out);
+}
+
 void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
                const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
-               const char* tag) {
+               const char* tag, float curv) {
     RVX_REQUIRE(k >= 1 && k <= SCAN_MAX_K, RVX_ERR_INVALID_PARAMETER,
                 "k must be in [1, " + std::to_string(SCAN_MAX_K) + "]");
     RVX_REQUIRE(d % 4 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)x & 15) == 0, RVX_ERR_UNSUPPORTED,
@@ -305,7 +346,7 @@ void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const
 
     float* part_d = (float*)scratch_bytes("scan_part_d", nq * nchunks * k * 4);
     int64_t* part_i = (int64_t*)scratch_bytes("scan_part_i", nq * nchunks * k * 8);
-    ScanArgs a{q, x, qnorm, xnorm, nq, n, d, k, rows_per_chunk, (int)nchunks, part_d, part_i, id_offset, deleted};
+    ScanArgs a{q, x, qnorm, xnorm, nq, n, d, k, rows_per_chunk, (int)nchunks, part_d, part_i, id_offset, deleted, curv};
     const size_t lds = scan_lds_bytes(k);
     static bool attr_done = false;
     if (!attr_done) {
@@ -313,6 +354,7 @@ void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const
         hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
     const dim3 grid((unsigned)qtiles, (unsigned)nchunks);
@@ -322,6 +364,7 @@ void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const
         case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_COSINE>, grid, dim3(256), lds, a); break;
         case RVX_METRIC_DOT: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_DOT>, grid, dim3(256), lds, a); break;
         case RVX_METRIC_L1: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_L1>, grid, dim3(256), lds, a); break;
+        case RVX_METRIC_POINCARE: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_POINCARE>, grid, dim3(256), lds, a); break;
         default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by the flat scan");
     }
     RVX_LAUNCH("scan_merge", k_merge_topk, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, part_d, part_i, nq,

@@ -10,9 +10,13 @@ constexpr int SCAN_MAX_K = 128;
 void row_norms(const float* x, int64_t n, int d, float* out);
 // Top-k (ascending (distance, id)) of every query against rows [0, n) of x.
 // Output ids are row + id_offset; rows with deleted[row] != 0 are skipped.
+// Poincaré (HyperbolicHnsw::distance with curvature curv): qnorm/xnorm are
+// squared norms from row_norm_sq.
 void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
                const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
-               const char* tag);
+               const char* tag, float curv = 1.0f);
+// Squared norms in poincare.rs norm_squared's chunked order, one per row.
+void row_norm_sq(const float* x, int64_t n, int d, float* out);
 // out[i][j] = distance(q_i, x_j) in the reference scalar order.
 void distance_matrix(int metric, const float* q, const float* qn, int64_t nq, const float* x, const float* xn, int64_t n,
                      int d, float* out);

@@ -152,7 +152,7 @@ class HyperbolicHnsw:
         return self._batch("rvx_hyperbolic_search_with_pruning", queries, k)
 
     def brute_force(self, queries, k: int):
-        """Exact scan by the index distance (ground truth, k <= 16)."""
+        """Exact scan by the index distance (ground truth, k <= 128)."""
         return self._batch("rvx_hyperbolic_brute_force", queries, k)
 
     def search_device(self, queries: Buffer, nq: int, k: int, ids: Buffer, dist: Buffer, ef: int = 0,
