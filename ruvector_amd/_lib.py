@@ -13,7 +13,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librvx.so")
+# RVX_LIB: load another in-tree build (A/B kernel experiments); default librvx.so
+LIB_PATH = os.environ.get("RVX_LIB") or os.path.join(_HERE, "librvx.so")
 
 COMM_ID_BYTES = 128
 

@@ -413,8 +413,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x3(GemmArgs g, int epi) {
 // so every A fragment is split by exactly one wave. Requires K % 32 == 0 (no
 // tail tile: the DMA has no zero fill); rows past M / N are clamped to a
 // valid row and never stored.
-template <bool DUAL>
-__global__ __launch_bounds__(256, 2) void gemm_nt_x3g(GemmArgs g, int epi) {
+template <bool DUAL, int WM>
+__global__ __launch_bounds__(64 * WM, WM == 4 ? 2 : 1) void gemm_nt_x3g(GemmArgs g, int epi) {
+    constexpr int BM = 32 * WM;               // rows per block: one 32-row strip per wave
+    constexpr int XA = BM * 128;              // f32 A tile bytes per stage
+    constexpr int STG = XA + 3 * XB_PLANE;    // stage bytes
+    constexpr int NB = 24 / WM;               // B DMA pieces per wave (3 planes x 8 pieces)
     extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
 
     const int64_t nwg = g.nblocks;
@@ -423,88 +427,105 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x3g(GemmArgs g, int epi) {
     const int64_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
     const int64_t tm = wgid / g.tiles_n;
     const int tn = (int)(wgid % g.tiles_n);
-    const int64_t m0 = tm * XBM;
+    const int64_t m0 = tm * BM;
     const int n0 = tn * XBN;
 
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: LDS DMA targets go to M0 directly
     const int lr = lane & 31, lh = lane >> 5;
 
     const int nk0 = g.K0 / 32;
     const int nk1 = DUAL ? g.K1 / 32 : 0;
-    const int nk = nk0 + nk1;
 
-    // per-lane source rows/chunks of this wave's DMA pieces (fixed over k)
+    // DMA sources: a scalar tile base (advanced 128 B / 64 B per k-tile) plus a
+    // per-lane 32-bit byte offset fixed over k (host guarantees it fits), so the
+    // k-loop carries no 64-bit address arithmetic.
     // A: pieces 4*wave .. 4*wave+3, each 8 rows x 8 chunks of 16 B
-    int64_t a_row_off[4];
-    int a_chunk[4];
+    // B: pieces NB*wave .. NB*wave+NB-1 over 3 planes x 8 pieces, each 16 rows x 4 chunks
+    uint32_t a_off[2][4], b_off[2][NB];
+    const char* a_base[2];
+    const char* b_base[2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int row = 8 * (4 * wave + j) + (lane >> 3);
-        a_chunk[j] = (lane & 7) ^ ((row >> 1) & 7);
-        a_row_off[j] = std::min<int64_t>(m0 + row, g.M - 1);
-    }
-    // B: pieces 6*wave .. 6*wave+5 over 3 planes x 8 pieces, each 16 rows x 4 chunks
-    int b_plane[6], b_chunk[6];
-    int64_t b_row[6];
+    for (int ph = 0; ph < (DUAL ? 2 : 1); ++ph) {
+        const float* A = ph ? g.A1 : g.A0;
+        const uint16_t* B = ph ? g.B1x3 : g.B0x3;
+        const int64_t lda = ph ? g.lda1 : g.lda0, ldb = ph ? g.ldb1 : g.ldb0, bpl = ph ? g.B1x3_plane : g.B0x3_plane;
+        a_base[ph] = reinterpret_cast<const char*>(A + m0 * lda);
+        b_base[ph] = reinterpret_cast<const char*>(B + (int64_t)n0 * ldb);
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        const int piece = 6 * wave + j;
-        const int row = 16 * (piece & 7) + (lane >> 2);
-        b_plane[j] = piece >> 3;
-        b_chunk[j] = (lane & 3) ^ ((row >> 2) & 3);
-        b_row[j] = std::min<int64_t>(n0 + row, (int64_t)g.N - 1);
+        for (int j = 0; j < 4; ++j) {
+            const int row = 8 * (4 * wave + j) + (lane >> 3);
+            const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+            const int64_t r = std::min<int64_t>(m0 + row, g.M - 1) - m0;
+            a_off[ph][j] = (uint32_t)((r * lda + 4 * chunk) * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int piece = NB * wave + j;
+            const int row = 16 * (piece & 7) + (lane >> 2);
+            const int chunk = (lane & 3) ^ ((row >> 2) & 3);
+            const int64_t r = std::min<int64_t>(n0 + row, (int64_t)g.N - 1) - n0;
+            b_off[ph][j] = (uint32_t)(((piece >> 3) * bpl + r * ldb + 8 * chunk) * 2);
+        }
     }
 
-    auto fill = [&](int kt, int stage) {
-        const float* A; const uint16_t* B; int64_t lda, ldb, bpl; int k0;
-        if (!DUAL || kt < nk0) { A = g.A0; B = g.B0x3; lda = g.lda0; ldb = g.ldb0; bpl = g.B0x3_plane; k0 = kt * 32; }
-        else { A = g.A1; B = g.B1x3; lda = g.lda1; ldb = g.ldb1; bpl = g.B1x3_plane; k0 = (kt - nk0) * 32; }
-        unsigned char* base = xsm + stage * X_STAGE;
+    auto fill_ph = [&](int ph, int k0, unsigned char* base) {
+        const char* ab = a_base[ph] + (int64_t)k0 * 4;
+        const char* bb = b_base[ph] + (int64_t)k0 * 2;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_global_load_lds((const void*)(A + a_row_off[j] * lda + k0 + 4 * a_chunk[j]),
+            __builtin_amdgcn_global_load_lds((const void*)(ab + a_off[ph][j]),
                                              (__attribute__((address_space(3))) void*)(base + (4 * wave + j) * 1024),
                                              16, 0, 0);
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            const int piece = 6 * wave + j;
+        for (int j = 0; j < NB; ++j) {
+            const int piece = NB * wave + j;
             __builtin_amdgcn_global_load_lds(
-                (const void*)(B + b_plane[j] * bpl + b_row[j] * ldb + k0 + 8 * b_chunk[j]),
-                (__attribute__((address_space(3))) void*)(base + XA_TILE + (piece >> 3) * XB_PLANE + (piece & 7) * 1024),
+                (const void*)(bb + b_off[ph][j]),
+                (__attribute__((address_space(3))) void*)(base + XA + (piece >> 3) * XB_PLANE + (piece & 7) * 1024),
                 16, 0, 0);
         }
     };
-
     f32x16 acc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.0f;
 
-    fill(0, 0);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        const int stage = kt & 1;
-        if (kt + 1 < nk) fill(kt + 1, stage ^ 1);
-        const unsigned char* base = xsm + stage * X_STAGE;
+    // per-lane LDS read offsets, fixed over k (stage offsets fold into immediates)
+    const int arow = wave * 32 + lr;
+    int a_rd[2][2], b_rd[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        a_rd[s][0] = xa_off(arow, 4 * s + 2 * lh);
+        a_rd[s][1] = xa_off(arow, 4 * s + 2 * lh + 1);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) b_rd[s][ni] = XA + xb_off(ni * 32 + lr, 2 * s + lh);
+    }
+
+    // One k-tile: issue the next tile's DMA into `nxt`, then read `cur`
+    // fragment by fragment interleaved with the split and the MFMAs. The
+    // __restrict__ parameters give the inlined accesses disjoint alias scopes,
+    // which lets the waitcnt pass see that the reads of `cur` do not depend on
+    // the DMA into `nxt` (otherwise every read waits vmcnt(0) for it).
+    auto tile = [&](const unsigned char* __restrict__ cur, unsigned char* __restrict__ nxt, int fph, int fk0) {
+        if (fph == 0) fill_ph(0, fk0, nxt);
+        else if (DUAL && fph == 1) fill_ph(1, fk0, nxt);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             bf16x8 af[3];
             {
-                const int row = wave * 32 + lr;
-                const int c = 4 * s + 2 * lh;
-                const float4 lo = *reinterpret_cast<const float4*>(base + xa_off(row, c));
-                const float4 hi = *reinterpret_cast<const float4*>(base + xa_off(row, c + 1));
+                const float4 lo = *reinterpret_cast<const float4*>(cur + a_rd[s][0]);
+                const float4 hi = *reinterpret_cast<const float4*>(cur + a_rd[s][1]);
                 split8(lo, hi, af[0], af[1], af[2]);
             }
 #pragma unroll
             for (int ni = 0; ni < 4; ++ni) {
-                const int off = xb_off(ni * 32 + lr, 2 * s + lh);
                 bf16x8 bf[3];
 #pragma unroll
                 for (int p = 0; p < 3; ++p)
-                    bf[p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(base + XA_TILE + p * XB_PLANE + off));
+                    bf[p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + b_rd[s][ni] + p * XB_PLANE));
                 f32x16 c = acc[ni];
                 c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bf[1], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bf[0], c, 0, 0, 0);
@@ -515,7 +536,25 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x3g(GemmArgs g, int epi) {
                 acc[ni] = c;
             }
         }
-        __syncthreads();  // retires the DMA of tile kt+1 and frees stage for tile kt+2
+    };
+
+    // one k-loop per phase (compile-time ph: no per-tile operand selection);
+    // the last tile of phase 0 prefetches the first tile of phase 1
+    fill_ph(0, 0, xsm);
+    __syncthreads();
+    int stage = 0;
+#pragma unroll
+    for (int ph = 0; ph < (DUAL ? 2 : 1); ++ph) {
+        const int nkp = ph ? nk1 : nk0;
+        for (int kt = 0; kt < nkp; ++kt) {
+            // the other stage was last read in the previous tile, before the barrier
+            int fph = -1, fk0 = 0;
+            if (kt + 1 < nkp) { fph = ph; fk0 = (kt + 1) * 32; }
+            else if (DUAL && ph == 0 && nk1 > 0) fph = 1;
+            tile(xsm + stage * STG, xsm + (stage ^ 1) * STG, fph, fk0);
+            __syncthreads();  // retires the DMA of the next tile (vmcnt) for all waves
+            stage ^= 1;
+        }
     }
 
 #pragma unroll
@@ -600,25 +639,41 @@ void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, con
     if (x3) {
         g.B0x3 = s0.Bx3; g.B0x3_plane = s0.Bx3_plane;
         if (s1) { g.B1x3 = s1->Bx3; g.B1x3_plane = s1->Bx3_plane; }
+        const int use_dma = env_int("RVX_GEMM_DMA", 1);  // read per call: tests cover both tilings
+        const int wm = env_int("RVX_GEMM_WM", 4) == 8 ? 8 : 4;  // 8: 256-row tile, one block / CU
+        // the DMA kernel addresses each k-tile as scalar base + 32-bit lane offset
+        const int bm = 32 * wm;
+        auto offs_fit = [bm](const GemmOperand& o) {
+            const int64_t lim = (int64_t)1 << 31;
+            return (int64_t)bm * o.lda * 4 < lim && (2 * o.Bx3_plane + (int64_t)XBN * o.ldb) * 2 < lim;
+        };
+        const bool dma = use_dma && s0.K % 32 == 0 && offs_fit(s0) && (!s1 || (s1->K % 32 == 0 && offs_fit(*s1)));
+        const int tile_m = dma ? bm : XBM;
         g.tiles_n = (N + XBN - 1) / XBN;
-        const int64_t tiles_m = (M + XBM - 1) / XBM;
+        const int64_t tiles_m = (M + tile_m - 1) / tile_m;
         g.nblocks = tiles_m * g.tiles_n;
         RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
+        const int lds_g = 2 * (bm * 128 + 3 * XB_PLANE);
         static bool attr = false;
         if (!attr) {
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3<true>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3<false>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
-            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<true>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
-            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<false>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
+            const int l8 = 2 * (256 * 128 + 3 * XB_PLANE);
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, l8));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, l8));
             attr = true;
         }
-        const dim3 grid((unsigned)g.nblocks), block(256);
-        static const int use_dma = env_int("RVX_GEMM_DMA", 1);
-        const bool dma = use_dma && s0.K % 32 == 0 && (!s1 || s1->K % 32 == 0);
-        if (dma && s1) RVX_LAUNCH(t, gemm_nt_x3g<true>, grid, block, X_LDS, g, epi);
-        else if (dma) RVX_LAUNCH(t, gemm_nt_x3g<false>, grid, block, X_LDS, g, epi);
-        else if (s1) RVX_LAUNCH(t, gemm_nt_x3<true>, grid, block, X_LDS, g, epi);
-        else RVX_LAUNCH(t, gemm_nt_x3<false>, grid, block, X_LDS, g, epi);
+        const dim3 grid((unsigned)g.nblocks);
+        if (dma) {
+            const dim3 block(64 * wm);
+            if (wm == 8 && s1) RVX_LAUNCH(t, (gemm_nt_x3g<true, 8>), grid, block, lds_g, g, epi);
+            else if (wm == 8) RVX_LAUNCH(t, (gemm_nt_x3g<false, 8>), grid, block, lds_g, g, epi);
+            else if (s1) RVX_LAUNCH(t, (gemm_nt_x3g<true, 4>), grid, block, lds_g, g, epi);
+            else RVX_LAUNCH(t, (gemm_nt_x3g<false, 4>), grid, block, lds_g, g, epi);
+        } else if (s1) RVX_LAUNCH(t, gemm_nt_x3<true>, grid, dim3(256), X_LDS, g, epi);
+        else RVX_LAUNCH(t, gemm_nt_x3<false>, grid, dim3(256), X_LDS, g, epi);
         return;
     }
     if (fast) {

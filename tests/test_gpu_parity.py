@@ -210,6 +210,27 @@ def test_graphsage_matches_oracle(in_f, out_f, n, deg):
         assert_close(y, ref)
 
 
+@pytest.mark.parametrize("wm,dma", [(4, 1), (8, 1), (8, 0)])
+# out_f = 200 is avoided: with the deterministic init a few rows cancel to a
+# pre-normalisation norm of ~1e-4 (ill-conditioned for any f32 evaluation,
+# the oracle included); 232 gives a ragged 104-column second N-tile.
+@pytest.mark.parametrize("in_f,out_f,n", [(768, 768, 600), (96, 232, 1000), (64, 130, 257), (96, 256, 1000),
+                                         (128, 232, 1000)])
+def test_graphsage_gemm_tilings(monkeypatch, wm, dma, in_f, out_f, n):
+    """Every split-bf16 GEMM tiling (128- and 256-row LDS-DMA tiles, register-staged
+    fallback) on ragged M and N against the oracle."""
+    monkeypatch.setenv("RVX_GEMM_WM", str(wm))
+    monkeypatch.setenv("RVX_GEMM_DMA", str(dma))
+    deg = 7
+    x = O.fill_uniform(n * in_f, 5 + n).reshape(n, in_f)
+    rp, col = O.random_csr(n, deg, 31)
+    g = rv.Graph.from_csr(rp, col)
+    layer = rv.GraphSAGELayer(in_f, out_f, num_samples=deg)
+    y = layer.forward_graph(x, g)
+    ref = O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0)
+    assert_close(y, ref)
+
+
 def test_graphsage_chunked_pipeline_and_exchange_entry():
     """n >= 16*16384 rows runs the two-stream row-chunk pipeline (api_graph.cpp
     sage_forward_dev); rvx_sage_forward_exchange at world 1 writes the same rows."""
