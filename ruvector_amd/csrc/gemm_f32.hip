@@ -32,6 +32,7 @@ constexpr int BM = 128, BN = 128, BK = 32, LDS_ROW = BK + 4;  // 36 floats = 144
 constexpr int TILE_FLOATS = 128 * LDS_ROW;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct GemmArgs {
     const float* A0; const float* B0; int64_t lda0, ldb0; int K0;
@@ -267,6 +268,24 @@ __device__ __forceinline__ void split8(const float4& lo, const float4& hi, bf16x
     p3 = __builtin_bit_cast(bf16x8, w3);
 }
 
+// One packed pair (two k-adjacent values) of split8: words of planes 1..3.
+__device__ __forceinline__ void split_pair(float a0, float a1, unsigned& w1, unsigned& w2, unsigned& w3) {
+    const unsigned h0 = __float_as_uint(a0) & 0xFFFF0000u, h1 = __float_as_uint(a1) & 0xFFFF0000u;
+    const float r0 = a0 - __uint_as_float(h0), r1 = a1 - __uint_as_float(h1);
+    const unsigned m0 = __float_as_uint(r0) & 0xFFFF0000u, m1 = __float_as_uint(r1) & 0xFFFF0000u;
+    const unsigned l0 = __float_as_uint(r0 - __uint_as_float(m0)), l1 = __float_as_uint(r1 - __uint_as_float(m1));
+    w1 = __builtin_amdgcn_perm(h1, h0, 0x07060302u);
+    w2 = __builtin_amdgcn_perm(m1, m0, 0x07060302u);
+    w3 = __builtin_amdgcn_perm(l1, l0, 0x07060302u);
+}
+
+__device__ __forceinline__ float f4_at(const float4& lo, const float4& hi, int i) {
+    switch (i) {
+        case 0: return lo.x; case 1: return lo.y; case 2: return lo.z; case 3: return lo.w;
+        case 4: return hi.x; case 5: return hi.y; case 6: return hi.z; default: return hi.w;
+    }
+}
+
 template <bool DUAL>
 __global__ __launch_bounds__(256, 2) void gemm_nt_x3(GemmArgs g, int epi) {
     extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
@@ -413,7 +432,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_x3(GemmArgs g, int epi) {
 // so every A fragment is split by exactly one wave. Requires K % 32 == 0 (no
 // tail tile: the DMA has no zero fill); rows past M / N are clamped to a
 // valid row and never stored.
-template <bool DUAL, int WM>
+template <bool DUAL, int WM, bool S16>
 __global__ __launch_bounds__(64 * WM, WM == 4 ? 2 : 1) void gemm_nt_x3g(GemmArgs g, int epi) {
     constexpr int BM = 32 * WM;               // rows per block: one 32-row strip per wave
     constexpr int XA = BM * 128;              // f32 A tile bytes per stage
@@ -438,6 +457,11 @@ __global__ __launch_bounds__(64 * WM, WM == 4 ? 2 : 1) void gemm_nt_x3g(GemmArgs
     const int nk0 = g.K0 / 32;
     const int nk1 = DUAL ? g.K1 / 32 : 0;
 
+    // LDS XOR swizzles (16-B chunk ^ f(row)), conflict-free for the fragment
+    // reads of each MFMA shape (checked against the ds_read_b128 lane groups)
+    auto sw_a = [](int row) { return S16 ? (row >> 1) & 5 : (row >> 1) & 7; };
+    auto sw_b = [](int row) { return S16 ? (4 - (row >> 2)) & 3 : (row >> 2) & 3; };
+
     // DMA sources: a scalar tile base (advanced 128 B / 64 B per k-tile) plus a
     // per-lane 32-bit byte offset fixed over k (host guarantees it fits), so the
     // k-loop carries no 64-bit address arithmetic.
@@ -456,7 +480,7 @@ __global__ __launch_bounds__(64 * WM, WM == 4 ? 2 : 1) void gemm_nt_x3g(GemmArgs
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int row = 8 * (4 * wave + j) + (lane >> 3);
-            const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+            const int chunk = (lane & 7) ^ sw_a(row);
             const int64_t r = std::min<int64_t>(m0 + row, g.M - 1) - m0;
             a_off[ph][j] = (uint32_t)((r * lda + 4 * chunk) * 4);
         }
@@ -464,7 +488,7 @@ __global__ __launch_bounds__(64 * WM, WM == 4 ? 2 : 1) void gemm_nt_x3g(GemmArgs
         for (int j = 0; j < NB; ++j) {
             const int piece = NB * wave + j;
             const int row = 16 * (piece & 7) + (lane >> 2);
-            const int chunk = (lane & 3) ^ ((row >> 2) & 3);
+            const int chunk = (lane & 3) ^ sw_b(row);
             const int64_t r = std::min<int64_t>(n0 + row, (int64_t)g.N - 1) - n0;
             b_off[ph][j] = (uint32_t)(((piece >> 3) * bpl + r * ldb + 8 * chunk) * 2);
         }
@@ -487,6 +511,106 @@ __global__ __launch_bounds__(64 * WM, WM == 4 ? 2 : 1) void gemm_nt_x3g(GemmArgs
                 16, 0, 0);
         }
     };
+    auto xa_sw = [&](int row, int chunk) { return row * 128 + ((chunk ^ sw_a(row)) << 4); };
+    auto xb_sw = [&](int row, int chunk) { return row * 64 + ((chunk ^ sw_b(row)) << 4); };
+    if constexpr (S16) {
+    // 16x16x32 form: per k-tile each wave owns 2 (M) x 8 (N) 16x16 tiles; one
+    // MFMA consumes the whole 32-deep k-tile, so both A row halves are split
+    // up front and the eight column groups run 12 MFMAs each
+    f32x4 acc[2][8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int l16 = lane & 15, lq = lane >> 4;
+    int a_rd[2][2], b_rd[8];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+        a_rd[mi][0] = xa_sw(wave * 32 + 16 * mi + l16, 2 * lq);
+        a_rd[mi][1] = xa_sw(wave * 32 + 16 * mi + l16, 2 * lq + 1);
+    }
+#pragma unroll
+    for (int nj = 0; nj < 8; ++nj) b_rd[nj] = XA + xb_sw(16 * nj + l16, lq);
+
+    auto tile = [&](const unsigned char* __restrict__ cur, unsigned char* __restrict__ nxt, int fph, int fk0) {
+        if (fph == 0) fill_ph(0, fk0, nxt);
+        else if (DUAL && fph == 1) fill_ph(1, fk0, nxt);
+        bf16x8 af[2][3];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+            const float4 lo = *reinterpret_cast<const float4*>(cur + a_rd[mi][0]);
+            const float4 hi = *reinterpret_cast<const float4*>(cur + a_rd[mi][1]);
+            split8(lo, hi, af[mi][0], af[mi][1], af[mi][2]);
+        }
+        u32x4 bq[2][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bq[0][p] = *reinterpret_cast<const u32x4*>(cur + b_rd[0] + p * XB_PLANE);
+#pragma unroll
+        for (int nj = 0; nj < 8; ++nj) {
+            if (nj + 1 < 8) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    bq[(nj + 1) & 1][p] = *reinterpret_cast<const u32x4*>(cur + b_rd[nj + 1] + p * XB_PLANE);
+            }
+            bf16x8 bf[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bf[p] = __builtin_bit_cast(bf16x8, bq[nj & 1][p]);
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) {
+                f32x4 c = acc[mi][nj];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][1], bf[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][2], bf[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][0], bf[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][1], bf[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][0], bf[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi][0], bf[0], c, 0, 0, 0);
+                acc[mi][nj] = c;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    // one k-loop per phase (compile-time ph: no per-tile operand selection);
+    // the last tile of phase 0 prefetches the first tile of phase 1
+    fill_ph(0, 0, xsm);
+    __syncthreads();
+    int stage = 0;
+#pragma unroll
+    for (int ph = 0; ph < (DUAL ? 2 : 1); ++ph) {
+        const int nkp = ph ? nk1 : nk0;
+        for (int kt = 0; kt < nkp; ++kt) {
+            // the other stage was last read in the previous tile, before the barrier
+            int fph = -1, fk0 = 0;
+            if (kt + 1 < nkp) { fph = ph; fk0 = (kt + 1) * 32; }
+            else if (DUAL && ph == 0 && nk1 > 0) fph = 1;
+            tile(xsm + stage * STG, xsm + (stage ^ 1) * STG, fph, fk0);
+            __syncthreads();  // retires the DMA of the next tile (vmcnt) for all waves
+            stage ^= 1;
+        }
+    }
+
+#pragma unroll
+    for (int nj = 0; nj < 8; ++nj) {
+        const int col = n0 + nj * 16 + l16;
+        if (col >= g.N) continue;
+        float b = 0.0f;
+        if (g.bias0) b = g.bias0[col];
+        if (g.bias1) b += g.bias1[col];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t row = m0 + wave * 32 + 16 * mi + 4 * lq + e;
+                if (row < g.M) {
+                    float v = acc[mi][nj][e];
+                    if (g.alpha != 1.0f) v *= g.alpha;
+                    if (g.bias0 || g.bias1) v += b;
+                    if (g.addend) v += g.addend[row * g.ld_add + col];
+                    g.C[row * g.ldc + col] = epi_apply(epi, v);
+                }
+            }
+    }
+    } else {
     f32x16 acc[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -498,10 +622,10 @@ __global__ __launch_bounds__(64 * WM, WM == 4 ? 2 : 1) void gemm_nt_x3g(GemmArgs
     int a_rd[2][2], b_rd[2][4];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-        a_rd[s][0] = xa_off(arow, 4 * s + 2 * lh);
-        a_rd[s][1] = xa_off(arow, 4 * s + 2 * lh + 1);
+        a_rd[s][0] = xa_sw(arow, 4 * s + 2 * lh);
+        a_rd[s][1] = xa_sw(arow, 4 * s + 2 * lh + 1);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) b_rd[s][ni] = XA + xb_off(ni * 32 + lr, 2 * s + lh);
+        for (int ni = 0; ni < 4; ++ni) b_rd[s][ni] = XA + xb_sw(ni * 32 + lr, 2 * s + lh);
     }
 
     // One k-tile: issue the next tile's DMA into `nxt`, then read `cur`
@@ -512,29 +636,53 @@ __global__ __launch_bounds__(64 * WM, WM == 4 ? 2 : 1) void gemm_nt_x3g(GemmArgs
     auto tile = [&](const unsigned char* __restrict__ cur, unsigned char* __restrict__ nxt, int fph, int fk0) {
         if (fph == 0) fill_ph(0, fk0, nxt);
         else if (DUAL && fph == 1) fill_ph(1, fk0, nxt);
+        // A fragments of both k-halves; the second half is split in four
+        // slices beside the first half's four 6-MFMA groups (software
+        // pipelined: only the first half's split precedes an MFMA)
+        float4 alo[2], ahi[2];
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            bf16x8 af[3];
-            {
-                const float4 lo = *reinterpret_cast<const float4*>(cur + a_rd[s][0]);
-                const float4 hi = *reinterpret_cast<const float4*>(cur + a_rd[s][1]);
-                split8(lo, hi, af[0], af[1], af[2]);
-            }
+            alo[s] = *reinterpret_cast<const float4*>(cur + a_rd[s][0]);
+            ahi[s] = *reinterpret_cast<const float4*>(cur + a_rd[s][1]);
+        }
+        unsigned w[2][3][4];
 #pragma unroll
-            for (int ni = 0; ni < 4; ++ni) {
-                bf16x8 bf[3];
+        for (int j = 0; j < 4; ++j)
+            split_pair(f4_at(alo[0], ahi[0], 2 * j), f4_at(alo[0], ahi[0], 2 * j + 1), w[0][0][j], w[0][1][j], w[0][2][j]);
+        // B fragments double-buffered across the eight (k-half, column) groups:
+        // group g+1's reads are in flight during group g's MFMAs
+        u32x4 bq[2][3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bq[0][p] = *reinterpret_cast<const u32x4*>(cur + b_rd[0][0] + p * XB_PLANE);
+#pragma unroll
+        for (int gi = 0; gi < 8; ++gi) {
+            const int s = gi >> 2, ni = gi & 3;
+            if (gi + 1 < 8) {
 #pragma unroll
                 for (int p = 0; p < 3; ++p)
-                    bf[p] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(cur + b_rd[s][ni] + p * XB_PLANE));
-                f32x16 c = acc[ni];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bf[1], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bf[0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[2], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bf[0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[1], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[0], c, 0, 0, 0);
-                acc[ni] = c;
+                    bq[(gi + 1) & 1][p] =
+                        *reinterpret_cast<const u32x4*>(cur + b_rd[(gi + 1) >> 2][(gi + 1) & 3] + p * XB_PLANE);
             }
+            bf16x8 af[3], bf[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                af[p] = __builtin_bit_cast(bf16x8, u32x4{w[s][p][0], w[s][p][1], w[s][p][2], w[s][p][3]});
+                bf[p] = __builtin_bit_cast(bf16x8, bq[gi & 1][p]);
+            }
+            if (s == 0)
+                split_pair(f4_at(alo[1], ahi[1], 2 * ni), f4_at(alo[1], ahi[1], 2 * ni + 1), w[1][0][ni], w[1][1][ni],
+                           w[1][2][ni]);
+            f32x16 c = acc[ni];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bf[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bf[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bf[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[0], c, 0, 0, 0);
+            acc[ni] = c;
+            // fence per 6-MFMA group: the scheduler otherwise hoists the second
+            // half's split into one VALU block ahead of its MFMAs
+            __builtin_amdgcn_sched_barrier(0);
         }
     };
 
@@ -575,6 +723,7 @@ __global__ __launch_bounds__(64 * WM, WM == 4 ? 2 : 1) void gemm_nt_x3g(GemmArgs
                 g.C[row * g.ldc + col] = epi_apply(epi, v);
             }
         }
+    }
     }
 }
 
@@ -658,20 +807,25 @@ void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, con
         if (!attr) {
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3<true>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3<false>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
-            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
-            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<true, 4, false>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<false, 4, false>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<true, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<false, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, X_LDS));
             const int l8 = 2 * (256 * 128 + 3 * XB_PLANE);
-            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<true, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, l8));
-            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, l8));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<true, 8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, l8));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_x3g<false, 8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, l8));
             attr = true;
         }
         const dim3 grid((unsigned)g.nblocks);
         if (dma) {
             const dim3 block(64 * wm);
-            if (wm == 8 && s1) RVX_LAUNCH(t, (gemm_nt_x3g<true, 8>), grid, block, lds_g, g, epi);
-            else if (wm == 8) RVX_LAUNCH(t, (gemm_nt_x3g<false, 8>), grid, block, lds_g, g, epi);
-            else if (s1) RVX_LAUNCH(t, (gemm_nt_x3g<true, 4>), grid, block, lds_g, g, epi);
-            else RVX_LAUNCH(t, (gemm_nt_x3g<false, 4>), grid, block, lds_g, g, epi);
+            const int s16 = env_int("RVX_GEMM_MFMA16", 0);  // 16x16x32 MFMA form (128-row tile)
+            if (s16 && s1) RVX_LAUNCH(t, (gemm_nt_x3g<true, 4, true>), grid, block, lds_g, g, epi);
+            else if (s16) RVX_LAUNCH(t, (gemm_nt_x3g<false, 4, true>), grid, block, lds_g, g, epi);
+            else if (wm == 8 && s1) RVX_LAUNCH(t, (gemm_nt_x3g<true, 8, false>), grid, block, lds_g, g, epi);
+            else if (wm == 8) RVX_LAUNCH(t, (gemm_nt_x3g<false, 8, false>), grid, block, lds_g, g, epi);
+            else if (s1) RVX_LAUNCH(t, (gemm_nt_x3g<true, 4, false>), grid, block, lds_g, g, epi);
+            else RVX_LAUNCH(t, (gemm_nt_x3g<false, 4, false>), grid, block, lds_g, g, epi);
         } else if (s1) RVX_LAUNCH(t, gemm_nt_x3<true>, grid, dim3(256), X_LDS, g, epi);
         else RVX_LAUNCH(t, gemm_nt_x3<false>, grid, dim3(256), X_LDS, g, epi);
         return;

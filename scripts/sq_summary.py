@@ -44,6 +44,10 @@ def main():
     c1 = counters(f"{OUT}/pmc_sq/run_counter_collection.csv")
     c2 = counters(f"{OUT}/pmc_sq2/run_counter_collection.csv")
     kt = durations(f"{OUT}/kt_sq/run_kernel_trace.csv")
+    try:
+        c3 = counters(f"{OUT}/pmc_sq3/run_counter_collection.csv")
+    except FileNotFoundError:
+        c3 = {}
     for sub in KERNELS:
         a, b, t = pick(c1, sub), pick(c2, sub), pick(kt, sub)
         if not (a and b and t):
@@ -59,6 +63,13 @@ def main():
               f"active {mean(a['SQ_ACTIVE_INST_ANY']) / wave:.2f}  "
               f"mfma_busy {mean(a['SQ_VALU_MFMA_BUSY_CYCLES']) / simd_cycles:.3f}  "
               f"lds_conflict {mean(a['SQ_LDS_BANK_CONFLICT']):.3g}  wait_lds {mean(a['SQ_WAIT_INST_LDS']):.3g}")
+        c = pick(c3, sub) if c3 else None
+        if c:
+            lds_cycles = dur * clk * CUS
+            print(f"    vmem_rd issue {mean(c['SQ_INST_CYCLES_VMEM_RD']) / wave:.3f}  active_vmem {mean(c['SQ_ACTIVE_INST_VMEM']) / wave:.3f}  "
+                  f"active_lds {mean(c['SQ_ACTIVE_INST_LDS']) / wave:.3f}  ta_addr_full {mean(c['SQ_VMEM_TA_ADDR_FIFO_FULL']):.3g}  "
+                  f"ta_cmd_full {mean(c['SQ_VMEM_TA_CMD_FIFO_FULL']):.3g}  lds_active {mean(c['SQ_LDS_IDX_ACTIVE']) / lds_cycles:.3f} "
+                  f"lds_data_full {mean(c['SQ_LDS_DATA_FIFO_FULL']):.3g}  coexec {mean(c['SQ_VALU_MFMA_COEXEC_CYCLES']) / simd_cycles:.3f}")
         if mfma:
             print(f"    per MFMA: VALU {mean(b['SQ_INSTS_VALU']) / mfma:.2f}  LDS {mean(b['SQ_INSTS_LDS']) / mfma:.2f}  "
                   f"(MFMA {mfma:.3g})")

@@ -210,17 +210,19 @@ def test_graphsage_matches_oracle(in_f, out_f, n, deg):
         assert_close(y, ref)
 
 
-@pytest.mark.parametrize("wm,dma", [(4, 1), (8, 1), (8, 0)])
+@pytest.mark.parametrize("wm,dma,m16", [(4, 1, 0), (8, 1, 0), (8, 0, 0), (4, 1, 1)])
 # out_f = 200 is avoided: with the deterministic init a few rows cancel to a
 # pre-normalisation norm of ~1e-4 (ill-conditioned for any f32 evaluation,
 # the oracle included); 232 gives a ragged 104-column second N-tile.
 @pytest.mark.parametrize("in_f,out_f,n", [(768, 768, 600), (96, 232, 1000), (64, 130, 257), (96, 256, 1000),
                                          (128, 232, 1000)])
-def test_graphsage_gemm_tilings(monkeypatch, wm, dma, in_f, out_f, n):
-    """Every split-bf16 GEMM tiling (128- and 256-row LDS-DMA tiles, register-staged
-    fallback) on ragged M and N against the oracle."""
+def test_graphsage_gemm_tilings(monkeypatch, wm, dma, m16, in_f, out_f, n):
+    """Every split-bf16 GEMM tiling (128- and 256-row LDS-DMA tiles with 32x32x16
+    MFMAs, the 16x16x32 form, register-staged fallback) on ragged M and N
+    against the oracle."""
     monkeypatch.setenv("RVX_GEMM_WM", str(wm))
     monkeypatch.setenv("RVX_GEMM_DMA", str(dma))
+    monkeypatch.setenv("RVX_GEMM_MFMA16", str(m16))
     deg = 7
     x = O.fill_uniform(n * in_f, 5 + n).reshape(n, in_f)
     rp, col = O.random_csr(n, deg, 31)
