@@ -206,10 +206,26 @@ rvx_status rvx_gnn_forward_graph(const rvx_layer* l, const rvx_graph* g, const f
 rvx_status rvx_gnn_forward_graph_device(const rvx_layer* l, const rvx_graph* g, const rvx_buffer* x,
                                         rvx_buffer* y);
 
+/* RuvectorLayer::forward(node, neighbours, edge_weights) (layer.rs:379-423), batched over
+ * nq independent nodes whose neighbours are rows of a resident table:
+ * nodes [nq][input_dim], table [table_rows][input_dim], cand_ids [nq][c] int64 (ids outside
+ * [0, table_rows) are absent neighbours), weights [nq][c] raw edge weights or NULL (no
+ * weights -> the zero weighted aggregate, layer.rs:427-429) -> out [nq][hidden_dim].
+ * The query-time re-embedding of RuvectorQuery's neural search (query.rs:44-58). */
+rvx_status rvx_gnn_forward_star_device(const rvx_layer* l, const rvx_buffer* nodes, int64_t nq, const rvx_buffer* table,
+                                       int64_t table_rows, const rvx_buffer* cand_ids, int32_t c,
+                                       const rvx_buffer* weights, rvx_buffer* out);
+
 /* differentiable_search (crates/ruvector-gnn/src/search.rs:56-94), batched:
  * q [nq][d], cand [nq][c][d] -> idx [nq][k] (int64, -1 padded), w [nq][k]. */
 rvx_status rvx_differentiable_search_batch(const float* q, int64_t nq, const float* cand, int32_t c,
                                            int32_t d, int32_t k, float temperature, int64_t* idx, float* w);
+/* Device form over candidates gathered by id from a resident table (every id must be a
+ * table row): q [nq][d], cand_ids [nq][c] -> idx [nq][k] (positions in the candidate
+ * list), w [nq][k]; soft (nullable) [nq][c] = the softmax weights in candidate order. */
+rvx_status rvx_differentiable_search_device(const rvx_buffer* q, int64_t nq, const rvx_buffer* table, int64_t table_rows,
+                                            const rvx_buffer* cand_ids, int32_t c, int32_t d, int32_t k,
+                                            float temperature, rvx_buffer* idx, rvx_buffer* w, rvx_buffer* soft);
 
 /* ------------------------------------------------------------------ */
 /* Graph attention head: EdgeFeaturedAttention                         */

@@ -13,11 +13,14 @@ from .device import Buffer, Profiler, device_count, device_info, set_device, syn
 from .graph import Graph  # noqa: E402
 from .core import (DistanceMetric, FlatIndex, HnswConfig, HnswIndex, RuvectorError, SearchResult,  # noqa: E402
                    batch_distances, distance, distance_matrix)
-from .gnn import (GCNLayer, GnnError, GraphSAGELayer, RuvectorLayer, aggregate, differentiable_search,  # noqa: E402
+from .gnn import (GCNLayer, GnnError, GraphSAGELayer, RuvectorLayer, aggregate, differentiable_search,
+                  differentiable_search_device,  # noqa: E402
                   differentiable_search_batch, hierarchical_forward)
 from .attention import EdgeFeaturedAttention, EdgeFeaturedConfig  # noqa: E402
 from .hyperbolic import (HyperbolicError, HyperbolicHnsw, HyperbolicHnswConfig,  # noqa: E402
                          ShardedHyperbolicHnsw)
+
+from .query import NeuralSearch, QueryMode, RuvectorQuery  # noqa: E402
 
 __all__ = [
     "RvxError", "Buffer", "Profiler", "device_count", "device_info", "set_device", "synchronize", "Graph",
@@ -25,5 +28,6 @@ __all__ = [
     "distance", "distance_matrix", "GCNLayer", "GnnError", "GraphSAGELayer", "RuvectorLayer", "aggregate",
     "differentiable_search", "differentiable_search_batch", "hierarchical_forward", "EdgeFeaturedAttention",
     "EdgeFeaturedConfig", "HyperbolicError", "HyperbolicHnsw", "HyperbolicHnswConfig", "ShardedHyperbolicHnsw",
+    "NeuralSearch", "QueryMode", "RuvectorQuery", "differentiable_search_device",
 ]
 __version__ = "0.1.0"

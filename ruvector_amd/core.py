@@ -172,6 +172,20 @@ class _Index:
                cnt.ctypes.data_as(L.PI32))
         return ids, dist, cnt
 
+    # ---- HBM-resident forms (rvx_buffer in, rvx_buffer out; no host staging)
+    def add_device(self, vectors, n: int, first_id: int = 0) -> None:
+        """Insert n rows of a device buffer with ids first_id .. first_id+n-1 (GPU HNSW build)."""
+        _check("rvx_index_add_batch_device", self._h, vectors.handle, int(n), int(first_id))
+        self._next = max(self._next, int(first_id) + int(n))
+
+    def search_device(self, q, nq: int, k: int, ef: int, ids, dist) -> None:
+        """ids [nq][k] u64 (all-ones = empty slot), dist [nq][k] f32, written in HBM."""
+        _check("rvx_index_search_device", self._h, q.handle, int(nq), int(k), int(ef), ids.handle, dist.handle)
+
+    def brute_force_device(self, q, nq: int, k: int, ids, dist) -> None:
+        """Exact scan (ties by id) into device buffers."""
+        _check("rvx_index_brute_force_device", self._h, q.handle, int(nq), int(k), ids.handle, dist.handle)
+
     def brute_force_array(self, queries: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
         q = L.f32c(queries)
         if q.ndim == 1:

@@ -3,6 +3,7 @@
 #include <cmath>
 
 #include "attn.hpp"
+#include "gnn.hpp"
 #include "graph.hpp"
 #include "kernels.hpp"
 
@@ -193,6 +194,39 @@ rvx_status rvx_differentiable_search_batch(const float* q, int64_t nq, const flo
         RVX_HIP(hipMemcpyAsync(idx, di, (size_t)(nq * k * 8), hipMemcpyDeviceToHost, stream()));
         RVX_HIP(hipMemcpyAsync(w, dw, (size_t)(nq * k * 4), hipMemcpyDeviceToHost, stream()));
         sync();
+    });
+}
+
+rvx_status rvx_differentiable_search_device(const rvx_buffer* q, int64_t nq, const rvx_buffer* table, int64_t table_rows,
+                                            const rvx_buffer* cand_ids, int32_t c, int32_t d, int32_t k,
+                                            float temperature, rvx_buffer* idx, rvx_buffer* w, rvx_buffer* soft) {
+    return guard([&] {
+        RVX_REQUIRE(nq >= 0 && c > 0 && d > 0 && k >= 0 && table_rows >= 0, RVX_ERR_INVALID_PARAMETER, "bad sizes");
+        if (nq == 0) return;
+        RVX_REQUIRE(q && table && cand_ids, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(k == 0 || (idx && w), RVX_ERR_INVALID_PARAMETER, "null outputs");
+        RVX_REQUIRE(q->mem.bytes >= nq * (int64_t)d * 4, RVX_ERR_DIMENSION_MISMATCH, "q smaller than nq*d");
+        RVX_REQUIRE(table->mem.bytes >= table_rows * (int64_t)d * 4, RVX_ERR_DIMENSION_MISMATCH,
+                    "table smaller than table_rows*d");
+        RVX_REQUIRE(cand_ids->mem.bytes >= nq * (int64_t)c * 8, RVX_ERR_DIMENSION_MISMATCH, "cand_ids smaller than nq*c");
+        RVX_REQUIRE(k == 0 || (idx->mem.bytes >= nq * (int64_t)k * 8 && w->mem.bytes >= nq * (int64_t)k * 4),
+                    RVX_ERR_DIMENSION_MISMATCH, "outputs smaller than nq*k");
+        RVX_REQUIRE(!soft || soft->mem.bytes >= nq * (int64_t)c * 4, RVX_ERR_DIMENSION_MISMATCH, "soft smaller than nq*c");
+        ComputeLock cl;
+        const int64_t* ids = cand_ids->mem.as<int64_t>();
+        // every slot must name a table row: the reference's candidate list has no holes
+        auto* deg = (int32_t*)scratch_bytes("dsd_deg", nq * 4);
+        star_degrees(ids, nq, c, table_rows, deg);
+        std::vector<int32_t> hdeg(nq);
+        RVX_HIP(hipMemcpyAsync(hdeg.data(), deg, (size_t)nq * 4, hipMemcpyDeviceToHost, stream()));
+        sync();
+        for (int64_t i = 0; i < nq; ++i)
+            RVX_REQUIRE(hdeg[i] == c, RVX_ERR_INVALID_PARAMETER, "candidate id outside the table");
+        float* dc = scratch_f32("dsd_c", nq * (int64_t)c * d);
+        float* ds = scratch_f32("dsd_s", nq * (int64_t)c);
+        star_gather(nullptr, nq, table->mem.as<float>(), table_rows, ids, c, d, dc);
+        differentiable_search(q->mem.as<float>(), nq, dc, c, d, k, temperature, ds, k ? idx->mem.as<int64_t>() : nullptr,
+                              k ? w->mem.as<float>() : nullptr, soft ? soft->mem.as<float>() : nullptr);
     });
 }
 

@@ -182,11 +182,16 @@ void put_linear(std::string& s, const HostLinear& l) {
 // + wagg, AGG = w_agg(COMB), z|r, r⊙h, h~, GRU blend + dropout + LayerNorm.
 // Peak scratch = 3 n H + CHUNK (6 H + max_deg heads) floats — a 10M x 768
 // layer fits beside its input and output in HBM.
+//
+// n_out (< 0: n): phase 2 runs for rows [0, n_out) only — the star form, whose
+// rows past n_out are neighbour-only (they feed phase 1's M and K|V); rp and y
+// then need only n_out + 1 / n_out rows.
 void forward_dev(const rvx_layer* l, int64_t n, const int64_t* rp, const int32_t* col, int64_t max_deg,
-                 const float* w, int wmode, const float* x, float* y) {
+                 const float* w, int wmode, const float* x, float* y, int64_t n_out = -1) {
     const int64_t H = l->H;
     const int64_t CHUNK = std::max<int64_t>(4096, env_int("RVX_GNN_CHUNK_ROWS", 1 << 20));  // read per call
-    const int64_t chunk = std::min<int64_t>(n, CHUNK);
+    const int64_t rows_out = n_out < 0 ? n : std::min(n_out, n);
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(rows_out, CHUNK));
     float* M = scratch_f32("rvl_m", n * H);
     float* KV = scratch_f32("rvl_kv", n * 2 * H);
     float* Q = scratch_f32("rvl_q", chunk * H);
@@ -203,8 +208,8 @@ void forward_dev(const rvx_layer* l, int64_t n, const int64_t* rp, const int32_t
     ep.bias0 = l->d_bqkv.as<float>() + H;
     gemm_nt(n, (int)(2 * H), l->d_wqkv.op(M, H, H), nullptr, ep, KV, 2 * H, "gnn_gemm_kv");
 
-    for (int64_t r0 = 0; r0 < n; r0 += chunk) {
-        const int64_t rows = std::min(chunk, n - r0);
+    for (int64_t r0 = 0; r0 < rows_out; r0 += chunk) {
+        const int64_t rows = std::min(chunk, rows_out - r0);
         const float* Mc = M + r0 * H;
         ep = GemmEpilogue();
         ep.bias0 = l->d_bqkv.as<float>();
@@ -391,10 +396,54 @@ rvx_status rvx_gnn_forward_one(const rvx_layer* l, const float* node, const floa
         RVX_HIP(hipMemcpyAsync(drp, rp.data(), (size_t)(n + 1) * 8, hipMemcpyHostToDevice, stream()));
         RVX_HIP(hipMemcpyAsync(dcol, col.data(), col.size() * 4, hipMemcpyHostToDevice, stream()));
         RVX_HIP(hipMemcpyAsync(dw, wn.data(), wn.size() * 4, hipMemcpyHostToDevice, stream()));
-        // rows 1..deg have no neighbours of their own: only row 0 is kept
-        forward_dev(l, n, drp, dcol, deg, dw, wmode, dx, dy);
+        // rows 1..deg are neighbour-only: phase 2 runs for row 0 alone
+        forward_dev(l, n, drp, dcol, deg, dw, wmode, dx, dy, 1);
         RVX_HIP(hipMemcpyAsync(out, dy, (size_t)l->H * 4, hipMemcpyDeviceToHost, stream()));
         sync();
+    });
+}
+
+rvx_status rvx_gnn_forward_star_device(const rvx_layer* l, const rvx_buffer* nodes, int64_t nq, const rvx_buffer* table,
+                                       int64_t table_rows, const rvx_buffer* cand_ids, int32_t c,
+                                       const rvx_buffer* weights, rvx_buffer* out) {
+    return guard([&] {
+        RVX_REQUIRE(l && nodes && table && cand_ids && out, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(nq >= 0 && c >= 0 && table_rows >= 0, RVX_ERR_INVALID_PARAMETER, "bad sizes");
+        if (nq == 0) return;
+        const int64_t in = l->in, H = l->H;
+        RVX_REQUIRE(nodes->mem.bytes >= nq * in * 4, RVX_ERR_DIMENSION_MISMATCH, "nodes smaller than nq*input_dim");
+        RVX_REQUIRE(table->mem.bytes >= table_rows * in * 4, RVX_ERR_DIMENSION_MISMATCH,
+                    "table smaller than table_rows*input_dim");
+        RVX_REQUIRE(cand_ids->mem.bytes >= nq * (int64_t)c * 8, RVX_ERR_DIMENSION_MISMATCH, "cand_ids smaller than nq*c");
+        RVX_REQUIRE(!weights || weights->mem.bytes >= nq * (int64_t)c * 4, RVX_ERR_DIMENSION_MISMATCH,
+                    "weights smaller than nq*c");
+        RVX_REQUIRE(out->mem.bytes >= nq * H * 4, RVX_ERR_DIMENSION_MISMATCH, "out smaller than nq*hidden_dim");
+        const int64_t n = nq + nq * (int64_t)c;
+        RVX_REQUIRE(n < ((int64_t)1 << 31), RVX_ERR_INVALID_SHAPE, "star table exceeds int32 neighbour ids");
+        ComputeLock cl;
+        const int64_t* ids = cand_ids->mem.as<int64_t>();
+        float* T = scratch_f32("rvs_t", n * in);
+        auto* deg = (int32_t*)scratch_bytes("rvs_deg", nq * 4);
+        auto* drp = (int64_t*)scratch_bytes("rvs_rp", (nq + 1) * 8);
+        auto* dcol = (int32_t*)scratch_bytes("rvs_col", std::max<int64_t>(nq * c, 1) * 4);
+        float* dw = weights ? scratch_f32("rvs_w", std::max<int64_t>(nq * c, 1)) : nullptr;
+        star_gather(nodes->mem.as<float>(), nq, table->mem.as<float>(), table_rows, ids, c, (int)in, T);
+        // row_ptr: prefix sum of the per-node valid-candidate counts on the host
+        star_degrees(ids, nq, c, table_rows, deg);
+        std::vector<int32_t> hdeg(nq);
+        std::vector<int64_t> hrp(nq + 1, 0);
+        RVX_HIP(hipMemcpyAsync(hdeg.data(), deg, (size_t)nq * 4, hipMemcpyDeviceToHost, stream()));
+        sync();
+        int64_t max_deg = 0;
+        for (int64_t i = 0; i < nq; ++i) {
+            hrp[i + 1] = hrp[i] + hdeg[i];
+            max_deg = std::max<int64_t>(max_deg, hdeg[i]);
+        }
+        RVX_HIP(hipMemcpyAsync(drp, hrp.data(), (size_t)(nq + 1) * 8, hipMemcpyHostToDevice, stream()));
+        star_csr(ids, weights ? weights->mem.as<float>() : nullptr, nq, c, table_rows, drp, dcol, dw);
+        // weights absent -> aggregate_messages returns zeros (layer.rs:427-429): wmode 0
+        forward_dev(l, n, drp, dcol, max_deg, dw, weights ? 2 : 0, T, out->mem.as<float>(), nq);
+        sync();  // hrp / hdeg are host temporaries
     });
 }
 

@@ -29,6 +29,6 @@ struct EfaArgs {
 
 void edge_feat_attention(const EfaArgs& a);
 void differentiable_search(const float* q, int64_t nq, const float* cand, int C, int d, int k, float temperature,
-                           float* sims, int64_t* out_idx, float* out_w);
+                           float* sims, int64_t* out_idx, float* out_w, float* soft = nullptr);
 
 }  // namespace rvx

@@ -44,4 +44,18 @@ int edge_group_lanes(int H, int heads);  // 0 when the grouped kernel does not a
 void mul_rows(const float* r, int64_t ldr, const float* h, float* out, int64_t n, int H);
 void gru_finish(const FinishArgs& a);
 
+// Star tables for batched per-node calls (RuvectorLayer::forward(node,
+// neighbours, weights) and differentiable_search over candidate lists):
+// dst rows [0, nq) = nodes (skipped when nodes == nullptr), rows nq + i*c + j =
+// table[ids[i*c + j]] (zeros for an id outside [0, trows)).
+void star_gather(const float* nodes, int64_t nq, const float* table, int64_t trows, const int64_t* ids, int c, int d,
+                 float* dst);
+// Valid-candidate count per node (ids in [0, trows)).
+void star_degrees(const int64_t* ids, int64_t nq, int c, int64_t trows, int32_t* deg);
+// CSR over the star table from host-summed row_ptr: col = nq + i*c + j for each
+// valid slot in order; w (nullable) -> aggregate_messages-normalised weights
+// (layer.rs:421-445: w / sum over the node's weights, 1/deg when sum <= 0).
+void star_csr(const int64_t* ids, const float* w, int64_t nq, int c, int64_t trows, const int64_t* rp, int32_t* col,
+              float* wn);
+
 }  // namespace rvx

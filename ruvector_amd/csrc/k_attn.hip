@@ -134,7 +134,8 @@ __global__ __launch_bounds__(256) void k_edge_feat_out(EfaArgs a) {
 
 // ---- differentiable_search -------------------------------------------------
 __global__ __launch_bounds__(64) void k_diff_search(const float* q, int64_t nq, const float* cand, int C, int d, int k,
-                                                    float temperature, float* sims, int64_t* out_idx, float* out_w) {
+                                                    float temperature, float* sims, int64_t* out_idx, float* out_w,
+                                                    float* soft) {
     const int lane = threadIdx.x;
     const int64_t qi = blockIdx.x;
     if (qi >= nq) return;
@@ -164,6 +165,8 @@ __global__ __launch_bounds__(64) void k_diff_search(const float* q, int64_t nq, 
     for (int j = 0; j < C; ++j) { const float e = expf((s[j] - mx) / temperature); s[j] = e; sum = sum + e; }
     sum = fmaxf(sum, 1e-10f);
     for (int j = 0; j < C; ++j) s[j] = s[j] / sum;
+    if (soft)
+        for (int j = 0; j < C; ++j) soft[qi * C + j] = s[j];
     // stable sort by weight descending (ties keep index order), take k
     const int kk = min(k, C);
     for (int t = 0; t < k; ++t) {
@@ -204,11 +207,11 @@ void edge_feat_attention(const EfaArgs& a) {
 }
 
 void differentiable_search(const float* q, int64_t nq, const float* cand, int C, int d, int k, float temperature,
-                           float* sims, int64_t* out_idx, float* out_w) {
+                           float* sims, int64_t* out_idx, float* out_w, float* soft) {
     if (nq <= 0) return;
     ProfScope ps("differentiable_search");
     hipLaunchKernelGGL(k_diff_search, dim3((unsigned)nq), dim3(64), 0, stream(), q, nq, cand, C, d, k, temperature, sims,
-                       out_idx, out_w);
+                       out_idx, out_w, soft);
     RVX_HIP(hipGetLastError());
 }
 

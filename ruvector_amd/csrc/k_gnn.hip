@@ -239,4 +239,86 @@ void gru_finish(const FinishArgs& a) {
     RVX_LAUNCH("gnn_finish", k_gru_finish, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, a);
 }
 
+namespace {
+
+__global__ __launch_bounds__(256) void k_star_gather(const float* nodes, int64_t nq, const float* table, int64_t trows,
+                                                     const int64_t* ids, int c, int d, float* dst) {
+    const int64_t rows = (nodes ? nq : 0) + nq * c;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t base = nodes ? nq : 0;
+    const float* src = nullptr;
+    if (nodes && r < nq) src = nodes + r * d;
+    else {
+        const int64_t id = ids[r - base];
+        if (id >= 0 && id < trows) src = table + id * d;
+    }
+    float* o = dst + r * d;
+    if (!src) {
+        for (int i = lane; i < d; i += 64) o[i] = 0.0f;
+        return;
+    }
+    if ((d & 3) == 0 && (((uintptr_t)src | (uintptr_t)o) & 15) == 0) {
+        for (int i = lane; i < d / 4; i += 64)
+            reinterpret_cast<float4*>(o)[i] = reinterpret_cast<const float4*>(src)[i];
+    } else {
+        for (int i = lane; i < d; i += 64) o[i] = src[i];
+    }
+}
+
+__global__ void k_star_degrees(const int64_t* ids, int64_t nq, int c, int64_t trows, int32_t* deg) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    int n = 0;
+    for (int j = 0; j < c; ++j) {
+        const int64_t id = ids[i * c + j];
+        n += (id >= 0 && id < trows);
+    }
+    deg[i] = n;
+}
+
+__global__ void k_star_csr(const int64_t* ids, const float* w, int64_t nq, int c, int64_t trows, const int64_t* rp,
+                           int32_t* col, float* wn) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    int64_t e = rp[i];
+    const int deg = (int)(rp[i + 1] - rp[i]);
+    float sum = 0.0f;
+    if (w)
+        for (int j = 0; j < c; ++j) {
+            const int64_t id = ids[i * c + j];
+            if (id >= 0 && id < trows) sum = sum + w[i * c + j];
+        }
+    for (int j = 0; j < c; ++j) {
+        const int64_t id = ids[i * c + j];
+        if (!(id >= 0 && id < trows)) continue;
+        col[e] = (int32_t)(nq + i * c + j);
+        if (w) wn[e] = sum > 0.0f ? w[i * c + j] / sum : 1.0f / (float)deg;
+        ++e;
+    }
+}
+
+}  // namespace
+
+void star_gather(const float* nodes, int64_t nq, const float* table, int64_t trows, const int64_t* ids, int c, int d,
+                 float* dst) {
+    const int64_t rows = (nodes ? nq : 0) + nq * c;
+    if (rows <= 0) return;
+    RVX_LAUNCH("star_gather", k_star_gather, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, nodes, nq, table, trows,
+               ids, c, d, dst);
+}
+
+void star_degrees(const int64_t* ids, int64_t nq, int c, int64_t trows, int32_t* deg) {
+    if (nq <= 0) return;
+    RVX_LAUNCH("star_csr", k_star_degrees, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, ids, nq, c, trows, deg);
+}
+
+void star_csr(const int64_t* ids, const float* w, int64_t nq, int c, int64_t trows, const int64_t* rp, int32_t* col,
+              float* wn) {
+    if (nq <= 0) return;
+    RVX_LAUNCH("star_csr", k_star_csr, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, ids, w, nq, c, trows, rp, col,
+               wn);
+}
+
 }  // namespace rvx

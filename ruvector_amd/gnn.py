@@ -90,6 +90,13 @@ class RuvectorLayer:
     def forward_graph_device(self, x: Buffer, graph: Graph, y: Buffer) -> None:
         _check("rvx_gnn_forward_graph_device", self._h, graph.handle, x.handle, y.handle)
 
+    def forward_star_device(self, nodes: Buffer, nq: int, table: Buffer, table_rows: int, cand_ids: Buffer, c: int,
+                            weights: Optional[Buffer], out: Buffer) -> None:
+        """forward(nodes[i], table[cand_ids[i]], weights[i]) for i < nq, all resident in HBM
+        (ids outside [0, table_rows) are absent neighbours; weights None -> no edge weights)."""
+        _check("rvx_gnn_forward_star_device", self._h, nodes.handle, int(nq), table.handle, int(table_rows),
+               cand_ids.handle, int(c), weights.handle if weights is not None else None, out.handle)
+
     def __del__(self):
         try:
             if self._h:
@@ -192,6 +199,17 @@ def differentiable_search_batch(queries: np.ndarray, candidates: np.ndarray, k: 
         _check("rvx_differentiable_search_batch", L.fptr(q), nq, L.fptr(cand), c, d, k, float(temperature),
                L.i64ptr(idx), L.fptr(w))
     return idx[:, :kk], w[:, :kk]
+
+
+def differentiable_search_device(q: Buffer, nq: int, table: Buffer, table_rows: int, cand_ids: Buffer, c: int,
+                                 d: int, k: int, temperature: float, idx: Optional[Buffer] = None,
+                                 w: Optional[Buffer] = None, soft: Optional[Buffer] = None) -> None:
+    """differentiable_search (search.rs:56-94) for nq queries whose candidates are table rows
+    cand_ids[i] (all valid): idx [nq][k] int64 positions in the candidate list, w [nq][k],
+    soft (optional) [nq][c] the softmax weights in candidate order."""
+    _check("rvx_differentiable_search_device", q.handle, int(nq), table.handle, int(table_rows), cand_ids.handle,
+           int(c), int(d), int(k), float(temperature), idx.handle if idx is not None else None,
+           w.handle if w is not None else None, soft.handle if soft is not None else None)
 
 
 def differentiable_search(query, candidate_embeddings, k: int, temperature: float) -> Tuple[List[int], List[float]]:

@@ -1,0 +1,115 @@
+"""GPU parity: batched RuvectorLayer::forward over star neighbourhoods, device
+differentiable_search, and the RuvectorQuery NeuralSearch pipeline (C3's re-rank),
+each against the oracle composition of the reference's per-node functions
+(layer.rs:379-423, search.rs:56-94) on the same inputs."""
+import json
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+rv = pytest.importorskip("ruvector_amd")
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-30))
+
+
+def _layer(in_dim, hidden, heads, seed):
+    layer = rv.RuvectorLayer(in_dim, hidden, heads, 0.0, seed=seed)
+    return layer, O.RvlWeights(json.loads(layer.to_json()))
+
+
+@pytest.mark.parametrize("weighted", [True, False])
+def test_forward_star_matches_per_node_forward(weighted):
+    d, nq, c, rows = 32, 24, 7, 300
+    layer, W = _layer(d, d, 4, 11)
+    table = O.fill_uniform(rows * d, 1).reshape(rows, d)
+    nodes = O.fill_uniform(nq * d, 2).reshape(nq, d)
+    ids = np.random.default_rng(3).integers(0, rows, (nq, c)).astype(np.int64)
+    ids[1, 3] = -1            # absent neighbour in the middle
+    ids[2, :] = -1            # no neighbours: normalised projection (layer.rs:386-390)
+    ids[5, 6] = rows + 4      # outside the table: absent
+    w = O.fill_uniform(nq * c, 4, 0.0, 1.0).reshape(nq, c)
+    w[7, :] = 0.0             # zero weight sum -> uniform 1/deg
+    out = rv.Buffer(nq * d * 4)
+    layer.forward_star_device(rv.Buffer.from_numpy(nodes), nq, rv.Buffer.from_numpy(table), rows,
+                              rv.Buffer.from_numpy(ids), c, rv.Buffer.from_numpy(w) if weighted else None, out)
+    got = out.download(np.float32, (nq, d))
+    for i in range(nq):
+        ok = (ids[i] >= 0) & (ids[i] < rows)
+        nb = table[ids[i][ok]]
+        ref = O.rvl_forward_one(W, nodes[i], nb, w[i][ok] if weighted else [])
+        assert rel_err(got[i], ref) <= TOL, i
+
+
+def test_differentiable_search_device_matches_oracle():
+    d, nq, c, rows, k = 48, 16, 20, 500, 10
+    table = O.fill_uniform(rows * d, 5).reshape(rows, d)
+    q = O.fill_uniform(nq * d, 6).reshape(nq, d)
+    ids = np.stack([np.random.default_rng(7 + i).choice(rows, c, replace=False) for i in range(nq)]).astype(np.int64)
+    idx, w, soft = rv.Buffer(nq * k * 8), rv.Buffer(nq * k * 4), rv.Buffer(nq * c * 4)
+    tb = rv.Buffer.from_numpy(table)
+    rv.differentiable_search_device(rv.Buffer.from_numpy(q), nq, tb, rows, rv.Buffer.from_numpy(ids), c, d, k, 0.5,
+                                    idx=idx, w=w, soft=soft)
+    gi, gw, gs = idx.download(np.int64, (nq, k)), w.download(np.float32, (nq, k)), soft.download(np.float32, (nq, c))
+    for i in range(nq):
+        ri, rw = O.differentiable_search(q[i], table[ids[i]], k, 0.5)
+        # positions bit-exact; weights within 1e-6 relative (device expf vs libm expf: <= 1 ulp)
+        assert np.array_equal(gi[i], ri) and rel_err(gw[i], rw) <= 1e-6
+        fi, fw = O.differentiable_search(q[i], table[ids[i]], c, 0.5)
+        full = np.empty(c, np.float32)
+        full[fi] = fw
+        assert np.max(np.abs(gs[i].astype(np.float64) - full) / full) <= 1e-6
+    bad = ids.copy()
+    bad[0, 0] = -1
+    with pytest.raises(rv.GnnError):  # the candidate list has no holes
+        rv.differentiable_search_device(rv.Buffer.from_numpy(q), nq, tb, rows, rv.Buffer.from_numpy(bad), c, d, k, 0.5,
+                                        idx=idx, w=w)
+
+
+def test_neural_search_pipeline_matches_oracle_composition():
+    n, d, nq = 3000, 32, 40
+    x = O.fill_uniform(n * d, 21).reshape(n, d)
+    q = O.fill_uniform(nq * d, 22).reshape(nq, d)
+    idx = rv.HnswIndex(d, rv.DistanceMetric.Euclidean, rv.HnswConfig(m=16, ef_construction=100, ef_search=50))
+    xb = rv.Buffer.from_numpy(x)
+    idx.add_device(xb, n, 0)
+    layers = [_layer(d, d, 4, 31 + i) for i in range(2)]
+    ns = rv.NeuralSearch(idx, xb, n, d, [l for l, _ in layers])
+    query = rv.RuvectorQuery(mode=rv.QueryMode.NeuralSearch)  # k 10, ef 50, depth 2, T 1 (query.rs:44-58)
+    ids, wts = ns.search(q, query)
+
+    # oracle: the reference functions composed per query on the same graph
+    h_ref = O.Hnsw.from_graph(x, idx.export_graph())
+    cand, _, _ = h_ref.search(q, query.ef, query.ef)
+    mism = 0
+    for i in range(nq):
+        cv = x[cand[i]]
+        fi, fw = O.differentiable_search(q[i], cv, len(cv), query.temperature)
+        soft = np.empty(len(cv), np.float32)
+        soft[fi] = fw
+        h = q[i]
+        for _, W in layers[:query.gnn_depth]:
+            h = O.rvl_forward_one(W, h, cv, soft)
+        pi, pw = O.differentiable_search(h, cv, query.k, query.temperature)
+        ref_ids = cand[i][pi].astype(np.uint64)
+        assert rel_err(wts[i], pw) <= 1e-4, i
+        if not np.array_equal(ids[i], ref_ids):
+            # only a near-tie in the final softmax may reorder (h agrees to ~1e-6)
+            mism += 1
+            gap = np.min(np.abs(np.diff(np.sort(pw)))) if len(pw) > 1 else 1.0
+            assert gap < 1e-5 * max(float(pw.max()), 1e-30), (i, ids[i], ref_ids)
+    assert mism <= nq // 20
+
+
+def test_ruvector_query_defaults():
+    qd = rv.RuvectorQuery()
+    assert (qd.k, qd.ef, qd.gnn_depth, qd.temperature, qd.mode) == (10, 50, 2, 1.0, rv.QueryMode.VectorSearch)
+    assert rv.RuvectorQuery.neural_search([0.1], 10, 3).gnn_depth == 3
+    assert rv.RuvectorQuery.differentiable_search([0.1], 5, 0.5).temperature == 0.5
