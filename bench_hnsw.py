@@ -20,13 +20,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
-def run(n, d, nq, m, efc, efs, k, metric_name, seed_base=1, cpu=False, cpu_seconds=10.0, cpu_build=False, log=print):
+def run(n, d, nq, m, efc, efs, k, metric_name, seed_base=1, cpu=False, cpu_seconds=10.0, cpu_build=False, log=print,
+        data="uniform", keep=None):
+    """data: 'uniform' [-1,1) (C1) or 'normal' N(0,1) Box-Muller (C3); base seed `seed_base`,
+    queries seed_base + 1. keep (dict, optional) receives the index and device buffers."""
     import ruvector_amd as rv
     metric = {"l2": rv.DistanceMetric.Euclidean, "cosine": rv.DistanceMetric.Cosine}[metric_name]
     xb = rv.Buffer(n * d * 4)
-    xb.fill_uniform(n * d, seed_base, -1.0, 1.0)
     qb = rv.Buffer(nq * d * 4)
-    qb.fill_uniform(nq * d, seed_base + 1, -1.0, 1.0)
+    if data == "normal":
+        xb.fill_normal(n * d, seed_base)
+        qb.fill_normal(nq * d, seed_base + 1)
+    else:
+        xb.fill_uniform(n * d, seed_base, -1.0, 1.0)
+        qb.fill_uniform(nq * d, seed_base + 1, -1.0, 1.0)
     if metric_name == "cosine":
         xb.normalize_rows(n, d)
         qb.normalize_rows(nq, d)
@@ -58,13 +65,21 @@ def run(n, d, nq, m, efc, efs, k, metric_name, seed_base=1, cpu=False, cpu_secon
             rv.synchronize()
             dt = time.perf_counter() - t0
         ker_ms, _ = prof.query("hnsw_search")
+        st = rv.hnsw_last_search_stats()
+        # bytes = n_dist * d * 4 + n_expand * deg_cap * 4 (deg_cap = 2M on layer 0)
+        alg_bytes = st["n_dist"] * d * 4 + st["n_expand"] * 2 * m * 4
         got = ids_b.download(np.uint64, (nq, k))
         rec = float(np.mean([len(set(a.tolist()) & set(b.tolist())) / k for a, b in zip(gt, got)]))
-        sweep.append({"ef": ef, "recall": round(rec, 4), "qps": round(nq / dt, 1), "kernel_ms": round(ker_ms, 3)})
-        log(f"ef={ef}: recall@{k}={rec:.4f} qps={nq / dt:.0f} (kernel {ker_ms:.2f} ms)")
+        sweep.append({"ef": ef, "recall": round(rec, 4), "qps": round(nq / dt, 1), "kernel_ms": round(ker_ms, 3),
+                      "dist_per_query": round(st["n_dist"] / nq, 1), "expand_per_query": round(st["n_expand"] / nq, 1),
+                      "alg_GBps": round(alg_bytes / (ker_ms * 1e-3) / 1e9, 1) if ker_ms > 0 else None})
+        log(f"ef={ef}: recall@{k}={rec:.4f} qps={nq / dt:.0f} (kernel {ker_ms:.2f} ms, "
+            f"{st['n_dist'] / nq:.0f} dist/query, {sweep[-1]['alg_GBps']} GB/s algorithmic)")
     ok = [s for s in sweep if s["recall"] >= 0.95]
     best = max(ok, key=lambda s: s["qps"]) if ok else None
-    out = {"config": f"{n}x{d} uniform, {nq} queries, M={m}, ef_c={efc}, k={k}, {metric_name}",
+    if keep is not None:
+        keep.update(index=idx, x=xb, q=qb, gt=gt)
+    out = {"config": f"{n}x{d} {data}, {nq} queries, M={m}, ef_c={efc}, k={k}, {metric_name}",
            "build_s": round(build_s, 3), "sweep": sweep, "qps_at_recall95": best["qps"] if best else None,
            "ef_at_recall95": best["ef"] if best else None}
     if cpu_build:
@@ -84,7 +99,8 @@ def run(n, d, nq, m, efc, efs, k, metric_name, seed_base=1, cpu=False, cpu_secon
             cs.append({"ef": ef, "recall": round(rec, 4)})
         out["cpu_build"] = {"build_s": round(cb, 2), "threads": min(16, os.cpu_count() or 1), "sweep_2k_queries": cs}
         log(f"cpu build {cb:.1f} s; recall {cs}")
-    if cpu and best:
+    pick = best or (max(sweep, key=lambda s: s["recall"]) if sweep else None)  # CPU leg at recall >= 0.95 if reached
+    if cpu and pick:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle as O
         x = xb.download(np.float32, (n, d))
@@ -93,15 +109,17 @@ def run(n, d, nq, m, efc, efs, k, metric_name, seed_base=1, cpu=False, cpu_secon
         threads = min(16, os.cpu_count() or 1)
         sample = min(nq, 500)
         t0 = time.perf_counter()
-        h.search(q[:sample], k, best["ef"], threads=threads)
+        h.search(q[:sample], k, pick["ef"], threads=threads)
         dt = time.perf_counter() - t0
         sample = int(min(nq, max(sample, sample * cpu_seconds / max(dt, 1e-3))))
         t0 = time.perf_counter()
-        cids, _, _ = h.search(q[:sample], k, best["ef"], threads=threads)
+        cids, _, _ = h.search(q[:sample], k, pick["ef"], threads=threads)
         dt = time.perf_counter() - t0
-        gpu_ids = idx.search_array(q[:sample], k, best["ef"])[0].astype(np.int64)
+        gpu_ids = idx.search_array(q[:sample], k, pick["ef"])[0].astype(np.int64)
         out["cpu_baseline"] = {"value": round(sample / dt, 1), "unit": "queries/s", "cores": threads, "kind": "port",
-                               "sample": f"oracle hnsw_rs search_filter on the same graph, {sample} queries, ef={best['ef']}"}
+                               "sample": f"oracle hnsw_rs search_filter on the same graph, {sample} queries, "
+                                         f"ef={pick['ef']} (recall {pick['recall']})",
+                               "gpu_qps_same_ef": pick["qps"]}
         out["cpu_gpu_ids_equal"] = bool(np.array_equal(cids, gpu_ids))
     return out
 
@@ -118,9 +136,12 @@ def main():
     p.add_argument("--metric", default="l2")
     p.add_argument("--cpu", action="store_true")
     p.add_argument("--cpu-build", action="store_true")
+    p.add_argument("--data", default="uniform", choices=["uniform", "normal"])
+    p.add_argument("--seed", type=int, default=1)
     a = p.parse_args()
     out = run(a.n, a.dim, a.queries, a.m, a.ef_construction, [int(e) for e in a.ef.split(",")], a.k, a.metric,
-              cpu=a.cpu, cpu_build=a.cpu_build, log=lambda s: print(s, file=sys.stderr, flush=True))
+              seed_base=a.seed, cpu=a.cpu, cpu_build=a.cpu_build, log=lambda s: print(s, file=sys.stderr, flush=True),
+              data=a.data)
     print(json.dumps(out))
 
 

@@ -288,6 +288,10 @@ rvx_status rvx_index_brute_force(const rvx_index* idx, const float* q, int64_t n
                                  uint64_t* out_ids, float* out_dist);
 rvx_status rvx_index_brute_force_device(const rvx_index* idx, const rvx_buffer* q, int64_t nq, int32_t k,
                                         rvx_buffer* out_ids_u64, rvx_buffer* out_dist_f32);
+/* Work of the most recent HNSW search launch in this process (any index): distance
+ * evaluations, layer-0 expansions and queries — the algorithmic traffic of the search is
+ * n_dist * dim * 4 + n_expand * deg_cap * 4 bytes. */
+rvx_status rvx_hnsw_last_search_stats(int64_t* n_dist, int64_t* n_expand, int64_t* nq);
 
 /* HNSW graph interchange (fixed-graph parity and GNN topology).
  * Layer 0: CSR over all n points in stored neighbour order (hnsw_rs keeps

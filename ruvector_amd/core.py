@@ -216,6 +216,13 @@ class _Index:
             pass
 
 
+def hnsw_last_search_stats() -> dict:
+    """Work of the most recent HNSW search launch: distance evaluations, layer-0 expansions, queries."""
+    a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+    _check("rvx_hnsw_last_search_stats", C.byref(a), C.byref(b), C.byref(c))
+    return {"n_dist": a.value, "n_expand": b.value, "nq": c.value}
+
+
 class FlatIndex(_Index):
     """FlatIndex (index/flat.rs): exact scan, results sorted by distance."""
     kind = L.INDEX_FLAT

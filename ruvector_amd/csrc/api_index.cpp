@@ -435,4 +435,12 @@ rvx_status rvx_distance_matrix(int32_t metric, const float* q, int64_t nq, const
     });
 }
 
+rvx_status rvx_hnsw_last_search_stats(int64_t* n_dist, int64_t* n_expand, int64_t* nq) {
+    return guard([&] {
+        if (n_dist) *n_dist = g_search_stats.n_dist;
+        if (n_expand) *n_expand = g_search_stats.n_expand;
+        if (nq) *nq = g_search_stats.nq;
+    });
+}
+
 }  // extern "C"

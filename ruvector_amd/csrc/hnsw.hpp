@@ -4,7 +4,7 @@
 
 namespace rvx {
 
-constexpr int HNSW_MAX_EF = 1024;
+constexpr int HNSW_MAX_EF = 8192;  // bounded in practice by one wave's LDS (hnsw_search_lds)
 constexpr int HNSW_MAX_LEVEL = 16;  // NB_LAYER_MAX (patches/hnsw_rs/src/hnsw.rs:41)
 
 // Layer 0 is a CSR over all n points; layer l>=1 is a CSR over the sorted ids
@@ -29,5 +29,12 @@ struct HnswDev {
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
                  const float* qnorm, int64_t nq, int k, int ef, float* out_d, int64_t* out_i, int32_t* out_n,
                  const char* tag, float curv = 1.0f, int hyper = 0);
+
+// Work tallies of the most recent hnsw_search launch (SURVEY.md §8d C1/C3:
+// bytes = n_dist * d * 4 + n_expand * deg_cap * 4 per launch).
+struct SearchStats {
+    int64_t n_dist = 0, n_expand = 0, nq = 0;
+};
+extern SearchStats g_search_stats;
 
 }  // namespace rvx

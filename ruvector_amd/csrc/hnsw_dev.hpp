@@ -13,30 +13,76 @@ namespace hnswdev {
 constexpr int VCAP_MIN = 32768;  // visited-set slots per query (power of two), grown with ef
 constexpr int C_EXTRA = 128; // candidate capacity = ef + C_EXTRA
 
+// One float4 step of the reference's scalar accumulation (distance.rs:34-85).
+template <int METRIC>
+__device__ __forceinline__ float acc4(float acc, const float4& q, const float4& v) {
+    if (METRIC == RVX_METRIC_L2) {
+        float t = q.x - v.x; acc = acc + t * t;
+        t = q.y - v.y; acc = acc + t * t;
+        t = q.z - v.z; acc = acc + t * t;
+        t = q.w - v.w; acc = acc + t * t;
+    } else if (METRIC == RVX_METRIC_L1) {
+        acc = acc + fabsf(q.x - v.x); acc = acc + fabsf(q.y - v.y);
+        acc = acc + fabsf(q.z - v.z); acc = acc + fabsf(q.w - v.w);
+    } else {
+        acc = acc + q.x * v.x; acc = acc + q.y * v.y; acc = acc + q.z * v.z; acc = acc + q.w * v.w;
+    }
+    return acc;
+}
+
+template <int METRIC>
+__device__ __forceinline__ float finish_dist(float acc, float qn, float xn) {
+    if (METRIC == RVX_METRIC_L2) return sqrtf(acc);
+    if (METRIC == RVX_METRIC_DOT) return -acc;
+    if (METRIC == RVX_METRIC_COSINE) return (qn > 1e-8f && xn > 1e-8f) ? 1.0f - acc / (qn * xn) : 1.0f;
+    return acc;
+}
+
+// One lane's exact-order distance over a stored row, the row streamed in
+// 128-B batches with the next batch's loads in flight while the current one
+// accumulates (one load at a time would expose a memory round trip per 16 B
+// of a 3 KB row). Q_GLOBAL: the other operand is a stored row too (pair_dist)
+// and is streamed the same way; otherwise it is read at use (LDS).
+constexpr int ROW_BATCH = 8;  // float4s per batch
+
+template <int METRIC, bool Q_GLOBAL>
+__device__ __forceinline__ float stream_acc(const float* __restrict__ qs, const float* __restrict__ x, int n4) {
+    const float4* r = reinterpret_cast<const float4*>(x);
+    const float4* qq = reinterpret_cast<const float4*>(qs);
+    float acc = 0.0f;
+    float4 xa[ROW_BATCH], xb[ROW_BATCH], qa[Q_GLOBAL ? ROW_BATCH : 1], qb[Q_GLOBAL ? ROW_BATCH : 1];
+    auto load = [&](float4* xv, float4* qv, int base) {
+#pragma unroll
+        for (int j = 0; j < ROW_BATCH; ++j)
+            if (base + j < n4) {
+                xv[j] = r[base + j];
+                if constexpr (Q_GLOBAL) qv[j] = qq[base + j];
+            }
+    };
+    auto run = [&](const float4* xv, const float4* qv, int base) {
+#pragma unroll
+        for (int j = 0; j < ROW_BATCH; ++j)
+            if (base + j < n4) acc = acc4<METRIC>(acc, Q_GLOBAL ? qv[j] : qq[base + j], xv[j]);
+    };
+    load(xa, qa, 0);
+    for (int base = 0; base < n4; base += 2 * ROW_BATCH) {
+        load(xb, qb, base + ROW_BATCH);
+        run(xa, qa, base);
+        load(xa, qa, base + 2 * ROW_BATCH);
+        run(xb, qb, base + ROW_BATCH);
+    }
+    return acc;
+}
+
 // curv: the Poincaré curvature (RVX_METRIC_POINCARE only: HyperbolicHnsw::distance,
 // fused norms + poincare_distance_from_norms, hnsw.rs:173-180)
-template <int METRIC>
+template <int METRIC, bool Q_GLOBAL = false>
 __device__ __forceinline__ float row_dist(const float* __restrict__ qs, const float* __restrict__ x, int d, float qn,
                                           float xn, float curv = 1.0f) {
     if constexpr (METRIC == RVX_METRIC_POINCARE) return pdev::hyp_dist(qs, x, d, curv);
     float acc = 0.0f;
     if ((d & 3) == 0) {
-        const float4* r = reinterpret_cast<const float4*>(x);
-        const float4* qq = reinterpret_cast<const float4*>(qs);
-        for (int k = 0; k < (d >> 2); ++k) {
-            const float4 v = r[k], q = qq[k];
-            if (METRIC == RVX_METRIC_L2) {
-                float t = q.x - v.x; acc = acc + t * t;
-                t = q.y - v.y; acc = acc + t * t;
-                t = q.z - v.z; acc = acc + t * t;
-                t = q.w - v.w; acc = acc + t * t;
-            } else if (METRIC == RVX_METRIC_L1) {
-                acc = acc + fabsf(q.x - v.x); acc = acc + fabsf(q.y - v.y);
-                acc = acc + fabsf(q.z - v.z); acc = acc + fabsf(q.w - v.w);
-            } else {
-                acc = acc + q.x * v.x; acc = acc + q.y * v.y; acc = acc + q.z * v.z; acc = acc + q.w * v.w;
-            }
-        }
+        acc = stream_acc<METRIC, Q_GLOBAL>(qs, x, d >> 2);
     } else {
         for (int k = 0; k < d; ++k) {
             const float q = qs[k], v = x[k];
@@ -45,10 +91,7 @@ __device__ __forceinline__ float row_dist(const float* __restrict__ qs, const fl
             else acc = acc + q * v;
         }
     }
-    if (METRIC == RVX_METRIC_L2) return sqrtf(acc);
-    if (METRIC == RVX_METRIC_DOT) return -acc;
-    if (METRIC == RVX_METRIC_COSINE) return (qn > 1e-8f && xn > 1e-8f) ? 1.0f - acc / (qn * xn) : 1.0f;
-    return acc;
+    return finish_dist<METRIC>(acc, qn, xn);
 }
 
 // Claim `node` in a query's visited set: true if it was not visited yet.
@@ -74,7 +117,8 @@ __device__ __forceinline__ bool visit_claim(unsigned long long* vis, unsigned vm
 // visited-table size for a search of width ef (load factor well below 1/2)
 inline unsigned visited_capacity(int ef) {
     unsigned v = VCAP_MIN;
-    while (v < (unsigned)ef * 128u && v < (1u << 22)) v <<= 1;
+    // a search of width ef expands ~ef..2ef nodes of <= 64 neighbours each
+    while (v < (unsigned)ef * 256u && v < (1u << 23)) v <<= 1;
     return v;
 }
 
@@ -113,7 +157,7 @@ __device__ __forceinline__ int sorted_insert(float* ad, int* ai, int size, float
 template <int METRIC>
 __device__ __forceinline__ float pair_dist(const float* __restrict__ a, const float* __restrict__ b, int d, float na,
                                            float nb, float curv = 1.0f) {
-    return row_dist<METRIC>(a, b, d, na, nb, curv);
+    return row_dist<METRIC, true>(a, b, d, na, nb, curv);
 }
 
 }  // namespace hnswdev

@@ -21,6 +21,8 @@
 // with wave-parallel sorted inserts; the visited set is an open-addressing
 // hash in a per-wave global scratch slot (32K entries, CAS-claimed by all
 // lanes at once); neighbour distances are computed one row per lane.
+#include <cstring>
+
 #include "common.hpp"
 #include "graph.hpp"
 #include "hnsw.hpp"
@@ -40,6 +42,7 @@ struct SearchArgs {
     unsigned vcap;
     float* out_d; int64_t* out_i; int32_t* out_n;  // [nq][k]
     int* status;       // set to 1 on candidate overflow
+    unsigned long long* stats;  // [2]: distance evaluations, layer-0 expansions (per launch)
     float curv;        // Poincaré curvature
     int hyper;         // HyperbolicHnsw::search semantics (see below)
 };
@@ -60,6 +63,7 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
     unsigned long long* vis = a.visited + (int64_t)blockIdx.x * a.vcap;
     const unsigned vmask = a.vcap - 1;
 
+    unsigned long long n_dist = 0, n_expand = 0;  // lane 0's tallies for this wave
     for (int64_t qi = blockIdx.x; qi < a.nq; qi += a.nslots) {
         const unsigned long long qtag = (unsigned long long)(qi + 1) << 32;
         for (int i = lane; i < dq; i += 64) qs[i] = (i < a.d) ? a.q[qi * a.d + i] : 0.0f;
@@ -93,6 +97,7 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
                     float dd = INFINITY;
                     int pos = INT_MAX, nid = -1;
                     if (p < e) { nid = col[p]; dd = dist_of(nid); pos = (int)(p - b); }
+                    n_dist += (unsigned long long)min<int64_t>(64, e - c0);
                     // first position holding the minimum of this chunk
 #pragma unroll
                     for (int o = 32; o > 0; o >>= 1) {
@@ -135,6 +140,7 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
             // -(c.dist) > f.dist -> return; HyperbolicHnsw also needs |R| >= ef (hnsw.rs:357-361)
             if (c_d > rd[rs - 1] && (!a.hyper || rs >= ef)) break;
             const int64_t b = a.g.rp0[c_id], e = a.g.rp0[c_id + 1];
+            n_expand += 1;
             for (int64_t c0 = b; c0 < e; c0 += 64) {
                 const int64_t p = c0 + lane;
                 int nid = -1;
@@ -147,6 +153,7 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
                 if (fresh) dd = dist_of(nid);
                 // sequential admission in neighbour order (hnsw.rs:1004-1046)
                 unsigned long long todo = __ballot(fresh);
+                n_dist += (unsigned long long)__popcll(todo);
                 while (todo) {
                     const int src = __ffsll((long long)todo) - 1;
                     todo &= todo - 1;
@@ -191,9 +198,15 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
         if (lane == 0) a.out_n[qi] = take;
         __builtin_amdgcn_wave_barrier();
     }
+    if (lane == 0 && a.stats) {
+        atomicAdd(&a.stats[0], n_dist + 2);  // + the entry point's distance and layer 0's start
+        atomicAdd(&a.stats[1], n_expand);
+    }
 }
 
 }  // namespace
+
+SearchStats g_search_stats;
 
 size_t hnsw_search_lds(int d, int ef) {
     const int dq = (d + 3) & ~3;
@@ -207,13 +220,14 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     RVX_REQUIRE(ef >= 1 && ef <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER,
                 "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
     const unsigned vcap = visited_capacity(ef);
-    const int64_t mem_slots = std::max<int64_t>(1024, ((int64_t)4 << 30) / ((int64_t)vcap * 8));
+    const int64_t mem_slots = std::max<int64_t>(256, ((int64_t)8 << 30) / ((int64_t)vcap * 8));
     const int nslots = (int)std::min<int64_t>(std::min<int64_t>(nq, 8192), mem_slots);
     auto* vis = (unsigned long long*)scratch_bytes("hnsw_visited", (int64_t)nslots * vcap * 8);
     int* status = (int*)scratch_bytes("hnsw_status", 256);
+    auto* stats = reinterpret_cast<unsigned long long*>(status + 16);
     RVX_HIP(hipMemsetAsync(vis, 0, (size_t)nslots * vcap * 8, stream()));
-    RVX_HIP(hipMemsetAsync(status, 0, 4, stream()));
-    SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, nslots, vcap, out_d, out_i, out_n, status, curv, hyper};
+    RVX_HIP(hipMemsetAsync(status, 0, 256, stream()));
+    SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, nslots, vcap, out_d, out_i, out_n, status, stats, curv, hyper};
     const size_t lds = hnsw_search_lds(d, ef);
     RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");
     static bool attr = false;
@@ -234,10 +248,15 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         case RVX_METRIC_POINCARE: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_POINCARE>, dim3(nslots), dim3(64), lds, a); break;
         default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by HNSW search");
     }
-    int st = 0;
-    RVX_HIP(hipMemcpyAsync(&st, status, 4, hipMemcpyDeviceToHost, stream()));
+    int st[32] = {0};
+    RVX_HIP(hipMemcpyAsync(st, status, sizeof(st), hipMemcpyDeviceToHost, stream()));
     sync();
-    RVX_REQUIRE(st == 0, RVX_ERR_INDEX, "HNSW candidate list overflow (pathological distance ties)");
+    unsigned long long tally[2];
+    std::memcpy(tally, st + 16, sizeof(tally));
+    g_search_stats.n_dist = (int64_t)tally[0];
+    g_search_stats.n_expand = (int64_t)tally[1];
+    g_search_stats.nq = nq;
+    RVX_REQUIRE(st[0] == 0, RVX_ERR_INDEX, "HNSW candidate list overflow (pathological distance ties)");
 }
 
 }  // namespace rvx
