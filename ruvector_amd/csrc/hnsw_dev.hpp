@@ -4,6 +4,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <climits>
+
 #include "poincare_dev.hpp"
 #include "rvx/rvx.h"
 
@@ -50,27 +52,33 @@ __device__ __forceinline__ float stream_acc(const float* __restrict__ qs, const 
     const float4* r = reinterpret_cast<const float4*>(x);
     const float4* qq = reinterpret_cast<const float4*>(qs);
     float acc = 0.0f;
-    float4 xa[ROW_BATCH], xb[ROW_BATCH], qa[Q_GLOBAL ? ROW_BATCH : 1], qb[Q_GLOBAL ? ROW_BATCH : 1];
-    auto load = [&](float4* xv, float4* qv, int base) {
+    // Main loop over whole double batches with no branch between a load and its
+    // use (a guarded load would sit in its own block and the waitcnt pass would
+    // fall back to vmcnt(0), serialising the row again); the last prefetch
+    // re-reads a batch already in cache instead of branching.
+    const int nfull = n4 / (2 * ROW_BATCH) * (2 * ROW_BATCH);
+    if (nfull > 0) {
+        float4 xa[ROW_BATCH], xb[ROW_BATCH], qa[Q_GLOBAL ? ROW_BATCH : 1], qb[Q_GLOBAL ? ROW_BATCH : 1];
+        auto load = [&](float4* xv, float4* qv, int base) {
 #pragma unroll
-        for (int j = 0; j < ROW_BATCH; ++j)
-            if (base + j < n4) {
+            for (int j = 0; j < ROW_BATCH; ++j) {
                 xv[j] = r[base + j];
                 if constexpr (Q_GLOBAL) qv[j] = qq[base + j];
             }
-    };
-    auto run = [&](const float4* xv, const float4* qv, int base) {
+        };
+        auto run = [&](const float4* xv, const float4* qv, int base) {
 #pragma unroll
-        for (int j = 0; j < ROW_BATCH; ++j)
-            if (base + j < n4) acc = acc4<METRIC>(acc, Q_GLOBAL ? qv[j] : qq[base + j], xv[j]);
-    };
-    load(xa, qa, 0);
-    for (int base = 0; base < n4; base += 2 * ROW_BATCH) {
-        load(xb, qb, base + ROW_BATCH);
-        run(xa, qa, base);
-        load(xa, qa, base + 2 * ROW_BATCH);
-        run(xb, qb, base + ROW_BATCH);
+            for (int j = 0; j < ROW_BATCH; ++j) acc = acc4<METRIC>(acc, Q_GLOBAL ? qv[j] : qq[base + j], xv[j]);
+        };
+        load(xa, qa, 0);
+        for (int base = 0; base < nfull; base += 2 * ROW_BATCH) {
+            load(xb, qb, base + ROW_BATCH);
+            run(xa, qa, base);
+            load(xa, qa, base + 2 * ROW_BATCH < nfull ? base + 2 * ROW_BATCH : base);
+            run(xb, qb, base + ROW_BATCH);
+        }
     }
+    for (int k = nfull; k < n4; ++k) acc = acc4<METRIC>(acc, qq[k], r[k]);
     return acc;
 }
 
@@ -152,6 +160,169 @@ __device__ __forceinline__ int sorted_insert(float* ad, int* ai, int size, float
     return size + 1;
 }
 
+
+// ---- batched admission ------------------------------------------------------
+// search_layer's neighbour loop (hnsw.rs:1004-1046) admits the fresh neighbours
+// of one expansion in list order: e is admitted iff d(e) < d(farthest in R) or
+// |R| < ef; admitted e goes into C and R, and R drops its farthest when
+// |R| > ef. Only the running farthest makes the order matter, so:
+//  1. decisions: walk the fresh lanes in order against a register window
+//     holding R's largest <= 64 entries (lane wn-1 = the max): each admission
+//     inserts into the window (or below it) and pops the window max when
+//     |R| > ef — the exact sequence of farthest values;
+//  2. merge: pops only ever remove the current maximum, so the final R is the
+//     |R_new| smallest of R ∪ A and C is C ∪ A (both by (d, id)); each array
+//     takes ONE in-place merge (ranks by binary search, moves from the back)
+//     instead of a wave-wide sorted insert per admitted neighbour.
+// A batch that could reach the candidate capacity takes the per-element path
+// (its farthest-candidate drop rule depends on the order).
+// scratch: LDS [64] floats + [64] ints. Returns false on candidate overflow.
+
+__device__ __forceinline__ bool lt_de(float d, int id, float bd, int bid) { return d < bd || (d == bd && id < bid); }
+
+// number of entries of the sorted array (asc: ascending, else descending by (d,id))
+// placed before (d, id); n <= 64 entries, binary search
+__device__ __forceinline__ int rank_in(const float* ad, const int* ai, int n, float d, int id, bool asc) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const bool before = asc ? lt_de(ad[mid], ai[mid], d, id) : lt_de(d, id, ad[mid], ai[mid]);
+        if (before) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// merge the sorted batch (sd, si)[0..na) into the sorted array (ad, ai)[0..n),
+// keeping the first nkeep entries; same order (asc) for both.
+__device__ __forceinline__ void merge_sorted(float* ad, int* ai, int n, const float* sd, const int* si, int na, int nkeep,
+                                             bool asc, int lane) {
+    // batch positions first (they search the array before it moves)
+    int bpos = -1;
+    float bd = 0.f; int bi = 0;
+    if (lane < na) {
+        bd = sd[lane]; bi = si[lane];
+        bpos = lane + rank_in(ad, ai, n, bd, bi, asc);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // array entries move right by the number of batch entries before them; walk
+    // chunks from the back so a chunk is read before anything can overwrite it
+    for (int base = ((n - 1) / 64) * 64; base >= 0; base -= 64) {
+        const int j = base + lane;
+        float vd = 0.f; int vi = 0, pos = -1;
+        if (j < n) {
+            vd = ad[j]; vi = ai[j];
+            pos = j + rank_in(sd, si, na, vd, vi, asc);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (pos >= 0 && pos < nkeep) { ad[pos] = vd; ai[pos] = vi; }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (bpos >= 0 && bpos < nkeep) { ad[bpos] = bd; ai[bpos] = bi; }
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ bool admit_batch(bool fresh, float dd, int nid, int ef, int ccap, float* rd, int* ri, int& rs, float* cd,
+                            int* ci, int& cs, float* sd, int* si, int lane) {
+    const unsigned long long fmask = __ballot(fresh);
+    if (!fmask) return true;
+    const int nf = __popcll(fmask);
+    if (cs + nf > ccap) {
+        // per-element path (rare: the candidate list is near its capacity)
+        unsigned long long todo = fmask;
+        while (todo) {
+            const int src = __ffsll((long long)todo) - 1;
+            todo &= todo - 1;
+            const float ed = __shfl(dd, src);
+            const int eid = __shfl(nid, src);
+            const float fd = rd[rs - 1];
+            if (ed < fd || rs < ef) {
+                if (cs >= ccap) {
+                    if (cd[0] > fd) {  // drop the farthest candidate: it can only terminate the search
+                        for (int base = 0; base < cs - 1; base += 64) {
+                            const int i = base + lane;
+                            float vd = 0.f; int vi = 0;
+                            const bool mv = i + 1 < cs;
+                            if (mv) { vd = cd[i + 1]; vi = ci[i + 1]; }
+                            __builtin_amdgcn_wave_barrier();
+                            if (mv) { cd[i] = vd; ci[i] = vi; }
+                            __builtin_amdgcn_wave_barrier();
+                        }
+                        cs -= 1;
+                    } else {
+                        return false;
+                    }
+                }
+                cs = sorted_insert(cd, ci, cs, ed, eid, /*asc=*/false, lane);
+                rs = sorted_insert(rd, ri, rs, ed, eid, /*asc=*/true, lane);
+                if (rs > ef) rs -= 1;
+            }
+        }
+        return true;
+    }
+    // 1. decisions against the window of R's largest entries
+    int wn = min(rs, 64);
+    int below = rs - wn;
+    float wd = INFINITY; int wi = INT_MAX;
+    if (lane < wn) { wd = rd[below + lane]; wi = ri[below + lane]; }
+    int r = rs;
+    unsigned long long adm = 0ull;
+    unsigned long long todo = fmask;
+    while (todo) {
+        const int src = __ffsll((long long)todo) - 1;
+        todo &= todo - 1;
+        const float ed = __shfl(dd, src);
+        const int eid = __shfl(nid, src);
+        const float fd = __shfl(wd, wn - 1);  // current farthest of R
+        if (!(ed < fd || r < ef)) continue;
+        adm |= 1ull << src;
+        r += 1;
+        const float w0d = __shfl(wd, 0);
+        const int w0i = __shfl(wi, 0);
+        if (below == 0 || !lt_de(ed, eid, w0d, w0i)) {
+            if (wn == 64) {  // keep 64: the smallest window entry moves below
+                wd = __shfl_down(wd, 1); wi = __shfl_down(wi, 1);
+                if (lane == 63) { wd = INFINITY; wi = INT_MAX; }
+                wn = 63; below += 1;
+            }
+            const int pos = __popcll(__ballot(lane < wn && lt_de(wd, wi, ed, eid)));
+            const float ud = __shfl_up(wd, 1);
+            const int ui = __shfl_up(wi, 1);
+            if (lane > pos && lane <= wn) { wd = ud; wi = ui; }
+            if (lane == pos) { wd = ed; wi = eid; }
+            wn += 1;
+        } else {
+            below += 1;
+        }
+        if (r > ef) {  // pop the farthest
+            if (lane == wn - 1) { wd = INFINITY; wi = INT_MAX; }
+            wn -= 1; r -= 1;
+        }
+    }
+    const int na = __popcll(adm);
+    if (na == 0) return true;
+    // 2. the admitted batch sorted ascending into the scratch
+    const bool mine = (adm >> lane) & 1ull;
+    int rank = 0;
+    for (unsigned long long t = adm; t; t &= t - 1) {
+        const int o = __ffsll((long long)t) - 1;
+        const float od = __shfl(dd, o);
+        const int oi = __shfl(nid, o);
+        rank += lt_de(od, oi, dd, nid) ? 1 : 0;
+    }
+    if (mine) { sd[rank] = dd; si[rank] = nid; }
+    __builtin_amdgcn_wave_barrier();
+    merge_sorted(rd, ri, rs, sd, si, na, r, /*asc=*/true, lane);
+    rs = r;
+    // C is descending: the same batch reversed
+    float xd = 0.f; int xi = 0;
+    if (lane < na) { xd = sd[na - 1 - lane]; xi = si[na - 1 - lane]; }
+    __builtin_amdgcn_wave_barrier();
+    if (lane < na) { sd[lane] = xd; si[lane] = xi; }
+    __builtin_amdgcn_wave_barrier();
+    merge_sorted(cd, ci, cs, sd, si, na, cs + na, /*asc=*/false, lane);
+    cs += na;
+    return true;
+}
 
 // distance between two stored rows, reference scalar order (distance.rs)
 template <int METRIC>

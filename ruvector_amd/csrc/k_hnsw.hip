@@ -18,7 +18,8 @@
 //
 // Per query: result set R as an ascending sorted array (farthest last) and the
 // candidate set C as a descending sorted array (nearest last) in LDS, updated
-// with wave-parallel sorted inserts; the visited set is an open-addressing
+// once per expansion by admit_batch (hnsw_dev.hpp: exact sequential decisions
+// in registers, then one merge per array); the visited set is an open-addressing
 // hash in a per-wave global scratch slot (32K entries, CAS-claimed by all
 // lanes at once); neighbour distances are computed one row per lane.
 #include <cstring>
@@ -59,6 +60,8 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
     int* ri = reinterpret_cast<int*>(rd + ef + 1);              // R id
     float* cd = reinterpret_cast<float*>(ri + ef + 1);          // C dist [ccap]
     int* ci = reinterpret_cast<int*>(cd + ccap);                // C id
+    float* sdb = reinterpret_cast<float*>(ci + ccap);           // admitted batch [64]
+    int* sib = reinterpret_cast<int*>(sdb + 64);
 
     unsigned long long* vis = a.visited + (int64_t)blockIdx.x * a.vcap;
     const unsigned vmask = a.vcap - 1;
@@ -151,39 +154,9 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
                 }
                 float dd = INFINITY;
                 if (fresh) dd = dist_of(nid);
-                // sequential admission in neighbour order (hnsw.rs:1004-1046)
-                unsigned long long todo = __ballot(fresh);
-                n_dist += (unsigned long long)__popcll(todo);
-                while (todo) {
-                    const int src = __ffsll((long long)todo) - 1;
-                    todo &= todo - 1;
-                    const float ed = __shfl(dd, src);
-                    const int eid = __shfl(nid, src);
-                    const float fd = rd[rs - 1];
-                    if (ed < fd || rs < ef) {
-                        if (cs >= ccap) {  // drop a candidate that can only terminate the search
-                            if (cd[0] > fd) {
-                                // compact: remove element 0 (the farthest)
-                                for (int base = 0; base < cs - 1; base += 64) {
-                                    const int i = base + lane;
-                                    float vd = 0.f; int vi = 0;
-                                    const bool mv = i + 1 < cs;
-                                    if (mv) { vd = cd[i + 1]; vi = ci[i + 1]; }
-                                    __builtin_amdgcn_wave_barrier();
-                                    if (mv) { cd[i] = vd; ci[i] = vi; }
-                                    __builtin_amdgcn_wave_barrier();
-                                }
-                                cs -= 1;
-                            } else {
-                                overflow = true;
-                                break;
-                            }
-                        }
-                        cs = sorted_insert(cd, ci, cs, ed, eid, /*asc=*/false, lane);
-                        rs = sorted_insert(rd, ri, rs, ed, eid, /*asc=*/true, lane);
-                        if (rs > ef) rs -= 1;  // pop farthest
-                    }
-                }
+                // admission in neighbour order (hnsw.rs:1004-1046), batched exactly
+                n_dist += (unsigned long long)__popcll(__ballot(fresh));
+                if (!admit_batch(fresh, dd, nid, ef, ccap, rd, ri, rs, cd, ci, cs, sdb, sib, lane)) overflow = true;
                 if (overflow) break;
             }
         }
@@ -210,7 +183,7 @@ SearchStats g_search_stats;
 
 size_t hnsw_search_lds(int d, int ef) {
     const int dq = (d + 3) & ~3;
-    return (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)(ef + C_EXTRA) * 8;
+    return (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)(ef + C_EXTRA) * 8 + 64 * 8;
 }
 
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,

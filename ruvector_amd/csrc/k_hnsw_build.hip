@@ -71,7 +71,7 @@ __device__ __forceinline__ int list_key(const BuildGraph& G, int p, int l) {  //
 template <int METRIC>
 __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn, int ep, float d_ep, int ef, int l,
                                   unsigned long long* vis, unsigned vmask, unsigned long long tag, float* rd, int* ri, float* cd,
-                                  int* ci, int ccap, int lane, bool& overflow) {
+                                  int* ci, int ccap, float* sdb, int* sib, int lane, bool& overflow) {
     if (!((a.nonempty_mask >> l) & 1u)) return 0;  // points_by_layer[layer].is_empty()
     int rs = 1, cs = 1;
     if (lane == 0) {
@@ -100,36 +100,7 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
             if (fresh)
                 dd = row_dist<METRIC>(qs, a.x + (int64_t)nid * a.d, a.d, qn,
                                       METRIC == RVX_METRIC_COSINE ? a.xnorm[nid] : 0.0f, a.curv);
-            unsigned long long todo = __ballot(fresh);
-            while (todo) {
-                const int src = __ffsll((long long)todo) - 1;
-                todo &= todo - 1;
-                const float ed = __shfl(dd, src);
-                const int eid = __shfl(nid, src);
-                const float fd = rd[rs - 1];
-                if (ed < fd || rs < ef) {
-                    if (cs >= ccap) {
-                        if (cd[0] > fd) {
-                            for (int base = 0; base < cs - 1; base += 64) {
-                                const int i = base + lane;
-                                float vd = 0.f; int vi = 0;
-                                const bool mv = i + 1 < cs;
-                                if (mv) { vd = cd[i + 1]; vi = ci[i + 1]; }
-                                __builtin_amdgcn_wave_barrier();
-                                if (mv) { cd[i] = vd; ci[i] = vi; }
-                                __builtin_amdgcn_wave_barrier();
-                            }
-                            cs -= 1;
-                        } else {
-                            overflow = true;
-                            break;
-                        }
-                    }
-                    cs = sorted_insert(cd, ci, cs, ed, eid, false, lane);
-                    rs = sorted_insert(rd, ri, rs, ed, eid, true, lane);
-                    if (rs > ef) rs -= 1;
-                }
-            }
+            if (!admit_batch(fresh, dd, nid, ef, ccap, rd, ri, rs, cd, ci, cs, sdb, sib, lane)) overflow = true;
             if (overflow) break;
         }
     }
@@ -171,8 +142,8 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
         // 1. greedy descent, ef = 1 (hnsw.rs:1105-1146)
         for (int l = a.entry_level; l >= lev + 1; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
-            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, 1, l, vis, vmask, tag, rd, ri, cd, ci, ccap, lane,
-                                                      overflow);
+            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, 1, l, vis, vmask, tag, rd, ri, cd, ci, ccap, sd,
+                                                      si, lane, overflow);
             if (rs > 0 && rd[0] < d_ep) { ep = ri[0]; d_ep = rd[0]; }
         }
         // 2. layers lev .. 0 (hnsw.rs:1149-1196); HyperbolicHnsw inserts at
@@ -180,8 +151,8 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
         const int ltop = a.hyper ? min(lev, a.entry_level) : lev;
         for (int l = ltop; l >= 0; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
-            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, ef, l, vis, vmask, tag, rd, ri, cd, ci, ccap, lane,
-                                                      overflow);
+            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, ef, l, vis, vmask, tag, rd, ri, cd, ci, ccap, sd,
+                                                      si, lane, overflow);
             if (rs == 0) continue;
             const int nb_conn = l == 0 ? a.G.C0 : a.G.M;
             int ss = 0;
