@@ -30,6 +30,11 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
                  const float* qnorm, int64_t nq, int k, int ef, float* out_d, int64_t* out_i, int32_t* out_n,
                  const char* tag, float curv = 1.0f, int hyper = 0);
 
+// Wave-cooperative (LDS-staged) distances: metric not Poincaré, d % 32 == 0, and
+// (RVX_HNSW_COOP=1, default) a table of >= RVX_HNSW_COOP_MIN_MB (4096) bytes, where
+// per-lane row reads outgrow the per-CU translation cache; 2 forces, 0 disables.
+bool hnsw_coop(int metric, int d, int64_t rows);
+
 // Work tallies of the most recent hnsw_search launch (SURVEY.md §8d C1/C3:
 // bytes = n_dist * d * 4 + n_expand * deg_cap * 4 per launch).
 struct SearchStats {

@@ -102,6 +102,93 @@ __device__ __forceinline__ float row_dist(const float* __restrict__ qs, const fl
     return finish_dist<METRIC>(acc, qn, xn);
 }
 
+// ---- wave-cooperative distances ----------------------------------------------
+// dist(q, x[row_lane]) for the 64 rows a wave's lanes name (-1: none, result
+// unused), each still ONE lane's sequential chain in the reference order. Rows
+// reach LDS by LDS-DMA, 32 dims per chunk: one wave instruction moves 8 rows x
+// 128 B, so it touches 8 pages where per-lane streaming touches 64 — beyond a
+// few GB of randomly read rows the per-CU translation cache, not HBM, bounds a
+// per-lane search (86% UTCL1 misses at 12 GB). Stage layout [64 rows][128 B],
+// 16-B slot p ^ ((row >> 1) & 7) (conflict-free for the per-lane ds_read_b128).
+// Two stages: the next chunk's DMA is in flight while this one accumulates.
+// Requires no other vector-memory op of the wave between a fill and its wait.
+constexpr int WD_CH = 32;                     // dims per chunk
+constexpr int WD_STAGE = 64 * WD_CH * 4;      // bytes per stage
+constexpr int WD_LDS = 2 * WD_STAGE;          // bytes per wave
+
+__host__ __device__ inline bool wave_dist_ok(int d) { return d % WD_CH == 0; }
+
+template <int METRIC>
+__device__ __forceinline__ void wd_fill(const float* __restrict__ x, int d, const int (&rid)[8], int c, int lane,
+                                        unsigned char* st) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int j = 8 * i + (lane >> 3);
+        const int piece = (lane & 7) ^ ((j >> 1) & 7);
+        __builtin_amdgcn_global_load_lds((const void*)(x + (int64_t)rid[i] * d + c * WD_CH + 4 * piece),
+                                         (__attribute__((address_space(3))) void*)(st + i * 1024), 16, 0, 0);
+    }
+}
+
+template <int METRIC>
+__device__ __forceinline__ float wd_chunk(float acc, const float* qs, int c, int lane, const unsigned char* st) {
+    const float4* qq = reinterpret_cast<const float4*>(qs + c * WD_CH);
+    const int sw = (lane >> 1) & 7;
+#pragma unroll
+    for (int p = 0; p < WD_CH / 4; ++p) {
+        const float4 v = *reinterpret_cast<const float4*>(st + lane * (WD_CH * 4) + ((p ^ sw) << 4));
+        acc = acc4<METRIC>(acc, qq[p], v);
+    }
+    return acc;
+}
+
+// Ordering is explicit: nothing in the compiler orders a ds_read behind an
+// LDS-DMA to the same bytes (only a barrier drains them), so before reading a
+// stage the wave waits vmcnt(8) — the 8 DMAs of the next chunk may still be
+// in flight, everything older (this chunk) has landed — and before refilling a
+// stage it waits lgkmcnt(0) so the stage's reads have returned. The asm
+// statements clobber memory, which also keeps the DMA groups in issue order.
+template <int METRIC>
+__device__ __forceinline__ float wd_run(const float* __restrict__ x, int d, const float* qs, const int (&rid)[8], int lane,
+                                        unsigned char* s0, unsigned char* s1) {
+    const int nch = d / WD_CH;
+    float acc = 0.0f;
+    wd_fill<METRIC>(x, d, rid, 0, lane, s0);
+    for (int c = 0; c < nch; c += 2) {
+        if (c + 1 < nch) {
+            wd_fill<METRIC>(x, d, rid, c + 1, lane, s1);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        acc = wd_chunk<METRIC>(acc, qs, c, lane, s0);
+        if (c + 1 >= nch) break;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (c + 2 < nch) {
+            wd_fill<METRIC>(x, d, rid, c + 2, lane, s0);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        acc = wd_chunk<METRIC>(acc, qs, c + 1, lane, s1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return acc;
+}
+
+// All 64 lanes call together. row < 0: no row (the lane's result is garbage).
+template <int METRIC>
+__device__ __forceinline__ float wave_dist(const float* qs, const float* __restrict__ x, int d, int row, float qn,
+                                           float xn, unsigned char* stage, int lane) {
+    int rid[8];
+    const int mine = row < 0 ? 0 : row;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) rid[i] = __shfl(mine, 8 * i + (lane >> 3));
+    const float acc = wd_run<METRIC>(x, d, qs, rid, lane, stage, stage + WD_STAGE);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stages are refilled by the next call
+    return finish_dist<METRIC>(acc, qn, xn);
+}
+
 // Claim `node` in a query's visited set: true if it was not visited yet.
 // Slots whose tag is another query's are free (the table is zeroed per launch).
 __device__ __forceinline__ bool visit_claim(unsigned long long* vis, unsigned vmask, unsigned long long qtag, int node) {

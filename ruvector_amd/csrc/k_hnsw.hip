@@ -46,6 +46,7 @@ struct SearchArgs {
     unsigned long long* stats;  // [2]: distance evaluations, layer-0 expansions (per launch)
     float curv;        // Poincaré curvature
     int hyper;         // HyperbolicHnsw::search semantics (see below)
+    int coop;          // wave-cooperative LDS-staged distances (hnsw_dev.hpp wave_dist)
 };
 
 template <int METRIC>
@@ -54,7 +55,10 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
     const int lane = threadIdx.x;
     const int ef = a.ef;
     const int ccap = ef + C_EXTRA;
-    float* qs = reinterpret_cast<float*>(lds_raw);             // [d rounded to 4]
+    constexpr bool COOP_OK = METRIC != RVX_METRIC_POINCARE;
+    const bool coop = COOP_OK && a.coop;
+    unsigned char* wst = lds_raw;                                // [WD_LDS] distance stages (coop)
+    float* qs = reinterpret_cast<float*>(lds_raw + (coop ? WD_LDS : 0));  // [d rounded to 4]
     const int dq = (a.d + 3) & ~3;
     float* rd = qs + dq;                                        // R dist [ef+1]
     int* ri = reinterpret_cast<int*>(rd + ef + 1);              // R id
@@ -77,6 +81,18 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
             return row_dist<METRIC>(qs, a.x + (int64_t)node * a.d, a.d,
                                     qn, METRIC == RVX_METRIC_COSINE ? a.xnorm[node] : 0.0f, a.curv);
         };
+        // every lane calls; node < 0: no row (INFINITY)
+        auto dist_lane = [&](int node) {
+            float dv;
+            if constexpr (COOP_OK) {
+                if (coop) {
+                    dv = wave_dist<METRIC>(qs, a.x, a.d, node, qn,
+                                           (METRIC == RVX_METRIC_COSINE && node >= 0) ? a.xnorm[node] : 0.0f, wst, lane);
+                    return node >= 0 ? dv : INFINITY;
+                }
+            }
+            return node >= 0 ? dist_of(node) : INFINITY;
+        };
 
         // ---- upper layers: single pass per layer (search_filter :1499-1517)
         int pivot = (int)a.g.entry;
@@ -97,9 +113,9 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
                 float new_best = best;
                 for (int64_t c0 = b; c0 < e; c0 += 64) {
                     const int64_t p = c0 + lane;
-                    float dd = INFINITY;
                     int pos = INT_MAX, nid = -1;
-                    if (p < e) { nid = col[p]; dd = dist_of(nid); pos = (int)(p - b); }
+                    if (p < e) { nid = col[p]; pos = (int)(p - b); }
+                    float dd = dist_lane(nid);
                     n_dist += (unsigned long long)min<int64_t>(64, e - c0);
                     // first position holding the minimum of this chunk
 #pragma unroll
@@ -153,7 +169,7 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
                     fresh = visit_claim(vis, vmask, qtag, nid);
                 }
                 float dd = INFINITY;
-                if (fresh) dd = dist_of(nid);
+                if (__ballot(fresh)) dd = dist_lane(fresh ? nid : -1);
                 // admission in neighbour order (hnsw.rs:1004-1046), batched exactly
                 n_dist += (unsigned long long)__popcll(__ballot(fresh));
                 if (!admit_batch(fresh, dd, nid, ef, ccap, rd, ri, rs, cd, ci, cs, sdb, sib, lane)) overflow = true;
@@ -181,9 +197,17 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
 
 SearchStats g_search_stats;
 
-size_t hnsw_search_lds(int d, int ef) {
+bool hnsw_coop(int metric, int d, int64_t rows) {
+    // 0 off, 1 auto (tables past the per-CU translation reach), 2 always
+    const int mode = env_int("RVX_HNSW_COOP", 1);  // read per launch: tests force both paths
+    const int64_t min_bytes = (int64_t)env_int("RVX_HNSW_COOP_MIN_MB", 4096) << 20;
+    if (!mode || metric == RVX_METRIC_POINCARE || !wave_dist_ok(d)) return false;
+    return mode == 2 || rows * (int64_t)d * 4 >= min_bytes;
+}
+
+size_t hnsw_search_lds(int d, int ef, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)(ef + C_EXTRA) * 8 + 64 * 8;
+    return (coop ? (size_t)WD_LDS : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)(ef + C_EXTRA) * 8 + 64 * 8;
 }
 
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
@@ -200,8 +224,10 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     auto* stats = reinterpret_cast<unsigned long long*>(status + 16);
     RVX_HIP(hipMemsetAsync(vis, 0, (size_t)nslots * vcap * 8, stream()));
     RVX_HIP(hipMemsetAsync(status, 0, 256, stream()));
-    SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, nslots, vcap, out_d, out_i, out_n, status, stats, curv, hyper};
-    const size_t lds = hnsw_search_lds(d, ef);
+    const bool coop = hnsw_coop(metric, d, g.n);
+    SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, nslots, vcap, out_d, out_i, out_n, status, stats, curv, hyper,
+                 coop ? 1 : 0};
+    const size_t lds = hnsw_search_lds(d, ef, coop);
     RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");
     static bool attr = false;
     if (!attr) {

@@ -47,6 +47,7 @@ struct BuildArgs {
     int* status;
     float curv;  // Poincaré curvature
     int hyper;   // HyperbolicHnsw::insert rules
+    int coop;    // wave-cooperative LDS-staged distances in the layer searches
 };
 
 __device__ __forceinline__ int list_get(const BuildGraph& G, int p, int l, const int** ids, const float** ds) {
@@ -71,7 +72,7 @@ __device__ __forceinline__ int list_key(const BuildGraph& G, int p, int l) {  //
 template <int METRIC>
 __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn, int ep, float d_ep, int ef, int l,
                                   unsigned long long* vis, unsigned vmask, unsigned long long tag, float* rd, int* ri, float* cd,
-                                  int* ci, int ccap, float* sdb, int* sib, int lane, bool& overflow) {
+                                  int* ci, int ccap, float* sdb, int* sib, unsigned char* wst, int lane, bool& overflow) {
     if (!((a.nonempty_mask >> l) & 1u)) return 0;  // points_by_layer[layer].is_empty()
     int rs = 1, cs = 1;
     if (lane == 0) {
@@ -97,9 +98,22 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
                 fresh = visit_claim(vis, vmask, tag, nid);
             }
             float dd = INFINITY;
-            if (fresh)
+            bool coop = false;
+            if constexpr (METRIC != RVX_METRIC_POINCARE) coop = a.coop != 0;
+            if (coop) {
+                if constexpr (METRIC != RVX_METRIC_POINCARE) {
+                    if (__ballot(fresh)) {
+                        const int row = fresh ? nid : -1;
+                        const float dv = wave_dist<METRIC>(qs, a.x, a.d, row, qn,
+                                                           (METRIC == RVX_METRIC_COSINE && fresh) ? a.xnorm[nid] : 0.0f,
+                                                           wst, lane);
+                        if (fresh) dd = dv;
+                    }
+                }
+            } else if (fresh) {
                 dd = row_dist<METRIC>(qs, a.x + (int64_t)nid * a.d, a.d, qn,
                                       METRIC == RVX_METRIC_COSINE ? a.xnorm[nid] : 0.0f, a.curv);
+            }
             if (!admit_batch(fresh, dd, nid, ef, ccap, rd, ri, rs, cd, ci, cs, sdb, sib, lane)) overflow = true;
             if (overflow) break;
         }
@@ -114,7 +128,8 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
     const int ef = a.ef_c;
     const int ccap = ef + C_EXTRA;
     const int dq = (a.d + 3) & ~3;
-    float* qs = reinterpret_cast<float*>(lds_raw);
+    unsigned char* wst = lds_raw;  // [WD_LDS] distance stages (coop)
+    float* qs = reinterpret_cast<float*>(lds_raw + (a.coop ? WD_LDS : 0));
     float* rd = qs + dq;
     int* ri = reinterpret_cast<int*>(rd + ef + 1);
     float* cd = reinterpret_cast<float*>(ri + ef + 1);
@@ -143,7 +158,7 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
         for (int l = a.entry_level; l >= lev + 1; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
             const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, 1, l, vis, vmask, tag, rd, ri, cd, ci, ccap, sd,
-                                                      si, lane, overflow);
+                                                      si, wst, lane, overflow);
             if (rs > 0 && rd[0] < d_ep) { ep = ri[0]; d_ep = rd[0]; }
         }
         // 2. layers lev .. 0 (hnsw.rs:1149-1196); HyperbolicHnsw inserts at
@@ -152,7 +167,7 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
         for (int l = ltop; l >= 0; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
             const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, ef, l, vis, vmask, tag, rd, ri, cd, ci, ccap, sd,
-                                                      si, lane, overflow);
+                                                      si, wst, lane, overflow);
             if (rs == 0) continue;
             const int nb_conn = l == 0 ? a.G.C0 : a.G.M;
             int ss = 0;
@@ -281,9 +296,9 @@ __global__ __launch_bounds__(256) void k_build_merge(BuildArgs a, int nrec) {
 
 }  // namespace
 
-size_t build_lds_bytes(int d, int ef) {
+size_t build_lds_bytes(int d, int ef, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)(ef + C_EXTRA) * 8 + 64 * 8;
+    return (coop ? (size_t)WD_LDS : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)(ef + C_EXTRA) * 8 + 64 * 8;
 }
 
 void build_insert_batch(const BuildGraph& G, int metric, const float* x, const float* xnorm, int d,
@@ -301,6 +316,7 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     a.batch_begin = batch_begin; a.batch_n = batch_n; a.entry = entry; a.entry_level = entry_level;
     a.nonempty_mask = nonempty_mask; a.ef_c = ef_c;
     a.curv = curv; a.hyper = hyper;
+    a.coop = hnsw_coop(metric, d, batch_begin + batch_n) ? 1 : 0;
     a.vcap = vcap;
     a.visited = (unsigned long long*)scratch_bytes("build_visited", (int64_t)nslots * vcap * 8);
     const int64_t nrec = (int64_t)batch_n * rev_cap;
@@ -314,7 +330,7 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     a.status = (int*)scratch_bytes("build_status", 256);
     RVX_HIP(hipMemsetAsync(a.visited, 0, (size_t)nslots * vcap * 8, stream()));
     RVX_HIP(hipMemsetAsync(a.status, 0, 4, stream()));
-    const size_t lds = build_lds_bytes(d, ef_c);
+    const size_t lds = build_lds_bytes(d, ef_c, a.coop != 0);
     RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");
     static bool attr = false;
     if (!attr) {

@@ -88,7 +88,17 @@ void DevMem::reset(int64_t b) {
     RVX_REQUIRE(b >= 0, RVX_ERR_INVALID_PARAMETER, "negative allocation");
     dev = device().id;
     if (b > 0) {
-        RVX_HIP(hipMalloc(&p, (size_t)b));
+        // Large tables are read at random (HNSW rows, gathered features): a
+        // physically contiguous allocation lets the VM map large fragments, so
+        // the per-CU translation cache covers far more of the table.
+        static const int64_t contig_min = (int64_t)env_int("RVX_CONTIG_MIN_MB", 256) << 20;
+        if (contig_min > 0 && b >= contig_min) {
+            if (hipExtMallocWithFlags(&p, (size_t)b, hipDeviceMallocContiguous) != hipSuccess) {
+                (void)hipGetLastError();
+                p = nullptr;
+            }
+        }
+        if (!p) RVX_HIP(hipMalloc(&p, (size_t)b));
         bytes = b;
     }
 }

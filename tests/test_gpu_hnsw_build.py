@@ -95,3 +95,27 @@ def test_remove_filters_hnsw_results():
     assert idx.remove("v10")
     after = idx.search(x[10], 5)
     assert "v10" not in [r.id for r in after] and len(after) == 4  # filter_map drops it (index/hnsw.rs:250-258)
+
+
+@pytest.mark.parametrize("metric,d", [("l2", 64), ("cosine", 96), ("l2", 768)])
+def test_cooperative_distances_identical(monkeypatch, metric, d):
+    """The wave-cooperative LDS-staged distance path (hnsw_dev.hpp wave_dist, the
+    default for tables past ~4 GB) builds the identical graph and returns bit-exact
+    search results: forced on here against the per-lane path and the oracle."""
+    n = 2500 if d < 768 else 1200
+    x = unit(n, d, 5) if metric == "cosine" else O.fill_uniform(n * d, 5).reshape(n, d)
+    q = O.fill_uniform(100 * d, 6).reshape(100, d)
+    monkeypatch.setenv("RVX_HNSW_COOP", "0")
+    lane = build_gpu(x, metric, 16, 100, seed=3)
+    g_lane = lane.export_graph()
+    ids_l, dist_l, _ = lane.search_array(q, 10, 80)
+    monkeypatch.setenv("RVX_HNSW_COOP", "2")
+    coop = build_gpu(x, metric, 16, 100, seed=3)
+    g_coop = coop.export_graph()
+    for key in ("levels", "row_ptr0", "col0"):
+        assert np.array_equal(g_lane[key], g_coop[key]), key
+    ids_c, dist_c, _ = coop.search_array(q, 10, 80)
+    assert np.array_equal(ids_l, ids_c) and np.array_equal(dist_l, dist_c)
+    ref = O.Hnsw.from_graph(x, g_coop, metric)
+    rids, rd, _ = ref.search(q, 10, 80)
+    assert np.array_equal(ids_c.astype(np.int64), rids) and np.array_equal(dist_c, rd)
