@@ -134,12 +134,17 @@ typedef struct rvx_comm rvx_comm; /* RCCL communicator, see Multi-GPU below */
 enum { RVX_SAGE_MEAN = 0, RVX_SAGE_MAXPOOL = 1, RVX_SAGE_LSTM = 2 /* = mean, graphsage.rs:159 */ };
 /* w_neighbor/w_self: [in][out] row-major as GraphSAGELayer stores them; NULL
  * for both selects the deterministic init of graphsage.rs:56-78.
- * num_samples < max degree needs the StdRng(42) partial_shuffle sampling of
- * graphsage.rs:92-102, which this engine rejects with RVX_ERR_UNSUPPORTED. */
+ * Rows with more than num_samples neighbours aggregate the subset
+ * sample_neighbors keeps (StdRng::seed_from_u64(42) + partial_shuffle, then
+ * the prefix; graphsage.rs:92-102), built once per graph as a sampled CSR. */
 rvx_status rvx_sage_layer_create(int32_t in_features, int32_t out_features, int32_t num_samples,
                                  int32_t aggregator, int32_t normalize, const float* w_neighbor,
                                  const float* w_self, rvx_sage_layer** out);
 rvx_status rvx_sage_layer_destroy(rvx_sage_layer* l);
+/* GraphSAGELayer::sample_neighbors (graphsage.rs:92-102) on positions
+ * 0..len-1 (len > k): writes the k positions the reference keeps, in order.
+ * Host-only (rand 0.8.5 StdRng + SliceRandom::partial_shuffle restated). */
+rvx_status rvx_sage_sample_positions(int32_t len, int32_t k, int32_t* out);
 /* GraphSAGELayer::forward (graphsage.rs:190-196) over host arrays. */
 rvx_status rvx_sage_forward(const rvx_sage_layer* l, const rvx_graph* g, const float* x, int64_t n,
                             float* y);

@@ -26,6 +26,7 @@
 #include <cstring>
 #include <functional>
 #include <limits>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <queue>
@@ -549,30 +550,139 @@ void orc_aggregate(const float* x, int64_t n, int32_t dim, const int64_t* rp, co
     }
 }
 
+// ---- rand 0.8.5 StdRng::seed_from_u64 + SliceRandom::partial_shuffle -----
+// (third-party, not vendored under /root/reference: rand 0.8.5 / rand_core
+// 0.6 / rand_chacha 0.3.1, Cargo.lock:6952,6993; called by
+// GraphSAGELayer::sample_neighbors, graphsage.rs:92-102). Restated from the
+// published algorithms:
+//  * StdRng = ChaCha12Rng: ChaCha block function, 12 rounds, 256-bit key =
+//    the 32-byte seed, 64-bit block counter (words 12-13) from 0, zero nonce;
+//    next_u32 returns the keystream's little-endian words in order.
+//  * SeedableRng::seed_from_u64 (rand_core 0.6): the seed is eight PCG32
+//    outputs (state = state*6364136223846793005 + 11634580027462260723,
+//    xorshifted = ((s>>18)^s)>>27, rotr by s>>59), each stored little-endian.
+//  * gen_range(0..ub) for u32 (UniformInt::sample_single_inclusive): range
+//    = ub, zone = (range << lzcnt(range)) - 1; draw v until lo32(v*range)
+//    <= zone, return hi32(v*range).
+//  * partial_shuffle(amount): for i in (len-amount..len).rev() swap(i,
+//    gen_index(i+1)); the reference then keeps sampled[..k] (the prefix).
+struct OrcChaCha {
+    uint32_t key[8];
+    uint64_t counter = 0;
+    uint32_t buf[16];
+    int idx = 16, rounds = 12;
+    static uint32_t rotl(uint32_t v, int c) { return (v << c) | (v >> (32 - c)); }
+    void refill() {
+        uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+        for (int i = 0; i < 8; ++i) s[4 + i] = key[i];
+        s[12] = (uint32_t)counter;
+        s[13] = (uint32_t)(counter >> 32);
+        s[14] = s[15] = 0;
+        uint32_t w[16];
+        std::memcpy(w, s, sizeof w);
+        auto qr = [&](int a, int b, int c, int d) {
+            w[a] += w[b]; w[d] = rotl(w[d] ^ w[a], 16);
+            w[c] += w[d]; w[b] = rotl(w[b] ^ w[c], 12);
+            w[a] += w[b]; w[d] = rotl(w[d] ^ w[a], 8);
+            w[c] += w[d]; w[b] = rotl(w[b] ^ w[c], 7);
+        };
+        for (int r = 0; r < rounds; r += 2) {
+            qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15);
+            qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14);
+        }
+        for (int i = 0; i < 16; ++i) buf[i] = w[i] + s[i];
+        ++counter;
+        idx = 0;
+    }
+    uint32_t next_u32() {
+        if (idx >= 16) refill();
+        return buf[idx++];
+    }
+    void seed_from_u64(uint64_t state) {
+        for (int i = 0; i < 8; ++i) {
+            state = state * 6364136223846793005ull + 11634580027462260723ull;
+            const uint32_t xs = (uint32_t)(((state >> 18) ^ state) >> 27);
+            const uint32_t rot = (uint32_t)(state >> 59);
+            key[i] = (xs >> rot) | (xs << ((32 - rot) & 31));
+        }
+        counter = 0;
+        idx = 16;
+    }
+    uint32_t gen_index(uint32_t ub) {
+        const uint32_t range = ub;
+        const uint32_t zone = (range << __builtin_clz(range)) - 1u;
+        for (;;) {
+            const uint64_t m = (uint64_t)next_u32() * range;
+            if ((uint32_t)m <= zone) return (uint32_t)(m >> 32);
+        }
+    }
+};
+
+// ChaCha keystream words (rounds 20 = the RFC 7539 / rand_chacha known-answer
+// vectors, 12 = StdRng) for a given 8-word key, from block 0.
+void orc_chacha_words(const uint32_t* key, int32_t rounds, int32_t nwords, uint32_t* out) {
+    OrcChaCha r;
+    std::memcpy(r.key, key, sizeof r.key);
+    r.rounds = rounds;
+    for (int i = 0; i < nwords; ++i) out[i] = r.next_u32();
+}
+
+// GraphSAGELayer::sample_neighbors (graphsage.rs:92-102) on positions
+// 0..len-1: writes the k positions the reference keeps (len > k).
+void orc_sage_sample_positions(int32_t len, int32_t k, int32_t* out) {
+    std::vector<int32_t> a(len);
+    for (int i = 0; i < len; ++i) a[i] = i;
+    OrcChaCha r;
+    r.seed_from_u64(42);
+    for (int i = len - 1; i >= len - k; --i) std::swap(a[i], a[r.gen_index((uint32_t)i + 1)]);
+    for (int t = 0; t < k; ++t) out[t] = a[t];
+}
+
 // GraphSAGELayer::forward_with_sampling (graphsage.rs:118-187) for rows
-// [row0, row0+nrows), with num_samples >= degree (no sampling).
+// [row0, row0+nrows); num_samples = k (rows with more than k neighbours
+// aggregate the reference's sample_neighbors subset, in its order).
 // aggregator 0 = Mean (and LSTM, :159), 1 = MaxPool.
 void orc_sage_forward(const float* x, int64_t n, int32_t in, int32_t out, const int64_t* rp, const int32_t* col,
                       const float* wn, const float* ws, int32_t aggregator, int32_t normalize, int64_t row0,
-                      int64_t nrows, float* y /*[nrows][out]*/, int32_t nthreads) {
+                      int64_t nrows, float* y /*[nrows][out]*/, int32_t nthreads, int32_t num_samples) {
+    std::mutex pm;
+    std::map<int64_t, std::vector<int32_t>> pos_cache;
     pfor(nrows, nthreads, [&](int64_t t) {
         const int64_t i = row0 + t;
         std::vector<float> agg(in, 0.0f);
-        const int64_t beg = rp[i], end = rp[i + 1];
+        // sampled neighbour list (sample_neighbors), then the id < n filter (:139-147)
+        std::vector<int32_t> nb(col + rp[i], col + rp[i + 1]);
+        if ((int64_t)nb.size() > num_samples) {
+            std::vector<int32_t> pos;
+            {
+                std::lock_guard<std::mutex> lk(pm);
+                auto& c = pos_cache[(int64_t)nb.size()];
+                if (c.empty()) {
+                    c.resize(num_samples);
+                    orc_sage_sample_positions((int32_t)nb.size(), num_samples, c.data());
+                }
+                pos = c;
+            }
+            std::vector<int32_t> s(num_samples);
+            for (int q = 0; q < num_samples; ++q) s[q] = nb[pos[q]];
+            nb.swap(s);
+        }
+        const int64_t beg = 0, end = (int64_t)nb.size();
+        const int32_t* colr = nb.data();
         int64_t cnt = 0;
-        for (int64_t e = beg; e < end; ++e) if (col[e] < n) ++cnt;
+        for (int64_t e = beg; e < end; ++e) if (colr[e] < n) ++cnt;
         if (cnt > 0) {
             if (aggregator == 1) {  // max_aggregate (aggregators.rs:77-92)
                 std::fill(agg.begin(), agg.end(), -INFINITY);
                 for (int64_t e = beg; e < end; ++e) {
-                    if (col[e] >= n) continue;
-                    const float* xv = x + (int64_t)col[e] * in;
+                    if (colr[e] >= n) continue;
+                    const float* xv = x + (int64_t)colr[e] * in;
                     for (int c = 0; c < in; ++c) agg[c] = std::fmax(agg[c], xv[c]);
                 }
             } else {  // mean_aggregate: sum then / count (aggregators.rs:35-68)
                 for (int64_t e = beg; e < end; ++e) {
-                    if (col[e] >= n) continue;
-                    const float* xv = x + (int64_t)col[e] * in;
+                    if (colr[e] >= n) continue;
+                    const float* xv = x + (int64_t)colr[e] * in;
                     for (int c = 0; c < in; ++c) agg[c] = agg[c] + xv[c];
                 }
                 const float cf = (float)cnt;

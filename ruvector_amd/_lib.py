@@ -99,6 +99,7 @@ SIGNATURES = {
     "rvx_aggregate_device": (None, [P, I32, I32, I32, P, I32, P]),
     "rvx_sage_layer_create": (None, [I32, I32, I32, I32, I32, PF32, PF32, PP]),
     "rvx_sage_layer_destroy": (None, [P]),
+    "rvx_sage_sample_positions": (None, [I32, I32, PI32]),
     "rvx_sage_forward": (None, [P, P, PF32, I64, PF32]),
     "rvx_sage_forward_device": (None, [P, P, P, P]),
     "rvx_sage_forward_shard_device": (None, [P, P, P, I64, P]),

@@ -139,9 +139,9 @@ using ChunkHook = std::function<void(int c, int64_t r0, int64_t rows)>;
 // of it are this graph's destination (self) rows.
 void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* x, float* y, int64_t row_offset = 0,
                       int chunks = 0, const ChunkHook& hook = nullptr) {
-    RVX_REQUIRE(g->max_deg <= l->num_samples, RVX_ERR_UNSUPPORTED,
-                "GraphSAGE neighbour sampling (num_samples < max degree, graphsage.rs:92-102) is not supported; "
-                "set num_samples >= max degree");
+    // rows with more than num_samples neighbours aggregate the reference's
+    // sample_neighbors subset (graphsage.rs:92-102, k_sample.hip)
+    g = sampled_graph(g, l->num_samples);
     const int64_t n = g->n;
     float* agg = scratch_f32("sage_agg", n * (int64_t)l->in);
     const int a = (l->aggregator == RVX_SAGE_MAXPOOL) ? AGG_MAX : AGG_MEAN;
@@ -336,6 +336,13 @@ rvx_status rvx_sage_layer_create(int32_t in, int32_t out_f, int32_t num_samples,
         split_x3(l->ws_t.as<float>(), (int64_t)in * out_f, l->ws_x3.as<uint16_t>());
         sync();
         *out = l.release();
+    });
+}
+
+rvx_status rvx_sage_sample_positions(int32_t len, int32_t k, int32_t* out) {
+    return guard([&] {
+        RVX_REQUIRE(out && k >= 0 && len > k, RVX_ERR_INVALID_PARAMETER, "need len > k >= 0");
+        sage_sample_positions(len, k, out);
     });
 }
 

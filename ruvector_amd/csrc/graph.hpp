@@ -1,6 +1,7 @@
 // graph.hpp — the HBM-resident CSR graph handle and a per-device scratch pool.
 #pragma once
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -20,6 +21,9 @@ struct rvx_graph {
     const int32_t* isolated = nullptr;                      // device list of rows with no neighbours
     int64_t n_isolated = 0;
     std::vector<float> host_w;                              // host copy of weights (RuvectorLayer sums)
+    // GraphSAGE sampled CSRs by num_samples (k_sample.hip), built on first use
+    mutable std::mutex sampled_mu;
+    mutable std::map<int32_t, std::unique_ptr<rvx_graph>> sampled;
 };
 
 namespace rvx {
@@ -36,5 +40,11 @@ struct ComputeLock {
 };
 
 void check_graph(const rvx_graph* g);
+
+// GraphSAGE neighbour sampling (k_sample.hip): the graph itself when no row
+// has more than k neighbours, else its cached sampled CSR.
+const rvx_graph* sampled_graph(const rvx_graph* g, int32_t k);
+// Positions sample_neighbors keeps from a list of `len` > k (graphsage.rs:92-102).
+void sage_sample_positions(int32_t len, int32_t k, int32_t* out);
 
 }  // namespace rvx

@@ -123,6 +123,16 @@ class GraphSAGELayer:
                L.fptr(ws) if ws is not None else None, C.byref(h))
         self._h = h
 
+    def sample_neighbors(self, neighbors: Sequence[int], k: int) -> list:
+        """GraphSAGELayer::sample_neighbors (graphsage.rs:92-102): the list itself when
+        len <= k, else the prefix [..k] left by StdRng::seed_from_u64(42) partial_shuffle."""
+        nb = list(neighbors)
+        if len(nb) <= k:
+            return nb
+        pos = np.empty(k, np.int32)
+        _check("rvx_sage_sample_positions", len(nb), k, pos.ctypes.data_as(L.PI32))
+        return [nb[p] for p in pos]
+
     def forward(self, node_features, edge_index: Sequence[Tuple[int, int]]) -> np.ndarray:
         """GraphSAGELayer::forward(node_features, edge_index) (graphsage.rs:190-196)."""
         x = L.f32c(node_features)

@@ -45,7 +45,9 @@ _SIG = {
     "orc_sage_init": (None, [I32, I32, I32, PF]),
     "orc_build_csr": (I64, [I64, PI64, PI64, I64, PF, PI64, PI32, PF]),
     "orc_aggregate": (None, [PF, I64, I32, PI64, PI32, PF, I32, I32, PF]),
-    "orc_sage_forward": (None, [PF, I64, I32, I32, PI64, PI32, PF, PF, I32, I32, I64, I64, PF, I32]),
+    "orc_sage_forward": (None, [PF, I64, I32, I32, PI64, PI32, PF, PF, I32, I32, I64, I64, PF, I32, I32]),
+    "orc_sage_sample_positions": (None, [I32, I32, PI32]),
+    "orc_chacha_words": (None, [C.POINTER(C.c_uint32), I32, I32, C.POINTER(C.c_uint32)]),
     "orc_gcn_forward": (None, [PF, I64, I32, I32, PI64, PI32, PF, PF, PF, I32, PF, I32]),
     "orc_rvl_forward_one": (None, [C.POINTER(Rvl), PF, PF, I32, PF, I32, PF]),
     "orc_rvl_forward_graph": (None, [C.POINTER(Rvl), PF, I64, PI64, PI32, PF, I64, I64, PF, I32]),
@@ -250,7 +252,7 @@ def aggregate(x, rp, col, method="sum", w=None, keep_isolated=False):
     return out
 
 
-def sage_forward(x, rp, col, wn, ws, aggregator=0, normalize=True, rows=None, threads=8):
+def sage_forward(x, rp, col, wn, ws, aggregator=0, normalize=True, rows=None, threads=8, num_samples=None):
     x, wn, ws = f32(x), f32(wn), f32(ws)
     n, in_f = x.shape
     out_f = wn.shape[1]
@@ -258,8 +260,24 @@ def sage_forward(x, rp, col, wn, ws, aggregator=0, normalize=True, rows=None, th
     y = np.empty((nr, out_f), np.float32)
     lib().orc_sage_forward(fp(x), n, in_f, out_f, ip64(np.ascontiguousarray(rp, np.int64)),
                            ip32(np.ascontiguousarray(col, np.int32)), fp(wn), fp(ws), aggregator, int(normalize), r0,
-                           nr, fp(y), threads)
+                           nr, fp(y), threads, 2**31 - 1 if num_samples is None else int(num_samples))
     return y
+
+
+def sage_sample_positions(length, k):
+    """Positions GraphSAGELayer::sample_neighbors keeps for a list of `length` > k (graphsage.rs:92-102)."""
+    out = np.empty(k, np.int32)
+    lib().orc_sage_sample_positions(int(length), int(k), ip32(out))
+    return out
+
+
+def chacha_words(key_words, rounds, nwords):
+    """ChaCha keystream (block 0 on, zero nonce) — the rand_chacha core of StdRng."""
+    key = np.ascontiguousarray(key_words, np.uint32)
+    out = np.empty(nwords, np.uint32)
+    lib().orc_chacha_words(key.ctypes.data_as(C.POINTER(C.c_uint32)), int(rounds), int(nwords),
+                           out.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return out
 
 
 def gcn_forward(x, rp, col, w, bias=None, ew=None, normalize=True, threads=8):

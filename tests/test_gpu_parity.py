@@ -210,6 +210,31 @@ def test_graphsage_matches_oracle(in_f, out_f, n, deg):
         assert_close(y, ref)
 
 
+@pytest.mark.parametrize("k", [0, 3, 16])
+@pytest.mark.parametrize("in_f,out_f,n", [(16, 32, 300), (768, 768, 500)])
+def test_graphsage_sampling_matches_oracle(k, in_f, out_f, n):
+    """num_samples < degree: rows aggregate the sample_neighbors subset
+    (StdRng(42) partial_shuffle prefix, graphsage.rs:92-102) via the sampled CSR."""
+    rng = np.random.default_rng(k + n)
+    degs = rng.integers(0, 41, n)
+    degs[:3] = (0, k, k + 1)
+    rp = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
+    col = rng.integers(0, n, int(rp[-1])).astype(np.int32)
+    x = O.fill_uniform(n * in_f, 17 + k).reshape(n, in_f)
+    g = rv.Graph.from_csr(rp, col)
+    for agg, a_id in (("mean", 0), ("maxpool", 1)):
+        layer = rv.GraphSAGELayer(in_f, out_f, num_samples=k, aggregator=agg)
+        y = layer.forward_graph(x, g)
+        ref = O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), a_id,
+                             num_samples=k)
+        assert_close(y, ref)
+        y2 = layer.forward_graph(x, g)  # cached sampled CSR
+        assert np.array_equal(y, y2)
+    nb = list(range(100, 140))
+    assert layer.sample_neighbors(nb, 7) == [nb[p] for p in O.sage_sample_positions(40, 7)]
+    assert layer.sample_neighbors(nb[:5], 7) == nb[:5]
+
+
 @pytest.mark.parametrize("wm,dma,m16", [(4, 1, 0), (8, 1, 0), (8, 0, 0), (4, 1, 1)])
 # out_f = 200 is avoided: with the deterministic init a few rows cancel to a
 # pre-normalisation norm of ~1e-4 (ill-conditioned for any f32 evaluation,
