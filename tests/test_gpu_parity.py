@@ -296,11 +296,16 @@ def test_graphsage_reference_unit_cases():
         assert abs(nrm - 1.0) < 1e-5 or nrm == 0.0
 
 
-def test_graphsage_sampling_rejected():
+def test_graphsage_sampling_edge_index_api():
+    """GraphSAGELayer::forward(features, edge_index) with num_samples below the degree
+    (graphsage.rs:118-196): node 1 has 2 neighbours, num_samples 1."""
+    x = O.fill_uniform(3 * 4, 12).reshape(3, 4)
+    edges = [(0, 1), (2, 1)]
     layer = rv.GraphSAGELayer(4, 4, num_samples=1)
-    with pytest.raises(rv.GnnError) as e:
-        layer.forward(np.ones((3, 4), np.float32), [(0, 1), (2, 1)])
-    assert e.value.kind == "Unsupported"
+    y = layer.forward(x, edges)
+    rp, col, _ = O.build_csr(3, edges)
+    ref = O.sage_forward(x, rp, col, O.sage_init(4, 4, 0), O.sage_init(4, 4, 1000), num_samples=1)
+    assert_close(y, ref)
 
 
 @pytest.mark.parametrize("weighted", [False, True])
