@@ -113,6 +113,7 @@ struct rvx_sage_layer {
     std::vector<float> wn, ws;  // host [in][out]
     DevMem wn_t, ws_t;          // device [out][in]
     DevMem wn_x3, ws_x3;        // exact 3-way bf16 splits of wn_t / ws_t (split-bf16 MFMA GEMM)
+    DevMem wn_h2, ws_h2, w_inv; // f16 [hi][lo] planes of wn_t / ws_t scaled per output feature (split-f16 GEMM)
 };
 
 struct rvx_gcn_layer {
@@ -145,6 +146,13 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
     const int64_t n = g->n;
     float* agg = scratch_f32("sage_agg", n * (int64_t)l->in);
     const int a = (l->aggregator == RVX_SAGE_MAXPOOL) ? AGG_MAX : AGG_MEAN;
+    // split-f16 dual GEMM when the shapes allow it: the gather also emits the
+    // per-row operand scale over the aggregate and self rows
+    const bool h2 = l->wn_h2.p && l->in <= 1024 && ((uintptr_t)x & 15) == 0 &&
+                    gemm_h2_ok(std::max<int64_t>(n, 1), l->out, GemmOperand{agg, l->in, nullptr, l->in, l->in},
+                               nullptr) &&
+                    gemm_h2_ok(std::max<int64_t>(n, 1), l->out, GemmOperand{x, l->in, nullptr, l->in, l->in}, nullptr);
+    float* scale = h2 ? scratch_f32("sage_scale", std::max<int64_t>(n, 1)) : nullptr;
     GemmEpilogue ep;
     ep.epi = GEMM_EPI_RELU;
     // Rows are independent, so the layer runs as a two-stage pipeline over
@@ -165,17 +173,23 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         if (chunks > 1) {
             StreamScope on_aux(d.aux);
             aggregate_rows(g->row_ptr + r0, g->col, nullptr, rows, x, l->in, a, /*empty_fill zeros*/ 0, 0,
-                           agg + r0 * l->in, "sage_aggregate", /*overlapped*/ true);
+                           agg + r0 * l->in, "sage_aggregate", /*overlapped*/ true,
+                           x + (row_offset + r0) * l->in, h2 ? scale + r0 : nullptr);
             RVX_HIP(hipEventRecord(ev[c], d.aux));
             RVX_HIP(hipStreamWaitEvent(d.stream, ev[c], 0));
         } else {
-            aggregate_rows(g->row_ptr, g->col, nullptr, n, x, l->in, a, 0, 0, agg, "sage_aggregate");
+            aggregate_rows(g->row_ptr, g->col, nullptr, n, x, l->in, a, 0, 0, agg, "sage_aggregate", false,
+                           x + row_offset * l->in, scale);
         }
         const int64_t plane = (int64_t)l->in * l->out;
         GemmOperand s0{agg + r0 * l->in, l->in, l->wn_t.as<float>(), l->in, l->in, l->wn_x3.as<uint16_t>(), plane};
         GemmOperand s1{x + (row_offset + r0) * l->in, l->in, l->ws_t.as<float>(), l->in, l->in,
                        l->ws_x3.as<uint16_t>(), plane};
-        gemm_nt(rows, l->out, s0, &s1, ep, y + r0 * l->out, l->out, "sage_gemm");
+        if (h2)
+            gemm_nt_h2(rows, l->out, s0, l->wn_h2.as<_Float16>(), &s1, l->ws_h2.as<_Float16>(), scale + r0,
+                       l->w_inv.as<float>(), ep, y + r0 * l->out, l->out, "sage_gemm");
+        else
+            gemm_nt(rows, l->out, s0, &s1, ep, y + r0 * l->out, l->out, "sage_gemm");
         if (l->normalize) normalize_rows(y + r0 * l->out, rows, l->out, true, "sage_normalize");
         if (hook) hook(c, r0, rows);
     }
@@ -334,6 +348,11 @@ rvx_status rvx_sage_layer_create(int32_t in, int32_t out_f, int32_t num_samples,
         l->ws_x3.reset((int64_t)in * out_f * 6);
         split_x3(l->wn_t.as<float>(), (int64_t)in * out_f, l->wn_x3.as<uint16_t>());
         split_x3(l->ws_t.as<float>(), (int64_t)in * out_f, l->ws_x3.as<uint16_t>());
+        l->wn_h2.reset((int64_t)in * out_f * 4);
+        l->ws_h2.reset((int64_t)in * out_f * 4);
+        l->w_inv.reset((int64_t)out_f * 4);
+        split_h2_rows(l->wn_t.as<float>(), l->ws_t.as<float>(), out_f, in, l->wn_h2.as<_Float16>(),
+                      l->ws_h2.as<_Float16>(), l->w_inv.as<float>());
         sync();
         *out = l.release();
     });

@@ -129,6 +129,15 @@ struct KernelTimer {
     ~KernelTimer();
 };
 
+// Power-of-two scale putting a row maximum m in [2^14, 2^15) (1 for zero or
+// non-finite rows): the split-f16 GEMM's operand scaling (gemm_f32.hip), also
+// produced by the gather kernel (k_aggregate.hip).
+__device__ __forceinline__ float h2_scale_dev(float m) {
+    if (!(m > 0.0f) || !__builtin_isfinite(m)) return 1.0f;
+    const int e = ilogbf(m);
+    return ldexpf(1.0f, min(127, max(-126, 14 - e)));
+}
+
 }  // namespace rvx
 
 // Launch on the library stream, timed per kernel when profiling is enabled.

@@ -44,6 +44,10 @@ struct GemmArgs {
     int64_t M; int N;
     int tiles_n; int64_t nblocks;
     float alpha;  // scale applied to acc before bias (dropout scale etc.)
+    // split-f16 path (gemm_nt_h2g): per-row power-of-2 scale of A, per-column
+    // inverse scale of B, and the two f16 planes of each B
+    const float* a_scale; const float* b_inv;
+    const _Float16* B0h; const _Float16* B1h; int64_t B0h_plane, B1h_plane;
 };
 
 __device__ __forceinline__ float epi_apply(int epi, float v) {
@@ -741,6 +745,242 @@ __global__ void k_split_x3(const float* __restrict__ src, int64_t n, uint16_t* _
     dst[2 * n + i] = (uint16_t)(__float_as_uint(s) >> 16);
 }
 
+// ---------------------------------------------------------------------------
+// Split-f16 MFMA GEMM ("h2"), the GraphSAGE layer's dual GEMM. Each f32
+// operand row is scaled by a power of two (exact) so its largest magnitude
+// lands in [2^14, 2^15) — A rows by the gather kernel (row_scale of
+// aggregate_rows, over the aggregate AND the self row of the dual GEMM), B
+// rows (output features) once at upload — then split with round-to-nearest
+// into two f16 parts, x = x1 + x2 + r with |r| <= 2^-22 |x|. Three f16 MFMA
+// products per fragment pair, a2b1 + a1b2 + a1b1 (the dropped a2b2 is
+// <= 2^-22 |ab|), accumulate in f32; the epilogue undoes the two scales
+// exactly. Per product that is f32-level accuracy at half the MFMA work of the
+// six-product bf16 split (x3) and two thirds of its B operand bytes.
+// Tiling as gemm_nt_x3g<.., 4, false>: 128x128x32, waves 4(M) x 1(N), LDS-DMA
+// stage fill with source-address XOR swizzle, 2 x 32 KB stages.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split_h2_pair(float a0, float a1, float sc, unsigned& w1, unsigned& w2) {
+    const float x0 = a0 * sc, x1 = a1 * sc;
+    const _Float16 h0 = (_Float16)x0, h1 = (_Float16)x1;
+    const _Float16 l0 = (_Float16)(x0 - (float)h0), l1 = (_Float16)(x1 - (float)h1);
+    w1 = (unsigned)__builtin_bit_cast(unsigned short, h0) | ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+    w2 = (unsigned)__builtin_bit_cast(unsigned short, l0) | ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
+}
+
+template <bool DUAL>
+__global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
+    constexpr int XA = 128 * 128;             // f32 A tile bytes per stage
+    constexpr int STG = XA + 2 * XB_PLANE;    // 32 KB stage
+    constexpr int NB = 4;                     // B DMA pieces per wave (2 planes x 8 pieces)
+    extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
+
+    const int64_t nwg = g.nblocks;
+    const int64_t bid = blockIdx.x;
+    const int64_t xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    const int64_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    const int64_t tm = wgid / g.tiles_n;
+    const int tn = (int)(wgid % g.tiles_n);
+    const int64_t m0 = tm * 128;
+    const int n0 = tn * XBN;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, lh = lane >> 5;
+
+    const int nk0 = g.K0 / 32;
+    const int nk1 = DUAL ? g.K1 / 32 : 0;
+
+    auto sw_a = [](int row) { return (row >> 1) & 7; };
+    auto sw_b = [](int row) { return (row >> 2) & 3; };
+
+    uint32_t a_off[2][4], b_off[2][NB];
+    const char* a_base[2];
+    const char* b_base[2];
+#pragma unroll
+    for (int ph = 0; ph < (DUAL ? 2 : 1); ++ph) {
+        const float* A = ph ? g.A1 : g.A0;
+        const _Float16* B = ph ? g.B1h : g.B0h;
+        const int64_t lda = ph ? g.lda1 : g.lda0, ldb = ph ? g.ldb1 : g.ldb0, bpl = ph ? g.B1h_plane : g.B0h_plane;
+        a_base[ph] = reinterpret_cast<const char*>(A + m0 * lda);
+        b_base[ph] = reinterpret_cast<const char*>(B + (int64_t)n0 * ldb);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = 8 * (4 * wave + j) + (lane >> 3);
+            const int chunk = (lane & 7) ^ sw_a(row);
+            const int64_t rr = std::min<int64_t>(m0 + row, g.M - 1) - m0;
+            a_off[ph][j] = (uint32_t)((rr * lda + 4 * chunk) * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int piece = NB * wave + j;
+            const int row = 16 * (piece & 7) + (lane >> 2);
+            const int chunk = (lane & 3) ^ sw_b(row);
+            const int64_t rr = std::min<int64_t>(n0 + row, (int64_t)g.N - 1) - n0;
+            b_off[ph][j] = (uint32_t)(((piece >> 3) * bpl + rr * ldb + 8 * chunk) * 2);
+        }
+    }
+
+    auto fill_ph = [&](int ph, int k0, unsigned char* base) {
+        const char* ab = a_base[ph] + (int64_t)k0 * 4;
+        const char* bb = b_base[ph] + (int64_t)k0 * 2;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_global_load_lds((const void*)(ab + a_off[ph][j]),
+                                             (__attribute__((address_space(3))) void*)(base + (4 * wave + j) * 1024),
+                                             16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int piece = NB * wave + j;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(bb + b_off[ph][j]),
+                (__attribute__((address_space(3))) void*)(base + XA + (piece >> 3) * XB_PLANE + (piece & 7) * 1024),
+                16, 0, 0);
+        }
+    };
+    auto xa_sw = [&](int row, int chunk) { return row * 128 + ((chunk ^ sw_a(row)) << 4); };
+    auto xb_sw = [&](int row, int chunk) { return row * 64 + ((chunk ^ sw_b(row)) << 4); };
+
+    f32x16 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.0f;
+
+    const int arow = wave * 32 + lr;
+    const float a_sc = g.a_scale[std::min<int64_t>(m0 + arow, g.M - 1)];
+    int a_rd[2][2], b_rd[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        a_rd[s][0] = xa_sw(arow, 4 * s + 2 * lh);
+        a_rd[s][1] = xa_sw(arow, 4 * s + 2 * lh + 1);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) b_rd[s][ni] = XA + xb_sw(ni * 32 + lr, 2 * s + lh);
+    }
+
+    auto tile = [&](const unsigned char* __restrict__ cur, unsigned char* __restrict__ nxt, int fph, int fk0) {
+        if (fph == 0) fill_ph(0, fk0, nxt);
+        else if (DUAL && fph == 1) fill_ph(1, fk0, nxt);
+        float4 alo[2], ahi[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            alo[s] = *reinterpret_cast<const float4*>(cur + a_rd[s][0]);
+            ahi[s] = *reinterpret_cast<const float4*>(cur + a_rd[s][1]);
+        }
+        unsigned w[2][2][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            split_h2_pair(f4_at(alo[0], ahi[0], 2 * j), f4_at(alo[0], ahi[0], 2 * j + 1), a_sc, w[0][0][j], w[0][1][j]);
+        u32x4 bq[2][2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) bq[0][p] = *reinterpret_cast<const u32x4*>(cur + b_rd[0][0] + p * XB_PLANE);
+#pragma unroll
+        for (int gi = 0; gi < 8; ++gi) {
+            const int s = gi >> 2, ni = gi & 3;
+            if (gi + 1 < 8) {
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+                    bq[(gi + 1) & 1][p] =
+                        *reinterpret_cast<const u32x4*>(cur + b_rd[(gi + 1) >> 2][(gi + 1) & 3] + p * XB_PLANE);
+            }
+            f16x8 af[2], bf[2];
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                af[p] = __builtin_bit_cast(f16x8, u32x4{w[s][p][0], w[s][p][1], w[s][p][2], w[s][p][3]});
+                bf[p] = __builtin_bit_cast(f16x8, bq[gi & 1][p]);
+            }
+            if (s == 0)
+                split_h2_pair(f4_at(alo[1], ahi[1], 2 * ni), f4_at(alo[1], ahi[1], 2 * ni + 1), a_sc, w[1][0][ni],
+                              w[1][1][ni]);
+            f32x16 c = acc[ni];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], c, 0, 0, 0);
+            acc[ni] = c;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    fill_ph(0, 0, xsm);
+    __syncthreads();
+    int stage = 0;
+#pragma unroll
+    for (int ph = 0; ph < (DUAL ? 2 : 1); ++ph) {
+        const int nkp = ph ? nk1 : nk0;
+        for (int kt = 0; kt < nkp; ++kt) {
+            int fph = -1, fk0 = 0;
+            if (kt + 1 < nkp) { fph = ph; fk0 = (kt + 1) * 32; }
+            else if (DUAL && ph == 0 && nk1 > 0) fph = 1;
+            tile(xsm + stage * STG, xsm + (stage ^ 1) * STG, fph, fk0);
+            __syncthreads();
+            stage ^= 1;
+        }
+    }
+
+    // epilogue: undo the row and column scales (powers of two: exact), then
+    // alpha / bias / addend / activation as the other kernels
+    float rinv[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int64_t row = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        rinv[e] = row < g.M ? 1.0f / g.a_scale[row] : 0.0f;
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+        const int col = n0 + ni * 32 + lr;
+        if (col >= g.N) continue;
+        const float cinv = g.b_inv[col];
+        float b = 0.0f;
+        if (g.bias0) b = g.bias0[col];
+        if (g.bias1) b += g.bias1[col];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int64_t row = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+            if (row < g.M) {
+                float v = (acc[ni][e] * rinv[e]) * cinv;
+                if (g.alpha != 1.0f) v *= g.alpha;
+                if (g.bias0 || g.bias1) v += b;
+                if (g.addend) v += g.addend[row * g.ld_add + col];
+                g.C[row * g.ldc + col] = epi_apply(epi, v);
+            }
+        }
+    }
+}
+
+// B rows n of one or two [N][K] matrices: common scale t_n, f16 planes of each
+// (plane stride N*K), inv[n] = 1 / t_n. One wave per row.
+__global__ __launch_bounds__(256) void k_split_h2_rows(const float* __restrict__ B0, const float* __restrict__ B1,
+                                                       int N, int K, _Float16* __restrict__ P0,
+                                                       _Float16* __restrict__ P1, float* __restrict__ inv) {
+    const int lane = threadIdx.x & 63;
+    const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (n >= N) return;
+    float m = 0.0f;
+    for (int k = lane; k < K; k += 64) {
+        m = fmaxf(m, fabsf(B0[(int64_t)n * K + k]));
+        if (B1) m = fmaxf(m, fabsf(B1[(int64_t)n * K + k]));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    const float t = h2_scale_dev(m);
+    const int64_t plane = (int64_t)N * K;
+    for (int k = lane; k < K; k += 64) {
+        const int64_t i = (int64_t)n * K + k;
+        const float x0 = B0[i] * t;
+        const _Float16 h0 = (_Float16)x0;
+        P0[i] = h0;
+        P0[plane + i] = (_Float16)(x0 - (float)h0);
+        if (B1) {
+            const float x1 = B1[i] * t;
+            const _Float16 h1 = (_Float16)x1;
+            P1[i] = h1;
+            P1[plane + i] = (_Float16)(x1 - (float)h1);
+        }
+    }
+    if (lane == 0) inv[n] = 1.0f / t;
+}
+
 // Correctness path for shapes the tiled kernel cannot take (K % 4 != 0 or
 // unaligned rows, e.g. the reference's 2-wide unit tests): one thread per
 // output, k-sequential fma chain.
@@ -845,6 +1085,49 @@ void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, con
         const int64_t total = M * (int64_t)N;
         RVX_LAUNCH(t, gemm_nt_simple, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, g, epi);
     }
+}
+
+bool gemm_h2_ok(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1) {
+    if (!env_int("RVX_GEMM_H2", 1) || M <= 0 || N <= 0) return false;  // read per call: tests cover both GEMMs
+    auto ok = [N](const GemmOperand& o) {
+        const int64_t lim = (int64_t)1 << 31;
+        return o.K % 32 == 0 && o.lda % 4 == 0 && o.ldb % 8 == 0 && aligned16(o.A) && (int64_t)128 * o.lda * 4 < lim &&
+               ((int64_t)o.ldb * N + (int64_t)XBN * o.ldb) * 2 < lim;
+    };
+    return ok(s0) && (!s1 || ok(*s1));
+}
+
+void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
+                const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
+                int64_t ldc, const char* tag) {
+    if (M <= 0 || N <= 0) return;
+    GemmArgs g{};
+    g.addend = ep.addend;
+    g.ld_add = ep.ld_addend;
+    g.A0 = s0.A; g.lda0 = s0.lda; g.ldb0 = s0.ldb; g.K0 = s0.K;
+    g.B0h = B0h; g.B0h_plane = (int64_t)N * s0.ldb;
+    if (s1) { g.A1 = s1->A; g.lda1 = s1->lda; g.ldb1 = s1->ldb; g.K1 = s1->K; g.B1h = B1h; g.B1h_plane = (int64_t)N * s1->ldb; }
+    g.bias0 = ep.bias0; g.bias1 = ep.bias1; g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.alpha = ep.alpha;
+    g.a_scale = a_scale; g.b_inv = b_inv;
+    g.tiles_n = (N + XBN - 1) / XBN;
+    g.nblocks = ((M + 127) / 128) * g.tiles_n;
+    RVX_REQUIRE(gemm_h2_ok(M, N, s0, s1), RVX_ERR_INVALID_SHAPE, "shape not supported by the split-f16 GEMM");
+    RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
+    constexpr int lds = 2 * (128 * 128 + 2 * XB_PLANE);
+    static bool attr = false;
+    if (!attr) {
+        RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2g<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2g<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        attr = true;
+    }
+    const char* t = tag ? tag : "gemm_nt_h2";
+    if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)g.nblocks), dim3(256), lds, g, ep.epi);
+    else RVX_LAUNCH(t, gemm_nt_h2g<false>, dim3((unsigned)g.nblocks), dim3(256), lds, g, ep.epi);
+}
+
+void split_h2_rows(const float* B0, const float* B1, int N, int K, _Float16* P0, _Float16* P1, float* inv) {
+    if (N <= 0) return;
+    RVX_LAUNCH("split_h2", k_split_h2_rows, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, B0, B1, N, K, P0, P1, inv);
 }
 
 }  // namespace rvx

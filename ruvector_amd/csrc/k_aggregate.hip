@@ -50,7 +50,8 @@ template <int NV, int AGG, bool W, int U = 4, bool NT = false>
 __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
                                                       const float* __restrict__ wts, int64_t n,
                                                       const float* __restrict__ x, int dim, int empty_fill,
-                                                      int post_scale, float* __restrict__ out) {
+                                                      int post_scale, float* __restrict__ out,
+                                                      const float* __restrict__ self_x, float* __restrict__ row_scale) {
     const int lane = threadIdx.x & 63;
     // grid-stride over rows: the grid may be capped (persistent) so the gather
     // leaves CU slots to a concurrently running GEMM
@@ -104,6 +105,34 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
     }
 
     float* dst = out + row * dim + 4 * lane;
+    if (cnt_total > 0) {
+        if (AGG == AGG_MEAN) {
+            const float cntf = (float)cnt_total;  // mean_aggregate: x / count (aggregators.rs:64-67)
+#pragma unroll
+            for (int j = 0; j < NV; ++j)
+                acc[j] = make_float4(acc[j].x / cntf, acc[j].y / cntf, acc[j].z / cntf, acc[j].w / cntf);
+        }
+        if (post_scale == 1) {  // GCN: aggregated *= 1/sqrt(degree) (gcn.rs:127-134)
+            const float nrm = 1.0f / sqrtf((float)cnt_total);
+#pragma unroll
+            for (int j = 0; j < NV; ++j) acc[j] = scale4(acc[j], nrm);
+        }
+    }
+    if (row_scale) {  // split-f16 GEMM operand scale over this row's aggregate and self rows
+        float m = 0.0f;
+        const float* sp = self_x + row * dim + 4 * lane;
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+            if (active[j]) {
+                const float4 v = *reinterpret_cast<const float4*>(sp + 256 * j);
+                m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+                if (cnt_total > 0)
+                    m = fmaxf(m, fmaxf(fmaxf(fabsf(acc[j].x), fabsf(acc[j].y)), fmaxf(fabsf(acc[j].z), fabsf(acc[j].w))));
+            }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+        if (lane == 0) row_scale[row] = h2_scale_dev(m);
+    }
     if (cnt_total == 0) {
         const float* self = x + row * dim + 4 * lane;
 #pragma unroll
@@ -112,17 +141,6 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
                 *reinterpret_cast<float4*>(dst + 256 * j) =
                     empty_fill == 1 ? *reinterpret_cast<const float4*>(self + 256 * j) : make_float4(0, 0, 0, 0);
         continue;
-    }
-    if (AGG == AGG_MEAN) {
-        const float cntf = (float)cnt_total;  // mean_aggregate: x / count (aggregators.rs:64-67)
-#pragma unroll
-        for (int j = 0; j < NV; ++j)
-            acc[j] = make_float4(acc[j].x / cntf, acc[j].y / cntf, acc[j].z / cntf, acc[j].w / cntf);
-    }
-    if (post_scale == 1) {  // GCN: aggregated *= 1/sqrt(degree) (gcn.rs:127-134)
-        const float nrm = 1.0f / sqrtf((float)cnt_total);
-#pragma unroll
-        for (int j = 0; j < NV; ++j) acc[j] = scale4(acc[j], nrm);
     }
 #pragma unroll
     for (int j = 0; j < NV; ++j)
@@ -158,7 +176,8 @@ __global__ __launch_bounds__(256) void k_aggregate_scalar(const int64_t* rp, con
 
 template <int AGG, bool W>
 void launch_agg(const char* t, const int64_t* rp, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
-                int empty_fill, int post_scale, float* out, int cap_per_cu, bool deep, bool nt) {
+                int empty_fill, int post_scale, float* out, int cap_per_cu, bool deep, bool nt, const float* self_x,
+                float* row_scale) {
     int64_t blocks = (n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
     if (cap_per_cu > 0) blocks = std::min<int64_t>(blocks, (int64_t)cap_per_cu * device().num_cus);
     const dim3 grid((unsigned)blocks), block(256);
@@ -167,20 +186,22 @@ void launch_agg(const char* t, const int64_t* rp, const int32_t* col, const floa
     do {                                                                                                         \
         if (deep && nt)                                                                                        \
             RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 8, true>), grid, block, 0, rp, col, w, n, x, dim,         \
-                       empty_fill, post_scale, out);                                                             \
+                       empty_fill, post_scale, out, self_x, row_scale);                                          \
         else if (deep)                                                                                           \
             RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 8>), grid, block, 0, rp, col, w, n, x, dim, empty_fill,   \
-                       post_scale, out);                                                                         \
+                       post_scale, out, self_x, row_scale);                                                      \
         else                                                                                                     \
             RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 4>), grid, block, 0, rp, col, w, n, x, dim, empty_fill,   \
-                       post_scale, out);                                                                         \
+                       post_scale, out, self_x, row_scale);                                                      \
     } while (0)
     if (vec && dim <= 256) RVX_AGG_VEC(1);
     else if (vec && dim <= 512) RVX_AGG_VEC(2);
     else if (vec && dim <= 768) RVX_AGG_VEC(3);
     else if (vec && dim <= 1024) RVX_AGG_VEC(4);
-    else
+    else {
+        RVX_REQUIRE(!row_scale, RVX_ERR_INVALID_SHAPE, "row_scale needs the vector gather (dim % 4 == 0, <= 1024)");
         RVX_LAUNCH(t, (k_aggregate_scalar<AGG, W>), grid, block, 0, rp, col, w, n, x, dim, empty_fill, post_scale, out);
+    }
 #undef RVX_AGG_VEC
 }
 
@@ -195,21 +216,23 @@ int g_agg_overlap_unroll = env_int("RVX_AGG_UNROLL", 8);
 int g_agg_nt = env_int("RVX_AGG_NT", 1);
 
 void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
-                    int agg, int empty_fill, int post_scale, float* out, const char* tag, bool overlapped) {
+                    int agg, int empty_fill, int post_scale, float* out, const char* tag, bool overlapped,
+                    const float* self_x, float* row_scale) {
     if (n <= 0) return;
+    static const int standalone_deep = env_int("RVX_AGG_STANDALONE_DEEP", 0);  // experiment knob
     const int cap = overlapped ? g_agg_overlap_cap : 0;
-    const bool deep = overlapped && g_agg_overlap_unroll >= 8;
-    const bool nt = overlapped && g_agg_nt;
+    const bool deep = (overlapped || standalone_deep) && g_agg_overlap_unroll >= 8;
+    const bool nt = (overlapped || standalone_deep) && g_agg_nt;
     RVX_REQUIRE(n / ROWS_PER_BLOCK < ((int64_t)1 << 31), RVX_ERR_INVALID_SHAPE, "graph too large for one launch");
     const char* t = tag ? tag : "aggregate";
     const bool W = w != nullptr;
     switch (agg) {
-        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt)
-                        : launch_agg<AGG_SUM, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt); break;
-        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt)
-                         : launch_agg<AGG_MEAN, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt); break;
-        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt)
-                        : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt); break;
+        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale)
+                        : launch_agg<AGG_SUM, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale); break;
+        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale)
+                         : launch_agg<AGG_MEAN, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale); break;
+        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale)
+                        : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale); break;
         default: fail(RVX_ERR_INVALID_PARAMETER, "unknown aggregator");
     }
 }

@@ -53,6 +53,37 @@ __global__ void k_normalize_rows(float* p, int64_t rows, int dim, int only_posit
     for (int c = lane; c < dim; c += 64) x[c] = x[c] / norm;
 }
 
+// Vector form for dim % 4 == 0, dim <= 256*NV: the row stays in registers
+// (one 1-KiB wave load per 256 columns), one read and one write per element.
+template <int NV>
+__global__ __launch_bounds__(256) void k_normalize_rows_vec(float* __restrict__ p, int64_t rows, int dim,
+                                                            int only_positive) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    float* x = p + row * dim + 4 * lane;
+    float4 v[NV];
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const bool on = 4 * lane + 256 * j < dim;
+        v[j] = on ? *reinterpret_cast<const float4*>(x + 256 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+        s = __fadd_rn(s, __fmul_rn(v[j].x, v[j].x));
+        s = __fadd_rn(s, __fmul_rn(v[j].y, v[j].y));
+        s = __fadd_rn(s, __fmul_rn(v[j].z, v[j].z));
+        s = __fadd_rn(s, __fmul_rn(v[j].w, v[j].w));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float norm = sqrtf(s);
+    if (only_positive && !(norm > 0.0f)) return;
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+        if (4 * lane + 256 * j < dim)
+            *reinterpret_cast<float4*>(x + 256 * j) =
+                make_float4(v[j].x / norm, v[j].y / norm, v[j].z / norm, v[j].w / norm);
+}
+
 // rows [row_begin, row_begin + n_rows) of an n_total-node graph; the edge id
 // stream is global so every shard reproduces its slice of the same graph.
 __global__ void k_random_csr(int64_t n_total, int64_t row_begin, int64_t n_rows, int deg, uint64_t s0,
@@ -103,8 +134,15 @@ void fill_normal(float* p, int64_t n, uint64_t seed) {
 }
 void normalize_rows(float* p, int64_t rows, int dim, bool only_positive, const char* tag) {
     if (rows <= 0) return;
-    RVX_LAUNCH(tag ? tag : "normalize_rows", k_normalize_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, p, rows,
-               dim, only_positive ? 1 : 0);
+    const char* t = tag ? tag : "normalize_rows";
+    const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+    const int op = only_positive ? 1 : 0;
+    const bool vec = dim % 4 == 0 && ((uintptr_t)p & 15) == 0;
+    if (vec && dim <= 256) RVX_LAUNCH(t, k_normalize_rows_vec<1>, grid, block, 0, p, rows, dim, op);
+    else if (vec && dim <= 512) RVX_LAUNCH(t, k_normalize_rows_vec<2>, grid, block, 0, p, rows, dim, op);
+    else if (vec && dim <= 768) RVX_LAUNCH(t, k_normalize_rows_vec<3>, grid, block, 0, p, rows, dim, op);
+    else if (vec && dim <= 1024) RVX_LAUNCH(t, k_normalize_rows_vec<4>, grid, block, 0, p, rows, dim, op);
+    else RVX_LAUNCH(t, k_normalize_rows, grid, block, 0, p, rows, dim, op);
 }
 void random_csr(int64_t n, int deg, uint64_t seed, int64_t* row_ptr, int32_t* col) {
     random_csr_shard(n, 0, n, deg, seed, row_ptr, col);

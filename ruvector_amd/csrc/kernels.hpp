@@ -32,6 +32,17 @@ void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, con
 // dst[p*n + i] = bf16 part p of src[i] (exact split src = p0 + p1 + p2)
 void split_x3(const float* src, int64_t n, uint16_t* dst);
 
+// Split-f16 GEMM (gemm_nt_h2g): A rows pre-scaled in-kernel by a_scale[row]
+// (powers of two from aggregate_rows' row_scale), B given as two f16 planes
+// ([2][N][K], from split_h2_rows) with b_inv[n] its inverse column scale.
+bool gemm_h2_ok(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1);
+void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
+                const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
+                int64_t ldc, const char* tag);
+// Common power-of-two scale t_n per row n of B0 (and B1), planes P = [hi][lo]
+// of B*t_n in f16, inv[n] = 1/t_n.
+void split_h2_rows(const float* B0, const float* B1, int N, int K, _Float16* P0, _Float16* P1, float* inv);
+
 // ---- data generators (k_data.hip) ---------------------------------------
 void fill_uniform(float* p, int64_t n, uint64_t seed, float lo, float hi);
 void fill_normal(float* p, int64_t n, uint64_t seed);
@@ -45,8 +56,12 @@ void transpose(const float* in, int64_t rows, int64_t cols, float* out);  // out
 enum { AGG_SUM = 0, AGG_MEAN = 1, AGG_MAX = 2 };
 // out[i] = agg over CSR row i of (w_e * x[col_e]) ; empty row -> `empty_fill`
 // (0 = zeros, 1 = copy x[i], 2 = -inf for max). post_scale: 0 none, 1 = ×1/sqrt(deg) (GCN).
+// row_scale (optional): also writes, per row, the power-of-two scale putting
+// max(|out row|, |self row|) in [2^14, 2^15) for the split-f16 GEMM, where
+// self = self_x + row*dim.
 void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, int64_t n, const float* x,
                     int dim, int agg, int empty_fill, int post_scale, float* out, const char* tag,
-                    bool overlapped = false);  // true: runs beside a GEMM (capped grid)
+                    bool overlapped = false,  // true: runs beside a GEMM (capped grid)
+                    const float* self_x = nullptr, float* row_scale = nullptr);
 
 }  // namespace rvx

@@ -244,7 +244,8 @@ def test_graphsage_sampling_matches_oracle(k, in_f, out_f, n):
 def test_graphsage_gemm_tilings(monkeypatch, wm, dma, m16, in_f, out_f, n):
     """Every split-bf16 GEMM tiling (128- and 256-row LDS-DMA tiles with 32x32x16
     MFMAs, the 16x16x32 form, register-staged fallback) on ragged M and N
-    against the oracle."""
+    against the oracle (the split-f16 GEMM, default for these shapes, is off)."""
+    monkeypatch.setenv("RVX_GEMM_H2", "0")
     monkeypatch.setenv("RVX_GEMM_WM", str(wm))
     monkeypatch.setenv("RVX_GEMM_DMA", str(dma))
     monkeypatch.setenv("RVX_GEMM_MFMA16", str(m16))
@@ -255,6 +256,44 @@ def test_graphsage_gemm_tilings(monkeypatch, wm, dma, m16, in_f, out_f, n):
     layer = rv.GraphSAGELayer(in_f, out_f, num_samples=deg)
     y = layer.forward_graph(x, g)
     ref = O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0)
+    assert_close(y, ref)
+
+
+@pytest.mark.parametrize("in_f,out_f,n", [(768, 768, 600), (96, 232, 1000), (64, 130, 257), (32, 32, 129)])
+def test_graphsage_split_f16_gemm(monkeypatch, in_f, out_f, n):
+    """The split-f16 dual GEMM (per-row/column power-of-two scales, two f16
+    planes, three MFMA products) on ragged M and N, and the same layer with it
+    off (split-bf16) — both within tolerance of the oracle."""
+    deg = 9
+    x = O.fill_uniform(n * in_f, 40 + n).reshape(n, in_f)
+    rp, col = O.random_csr(n, deg, 41)
+    g = rv.Graph.from_csr(rp, col)
+    layer = rv.GraphSAGELayer(in_f, out_f, num_samples=deg)
+    ref = O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0)
+    y = layer.forward_graph(x, g)
+    assert_close(y, ref)
+    monkeypatch.setenv("RVX_GEMM_H2", "0")
+    assert_close(layer.forward_graph(x, g), ref)
+
+
+@pytest.mark.parametrize("scale", [1e-30, 1e-8, 1e12, 1e15])
+def test_graphsage_split_f16_operand_range(scale):
+    """Power-of-two operand scaling keeps f16 in range for any f32 magnitude:
+    tiny and huge inputs (and all-zero rows) match the oracle at that scale."""
+    in_f = out_f = 128
+    n, deg = 400, 6
+    x = (O.fill_uniform(n * in_f, 50).reshape(n, in_f) * np.float32(scale)).astype(np.float32)
+    x[5] = 0.0
+    x[7, :64] *= np.float32(1e-6)  # a row spanning many binades
+    rp, col = O.random_csr(n, deg, 51)
+    g = rv.Graph.from_csr(rp, col)
+    wn = O.fill_uniform(in_f * out_f, 52).reshape(in_f, out_f)
+    ws = O.fill_uniform(in_f * out_f, 53).reshape(in_f, out_f)
+    ws[:, 3] *= np.float32(1e-5)  # an output feature with much smaller weights
+    layer = rv.GraphSAGELayer(in_f, out_f, num_samples=deg, neighbor_weights=wn, self_weights=ws)
+    y = layer.forward_graph(x, g)
+    ref = O.sage_forward(x, rp, col, wn, ws, 0)
+    assert np.all(np.isfinite(y))
     assert_close(y, ref)
 
 
