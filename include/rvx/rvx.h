@@ -326,6 +326,55 @@ rvx_status rvx_index_export_graph(const rvx_index* idx, uint8_t* levels, int64_t
 rvx_status rvx_index_layer0_size(const rvx_index* idx, int64_t* n, int64_t* num_edges);
 rvx_status rvx_index_export_layer0(const rvx_index* idx, int64_t* row_ptr, int32_t* col, float* dist);
 
+/* hnsw_rs dump files `<dir>/<basename>.hnsw.graph` + `.hnsw.data`
+ * (patches/hnsw_rs/src/hnswio.rs: Description::dump :878-919,
+ * PointIndexation::dump :1301-1332, dump_point :1063-1110; reload
+ * load_description :937-1040, load_point_indexation :615-790). Written in
+ * format 4, Full mode (the only mode the reference reloads), distance named
+ * after the anndists type of the metric; user ids are the origin ids.
+ * rvx_index_file_dump replaces Hnsw::file_dump; rvx_index_file_load replaces
+ * HnswIo::load_hnsw and puts the dumped graph (and vectors) on the GPU as the
+ * searchable graph (metric < 0: from the distance name). */
+typedef struct {
+    int32_t format_version;      /* 2, 3, 4 (MAGICDESCR_*) */
+    int32_t dump_mode;           /* 1 = Full */
+    int32_t max_nb_connection;
+    int32_t nb_layer;
+    double  level_scale;
+    int64_t ef_construction;
+    int64_t nb_point;
+    int64_t dimension;
+    char    distname[257];
+    char    t_name[257];
+} rvx_hnswio_description;
+rvx_status rvx_hnswio_describe(const char* dir, const char* basename, rvx_hnswio_description* out);
+rvx_status rvx_index_file_dump(const rvx_index* idx, const char* dir, const char* basename);
+rvx_status rvx_index_file_load(const char* dir, const char* basename, int32_t metric, int32_t ef_search,
+                               uint64_t seed, rvx_index** out);
+/* Stored rows [row0, row0+count) of an index (insertion order): vectors
+ * (count x dim), user ids, tombstones; total_rows = rows stored. The data
+ * behind VectorDB::get and HnswIndex::serialize (index/hnsw.rs:136-169). */
+rvx_status rvx_index_export_rows(const rvx_index* idx, int64_t row0, int64_t count, float* vecs, uint64_t* ids,
+                                 uint8_t* deleted, int64_t* total_rows);
+
+/* ------------------------------------------------------------------ */
+/* Node-feature files <-> HBM                                          */
+/* ------------------------------------------------------------------ */
+/* RVX_FEATURE_RAW: MmapManager's embedding file (crates/ruvector-gnn/src/
+ *   mmap.rs:147-218): row i at byte i*dim*4, no header (dim given by caller).
+ * RVX_FEATURE_COLD_TIER: FeatureStorage (crates/ruvector-gnn/src/cold_tier.rs:
+ *   17-151): header {dim, num_nodes, block_size} u64 LE, row i at
+ *   24 + i*block_size, block_size = dim*4 rounded up to the page size.
+ * Loads stream through pinned double-buffered staging (pread overlaps DMA). */
+enum { RVX_FEATURE_RAW = 0, RVX_FEATURE_COLD_TIER = 1 };
+rvx_status rvx_feature_file_info(const char* path, int32_t layout, int64_t dim, int64_t* rows, int64_t* dim_out,
+                                 int64_t* block_size);
+rvx_status rvx_feature_file_load(const char* path, int32_t layout, int64_t dim, int64_t row0, int64_t nrows,
+                                 rvx_buffer* dst, int64_t dst_row0);
+/* block_size (COLD_TIER only): page size to align blocks to; 0 = the host's. */
+rvx_status rvx_feature_file_store(const char* path, int32_t layout, const rvx_buffer* src, int64_t dim, int64_t nrows,
+                                  int64_t block_size);
+
 /* ------------------------------------------------------------------ */
 /* Distances (distance.rs:9-107, poincare.rs:227-301)                  */
 /* ------------------------------------------------------------------ */

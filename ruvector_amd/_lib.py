@@ -65,6 +65,13 @@ class HnswGraph(C.Structure):
                 ("upper_col", C.POINTER(C.POINTER(C.c_int32)))]
 
 
+class HnswioDescription(C.Structure):
+    _fields_ = [("format_version", C.c_int32), ("dump_mode", C.c_int32), ("max_nb_connection", C.c_int32),
+                ("nb_layer", C.c_int32), ("level_scale", C.c_double), ("ef_construction", C.c_int64),
+                ("nb_point", C.c_int64), ("dimension", C.c_int64), ("distname", C.c_char * 257),
+                ("t_name", C.c_char * 257)]
+
+
 P = C.c_void_p
 I32, I64, U64, F32, SZ = C.c_int32, C.c_int64, C.c_uint64, C.c_float, C.c_size_t
 PI32, PI64, PU64, PF32 = C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_uint64), C.POINTER(C.c_float)
@@ -154,6 +161,13 @@ SIGNATURES = {
     "rvx_index_export_graph": (None, [P, C.POINTER(C.c_uint8), PI64, PI32, PI32, PI64, PI32]),
     "rvx_index_layer0_size": (None, [P, PI64, PI64]),
     "rvx_index_export_layer0": (None, [P, PI64, PI32, PF32]),
+    "rvx_hnswio_describe": (None, [C.c_char_p, C.c_char_p, P]),
+    "rvx_index_file_dump": (None, [P, C.c_char_p, C.c_char_p]),
+    "rvx_index_file_load": (None, [C.c_char_p, C.c_char_p, I32, I32, U64, PP]),
+    "rvx_index_export_rows": (None, [P, I64, I64, PF32, PU64, C.POINTER(C.c_uint8), PI64]),
+    "rvx_feature_file_info": (None, [C.c_char_p, I32, I64, PI64, PI64, PI64]),
+    "rvx_feature_file_load": (None, [C.c_char_p, I32, I64, I64, I64, P, I64]),
+    "rvx_feature_file_store": (None, [C.c_char_p, I32, P, I64, I64, I64]),
     "rvx_distance_matrix": (None, [I32, PF32, I64, PF32, I64, I32, F32, PF32]),
     "rvx_profile_enable": (None, [I32]),
     "rvx_profile_reset": (None, []),

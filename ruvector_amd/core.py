@@ -245,6 +245,85 @@ class HnswIndex(_Index):
         """The searchable graph in the rvx_hnsw_graph layout (same dict as load_graph takes)."""
         return export_graph_handle(self._h)
 
+    # ---- persistence (SURVEY.md §8f rank 3)
+    def export_rows(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """All stored rows in insertion order: (vectors [n][d], u64 keys, tombstones)."""
+        total = C.c_int64(0)
+        _check("rvx_index_export_rows", self._h, 0, 0, None, None, None, C.byref(total))
+        n = total.value
+        vecs = np.empty((max(n, 1), self.dimensions), np.float32)
+        keys = np.empty(max(n, 1), np.uint64)
+        dead = np.empty(max(n, 1), np.uint8)
+        _check("rvx_index_export_rows", self._h, 0, n, L.fptr(vecs), L.u64ptr(keys),
+               dead.ctypes.data_as(C.POINTER(C.c_uint8)), C.byref(total))
+        return vecs[:n], keys[:n], dead[:n]
+
+    def serialize(self) -> bytes:
+        """HnswIndex::serialize (index/hnsw.rs:136-169): bincode HnswState of the live vectors."""
+        from .formats import HnswState, METRIC_VARIANTS
+        vecs, keys, dead = self.export_rows()
+        st = HnswState(next_idx=self._next, m=self.config.m, ef_construction=self.config.ef_construction,
+                       ef_search=self.config.ef_search, max_elements=self.config.max_elements,
+                       dimensions=self.dimensions, metric=METRIC_VARIANTS[self.metric.value])
+        for v, k, d in zip(vecs, keys, dead):
+            if d:
+                continue
+            name = self._names.get(int(k), str(int(k)))
+            st.vectors.append((name, v))
+            st.id_to_idx.append((name, int(k)))
+            st.idx_to_id.append((int(k), name))
+        return st.encode()
+
+    @classmethod
+    def deserialize(cls, data: bytes, seed: int = 0) -> "HnswIndex":
+        """HnswIndex::deserialize (index/hnsw.rs:171-226): rebuild by inserting every vector
+        (here in ascending idx order, on the GPU builder)."""
+        from .formats import HnswState, METRIC_VARIANTS
+        st = HnswState.decode(data)
+        cfg = HnswConfig(m=st.m, ef_construction=st.ef_construction, ef_search=st.ef_search,
+                         max_elements=st.max_elements)
+        ix = cls(st.dimensions, DistanceMetric(METRIC_VARIANTS.index(st.metric)), cfg, seed=seed)
+        by_name = {vid: vec for vid, vec in st.vectors}
+        order = sorted((idx, vid) for idx, vid in st.idx_to_id if vid in by_name)
+        if order:
+            keys = np.array([idx for idx, _ in order], np.uint64)
+            ix.add_array(np.stack([by_name[vid] for _, vid in order]), keys)
+            for idx, vid in order:
+                ix._ids[vid] = idx
+                ix._names[idx] = vid
+        ix._next = max(ix._next, st.next_idx)
+        return ix
+
+    def file_dump(self, directory: str, basename: str) -> None:
+        """Hnsw::file_dump (patches/hnsw_rs/src/hnswio.rs): `<basename>.hnsw.graph` + `.hnsw.data`."""
+        _check("rvx_index_file_dump", self._h, directory.encode(), basename.encode())
+
+    @classmethod
+    def file_load(cls, directory: str, basename: str, metric: Optional[DistanceMetric] = None,
+                  ef_search: int = 100) -> "HnswIndex":
+        """HnswIo::load_hnsw: the dumped graph and vectors become the GPU-searchable index."""
+        h = C.c_void_p()
+        _check("rvx_index_file_load", directory.encode(), basename.encode(), -1 if metric is None else metric.value,
+               int(ef_search), 0, C.byref(h))
+        from .formats import describe_dump
+        ds = describe_dump(directory, basename)
+        ix = cls.__new__(cls)
+        ix._h = h
+        ix.dimensions = ds["dimension"]
+        cfg_metric = metric
+        if cfg_metric is None:
+            name = ds["distname"]
+            cfg_metric = next(m for m, suf in ((DistanceMetric.Euclidean, "DistL2"), (DistanceMetric.Cosine, "DistCosine"),
+                                                (DistanceMetric.DotProduct, "DistDot"),
+                                                (DistanceMetric.Manhattan, "DistL1")) if name.endswith(suf))
+        ix.metric = cfg_metric
+        ix.config = HnswConfig(m=ds["max_nb_connection"], ef_construction=ds["ef"], ef_search=ef_search,
+                               max_elements=max(ds["nb_point"], 1))
+        _, keys, _ = ix.export_rows()
+        ix._ids, ix._names = {}, {int(k): str(int(k)) for k in keys}
+        ix._next = int(keys.max()) + 1 if len(keys) else 0
+        return ix
+
     def layer0(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Layer-0 adjacency (row_ptr, col, edge distance) for the GNN."""
         n, e = C.c_int64(), C.c_int64()
