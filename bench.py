@@ -35,12 +35,22 @@ METRIC = "GNN-layer edges/sec + HNSW queries/sec@recall95, 10M\u00d7768, 1/2/4/8
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_MFMA_PEAK_TFS = 157.3   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (dense spec)
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense (spec)
-# The layer GEMM runs as split-bf16 MFMA (gemm_f32.hip gemm_nt_x3): each f32
-# product = 6 exact bf16 partial products accumulated in f32, so its ceiling in
-# f32-equivalent FLOP/s is the bf16 peak / 6. RVX_GEMM_X3=0 selects the FP32
-# MFMA kernel (ceiling 157.3 TF).
+# The layer GEMM runs as split-f16 MFMA (gemm_f32.hip gemm_nt_h2g): operands
+# scaled by powers of two and split into two f16 parts, 3 f16 partial products
+# per f32 product accumulated in f32 (f16 MFMA = the bf16 rate), so its ceiling
+# in f32-equivalent FLOP/s is the f16/bf16 peak / 3. RVX_GEMM_H2=0 selects the
+# split-bf16 GEMM (6 products, peak / 6); RVX_GEMM_X3=0 too, the FP32 MFMA
+# kernel (ceiling 157.3 TF).
+GEMM_H2 = os.environ.get("RVX_GEMM_H2", "1") != "0"
 GEMM_X3 = os.environ.get("RVX_GEMM_X3", "1") != "0"
-GEMM_PEAK_TFS = BF16_MFMA_PEAK_TFS / 6 if GEMM_X3 else FP32_MFMA_PEAK_TFS
+GEMM_PEAK_TFS = (BF16_MFMA_PEAK_TFS / 3 if GEMM_H2 else
+                 BF16_MFMA_PEAK_TFS / 6 if GEMM_X3 else FP32_MFMA_PEAK_TFS)
+GEMM_DESC = ("split-f16 MFMA (per-row/column power-of-two operand scaling, two f16 parts per f32 operand, 3 partial "
+             "products a2b1+a1b2+a1b1, f32 accumulate; <= 2^-21 relative error per product), peak = 2.5 PF f16 / 3"
+             if GEMM_H2 else
+             "split-bf16 MFMA (exact 3-way bf16 split of each f32 operand, 6 partial products, f32 accumulate; "
+             "f32 GEMM to within 2^-23 per product), peak = 2.5 PF bf16 / 6" if GEMM_X3 else
+             "FP32 MFMA v_mfma_f32_32x32x2_f32")
 XGMI_PEAK_GBS = 7 * 153.0    # 7 xGMI links x ~153 GB/s per direction per GPU
 PIPELINE = "row chunks x16 (>=262144 rows), gather on aux stream overlapping GEMM+normalize"
 
@@ -170,9 +180,7 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-        "gemm": ("split-bf16 MFMA (exact 3-way bf16 split of each f32 operand, 6 partial products, f32 accumulate; "
-                 "f32 GEMM to within 2^-23 per product), peak = 2.5 PF bf16 / 6" if GEMM_X3 else
-                 "FP32 MFMA v_mfma_f32_32x32x2_f32"),
+        "gemm": GEMM_DESC,
         "data": "synthetic: X ~ N(0,1) Box-Muller on device (seed 3); uniform random out-degree CSR (seed 4); "
                 "GraphSAGE deterministic init (graphsage.rs:56-78)",
         "config": {"workload": "10M x 768 2-layer ruvector-gnn GraphSAGE-mean forward (configs[1] layers at the "

@@ -19,6 +19,7 @@ TAGS = {  # kernel symbol substring -> bench tag
     "k_aggregate_vec": "sage_aggregate",
     "gemm_nt_mfma": "sage_gemm",
     "gemm_nt_x3": "sage_gemm",
+    "gemm_nt_h2g": "sage_gemm",
     "k_normalize_rows": "sage_normalize",
     "k_scan_topk": "scan_topk",
     "k_hnsw_search": "hnsw_search",
