@@ -297,6 +297,11 @@ rvx_status rvx_index_brute_force_device(const rvx_index* idx, const rvx_buffer* 
  * evaluations, layer-0 expansions and queries — the algorithmic traffic of the search is
  * n_dist * dim * 4 + n_expand * deg_cap * 4 bytes. */
 rvx_status rvx_hnsw_last_search_stats(int64_t* n_dist, int64_t* n_expand, int64_t* nq);
+/* Path taken by the most recent exact scan in this process (rvx_index_brute_force*, FlatIndex
+ * search): queries ranked by the MFMA filter + exact re-rank, queries scanned by the exact VALU
+ * kernel, and queries the filter handed back to the VALU kernel (completeness not provable).
+ * Results are identical either way; this is for tests and benchmarks. */
+rvx_status rvx_scan_last_stats(int64_t* mfma_queries, int64_t* valu_queries, int64_t* fallback_queries);
 
 /* HNSW graph interchange (fixed-graph parity and GNN topology).
  * Layer 0: CSR over all n points in stored neighbour order (hnsw_rs keeps

@@ -12,7 +12,7 @@ from ._lib import RvxError  # noqa: E402
 from .device import Buffer, Profiler, device_count, device_info, set_device, synchronize  # noqa: E402
 from .graph import Graph  # noqa: E402
 from .core import (DistanceMetric, FlatIndex, HnswConfig, HnswIndex, RuvectorError, SearchResult,  # noqa: E402
-                   batch_distances, distance, distance_matrix, hnsw_last_search_stats)
+                   batch_distances, distance, distance_matrix, hnsw_last_search_stats, scan_last_stats)
 from .gnn import (GCNLayer, GnnError, GraphSAGELayer, RuvectorLayer, aggregate, differentiable_search,
                   differentiable_search_device,  # noqa: E402
                   differentiable_search_batch, hierarchical_forward)
@@ -28,6 +28,6 @@ __all__ = [
     "distance", "distance_matrix", "GCNLayer", "GnnError", "GraphSAGELayer", "RuvectorLayer", "aggregate",
     "differentiable_search", "differentiable_search_batch", "hierarchical_forward", "EdgeFeaturedAttention",
     "EdgeFeaturedConfig", "HyperbolicError", "HyperbolicHnsw", "HyperbolicHnswConfig", "ShardedHyperbolicHnsw",
-    "NeuralSearch", "QueryMode", "RuvectorQuery", "differentiable_search_device", "hnsw_last_search_stats",
+    "NeuralSearch", "QueryMode", "RuvectorQuery", "differentiable_search_device", "hnsw_last_search_stats", "scan_last_stats",
 ]
 __version__ = "0.1.0"

@@ -125,6 +125,7 @@ SIGNATURES = {
     "rvx_differentiable_search_batch": (None, [PF32, I64, PF32, I32, I32, I32, F32, PI64, PF32]),
     "rvx_gnn_forward_star_device": (None, [P, P, I64, P, I64, P, I32, P, P]),
     "rvx_hnsw_last_search_stats": (None, [PI64, PI64, PI64]),
+    "rvx_scan_last_stats": (None, [PI64, PI64, PI64]),
     "rvx_differentiable_search_device": (None, [P, I64, P, I64, P, I32, I32, I32, F32, P, P, P]),
     "rvx_edge_attention_create": (None, [C.POINTER(EdgeAttentionConfig), PP]),
     "rvx_edge_attention_destroy": (None, [P]),

@@ -223,6 +223,13 @@ def hnsw_last_search_stats() -> dict:
     return {"n_dist": a.value, "n_expand": b.value, "nq": c.value}
 
 
+def scan_last_stats() -> dict:
+    """Path of the most recent exact scan: MFMA-filtered queries, exact-VALU queries, filter fallbacks."""
+    a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
+    _check("rvx_scan_last_stats", C.byref(a), C.byref(b), C.byref(c))
+    return {"mfma": a.value, "valu": b.value, "fallback": c.value}
+
+
 class FlatIndex(_Index):
     """FlatIndex (index/flat.rs): exact scan, results sorted by distance."""
     kind = L.INDEX_FLAT

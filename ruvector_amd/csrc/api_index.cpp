@@ -435,6 +435,15 @@ rvx_status rvx_distance_matrix(int32_t metric, const float* q, int64_t nq, const
     });
 }
 
+rvx_status rvx_scan_last_stats(int64_t* mfma_queries, int64_t* valu_queries, int64_t* fallback_queries) {
+    return guard([&] {
+        const ScanStats& s = last_scan_stats();
+        if (mfma_queries) *mfma_queries = s.mfma_queries;
+        if (valu_queries) *valu_queries = s.valu_queries;
+        if (fallback_queries) *fallback_queries = s.fallback_queries;
+    });
+}
+
 rvx_status rvx_hnsw_last_search_stats(int64_t* n_dist, int64_t* n_expand, int64_t* nq) {
     return guard([&] {
         if (n_dist) *n_dist = g_search_stats.n_dist;

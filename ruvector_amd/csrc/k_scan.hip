@@ -309,6 +309,565 @@ size_t scan_lds_bytes(int k) {
     return (size_t)(TQ + TR) * ROWF * 4 + (size_t)TQ * k * 12 + (size_t)TQ * TR * 8 + TQ * 12;
 }
 
+// ---------------------------------------------------------------------------
+// MFMA-filtered exact scan (L2 / cosine / dot, large query batches).
+//
+// The scan above is VALU-bound (three exact f32 ops per dimension per pair).
+// For a batch of queries the (query, row) dot products are a GEMM, so this
+// path ranks rows with f16 MFMA and computes REFERENCE distances only for the
+// few rows that can still be in the top-k:
+//   1. rows and queries are scaled by a power of two (exact) so the row max
+//      lands in [2^14, 2^15) and rounded to f16 (k_rows_to_f16);
+//   2. k_scan_filter: v_mfma_f32_32x32x16_f16 dot products over 128 rows x 128
+//      queries tiles, the approximate distance v (L2: |x|^2 + |q|^2 - 2 x.q
+//      in squared units; cosine / dot as the reference forms), and a running
+//      per-(query, row split) list of the FKP smallest v in LDS;
+//   3. k_scan_rerank (one wave per query): D = k-th smallest v + 2 eps_q, where
+//      eps_q bounds |v - reference value| for every row (f16 rounding 2^-11 per
+//      operand, f32 accumulation, the reference's own f32 sum; 2x slack). Every
+//      row whose reference value is <= the k-th reference value has v <= D, so
+//      the candidates {v <= D} hold the exact top-k unless a split's list was
+//      full below D (then the query is re-run on the exact VALU scan). The
+//      candidates' distances are recomputed with the reference arithmetic
+//      (pair_step / pair_finish, same bits as k_scan_topk) and the top-k is
+//      taken in (distance, id) order: results are identical to k_scan_topk.
+// Inputs that are non-finite or outside 2^+-60 (where the scaled products could
+// leave f32 range) send the whole call to the VALU scan.
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int FQ = 128, FR = 128, FK = 32;  // queries x rows per tile, K per stage
+constexpr int FKP = 16;                     // list length per (query, split)
+constexpr int FCB = 8;                      // candidate slots per query per merge round
+constexpr int F_STAGE = (FR + FQ) * FK * 2;  // 16 KB: f16 rows then f16 queries, 64 B per row
+constexpr int F_NSTAGE = 3;                 // LDS-DMA ring: two k-steps in flight across the barrier
+constexpr int F_LDS = F_NSTAGE * F_STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 8;  // 74.5 KB: 2 blocks / CU
+constexpr int F_MAXE = 16;                  // rerank: list entries per lane (nsplit_total * FKP <= 64 * F_MAXE)
+
+struct FilterArgs {
+    // per-row constants {1/scale (NaN for a deleted row), |x|^2 (L2, dot) or the
+    // reference norm (cosine)}; xh / xc are chunk rows indexed from row0
+    const _Float16* xh; const float2* xc;
+    const _Float16* qh; const float2* qc;
+    int64_t nq, row0, row_end; int d;
+    int64_t rows_per_split; int split0, qtiles, nsplit_total;
+    float* part_v; int32_t* part_r;  // [nq][nsplit_total][FKP]
+};
+
+template <int METRIC>
+__device__ __forceinline__ float approx_value(float acc, float xi, float qi, float xs, float qs, float xn, float qn) {
+    const float dot = (acc * xi) * qi;  // undo the power-of-two scales (exact)
+    if (METRIC == RVX_METRIC_L2) return (xs + qs) - 2.0f * dot;
+    if (METRIC == RVX_METRIC_DOT) return -dot;
+    return (qn > 1e-8f && xn > 1e-8f) ? 1.0f - dot / (qn * xn) : 1.0f;
+}
+
+__device__ __forceinline__ bool lt_vr(float v, int r, float bv, int br) { return v < bv || (v == bv && r < br); }
+
+template <int METRIC>
+__global__ __launch_bounds__(256, 2) void k_scan_filter(FilterArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
+    float* best_v = reinterpret_cast<float*>(fsm + F_NSTAGE * F_STAGE);  // [FQ][FKP] ascending (v, row)
+    int32_t* best_r = reinterpret_cast<int32_t*>(best_v + FQ * FKP);
+    float* cand_v = reinterpret_cast<float*>(best_r + FQ * FKP);  // [FQ][FCB]
+    int32_t* cand_r = reinterpret_cast<int32_t*>(cand_v + FQ * FCB);
+    int32_t* cand_n = cand_r + FQ * FCB;                            // [FQ]
+    float* thr = reinterpret_cast<float*>(cand_n + FQ);             // [FQ] list's FKP-th v (INF until full)
+    int32_t* fillc = reinterpret_cast<int32_t*>(thr + FQ);          // [FQ]
+    int32_t* ovf = fillc + FQ;                                      // [2] candidate-slot overflow per round
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, lh = lane >> 5, wm = wave & 1, wn = wave >> 1;
+    // consecutive blocks share a row split (and, 8 at a time, an XCD's L2)
+    const int qt = (int)(blockIdx.x % (unsigned)a.qtiles);
+    const int sl = (int)(blockIdx.x / (unsigned)a.qtiles);
+    const int64_t q0 = (int64_t)qt * FQ;
+    const int64_t r_beg = a.row0 + (int64_t)sl * a.rows_per_split;
+    const int64_t r_end = min(a.row_end, r_beg + a.rows_per_split);
+
+    float2* rowc = reinterpret_cast<float2*>(ovf + 4);              // [FR] current tile's row constants
+
+    for (int i = tid; i < FQ * FKP; i += 256) { best_v[i] = INFINITY; best_r[i] = -1; }
+    if (tid < FQ) { cand_n[tid] = 0; thr[tid] = INFINITY; fillc[tid] = 0; }
+    if (tid < 2) ovf[tid] = 0;
+
+    float qi_[2], qs_[2], qn_[2];
+    bool qv_[2];
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn) {
+        const int64_t qg = q0 + wn * 64 + fn * 32 + lr;
+        qv_[fn] = qg < a.nq;
+        const int64_t qc = min(qg, a.nq - 1);
+        const float2 c = a.qc[qc];
+        qi_[fn] = c.x;
+        qs_[fn] = (METRIC == RVX_METRIC_L2) ? c.y : 0.0f;
+        qn_[fn] = (METRIC == RVX_METRIC_COSINE) ? c.y : 0.0f;
+    }
+
+    // LDS-DMA fill: 1 KB pieces of 16 rows x 64 B; lane -> (row, 16-B chunk)
+    // with the chunk XOR-swizzled by (row >> 2) & 3 on the source address, so
+    // the fragment reads below are bank-conflict free.
+    int prow[2], pchunk[2];
+    int64_t qsrc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        prow[j] = 16 * (2 * wave + j) + (lane >> 2);
+        pchunk[j] = (lane & 3) ^ ((prow[j] >> 2) & 3);
+        qsrc[j] = min(q0 + prow[j], a.nq - 1) * a.d + pchunk[j] * 8;
+    }
+    const int nk = a.d / FK;
+    const int64_t ntile = r_end > r_beg ? (r_end - r_beg + FR - 1) / FR : 0;
+    const int64_t iters = ntile * nk;
+    auto fill = [&](int64_t rt, int k0, unsigned char* dst) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int64_t rr = min(rt + prow[j], r_end - 1) - a.row0;
+            __builtin_amdgcn_global_load_lds((const void*)(a.xh + rr * a.d + k0 + pchunk[j] * 8),
+                                             (__attribute__((address_space(3))) void*)(dst + (2 * wave + j) * 1024),
+                                             16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(a.qh + qsrc[j] + k0),
+                                             (__attribute__((address_space(3))) void*)(dst + FR * 64 +
+                                                                                      (2 * wave + j) * 1024),
+                                             16, 0, 0);
+        }
+    };
+    int a_rd[2][2], b_rd[2][2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+        const int ra = wm * 64 + f * 32 + lr, rb = wn * 64 + f * 32 + lr;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            a_rd[f][ks] = ra * 64 + (((2 * ks + lh) ^ ((ra >> 2) & 3)) << 4);
+            b_rd[f][ks] = FR * 64 + rb * 64 + (((2 * ks + lh) ^ ((rb >> 2) & 3)) << 4);
+        }
+    }
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+    // Tile epilogue. The accumulators are overwritten in place by the
+    // approximate values (INF for rows past the split, deleted rows and padding
+    // queries); every value below its query's list threshold is offered, and an
+    // offered or rejected value becomes INF. Slots per query per round are
+    // bounded (FCB), so rounds repeat with the tightened thresholds until no
+    // offer overflowed (thresholds only fall, so a rejection is final).
+    auto epilogue = [&](int64_t rt, float2 pre) {
+        if (tid < FR) rowc[tid] = pre;
+        __syncthreads();
+#pragma unroll
+        for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const float2 c = rowc[wm * 64 + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh];
+                const bool rv = !__builtin_isnan(c.x);  // past the split, or deleted
+                const float xs = (METRIC == RVX_METRIC_L2) ? c.y : 0.0f;
+                const float xn = (METRIC == RVX_METRIC_COSINE) ? c.y : 0.0f;
+#pragma unroll
+                for (int fn = 0; fn < 2; ++fn)
+                    acc[fm][fn][e] = (rv && qv_[fn])
+                                         ? approx_value<METRIC>(acc[fm][fn][e], c.x, qi_[fn], xs, qs_[fn], xn, qn_[fn])
+                                         : INFINITY;
+            }
+        for (int round = 0;; ++round) {
+#pragma unroll
+            for (int fn = 0; fn < 2; ++fn) {
+                const int ql = wn * 64 + fn * 32 + lr;
+                const float t = thr[ql];
+#pragma unroll
+                for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        const float v = acc[fm][fn][e];
+                        if (!(v < t)) { acc[fm][fn][e] = INFINITY; continue; }
+                        const int slot = atomicAdd(&cand_n[ql], 1);
+                        if (slot < FCB) {
+                            cand_v[ql * FCB + slot] = v;
+                            cand_r[ql * FCB + slot] =
+                                (int32_t)(rt + wm * 64 + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh);
+                            acc[fm][fn][e] = INFINITY;
+                        } else {
+                            ovf[round & 1] = 1;
+                        }
+                    }
+            }
+            __syncthreads();
+            if (tid < FQ) {  // one lane per query: insertion into its sorted list
+                const int ql = tid;
+                const int nc = min(cand_n[ql], FCB);
+                float* bv = best_v + ql * FKP;
+                int32_t* br = best_r + ql * FKP;
+                int fill_n = fillc[ql];
+                for (int c = 0; c < nc; ++c) {
+                    const float v = cand_v[ql * FCB + c];
+                    const int32_t r = cand_r[ql * FCB + c];
+                    if (fill_n == FKP && !lt_vr(v, r, bv[FKP - 1], br[FKP - 1])) continue;
+                    int p = fill_n < FKP ? fill_n : FKP - 1;
+                    while (p > 0 && lt_vr(v, r, bv[p - 1], br[p - 1])) { bv[p] = bv[p - 1]; br[p] = br[p - 1]; --p; }
+                    bv[p] = v;
+                    br[p] = r;
+                    if (fill_n < FKP) ++fill_n;
+                }
+                fillc[ql] = fill_n;
+                cand_n[ql] = 0;
+                thr[ql] = fill_n == FKP ? bv[FKP - 1] : INFINITY;
+            }
+            if (tid == 0) ovf[(round + 1) & 1] = 0;
+            __syncthreads();
+            if (!ovf[round & 1]) break;
+        }
+    };
+
+    // Ring of F_NSTAGE stages: step it reads stage it % 3 while the DMA of
+    // steps it+1 and it+2 is in flight. Each wave issues 4 DMAs per step, so
+    // vmcnt(4) retires its share of step it; the raw barrier then publishes
+    // every wave's share (barriers do not drain VMEM; __syncthreads would).
+    // The tile epilogue's own barriers drain the ring once per 128-row tile.
+    float2 pre = make_float2(NAN, 0.0f);
+    int64_t rt = r_beg, frt = r_beg;  // current tile; tile of the next fill
+    int kt = 0, fkt = 0;              // k-step of the current step; of the next fill
+    auto advance = [&](int64_t& t, int& k) { if (++k == nk) { k = 0; t += FR; } };
+    __syncthreads();  // list init visible before the first epilogue
+    for (int64_t f = 0; f < 2 && f < iters; ++f) {
+        fill(frt, fkt * FK, fsm + f * F_STAGE);
+        advance(frt, fkt);
+    }
+    for (int64_t it = 0; it < iters; ++it) {
+        if (it + 1 < iters) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (it + 2 < iters) {  // the stage read in step it-1: every wave is past that read
+            fill(frt, fkt * FK, fsm + ((it + 2) % F_NSTAGE) * F_STAGE);
+            advance(frt, fkt);
+        }
+        if (kt == 0 && tid < FR) {  // the tile's row constants, consumed by its epilogue
+            const int64_t row = rt + tid;
+            pre = row < r_end ? a.xc[row - a.row0] : make_float2(NAN, 0.0f);
+        }
+        const unsigned char* cur = fsm + (it % F_NSTAGE) * F_STAGE;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            h16x8 af[2], bf[2];
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                af[f] = __builtin_bit_cast(h16x8, *reinterpret_cast<const u32x4*>(cur + a_rd[f][ks]));
+                bf[f] = __builtin_bit_cast(h16x8, *reinterpret_cast<const u32x4*>(cur + b_rd[f][ks]));
+            }
+#pragma unroll
+            for (int fm = 0; fm < 2; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < 2; ++fn)
+                    acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+        }
+        if (kt == nk - 1) {
+            epilogue(rt, pre);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+        }
+        advance(rt, kt);
+    }
+    __syncthreads();
+
+    for (int i = tid; i < FQ * FKP; i += 256) {
+        const int64_t qg = q0 + i / FKP;
+        if (qg >= a.nq) continue;
+        const int64_t o = (qg * a.nsplit_total + a.split0 + sl) * FKP + (i % FKP);
+        a.part_v[o] = best_v[i];
+        a.part_r[o] = best_r[i];
+    }
+}
+
+struct RerankArgs {
+    const float* q; const float* qnorm; const float2* qc;
+    const float* x; const float* xnorm;
+    int64_t nq; int d, k, nsplit_total;
+    const float* part_v; const int32_t* part_r;
+    const unsigned* xsq_max_bits;  // max_x |x|^2 (float bits)
+    int64_t id_offset;
+    float* out_d; int64_t* out_i; int32_t* unsure;
+};
+
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_scan_rerank(RerankArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (qi >= a.nq) return;
+    const int total = a.nsplit_total * FKP;
+    const float* pv = a.part_v + qi * total;
+    const int32_t* pr = a.part_r + qi * total;
+    float v[F_MAXE];
+    int32_t r[F_MAXE];
+#pragma unroll
+    for (int j = 0; j < F_MAXE; ++j) {
+        const int c = lane + 64 * j;
+        const bool ok = c < total && pr[c] >= 0;
+        v[j] = ok ? pv[c] : INFINITY;
+        r[j] = ok ? pr[c] : INT32_MAX;
+    }
+    // k-th smallest approximate value (rows are distinct across lists)
+    float lv = -INFINITY, vk = INFINITY;
+    int32_t lrow = INT32_MIN;
+    for (int s = 0; s < a.k; ++s) {
+        float bv = INFINITY;
+        int32_t brr = INT32_MAX;
+#pragma unroll
+        for (int j = 0; j < F_MAXE; ++j) {
+            const bool after = v[j] > lv || (v[j] == lv && r[j] > lrow);
+            if (after && lt_vr(v[j], r[j], bv, brr)) { bv = v[j]; brr = r[j]; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(bv, o);
+            const int32_t orr = __shfl_xor(brr, o);
+            if (lt_vr(ov, orr, bv, brr)) { bv = ov; brr = orr; }
+        }
+        lv = bv;
+        lrow = brr;
+        vk = bv;
+    }
+    float eps;
+    if (METRIC == RVX_METRIC_COSINE) {
+        eps = 0x1p-8f + 0x1p-12f;
+    } else {
+        const float xs_max = __uint_as_float(*a.xsq_max_bits);
+        const float qs = a.qc[qi].y;
+        const float qx = sqrtf(qs) * sqrtf(xs_max);
+        eps = (METRIC == RVX_METRIC_L2) ? 0x1p-8f * qx + 0x1p-12f * (qs + xs_max) : (0x1p-8f + 0x1p-12f) * qx;
+    }
+    const float D = vk + 2.0f * eps;  // INF when fewer than k rows exist
+    // a full list whose last entry is <= D may have dropped a needed row
+    bool unsure = false;
+    for (int s = lane; s < a.nsplit_total; s += 64) {
+        const int c = s * FKP + FKP - 1;
+        if (pr[c] >= 0 && pv[c] <= D) unsure = true;
+    }
+    if (__any(unsure)) {
+        if (lane == 0) a.unsure[qi] = 1;
+        return;
+    }
+    // reference distances of the candidates (one lane each, sequential order)
+    const float* qrow = a.q + qi * a.d;
+    const float qn = (METRIC == RVX_METRIC_COSINE) ? a.qnorm[qi] : 0.0f;
+    float ex[F_MAXE];
+#pragma unroll
+    for (int j = 0; j < F_MAXE; ++j) {
+        ex[j] = INFINITY;
+        if (r[j] == INT32_MAX || !(v[j] <= D)) continue;
+        const float* xr = a.x + (int64_t)r[j] * a.d;
+        float acc = 0.0f;
+        for (int kk = 0; kk < a.d; kk += 4) {
+            const float4 qv = *reinterpret_cast<const float4*>(qrow + kk);
+            const float4 xv = *reinterpret_cast<const float4*>(xr + kk);
+            acc = pair_step<METRIC>(acc, qv.x, xv.x);
+            acc = pair_step<METRIC>(acc, qv.y, xv.y);
+            acc = pair_step<METRIC>(acc, qv.z, xv.z);
+            acc = pair_step<METRIC>(acc, qv.w, xv.w);
+        }
+        ex[j] = pair_finish<METRIC>(acc, qn, (METRIC == RVX_METRIC_COSINE) ? a.xnorm[r[j]] : 0.0f);
+    }
+    float ld = -INFINITY;
+    int64_t li = INT64_MIN;
+    for (int s = 0; s < a.k; ++s) {
+        float bd = INFINITY;
+        int64_t bi = INT64_MAX;
+#pragma unroll
+        for (int j = 0; j < F_MAXE; ++j) {
+            const int64_t id = r[j] == INT32_MAX ? INT64_MAX : (int64_t)r[j] + a.id_offset;
+            if (ex[j] == INFINITY && id == INT64_MAX) continue;
+            const bool after = ex[j] > ld || (ex[j] == ld && id > li);
+            if (after && better(ex[j], id, bd, bi)) { bd = ex[j]; bi = id; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float od = __shfl_xor(bd, o);
+            const int64_t oi = __shfl_xor(bi, o);
+            if (better(od, oi, bd, bi)) { bd = od; bi = oi; }
+        }
+        if (lane == 0) { a.out_d[qi * a.k + s] = bd; a.out_i[qi * a.k + s] = bi; }
+        ld = bd;
+        li = bi;
+    }
+}
+
+// Waves stride over rows: power-of-two scale t (row max in [2^14, 2^15)),
+// f16(x*t), and the row constants {1/t, or NaN for a deleted row; cnorm[row]
+// when given (cosine) else sum x^2 (any order; only the filter uses it)}, the
+// running max of sum x^2 (one atomic per wave), and a flag for rows the filter
+// cannot bound (non-finite, |x| beyond 2^+-60).
+__global__ __launch_bounds__(256) void k_rows_to_f16(const float* __restrict__ x, int64_t n, int d,
+                                                    _Float16* __restrict__ xh, float2* __restrict__ rc,
+                                                    const float* __restrict__ cnorm, const uint8_t* __restrict__ deleted,
+                                                    unsigned* max_sq_bits, int32_t* bad) {
+    typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    float run_max = 0.0f;
+    bool run_ok = true;
+    for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += nwaves) {
+        const float* xr = x + row * d;
+        float m = 0.0f, s = 0.0f;
+        bool fin = true;
+        for (int k = 4 * lane; k < d; k += 256) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + k);
+            fin = fin && __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z) &&
+                  __builtin_isfinite(v.w);
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+            s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            m = fmaxf(m, __shfl_xor(m, o));
+            s += __shfl_xor(s, o);
+        }
+        fin = !__any(!fin);
+        const float t = h2_scale_dev(m);
+        for (int k = 4 * lane; k < d; k += 256) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + k);
+            h16x4 h = {(_Float16)(v.x * t), (_Float16)(v.y * t), (_Float16)(v.z * t), (_Float16)(v.w * t)};
+            *reinterpret_cast<h16x4*>(xh + row * d + k) = h;
+        }
+        if (lane == 0) {
+            const bool del = deleted && deleted[row];
+            rc[row] = make_float2(del ? NAN : 1.0f / t, cnorm ? cnorm[row] : s);
+        }
+        run_ok = run_ok && fin && __builtin_isfinite(s) && (m == 0.0f || (ilogbf(m) >= -60 && ilogbf(m) <= 60));
+        run_max = fmaxf(run_max, s);
+    }
+    if (lane == 0) {
+        if (!run_ok) atomicOr(bad, 1);
+        if (max_sq_bits && run_max > 0.0f) atomicMax(max_sq_bits, __float_as_uint(run_max));
+    }
+}
+
+void rows_to_f16(const float* x, int64_t n, int d, _Float16* xh, float2* rc, const float* cnorm,
+                 const uint8_t* deleted, unsigned* max_bits, int32_t* bad) {
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + 3) / 4, 4096));
+    RVX_LAUNCH("scan_f16", k_rows_to_f16, dim3((unsigned)blocks), dim3(256), 0, x, n, d, xh, rc, cnorm, deleted,
+               max_bits, bad);
+}
+
+__global__ void k_gather_rows(const float* src, const int32_t* idx, int64_t cnt, int d, float* dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cnt * d) return;
+    dst[i] = src[(int64_t)idx[i / d] * d + i % d];
+}
+
+__global__ void k_scatter_topk(const float* sd, const int64_t* si, const int32_t* idx, int64_t cnt, int k, float* dd,
+                               int64_t* di) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cnt * k) return;
+    const int64_t q = idx[i / k];
+    dd[q * k + i % k] = sd[i];
+    di[q * k + i % k] = si[i];
+}
+
+void scan_topk_valu(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
+                    const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
+                    const char* tag, float curv);
+
+// Returns false (nothing written) when the call should take the VALU scan.
+bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
+                    const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i) {
+    const int mode = env_int("RVX_SCAN_MFMA", 1);  // 0 off, 1 auto, 2 force (tests); read per call
+    if (mode == 0) return false;
+    if (metric != RVX_METRIC_L2 && metric != RVX_METRIC_COSINE && metric != RVX_METRIC_DOT) return false;
+    if (d % FK != 0 || k > FKP || n >= ((int64_t)1 << 31) - FR || nq <= 0 || n <= 0) return false;
+    if (metric == RVX_METRIC_COSINE && (!qnorm || !xnorm)) return false;
+    if (mode == 1 && (nq < 256 || n < 65536)) return false;
+    // rows converted per chunk: <= 4 GiB of f16 scratch (RVX_SCAN_MFMA_CHUNK_ROWS overrides, tests)
+    int64_t chunk_rows = env_int("RVX_SCAN_MFMA_CHUNK_ROWS", 0);
+    if (chunk_rows <= 0) chunk_rows = ((int64_t)4 << 30) / ((int64_t)d * 2);
+    chunk_rows = std::max<int64_t>(FR, std::min<int64_t>(chunk_rows, n) / FR * FR);
+    const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
+    const int64_t qtiles = (nq + FQ - 1) / FQ;
+    const int64_t max_splits = 64 * F_MAXE / FKP;  // rerank capacity
+    if (nchunks > max_splits || qtiles > 65535) return false;
+    int64_t s_c = std::max<int64_t>(1, std::min<int64_t>((2048 + qtiles - 1) / qtiles, max_splits / nchunks));
+    s_c = std::min<int64_t>(s_c, std::max<int64_t>(1, chunk_rows / (8 * FR)));  // >= 8 tiles per split
+    int64_t rows_per_split = ((chunk_rows + s_c - 1) / s_c + FR - 1) / FR * FR;
+    s_c = (chunk_rows + rows_per_split - 1) / rows_per_split;
+    const int nsplit_total = (int)(nchunks * s_c);
+
+    _Float16* qh = (_Float16*)scratch_bytes("mscan_qh", nq * d * 2);
+    float2* qc = (float2*)scratch_bytes("mscan_qc", nq * 8);
+    _Float16* xh = (_Float16*)scratch_bytes("mscan_xh", chunk_rows * d * 2);
+    float2* xc = (float2*)scratch_bytes("mscan_xc", chunk_rows * 8);
+    float* part_v = scratch_f32("mscan_part_v", nq * nsplit_total * FKP);
+    int32_t* part_r = (int32_t*)scratch_bytes("mscan_part_r", nq * nsplit_total * FKP * 4);
+    int32_t* flags = (int32_t*)scratch_bytes("mscan_flags", 16 + nq * 4);  // [0] bad, [1] max |x|^2 bits, [4..] unsure
+    unsigned* max_bits = (unsigned*)(flags + 1);
+    int32_t* unsure = flags + 4;
+    RVX_HIP(hipMemsetAsync(flags, 0, (size_t)(16 + nq * 4), stream()));
+
+    static bool attr = false;
+    if (!attr) {
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS));
+        attr = true;
+    }
+    const bool cos = metric == RVX_METRIC_COSINE;
+    rows_to_f16(q, nq, d, qh, qc, cos ? qnorm : nullptr, nullptr, nullptr, flags);
+    for (int64_t c = 0; c < nchunks; ++c) {
+        const int64_t c0 = c * chunk_rows, c1 = std::min(n, c0 + chunk_rows);
+        rows_to_f16(x + c0 * d, c1 - c0, d, xh, xc, cos ? xnorm + c0 : nullptr, deleted ? deleted + c0 : nullptr,
+                    max_bits, flags);
+        FilterArgs fa{xh, xc, qh, qc, nq, c0, c1, d, rows_per_split, (int)(c * s_c), (int)qtiles, nsplit_total,
+                      part_v, part_r};
+        const dim3 grid((unsigned)(qtiles * s_c));
+        switch (metric) {
+            case RVX_METRIC_L2: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_L2>, grid, dim3(256), F_LDS, fa); break;
+            case RVX_METRIC_COSINE: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_COSINE>, grid, dim3(256), F_LDS, fa); break;
+            default: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_DOT>, grid, dim3(256), F_LDS, fa); break;
+        }
+    }
+    RerankArgs ra{q, qnorm, qc, x, xnorm, nq, d, k, nsplit_total, part_v, part_r, max_bits, id_offset, out_d, out_i,
+                  unsure};
+    const dim3 rg((unsigned)((nq + 3) / 4));
+    switch (metric) {
+        case RVX_METRIC_L2: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_L2>, rg, dim3(256), 0, ra); break;
+        case RVX_METRIC_COSINE: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_COSINE>, rg, dim3(256), 0, ra); break;
+        default: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_DOT>, rg, dim3(256), 0, ra); break;
+    }
+    std::vector<int32_t> h(4 + nq);
+    RVX_HIP(hipMemcpyAsync(h.data(), flags, (size_t)(16 + nq * 4), hipMemcpyDeviceToHost, stream()));
+    sync();
+    if (h[0]) return false;  // unbounded inputs: the VALU scan owns the whole call
+    std::vector<int32_t> redo;
+    for (int64_t i = 0; i < nq; ++i)
+        if (h[4 + i]) redo.push_back((int32_t)i);
+    last_scan_stats().mfma_queries += nq;
+    last_scan_stats().fallback_queries += (int64_t)redo.size();
+    if (redo.empty()) return true;
+    // queries whose lists could not prove completeness: exact VALU scan
+    const int64_t cnt = (int64_t)redo.size();
+    int32_t* didx = (int32_t*)scratch_bytes("mscan_redo_idx", cnt * 4);
+    RVX_HIP(hipMemcpyAsync(didx, redo.data(), (size_t)cnt * 4, hipMemcpyHostToDevice, stream()));
+    float* rq = scratch_f32("mscan_redo_q", cnt * d);
+    float* rqn = metric == RVX_METRIC_COSINE ? scratch_f32("mscan_redo_qn", cnt) : nullptr;
+    float* rd = scratch_f32("mscan_redo_d", cnt * k);
+    int64_t* ri = (int64_t*)scratch_bytes("mscan_redo_i", cnt * k * 8);
+    RVX_LAUNCH("scan_gather", k_gather_rows, dim3((unsigned)((cnt * d + 255) / 256)), dim3(256), 0, q, didx, cnt, d, rq);
+    if (rqn)
+        RVX_LAUNCH("scan_gather", k_gather_rows, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, qnorm, didx, cnt, 1,
+                   rqn);
+    scan_topk_valu(metric, rq, rqn, cnt, x, xnorm, deleted, n, d, k, id_offset, rd, ri, "scan_fallback", 1.0f);
+    RVX_LAUNCH("scan_gather", k_scatter_topk, dim3((unsigned)((cnt * k + 255) / 256)), dim3(256), 0, rd, ri, didx, cnt,
+               k, out_d, out_i);
+    return true;
+}
+
 }  // namespace
 
 void row_norms(const float* x, int64_t n, int d, float* out) {
@@ -328,6 +887,11 @@ void row_norm_sq(const float* x, int64_t n, int d, float* out) {
     RVX_LAUNCH("row_norm_sq", k_row_norm_sq, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, x, n, d, out);
 }
 
+ScanStats& last_scan_stats() {
+    static ScanStats s;
+    return s;
+}
+
 void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
                const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
                const char* tag, float curv) {
@@ -336,6 +900,17 @@ void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const
     RVX_REQUIRE(d % 4 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)x & 15) == 0, RVX_ERR_UNSUPPORTED,
                 "scan needs dim % 4 == 0 and 16-B aligned rows");
     if (nq <= 0) return;
+    last_scan_stats() = ScanStats{};
+    if (scan_topk_mfma(metric, q, qnorm, nq, x, xnorm, deleted, n, d, k, id_offset, out_d, out_i)) return;
+    scan_topk_valu(metric, q, qnorm, nq, x, xnorm, deleted, n, d, k, id_offset, out_d, out_i, tag, curv);
+}
+
+namespace {
+void scan_topk_valu(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
+                    const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
+                    const char* tag, float curv) {
+    if (nq <= 0) return;
+    last_scan_stats().valu_queries += nq;
     const int64_t qtiles = (nq + TQ - 1) / TQ;
     int64_t nchunks = (2048 + qtiles - 1) / qtiles;
     const int64_t max_chunks = std::max<int64_t>(1, (n + TR - 1) / TR);
@@ -370,6 +945,7 @@ void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const
     RVX_LAUNCH("scan_merge", k_merge_topk, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, part_d, part_i, nq,
                (int)nchunks, k, out_d, out_i);
 }
+}  // namespace
 
 void merge_topk(const float* part_d, const int64_t* part_i, int64_t nq, int nchunks, int k, float* out_d,
                 int64_t* out_i) {

@@ -6,6 +6,12 @@ namespace rvx {
 
 constexpr int SCAN_MAX_K = 128;
 
+// Path of the most recent scan_topk call (rvx_scan_last_stats).
+struct ScanStats {
+    int64_t mfma_queries = 0, valu_queries = 0, fallback_queries = 0;
+};
+ScanStats& last_scan_stats();
+
 // Sequential-order row norms sqrt(sum x*x) (distance.rs:56-57), one per row.
 void row_norms(const float* x, int64_t n, int d, float* out);
 // Top-k (ascending (distance, id)) of every query against rows [0, n) of x.

@@ -1,0 +1,125 @@
+"""MFMA-filtered exact scan (k_scan.hip k_scan_filter + k_scan_rerank).
+
+The filter ranks rows with f16 MFMA dot products and recomputes the reference
+distance (distance.rs:34-42, :52-63, :77-78 scalar order) only for rows that can
+still be in the top-k, so FlatIndex::search / brute force results must be
+bit-identical to the oracle's flat scan (flat.rs:36-76, ties by id) and to the
+exact VALU scan — ids AND distances. RVX_SCAN_MFMA=2 forces the path at test
+sizes; RVX_SCAN_MFMA_CHUNK_ROWS forces several conversion chunks.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+rv = pytest.importorskip("ruvector_amd")
+pytestmark = pytest.mark.gpu
+
+METRICS = [(rv.DistanceMetric.Euclidean, "l2"), (rv.DistanceMetric.Cosine, "cosine"),
+           (rv.DistanceMetric.DotProduct, "dot")]
+
+
+def flat(x, metric):
+    idx = rv.FlatIndex(x.shape[1], metric)
+    idx.add_array(x, np.arange(len(x), dtype=np.uint64))
+    return idx
+
+
+def normal(n, d, seed):
+    b = rv.Buffer(n * d * 4)
+    b.fill_normal(n * d, seed)
+    return b.download(np.float32, (n, d))
+
+
+@pytest.mark.parametrize("metric,name", METRICS)
+@pytest.mark.parametrize("k", [1, 10, 16])
+def test_forced_filter_bit_exact(monkeypatch, metric, name, k):
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    n, d, nq = 20011, 64, 300
+    x = O.fill_uniform(n * d, 41).reshape(n, d)
+    q = O.fill_uniform(nq * d, 42).reshape(nq, d)
+    ids, dist = flat(x, metric).brute_force_array(q, k)
+    st = rv.scan_last_stats()
+    assert st["mfma"] == nq and st["fallback"] == 0, st
+    rids, rd = O.flat_search(x, q, k, name)
+    assert np.array_equal(ids.astype(np.int64), rids)
+    assert np.array_equal(dist, rd)
+
+
+@pytest.mark.parametrize("metric,name", METRICS)
+def test_chunked_conversion_and_flat_search(monkeypatch, metric, name):
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    monkeypatch.setenv("RVX_SCAN_MFMA_CHUNK_ROWS", "2048")  # 6 chunks, ragged last one
+    n, d, nq = 11000, 128, 257
+    x = normal(n, d, 5)
+    q = normal(nq, d, 6)
+    ids, dist, _ = flat(x, metric).search_array(q, 10)
+    assert rv.scan_last_stats()["mfma"] == nq
+    rids, rd = O.flat_search(x, q, 10, name)
+    assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd)
+
+
+def test_removed_rows_are_skipped(monkeypatch):
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    n, d = 6000, 32
+    x = O.fill_uniform(n * d, 7).reshape(n, d)
+    idx = rv.FlatIndex(d, rv.DistanceMetric.Euclidean)
+    idx.add_batch([(f"v{i}", x[i]) for i in range(n)])
+    gone = list(range(0, n, 3))
+    for i in gone:
+        assert idx.remove(f"v{i}")
+    q = x[:200]
+    ids, dist, _ = idx.search_array(q, 10)
+    deleted = np.zeros(n, np.uint8)
+    deleted[gone] = 1
+    rids, rd = O.flat_search(x, q, 10, "l2", deleted=deleted)
+    assert rv.scan_last_stats()["mfma"] == 200
+    assert np.array_equal(dist, rd)
+    # FlatIndex ids are its internal keys; map the oracle rows through the same order
+    assert np.array_equal(ids.astype(np.int64), rids)
+
+
+def test_duplicates_fall_back_and_stay_exact(monkeypatch):
+    # 40 copies of every base row: a split's list fills with equal values, so
+    # completeness cannot be proven and those queries take the exact VALU scan
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    d = 32
+    base = O.fill_uniform(150 * d, 9).reshape(150, d)
+    x = np.repeat(base, 40, axis=0)
+    q = O.fill_uniform(260 * d, 10).reshape(260, d)
+    for metric, name in METRICS:
+        ids, dist = flat(x, metric).brute_force_array(q, 12)
+        st = rv.scan_last_stats()
+        assert st["mfma"] == 260 and st["fallback"] > 0, st
+        rids, rd = O.flat_search(x, q, 12, name)
+        assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd)
+
+
+def test_unbounded_inputs_take_the_valu_scan(monkeypatch):
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    n, d = 3000, 32
+    x = O.fill_uniform(n * d, 11).reshape(n, d)
+    x[17, 3] = 3.0e30  # beyond the filter's 2^60 bound
+    q = O.fill_uniform(300 * d, 12).reshape(300, d)
+    ids, dist = flat(x, rv.DistanceMetric.Euclidean).brute_force_array(q, 10)
+    st = rv.scan_last_stats()
+    assert st["valu"] == 300, st
+    rids, rd = O.flat_search(x, q, 10, "l2")
+    assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd)
+
+
+@pytest.mark.parametrize("metric", [rv.DistanceMetric.Euclidean, rv.DistanceMetric.Cosine])
+def test_auto_mode_matches_valu_scan_at_768(monkeypatch, metric):
+    # auto mode takes the filter from 256 queries x 65536 rows; compare with the
+    # VALU kernel on the same device data (both exact), C3's dimension
+    n, d, nq = 70000, 768, 300
+    x = normal(n, d, 13)
+    q = normal(nq, d, 14)
+    idx = flat(x, metric)
+    monkeypatch.setenv("RVX_SCAN_MFMA", "1")
+    ids, dist = idx.brute_force_array(q, 10)
+    assert rv.scan_last_stats()["mfma"] == nq
+    monkeypatch.setenv("RVX_SCAN_MFMA", "0")
+    vids, vdist = idx.brute_force_array(q, 10)
+    assert rv.scan_last_stats()["valu"] == nq
+    assert np.array_equal(ids, vids) and np.array_equal(dist, vdist)
