@@ -420,14 +420,19 @@ __global__ __launch_bounds__(256, 2) void k_scan_filter(FilterArgs a) {
     const int nk = a.d / FK;
     const int64_t ntile = r_end > r_beg ? (r_end - r_beg + FR - 1) / FR : 0;
     const int64_t iters = ntile * nk;
-    auto fill = [&](int64_t rt, int k0, unsigned char* dst) {
+    const _Float16* fa[2];  // source rows of the tile being filled
+    const _Float16* fq[2] = {a.qh + qsrc[0], a.qh + qsrc[1]};
+    auto fill_tile = [&](int64_t t) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fa[j] = a.xh + (min(t + prow[j], r_end - 1) - a.row0) * a.d + pchunk[j] * 8;
+    };
+    auto fill = [&](int k0, unsigned char* dst) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            const int64_t rr = min(rt + prow[j], r_end - 1) - a.row0;
-            __builtin_amdgcn_global_load_lds((const void*)(a.xh + rr * a.d + k0 + pchunk[j] * 8),
+            __builtin_amdgcn_global_load_lds((const void*)(fa[j] + k0),
                                              (__attribute__((address_space(3))) void*)(dst + (2 * wave + j) * 1024),
                                              16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)(a.qh + qsrc[j] + k0),
+            __builtin_amdgcn_global_load_lds((const void*)(fq[j] + k0),
                                              (__attribute__((address_space(3))) void*)(dst + FR * 64 +
                                                                                       (2 * wave + j) * 1024),
                                              16, 0, 0);
@@ -532,11 +537,16 @@ __global__ __launch_bounds__(256, 2) void k_scan_filter(FilterArgs a) {
     float2 pre = make_float2(NAN, 0.0f);
     int64_t rt = r_beg, frt = r_beg;  // current tile; tile of the next fill
     int kt = 0, fkt = 0;              // k-step of the current step; of the next fill
-    auto advance = [&](int64_t& t, int& k) { if (++k == nk) { k = 0; t += FR; } };
+    int st = 0, fst = 0;              // ring stage of the current step; of the next fill
+    auto advance_fill = [&]() {
+        if (++fkt == nk) { fkt = 0; frt += FR; fill_tile(frt); }
+        fst = fst == F_NSTAGE - 1 ? 0 : fst + 1;
+    };
     __syncthreads();  // list init visible before the first epilogue
+    fill_tile(frt);
     for (int64_t f = 0; f < 2 && f < iters; ++f) {
-        fill(frt, fkt * FK, fsm + f * F_STAGE);
-        advance(frt, fkt);
+        fill(fkt * FK, fsm + fst * F_STAGE);
+        advance_fill();
     }
     for (int64_t it = 0; it < iters; ++it) {
         if (it + 1 < iters) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -544,14 +554,14 @@ __global__ __launch_bounds__(256, 2) void k_scan_filter(FilterArgs a) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (it + 2 < iters) {  // the stage read in step it-1: every wave is past that read
-            fill(frt, fkt * FK, fsm + ((it + 2) % F_NSTAGE) * F_STAGE);
-            advance(frt, fkt);
+            fill(fkt * FK, fsm + fst * F_STAGE);
+            advance_fill();
         }
         if (kt == 0 && tid < FR) {  // the tile's row constants, consumed by its epilogue
             const int64_t row = rt + tid;
             pre = row < r_end ? a.xc[row - a.row0] : make_float2(NAN, 0.0f);
         }
-        const unsigned char* cur = fsm + (it % F_NSTAGE) * F_STAGE;
+        const unsigned char* cur = fsm + st * F_STAGE;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             h16x8 af[2], bf[2];
@@ -566,7 +576,11 @@ __global__ __launch_bounds__(256, 2) void k_scan_filter(FilterArgs a) {
                 for (int fn = 0; fn < 2; ++fn)
                     acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
         }
+#ifdef RVX_ABLATE_EPI
+        if (kt == nk - 1 && it + 1 == iters) {
+#else
         if (kt == nk - 1) {
+#endif
             epilogue(rt, pre);
 #pragma unroll
             for (int i = 0; i < 2; ++i)
@@ -575,7 +589,8 @@ __global__ __launch_bounds__(256, 2) void k_scan_filter(FilterArgs a) {
 #pragma unroll
                     for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
         }
-        advance(rt, kt);
+        if (++kt == nk) { kt = 0; rt += FR; }
+        st = st == F_NSTAGE - 1 ? 0 : st + 1;
     }
     __syncthreads();
 
@@ -925,11 +940,11 @@ void scan_topk_valu(int metric, const float* q, const float* qnorm, int64_t nq, 
     const size_t lds = scan_lds_bytes(k);
     static bool attr_done = false;
     if (!attr_done) {
-        hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_done = true;
     }
     const dim3 grid((unsigned)qtiles, (unsigned)nchunks);
