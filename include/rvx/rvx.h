@@ -210,6 +210,17 @@ rvx_status rvx_gnn_forward_graph(const rvx_layer* l, const rvx_graph* g, const f
                                  float* y);
 rvx_status rvx_gnn_forward_graph_device(const rvx_layer* l, const rvx_graph* g, const rvx_buffer* x,
                                         rvx_buffer* y);
+/* Node-range-sharded RuvectorLayer forward, one process per GPU: this
+ * rank owns destination rows [offsets[rank], offsets[rank+1]) and `g` holds their CSR
+ * rows with GLOBAL column ids. x_full / y_full are [N][in] / [N][hidden] tables, of which
+ * only the owned rows of x_full are read and only the owned rows of y_full written.
+ * Phase 1 (M = w_msg(x), K|V) runs on the owned rows; their rows of M and K|V go to every
+ * peer over RCCL p2p (comm, rvx_comm_init); phase 2 (attention over neighbours, GRU,
+ * LayerNorm; layer.rs:379-418) runs on the owned rows. The next layer needs only the
+ * owned rows of y_full, so stacked layers exchange M|K|V once per layer and nothing
+ * else. comm NULL: one process, offsets {0, N}; identical to rvx_gnn_forward_graph_device. */
+rvx_status rvx_gnn_forward_exchange(const rvx_layer* l, const rvx_graph* g, const rvx_buffer* x_full,
+                                    rvx_buffer* y_full, const int64_t* offsets, rvx_comm* comm);
 
 /* RuvectorLayer::forward(node, neighbours, edge_weights) (layer.rs:379-423), batched over
  * nq independent nodes whose neighbours are rows of a resident table:

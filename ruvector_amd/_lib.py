@@ -122,6 +122,7 @@ SIGNATURES = {
     "rvx_gnn_forward_one": (None, [P, PF32, PF32, I32, PF32, I32, PF32]),
     "rvx_gnn_forward_graph": (None, [P, P, PF32, I64, PF32]),
     "rvx_gnn_forward_graph_device": (None, [P, P, P, P]),
+    "rvx_gnn_forward_exchange": (None, [P, P, P, P, PI64, P]),
     "rvx_differentiable_search_batch": (None, [PF32, I64, PF32, I32, I32, I32, F32, PI64, PF32]),
     "rvx_gnn_forward_star_device": (None, [P, P, I64, P, I64, P, I32, P, P]),
     "rvx_hnsw_last_search_stats": (None, [PI64, PI64, PI64]),

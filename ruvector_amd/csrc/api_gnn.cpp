@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstring>
 
+#include "comm.hpp"
 #include "gnn.hpp"
 #include "graph.hpp"
 #include "json.hpp"
@@ -186,31 +187,35 @@ void put_linear(std::string& s, const HostLinear& l) {
 // n_out (< 0: n): phase 2 runs for rows [0, n_out) only — the star form, whose
 // rows past n_out are neighbour-only (they feed phase 1's M and K|V); rp and y
 // then need only n_out + 1 / n_out rows.
-void forward_dev(const rvx_layer* l, int64_t n, const int64_t* rp, const int32_t* col, int64_t max_deg,
-                 const float* w, int wmode, const float* x, float* y, int64_t n_out = -1) {
+// Phase 1 for `rows` rows: M = w_msg(x) and K|V = M·[W_k;W_v]^T.
+void phase1_dev(const rvx_layer* l, int64_t rows, const float* x, float* M, float* KV) {
+    const int64_t H = l->H;
+    GemmEpilogue ep;
+    ep.bias0 = l->d_bmsg.as<float>();
+    gemm_nt(rows, (int)H, l->d_wmsg.op(x, l->in), nullptr, ep, M, H, "gnn_gemm_msg");
+    ep = GemmEpilogue();
+    ep.bias0 = l->d_bqkv.as<float>() + H;
+    gemm_nt(rows, (int)(2 * H), l->d_wqkv.op(M, H, H), nullptr, ep, KV, 2 * H, "gnn_gemm_kv");
+}
+
+// Phase 2 for destination rows [0, rows_out) of rp: neighbours index the whole
+// M / KV tables (global ids), the destination rows themselves are rows
+// self_off + r of them; y receives rows_out rows.
+void phase2_dev(const rvx_layer* l, int64_t rows_out, const int64_t* rp, const int32_t* col, int64_t max_deg,
+                const float* w, int wmode, const float* M, const float* KV, int64_t self_off, float* y) {
     const int64_t H = l->H;
     const int64_t CHUNK = std::max<int64_t>(4096, env_int("RVX_GNN_CHUNK_ROWS", 1 << 20));  // read per call
-    const int64_t rows_out = n_out < 0 ? n : std::min(n_out, n);
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(rows_out, CHUNK));
-    float* M = scratch_f32("rvl_m", n * H);
-    float* KV = scratch_f32("rvl_kv", n * 2 * H);
     float* Q = scratch_f32("rvl_q", chunk * H);
     float* S1 = scratch_f32("rvl_s1", chunk * 2 * H);
     float* S2 = scratch_f32("rvl_s2", chunk * H);
     float* S3 = scratch_f32("rvl_s3", chunk * H);
     float* S4 = scratch_f32("rvl_s4", chunk * H);
     float* scores = scratch_f32("rvl_scores", std::max<int64_t>(chunk * max_deg, 1) * l->heads);
-
     GemmEpilogue ep;
-    ep.bias0 = l->d_bmsg.as<float>();
-    gemm_nt(n, (int)H, l->d_wmsg.op(x, l->in), nullptr, ep, M, H, "gnn_gemm_msg");
-    ep = GemmEpilogue();
-    ep.bias0 = l->d_bqkv.as<float>() + H;
-    gemm_nt(n, (int)(2 * H), l->d_wqkv.op(M, H, H), nullptr, ep, KV, 2 * H, "gnn_gemm_kv");
-
     for (int64_t r0 = 0; r0 < rows_out; r0 += chunk) {
         const int64_t rows = std::min(chunk, rows_out - r0);
-        const float* Mc = M + r0 * H;
+        const float* Mc = M + (self_off + r0) * H;
         ep = GemmEpilogue();
         ep.bias0 = l->d_bqkv.as<float>();
         gemm_nt(rows, (int)H, l->d_wqkv.op(Mc, H, 0), nullptr, ep, Q, H, "gnn_gemm_q");
@@ -246,6 +251,16 @@ void forward_dev(const rvx_layer* l, int64_t n, const int64_t* rp, const int32_t
         fa.y = y + r0 * H;
         gru_finish(fa);
     }
+}
+
+void forward_dev(const rvx_layer* l, int64_t n, const int64_t* rp, const int32_t* col, int64_t max_deg,
+                 const float* w, int wmode, const float* x, float* y, int64_t n_out = -1) {
+    const int64_t H = l->H;
+    const int64_t rows_out = n_out < 0 ? n : std::min(n_out, n);
+    float* M = scratch_f32("rvl_m", n * H);
+    float* KV = scratch_f32("rvl_kv", n * 2 * H);
+    phase1_dev(l, n, x, M, KV);
+    phase2_dev(l, rows_out, rp, col, max_deg, w, wmode, M, KV, 0, y);
 }
 
 }  // namespace
@@ -455,6 +470,38 @@ rvx_status rvx_gnn_forward_graph_device(const rvx_layer* l, const rvx_graph* g, 
         RVX_REQUIRE(y->mem.bytes >= g->n * l->H * 4, RVX_ERR_DIMENSION_MISMATCH, "y smaller than n*hidden_dim");
         ComputeLock cl;
         forward_dev(l, g->n, g->row_ptr, g->col, g->max_deg, g->w, 1, x->mem.as<float>(), y->mem.as<float>());
+    });
+}
+
+rvx_status rvx_gnn_forward_exchange(const rvx_layer* l, const rvx_graph* g, const rvx_buffer* x_full,
+                                    rvx_buffer* y_full, const int64_t* offsets, rvx_comm* comm) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(l && x_full && y_full && offsets, RVX_ERR_INVALID_PARAMETER, "null argument");
+        const int world = comm_size(comm), me = comm_rank(comm);
+        for (int p = 0; p < world; ++p)
+            RVX_REQUIRE(offsets[p] >= 0 && offsets[p] <= offsets[p + 1], RVX_ERR_INVALID_PARAMETER,
+                        "offsets must be non-decreasing");
+        RVX_REQUIRE(offsets[me + 1] - offsets[me] == g->n, RVX_ERR_DIMENSION_MISMATCH,
+                    "graph rows differ from this rank's shard");
+        const int64_t N = offsets[world], o = offsets[me], H = l->H;
+        RVX_REQUIRE(x_full->mem.bytes >= N * l->in * 4, RVX_ERR_DIMENSION_MISMATCH, "x_full smaller than N*input_dim");
+        RVX_REQUIRE(y_full->mem.bytes >= N * H * 4, RVX_ERR_DIMENSION_MISMATCH, "y_full smaller than N*hidden_dim");
+        ComputeLock cl;
+        // phase 1 on the owned rows, straight into the whole-table M and K|V,
+        // then every rank's rows of both tables to every peer (one grouped
+        // p2p round each on the library stream), then phase 2 on owned rows
+        float* M = scratch_f32("rvl_m", N * H);
+        float* KV = scratch_f32("rvl_kv", N * 2 * H);
+        phase1_dev(l, g->n, x_full->mem.as<float>() + o * l->in, M + o * H, KV + o * 2 * H);
+        if (world > 1) {
+            ProfScope ps("gnn_halo_exchange");
+            std::vector<int64_t> rows(world);
+            for (int p = 0; p < world; ++p) rows[p] = offsets[p + 1] - offsets[p];
+            comm_exchange_rows(comm, M, H, offsets, rows.data(), stream());
+            comm_exchange_rows(comm, KV, 2 * H, offsets, rows.data(), stream());
+        }
+        phase2_dev(l, g->n, g->row_ptr, g->col, g->max_deg, g->w, 1, M, KV, o, y_full->mem.as<float>() + o * H);
     });
 }
 

@@ -893,11 +893,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
             if (s == 0)
                 split_h2_pair(f4_at(alo[1], ahi[1], 2 * ni), f4_at(alo[1], ahi[1], 2 * ni + 1), a_sc, w[1][0][ni],
                               w[1][1][ni]);
-            f32x16 c = acc[ni];
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], c, 0, 0, 0);
-            acc[ni] = c;
+            acc[ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[0], acc[ni], 0, 0, 0);
+            acc[ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[1], acc[ni], 0, 0, 0);
+            acc[ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[0], acc[ni], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -1109,9 +1107,9 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
     if (s1) { g.A1 = s1->A; g.lda1 = s1->lda; g.ldb1 = s1->ldb; g.K1 = s1->K; g.B1h = B1h; g.B1h_plane = (int64_t)N * s1->ldb; }
     g.bias0 = ep.bias0; g.bias1 = ep.bias1; g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.alpha = ep.alpha;
     g.a_scale = a_scale; g.b_inv = b_inv;
+    RVX_REQUIRE(gemm_h2_ok(M, N, s0, s1), RVX_ERR_INVALID_SHAPE, "shape not supported by the split-f16 GEMM");
     g.tiles_n = (N + XBN - 1) / XBN;
     g.nblocks = ((M + 127) / 128) * g.tiles_n;
-    RVX_REQUIRE(gemm_h2_ok(M, N, s0, s1), RVX_ERR_INVALID_SHAPE, "shape not supported by the split-f16 GEMM");
     RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
     constexpr int lds = 2 * (128 * 128 + 2 * XB_PLANE);
     static bool attr = false;

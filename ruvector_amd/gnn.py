@@ -90,6 +90,13 @@ class RuvectorLayer:
     def forward_graph_device(self, x: Buffer, graph: Graph, y: Buffer) -> None:
         _check("rvx_gnn_forward_graph_device", self._h, graph.handle, x.handle, y.handle)
 
+    def forward_exchange(self, local_graph: Graph, x_full: Buffer, y_full: Buffer, offsets, comm=None) -> None:
+        """Node-range-sharded forward (rvx_gnn_forward_exchange): this rank's rows of
+        y_full from its rows of x_full; M|K|V rows travel to the peers over RCCL."""
+        off = np.ascontiguousarray(np.asarray(offsets, dtype=np.int64))
+        _check("rvx_gnn_forward_exchange", self._h, local_graph.handle, x_full.handle, y_full.handle,
+               off.ctypes.data_as(C.POINTER(C.c_int64)), comm._h if comm is not None else None)
+
     def forward_star_device(self, nodes: Buffer, nq: int, table: Buffer, table_rows: int, cand_ids: Buffer, c: int,
                             weights: Optional[Buffer], out: Buffer) -> None:
         """forward(nodes[i], table[cand_ids[i]], weights[i]) for i < nq, all resident in HBM

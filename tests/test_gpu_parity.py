@@ -444,6 +444,33 @@ def test_ruvector_forward_graph_row_chunks(monkeypatch):
         assert_close(y[r0:r0 + 200], ref)
 
 
+def test_ruvector_forward_exchange_entry():
+    """rvx_gnn_forward_exchange (node-range-sharded RuvectorLayer: phase 1 on owned
+    rows into the whole-table M and K|V, p2p exchange, phase 2 on owned rows) at
+    world 1 writes the same bits as the unsharded forward; stacked twice (the
+    next layer reads only owned rows of the previous output)."""
+    n, deg, hidden, heads = 6000, 7, 64, 4
+    layer, W, _ = _layer_and_weights(hidden, hidden, heads, 0.0, seed=12)
+    rp, col = O.random_csr(n, deg, 17)
+    ew = O.fill_uniform(len(col), 18, 0.0, 1.0)
+    g = rv.Graph.from_csr(rp, col, ew)
+    x = rv.Buffer(n * hidden * 4)
+    x.fill_uniform(n * hidden, 19, -1.0, 1.0)
+    y_ref, y = rv.Buffer(n * hidden * 4), rv.Buffer(n * hidden * 4)
+    layer.forward_graph_device(x, g, y_ref)
+    layer.forward_exchange(g, x, y, [0, n])
+    a = y.download(np.float32, (n, hidden))
+    assert np.array_equal(a, y_ref.download(np.float32, (n, hidden)))
+    z_ref, z = rv.Buffer(n * hidden * 4), rv.Buffer(n * hidden * 4)
+    layer.forward_graph_device(y_ref, g, z_ref)
+    layer.forward_exchange(g, y, z, [0, n])
+    assert np.array_equal(z.download(np.float32, (n, hidden)), z_ref.download(np.float32, (n, hidden)))
+    xs = x.download(np.float32, (n, hidden))
+    assert_close(a[:300], O.rvl_forward_graph(W, xs, rp, col, ew, rows=(0, 300)))
+    with pytest.raises(rv.RvxError):  # the shard must match the graph
+        layer.forward_exchange(g, x, y, [0, n - 1])
+
+
 def test_differentiable_search_matches_oracle():
     # indices bit-exact; softmax weights within f32 tolerance (device expf vs
     # glibc expf differ by <= 1 ulp; cosine similarities are bit-exact)
