@@ -668,7 +668,10 @@ __global__ __launch_bounds__(256) void k_scan_rerank(RerankArgs a) {
         if (pr[c] >= 0 && pv[c] <= D) unsure = true;
     }
     if (__any(unsure)) {
-        if (lane == 0) a.unsure[qi] = 1;
+        if (lane == 0) {
+            a.unsure[qi] = 1;
+            atomicAdd(a.unsure - 2, 1);  // flags[2]: how many queries need the VALU scan
+        }
         return;
     }
     // reference distances of the candidates (one lane each, sequential order)
@@ -803,7 +806,7 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     // rows converted per chunk: <= 4 GiB of f16 scratch (RVX_SCAN_MFMA_CHUNK_ROWS overrides, tests)
     int64_t chunk_rows = env_int("RVX_SCAN_MFMA_CHUNK_ROWS", 0);
     if (chunk_rows <= 0) chunk_rows = ((int64_t)4 << 30) / ((int64_t)d * 2);
-    chunk_rows = std::max<int64_t>(FR, std::min<int64_t>(chunk_rows, n) / FR * FR);
+    chunk_rows = chunk_rows >= n ? (n + FR - 1) / FR * FR : std::max<int64_t>(FR, chunk_rows / FR * FR);
     const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
     const int64_t qtiles = (nq + FQ - 1) / FQ;
     const int64_t max_splits = 64 * F_MAXE / FKP;  // rerank capacity
@@ -820,7 +823,7 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     float2* xc = (float2*)scratch_bytes("mscan_xc", chunk_rows * 8);
     float* part_v = scratch_f32("mscan_part_v", nq * nsplit_total * FKP);
     int32_t* part_r = (int32_t*)scratch_bytes("mscan_part_r", nq * nsplit_total * FKP * 4);
-    int32_t* flags = (int32_t*)scratch_bytes("mscan_flags", 16 + nq * 4);  // [0] bad, [1] max |x|^2 bits, [4..] unsure
+    int32_t* flags = (int32_t*)scratch_bytes("mscan_flags", 16 + nq * 4);  // [0] bad, [1] max |x|^2 bits, [2] unsure count, [4..] unsure
     unsigned* max_bits = (unsigned*)(flags + 1);
     int32_t* unsure = flags + 4;
     RVX_HIP(hipMemsetAsync(flags, 0, (size_t)(16 + nq * 4), stream()));
@@ -855,13 +858,21 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
         case RVX_METRIC_COSINE: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_COSINE>, rg, dim3(256), 0, ra); break;
         default: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_DOT>, rg, dim3(256), 0, ra); break;
     }
-    std::vector<int32_t> h(4 + nq);
-    RVX_HIP(hipMemcpyAsync(h.data(), flags, (size_t)(16 + nq * 4), hipMemcpyDeviceToHost, stream()));
+    // flags[0] bad input, flags[2] unsure-query count: 16 B through a pinned
+    // host word; the per-query flags come down only when some query is unsure
+    static int32_t* hflags = nullptr;
+    if (!hflags) RVX_HIP(hipHostMalloc((void**)&hflags, 16, hipHostMallocDefault));
+    RVX_HIP(hipMemcpyAsync(hflags, flags, 16, hipMemcpyDeviceToHost, stream()));
     sync();
-    if (h[0]) return false;  // unbounded inputs: the VALU scan owns the whole call
+    if (hflags[0]) return false;  // unbounded inputs: the VALU scan owns the whole call
     std::vector<int32_t> redo;
-    for (int64_t i = 0; i < nq; ++i)
-        if (h[4 + i]) redo.push_back((int32_t)i);
+    if (hflags[2] > 0) {
+        std::vector<int32_t> h(nq);
+        RVX_HIP(hipMemcpyAsync(h.data(), unsure, (size_t)(nq * 4), hipMemcpyDeviceToHost, stream()));
+        sync();
+        for (int64_t i = 0; i < nq; ++i)
+            if (h[i]) redo.push_back((int32_t)i);
+    }
     last_scan_stats().mfma_queries += nq;
     last_scan_stats().fallback_queries += (int64_t)redo.size();
     if (redo.empty()) return true;
