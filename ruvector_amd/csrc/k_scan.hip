@@ -338,10 +338,16 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int FQ = 128, FR = 128, FK = 32;  // queries x rows per tile, K per stage
-constexpr int FKP = 16;                     // list length per (query, split)
-constexpr int FCB = 8;                      // candidate slots per query per merge round
+#ifndef RVX_SCAN_FKP
+#define RVX_SCAN_FKP 16
+#define RVX_SCAN_FCB 8
+#define RVX_SCAN_NSTAGE 3
+#define RVX_SCAN_BLOCKS 2
+#endif
+constexpr int FKP = RVX_SCAN_FKP;           // list length per (query, split)
+constexpr int FCB = RVX_SCAN_FCB;           // candidate slots per query per merge round
 constexpr int F_STAGE = (FR + FQ) * FK * 2;  // 16 KB: f16 rows then f16 queries, 64 B per row
-constexpr int F_NSTAGE = 3;                 // LDS-DMA ring: two k-steps in flight across the barrier
+constexpr int F_NSTAGE = RVX_SCAN_NSTAGE;   // LDS-DMA ring: F_NSTAGE - 1 k-steps in flight across the barrier
 constexpr int F_LDS = F_NSTAGE * F_STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 8;  // 74.5 KB: 2 blocks / CU
 constexpr int F_MAXE = 16;                  // rerank: list entries per lane (nsplit_total * FKP <= 64 * F_MAXE)
 
@@ -366,7 +372,7 @@ __device__ __forceinline__ float approx_value(float acc, float xi, float qi, flo
 __device__ __forceinline__ bool lt_vr(float v, int r, float bv, int br) { return v < bv || (v == bv && r < br); }
 
 template <int METRIC>
-__global__ __launch_bounds__(256, 2) void k_scan_filter(FilterArgs a) {
+__global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
     float* best_v = reinterpret_cast<float*>(fsm + F_NSTAGE * F_STAGE);  // [FQ][FKP] ascending (v, row)
     int32_t* best_r = reinterpret_cast<int32_t*>(best_v + FQ * FKP);
@@ -544,16 +550,20 @@ __global__ __launch_bounds__(256, 2) void k_scan_filter(FilterArgs a) {
     };
     __syncthreads();  // list init visible before the first epilogue
     fill_tile(frt);
-    for (int64_t f = 0; f < 2 && f < iters; ++f) {
+    for (int64_t f = 0; f < F_NSTAGE - 1 && f < iters; ++f) {
         fill(fkt * FK, fsm + fst * F_STAGE);
         advance_fill();
     }
     for (int64_t it = 0; it < iters; ++it) {
-        if (it + 1 < iters) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        {  // retire step it: later steps already issued may stay in flight (4 DMAs each)
+            const int64_t later = min((int64_t)F_NSTAGE - 2, iters - it - 1);
+            if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (it + 2 < iters) {  // the stage read in step it-1: every wave is past that read
+        if (it + F_NSTAGE - 1 < iters) {  // the stage read in step it-1: every wave is past that read
             fill(fkt * FK, fsm + fst * F_STAGE);
             advance_fill();
         }
