@@ -60,9 +60,13 @@ HostLinear make_linear(int in, int out, uint64_t seed) {
 }  // namespace
 
 namespace rvx {
-// A [rows][cols] weight on the device: f32 and its split_x3 planes.
+// A [rows][cols] weight on the device: f32, its split_x3 planes (split-bf16
+// GEMM) and its split-f16 planes with per-output-row inverse scales (gemm_auto
+// -> gemm_nt_h2). A weight paired with another in a dual GEMM shares that
+// one's column scales (joint_h2).
 struct DevWeight {
-    DevMem w, x3;
+    DevMem w, x3, h2, inv;
+    const float* inv_ptr = nullptr;
     int64_t rows = 0, cols = 0;
     void upload(const std::vector<float>& v, int64_t r, int64_t c) {
         rows = r; cols = c;
@@ -70,13 +74,28 @@ struct DevWeight {
         w.upload(v.data(), r * c * 4);
         x3.reset(std::max<int64_t>(r * c, 1) * 6);
         split_x3(w.as<float>(), r * c, x3.as<uint16_t>());
+        h2.reset(std::max<int64_t>(r * c, 1) * 4);
+        inv.reset(std::max<int64_t>(r, 1) * 4);
+        split_h2_rows(w.as<float>(), nullptr, (int)r, (int)c, h2.as<_Float16>(), nullptr, inv.as<float>());
+        inv_ptr = inv.as<float>();
     }
     // operand C = A · W[row_off : row_off+n]^T with A [M][cols] (lda)
     GemmOperand op(const float* A, int64_t lda, int64_t row_off = 0) const {
-        return GemmOperand{A, lda, w.as<float>() + row_off * cols, cols, (int)cols,
-                           x3.as<uint16_t>() + row_off * cols, rows * cols};
+        GemmOperand o{A, lda, w.as<float>() + row_off * cols, cols, (int)cols,
+                      x3.as<uint16_t>() + row_off * cols, rows * cols};
+        o.Bh = h2.as<_Float16>() + row_off * cols;
+        o.Bh_plane = rows * cols;
+        o.b_inv = inv_ptr + row_off;
+        return o;
     }
 };
+
+// Re-split a dual GEMM's two weights (same shape) with one scale per output row.
+void joint_h2(DevWeight& a, DevWeight& b) {
+    split_h2_rows(a.w.as<float>(), b.w.as<float>(), (int)a.rows, (int)a.cols, a.h2.as<_Float16>(),
+                  b.h2.as<_Float16>(), a.inv.as<float>());
+    b.inv_ptr = a.inv.as<float>();
+}
 }  // namespace rvx
 
 struct rvx_layer {
@@ -127,6 +146,8 @@ void upload_layer(rvx_layer* l) {
     l->d_wzr.upload(cat({&l->w_z.w, &l->w_r.w}), 2 * H, H); l->d_uzr.upload(cat({&l->u_z.w, &l->u_r.w}), 2 * H, H);
     upload(l->d_bwzr, cat({&l->w_z.b, &l->w_r.b})); upload(l->d_buzr, cat({&l->u_z.b, &l->u_r.b}));
     l->d_wh.upload(l->w_h.w, H, H); l->d_uh.upload(l->u_h.w, H, H);
+    joint_h2(l->d_wzr, l->d_uzr);
+    joint_h2(l->d_wh, l->d_uh);
     upload(l->d_bwh, l->w_h.b); upload(l->d_buh, l->u_h.b);
     upload(l->d_gamma, l->gamma); upload(l->d_beta, l->beta);
     sync();
@@ -192,10 +213,10 @@ void phase1_dev(const rvx_layer* l, int64_t rows, const float* x, float* M, floa
     const int64_t H = l->H;
     GemmEpilogue ep;
     ep.bias0 = l->d_bmsg.as<float>();
-    gemm_nt(rows, (int)H, l->d_wmsg.op(x, l->in), nullptr, ep, M, H, "gnn_gemm_msg");
+    gemm_auto(rows, (int)H, l->d_wmsg.op(x, l->in), nullptr, ep, M, H, "gnn_gemm_msg");
     ep = GemmEpilogue();
     ep.bias0 = l->d_bqkv.as<float>() + H;
-    gemm_nt(rows, (int)(2 * H), l->d_wqkv.op(M, H, H), nullptr, ep, KV, 2 * H, "gnn_gemm_kv");
+    gemm_auto(rows, (int)(2 * H), l->d_wqkv.op(M, H, H), nullptr, ep, KV, 2 * H, "gnn_gemm_kv");
 }
 
 // Phase 2 for destination rows [0, rows_out) of rp: neighbours index the whole
@@ -218,7 +239,7 @@ void phase2_dev(const rvx_layer* l, int64_t rows_out, const int64_t* rp, const i
         const float* Mc = M + (self_off + r0) * H;
         ep = GemmEpilogue();
         ep.bias0 = l->d_bqkv.as<float>();
-        gemm_nt(rows, (int)H, l->d_wqkv.op(Mc, H, 0), nullptr, ep, Q, H, "gnn_gemm_q");
+        gemm_auto(rows, (int)H, l->d_wqkv.op(Mc, H, 0), nullptr, ep, Q, H, "gnn_gemm_q");
 
         EdgeArgs ea;
         ea.n = rows; ea.H = (int)H; ea.heads = l->heads; ea.hd = l->hd; ea.G = edge_group_lanes((int)H, l->heads);
@@ -230,19 +251,19 @@ void phase2_dev(const rvx_layer* l, int64_t rows_out, const int64_t* rp, const i
         ep = GemmEpilogue();
         ep.bias0 = l->d_bo.as<float>();
         ep.addend = S3; ep.ld_addend = H;
-        gemm_nt(rows, (int)H, l->d_wo.op(S2, H), nullptr, ep, S4, H, "gnn_gemm_out");  // COMB
+        gemm_auto(rows, (int)H, l->d_wo.op(S2, H), nullptr, ep, S4, H, "gnn_gemm_out");  // COMB
         ep = GemmEpilogue();
         ep.bias0 = l->d_bagg.as<float>();
-        gemm_nt(rows, (int)H, l->d_wagg.op(S4, H), nullptr, ep, S2, H, "gnn_gemm_agg");  // AGG
+        gemm_auto(rows, (int)H, l->d_wagg.op(S4, H), nullptr, ep, S2, H, "gnn_gemm_agg");  // AGG
         ep = GemmEpilogue();
         ep.epi = GEMM_EPI_SIGMOID; ep.bias0 = l->d_bwzr.as<float>(); ep.bias1 = l->d_buzr.as<float>();
         const GemmOperand zr_b = l->d_uzr.op(Mc, H);
-        gemm_nt(rows, (int)(2 * H), l->d_wzr.op(S2, H), &zr_b, ep, S1, 2 * H, "gnn_gemm_zr");
+        gemm_auto(rows, (int)(2 * H), l->d_wzr.op(S2, H), &zr_b, ep, S1, 2 * H, "gnn_gemm_zr");
         mul_rows(S1 + H, 2 * H, Mc, S3, rows, (int)H);  // RH = r ⊙ h
         ep = GemmEpilogue();
         ep.epi = GEMM_EPI_TANH; ep.bias0 = l->d_bwh.as<float>(); ep.bias1 = l->d_buh.as<float>();
         const GemmOperand h_b = l->d_uh.op(S3, H);
-        gemm_nt(rows, (int)H, l->d_wh.op(S2, H), &h_b, ep, S4, H, "gnn_gemm_h");  // HT
+        gemm_auto(rows, (int)H, l->d_wh.op(S2, H), &h_b, ep, S4, H, "gnn_gemm_h");  // HT
 
         FinishArgs fa;
         fa.n = rows; fa.H = (int)H; fa.rp = rp + r0; fa.m = Mc; fa.zr = S1; fa.ht = S4;

@@ -22,6 +22,7 @@
 // prefetch of tile k+1 during the MFMAs of tile k, XCD-aware block swizzle so
 // the column tiles of one row block share an XCD's L2.
 #include "common.hpp"
+#include "graph.hpp"
 #include "kernels.hpp"
 
 namespace rvx {
@@ -1089,8 +1090,9 @@ bool gemm_h2_ok(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1) 
     if (!env_int("RVX_GEMM_H2", 1) || M <= 0 || N <= 0) return false;  // read per call: tests cover both GEMMs
     auto ok = [N](const GemmOperand& o) {
         const int64_t lim = (int64_t)1 << 31;
+        const int64_t plane = o.Bh_plane ? o.Bh_plane : (int64_t)o.ldb * N;
         return o.K % 32 == 0 && o.lda % 4 == 0 && o.ldb % 8 == 0 && aligned16(o.A) && (int64_t)128 * o.lda * 4 < lim &&
-               ((int64_t)o.ldb * N + (int64_t)XBN * o.ldb) * 2 < lim;
+               (plane + (int64_t)XBN * o.ldb) * 2 < lim;
     };
     return ok(s0) && (!s1 || ok(*s1));
 }
@@ -1103,8 +1105,11 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
     g.addend = ep.addend;
     g.ld_add = ep.ld_addend;
     g.A0 = s0.A; g.lda0 = s0.lda; g.ldb0 = s0.ldb; g.K0 = s0.K;
-    g.B0h = B0h; g.B0h_plane = (int64_t)N * s0.ldb;
-    if (s1) { g.A1 = s1->A; g.lda1 = s1->lda; g.ldb1 = s1->ldb; g.K1 = s1->K; g.B1h = B1h; g.B1h_plane = (int64_t)N * s1->ldb; }
+    g.B0h = B0h; g.B0h_plane = s0.Bh_plane ? s0.Bh_plane : (int64_t)N * s0.ldb;
+    if (s1) {
+        g.A1 = s1->A; g.lda1 = s1->lda; g.ldb1 = s1->ldb; g.K1 = s1->K; g.B1h = B1h;
+        g.B1h_plane = s1->Bh_plane ? s1->Bh_plane : (int64_t)N * s1->ldb;
+    }
     g.bias0 = ep.bias0; g.bias1 = ep.bias1; g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.alpha = ep.alpha;
     g.a_scale = a_scale; g.b_inv = b_inv;
     RVX_REQUIRE(gemm_h2_ok(M, N, s0, s1), RVX_ERR_INVALID_SHAPE, "shape not supported by the split-f16 GEMM");
@@ -1121,6 +1126,52 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
     const char* t = tag ? tag : "gemm_nt_h2";
     if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)g.nblocks), dim3(256), lds, g, ep.epi);
     else RVX_LAUNCH(t, gemm_nt_h2g<false>, dim3((unsigned)g.nblocks), dim3(256), lds, g, ep.epi);
+}
+
+namespace {
+// One wave per row: max |a| over A0's and A1's row -> h2_scale_dev.
+__global__ __launch_bounds__(256) void k_row_scale_h2(const float* __restrict__ A0, int64_t lda0, int K0,
+                                                     const float* __restrict__ A1, int64_t lda1, int K1, int64_t M,
+                                                     float* __restrict__ scale) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    float m = 0.0f;
+    const float* a0 = A0 + row * lda0;
+    for (int k = 4 * lane; k < K0; k += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(a0 + k);
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    if (A1) {
+        const float* a1 = A1 + row * lda1;
+        for (int k = 4 * lane; k < K1; k += 256) {
+            const float4 v = *reinterpret_cast<const float4*>(a1 + k);
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) scale[row] = h2_scale_dev(m);
+}
+}  // namespace
+
+void row_scale_h2(const float* A0, int64_t lda0, int K0, const float* A1, int64_t lda1, int K1, int64_t M,
+                  float* scale) {
+    if (M <= 0) return;
+    RVX_LAUNCH("gemm_row_scale", k_row_scale_h2, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, A0, lda0, K0, A1, lda1,
+               K1, M, scale);
+}
+
+void gemm_auto(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, const GemmEpilogue& ep, float* C,
+               int64_t ldc, const char* tag) {
+    const bool planes = s0.Bh && s0.b_inv && (!s1 || (s1->Bh && s1->b_inv == s0.b_inv));
+    if (planes && env_int("RVX_GNN_H2", 1) && gemm_h2_ok(M, N, s0, s1)) {  // read per call: tests cover both
+        float* scale = scratch_f32("gemm_auto_scale", M);
+        row_scale_h2(s0.A, s0.lda, s0.K, s1 ? s1->A : nullptr, s1 ? s1->lda : 0, s1 ? s1->K : 0, M, scale);
+        gemm_nt_h2(M, N, s0, s0.Bh, s1, s1 ? s1->Bh : nullptr, scale, s0.b_inv, ep, C, ldc, tag);
+        return;
+    }
+    gemm_nt(M, N, s0, s1, ep, C, ldc, tag);
 }
 
 void split_h2_rows(const float* B0, const float* B1, int N, int K, _Float16* P0, _Float16* P1, float* inv) {

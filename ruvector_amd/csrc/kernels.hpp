@@ -15,6 +15,12 @@ struct GemmOperand {
     // uint16 at Bx3 + p*Bx3_plane; selects the split-bf16 MFMA kernel
     const uint16_t* Bx3 = nullptr;
     int64_t Bx3_plane = 0;
+    // optional split-f16 planes of B (split_h2_rows): [hi][lo] f16 at
+    // Bh + p*Bh_plane, b_inv[n] = 1 / column scale; selects gemm_nt_h2 in
+    // gemm_auto (dual operands need planes split with one common column scale)
+    const _Float16* Bh = nullptr;
+    int64_t Bh_plane = 0;
+    const float* b_inv = nullptr;
 };
 // Epilogue: C = epi(alpha * acc + bias0 + bias1 + addend[row][col])
 struct GemmEpilogue {
@@ -39,6 +45,13 @@ bool gemm_h2_ok(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1);
 void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
                 const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
                 int64_t ldc, const char* tag);
+// gemm_nt_h2 when every operand carries f16 planes and the shapes allow it
+// (per-row A scales computed here, row_scale_h2), else gemm_nt.
+void gemm_auto(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, const GemmEpilogue& ep, float* C,
+               int64_t ldc, const char* tag);
+// scale[r] = power of two putting max(|A0 row r|, |A1 row r|) in [2^14, 2^15).
+void row_scale_h2(const float* A0, int64_t lda0, int K0, const float* A1, int64_t lda1, int K1, int64_t M,
+                  float* scale);
 // Common power-of-two scale t_n per row n of B0 (and B1), planes P = [hi][lo]
 // of B*t_n in f16, inv[n] = 1/t_n.
 void split_h2_rows(const float* B0, const float* B1, int N, int K, _Float16* P0, _Float16* P1, float* inv);

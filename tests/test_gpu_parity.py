@@ -408,8 +408,14 @@ def test_ruvector_json_roundtrip_is_exact():
         rv.RuvectorLayer.from_json('{"w_msg": 1}')
 
 
-@pytest.mark.parametrize("hidden,heads", [(64, 4), (768, 8)])
-def test_ruvector_forward_graph_matches_oracle(hidden, heads):
+@pytest.mark.parametrize("h2", ["1", "0"])
+@pytest.mark.parametrize("hidden,heads", [(64, 4), (768, 8), (96, 4)])
+def test_ruvector_forward_graph_matches_oracle(monkeypatch, hidden, heads, h2):
+    """RVX_GNN_H2=1 (default): the layer's GEMMs run split-f16 (gemm_auto ->
+    gemm_nt_h2, per-row A scales, weights pre-split with per-output scales, the
+    dual z|r and h GEMMs with shared scales); 0: split-bf16. Both within the
+    1e-5 bar of the oracle."""
+    monkeypatch.setenv("RVX_GNN_H2", h2)
     n, deg = 300, 12
     layer, W, _ = _layer_and_weights(hidden, hidden, heads, 0.1, seed=7)
     x = O.fill_uniform(n * hidden, 4).reshape(n, hidden)
