@@ -267,6 +267,31 @@ rvx_status rvx_edge_attention_forward_graph_device(const rvx_edge_attention* a, 
                                                    const rvx_buffer* x, const rvx_buffer* edge_feat,
                                                    rvx_buffer* y);
 
+/* DualSpaceAttention (crates/ruvector-attention/src/graph/dual_space.rs:95-293):
+ * Euclidean (scaled dot of x W_euclidean^T) and hyperbolic (-poincare_dist of
+ * project_to_ball(x W_hyperbolic^T)) scores combined as (we*e + wh*h)/temperature,
+ * stable_softmax, weighted sum of values, output projection W_out when the values
+ * have `dim` columns. Weights: the reference's LCG stream (seed 42, new():107-131). */
+typedef struct rvx_dual_attention rvx_dual_attention;
+typedef struct {                  /* DualSpaceConfig (dual_space.rs:30-50) */
+    int32_t dim;                  /* 256 */
+    float   curvature;            /* 1.0 */
+    float   euclidean_weight;     /* 0.5 */
+    float   hyperbolic_weight;    /* 0.5 */
+    float   temperature;          /* 1.0 */
+} rvx_dual_attention_config;
+rvx_status rvx_dual_attention_create(const rvx_dual_attention_config* cfg, rvx_dual_attention** out);
+rvx_status rvx_dual_attention_destroy(rvx_dual_attention* a);
+/* Attention::compute (dual_space.rs:207-268): query [dim], keys [n][dim], values
+ * [n][value_dim] (value_dim <= 1024) -> out [value_dim]. n == 0 -> RVX_ERR_INVALID_PARAMETER
+ * ("Empty keys", the reference's InvalidConfig). */
+rvx_status rvx_dual_attention_compute(const rvx_dual_attention* a, const float* query, const float* keys,
+                                      const float* values, int32_t n, int32_t value_dim, float* out);
+/* Every node of a CSR graph attends over its neighbours (keys = values = their rows
+ * of x [N][dim]); y [N][dim]; isolated rows give zeros. */
+rvx_status rvx_dual_attention_forward_graph_device(const rvx_dual_attention* a, const rvx_graph* g,
+                                                   const rvx_buffer* x, rvx_buffer* y);
+
 /* ------------------------------------------------------------------ */
 /* Vector index: VectorIndex (crates/ruvector-core/src/index.rs:11-36) */
 /*   FlatIndex (index/flat.rs) and HnswIndex (index/hnsw.rs)           */

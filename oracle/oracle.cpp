@@ -950,6 +950,94 @@ static void stable_softmax(std::vector<float>& v) {
     for (auto& x : v) x = x * inv;
 }
 
+// ============================================================ dual_space.rs
+// DualSpaceAttention::new (crates/ruvector-attention/src/graph/dual_space.rs:107-131):
+// three dim x dim matrices [out][in] from one LCG stream (seed 42), Xavier scale.
+void orc_dsa_init(int32_t dim, float* w_euc, float* w_hyp, float* w_out) {
+    const float w_scale = std::sqrt(2.0f / (float)(dim + dim));
+    uint64_t seed = 42;
+    auto rnd = [&]() {
+        seed = seed * 6364136223846793005ull + 1ull;
+        return ((float)seed / (float)UINT64_MAX - 0.5f) * 2.0f * w_scale;
+    };
+    const int64_t nn = (int64_t)dim * dim;
+    for (int64_t i = 0; i < nn; ++i) w_euc[i] = rnd();
+    for (int64_t i = 0; i < nn; ++i) w_hyp[i] = rnd();
+    for (int64_t i = 0; i < nn; ++i) w_out[i] = rnd();
+}
+
+// y_i = sum_j x_j * W[i*dim + j], sequential in j (to_euclidean / to_hyperbolic /
+// project_output, dual_space.rs:134-183)
+static std::vector<float> dsa_project(const float* x, const float* W, int dim) {
+    std::vector<float> y(dim);
+    for (int i = 0; i < dim; ++i) {
+        float s = 0.0f;
+        for (int j = 0; j < dim; ++j) s = s + x[j] * W[(int64_t)i * dim + j];
+        y[i] = s;
+    }
+    return y;
+}
+
+// project_to_ball (crates/ruvector-attention/src/hyperbolic/poincare.rs:121-132), EPS 1e-7
+static void dsa_project_to_ball(std::vector<float>& x, float c, float eps) {
+    c = std::fabs(c);
+    float ns = 0.0f;
+    for (float v : x) ns = ns + v * v;
+    const float norm_x = std::sqrt(ns);
+    const float max_norm = (1.0f / std::sqrt(c)) - eps;
+    if (norm_x < max_norm) return;
+    const float scale = max_norm / std::fmax(norm_x, 1e-7f);
+    for (auto& v : x) v = scale * v;
+}
+
+// poincare_dist (dual_space.rs:14-27)
+static float dsa_poincare_dist(const std::vector<float>& u, const std::vector<float>& v, float curvature) {
+    const float c = std::fabs(curvature);
+    const float sqrt_c = std::sqrt(c);
+    float diff_sq = 0.0f, nu = 0.0f, nv = 0.0f;
+    for (size_t i = 0; i < u.size(); ++i) { const float d = u[i] - v[i]; diff_sq = diff_sq + d * d; }
+    for (float a : u) nu = nu + a * a;
+    for (float b : v) nv = nv + b * b;
+    const float denom = std::fmax(1.0f - c * nu, 1e-7f) * std::fmax(1.0f - c * nv, 1e-7f);
+    const float arg = 1.0f + 2.0f * c * diff_sq / denom;
+    return (1.0f / sqrt_c) * std::acosh(std::fmax(arg, 1.0f));
+}
+
+// Attention::compute (dual_space.rs:207-268): n >= 1 keys (the reference errors on
+// empty keys), values of value_dim; output projection only when value_dim == dim.
+int32_t orc_dsa_compute(int32_t dim, float curvature, float euclidean_weight, float hyperbolic_weight,
+                        float temperature, const float* w_euc, const float* w_hyp, const float* w_out,
+                        const float* query, const float* keys, const float* values, int32_t n, int32_t value_dim,
+                        float* out) {
+    if (n <= 0) return -1;
+    const float scale = 1.0f / std::sqrt((float)dim);
+    const std::vector<float> q_euc = dsa_project(query, w_euc, dim);
+    std::vector<float> q_hyp = dsa_project(query, w_hyp, dim);
+    dsa_project_to_ball(q_hyp, curvature, 1e-5f);
+    std::vector<float> scores(n);
+    for (int i = 0; i < n; ++i) {
+        const std::vector<float> k_euc = dsa_project(keys + (int64_t)i * dim, w_euc, dim);
+        std::vector<float> k_hyp = dsa_project(keys + (int64_t)i * dim, w_hyp, dim);
+        dsa_project_to_ball(k_hyp, curvature, 1e-5f);
+        float dot = 0.0f;
+        for (int t = 0; t < dim; ++t) dot = dot + q_euc[t] * k_euc[t];
+        const float euc = dot * scale;
+        const float hyp = -dsa_poincare_dist(q_hyp, k_hyp, curvature);
+        scores[i] = (euclidean_weight * euc + hyperbolic_weight * hyp) / temperature;
+    }
+    stable_softmax(scores);
+    std::vector<float> o(value_dim, 0.0f);
+    for (int i = 0; i < n; ++i)
+        for (int t = 0; t < value_dim; ++t) o[t] = o[t] + scores[i] * values[(int64_t)i * value_dim + t];
+    if (value_dim == dim) {
+        const std::vector<float> p = dsa_project(o.data(), w_out, dim);
+        std::copy(p.begin(), p.end(), out);
+    } else {
+        std::copy(o.begin(), o.end(), out);
+    }
+    return value_dim;
+}
+
 // compute_with_edges (edge_featured.rs:196-258); edges nullable = zero
 // features (Attention::compute, :267-288). Returns output length.
 int32_t orc_efa_compute(int32_t node_dim, int32_t edge_dim, int32_t heads, int32_t concat, float slope,

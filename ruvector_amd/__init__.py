@@ -16,7 +16,7 @@ from .core import (DistanceMetric, FlatIndex, HnswConfig, HnswIndex, RuvectorErr
 from .gnn import (GCNLayer, GnnError, GraphSAGELayer, RuvectorLayer, aggregate, differentiable_search,
                   differentiable_search_device,  # noqa: E402
                   differentiable_search_batch, hierarchical_forward)
-from .attention import EdgeFeaturedAttention, EdgeFeaturedConfig  # noqa: E402
+from .attention import DualSpaceAttention, DualSpaceConfig, EdgeFeaturedAttention, EdgeFeaturedConfig  # noqa: E402
 from .hyperbolic import (HyperbolicError, HyperbolicHnsw, HyperbolicHnswConfig,  # noqa: E402
                          ShardedHyperbolicHnsw)
 
@@ -27,6 +27,7 @@ __all__ = [
     "DistanceMetric", "FlatIndex", "HnswConfig", "HnswIndex", "RuvectorError", "SearchResult", "batch_distances",
     "distance", "distance_matrix", "GCNLayer", "GnnError", "GraphSAGELayer", "RuvectorLayer", "aggregate",
     "differentiable_search", "differentiable_search_batch", "hierarchical_forward", "EdgeFeaturedAttention",
+    "DualSpaceAttention", "DualSpaceConfig",
     "EdgeFeaturedConfig", "HyperbolicError", "HyperbolicHnsw", "HyperbolicHnswConfig", "ShardedHyperbolicHnsw",
     "NeuralSearch", "QueryMode", "RuvectorQuery", "differentiable_search_device", "hnsw_last_search_stats", "scan_last_stats",
 ]

@@ -51,6 +51,11 @@ class EdgeAttentionConfig(C.Structure):
                 ("concat_heads", C.c_int32), ("add_self_loops", C.c_int32), ("negative_slope", C.c_float)]
 
 
+class DualAttentionConfig(C.Structure):
+    _fields_ = [("dim", C.c_int32), ("curvature", C.c_float), ("euclidean_weight", C.c_float),
+                ("hyperbolic_weight", C.c_float), ("temperature", C.c_float)]
+
+
 class HyperbolicConfig(C.Structure):
     _fields_ = [("dim", C.c_int32), ("max_connections", C.c_int32), ("max_connections_0", C.c_int32),
                 ("ef_construction", C.c_int32), ("ef_search", C.c_int32), ("level_mult", C.c_float),
@@ -133,6 +138,10 @@ SIGNATURES = {
     "rvx_edge_attention_dim": (None, [P, PI32]),
     "rvx_edge_attention_compute": (None, [P, PF32, PF32, PF32, PF32, I32, PF32]),
     "rvx_edge_attention_forward_graph_device": (None, [P, P, P, P, P]),
+    "rvx_dual_attention_create": (None, [C.POINTER(DualAttentionConfig), PP]),
+    "rvx_dual_attention_destroy": (None, [P]),
+    "rvx_dual_attention_compute": (None, [P, PF32, PF32, PF32, I32, I32, PF32]),
+    "rvx_dual_attention_forward_graph_device": (None, [P, P, P, P]),
     "rvx_index_create": (None, [C.POINTER(IndexConfig), PP]),
     "rvx_index_destroy": (None, [P]),
     "rvx_index_add_batch": (None, [P, PF32, PU64, I64]),

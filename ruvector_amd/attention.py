@@ -100,3 +100,63 @@ class EdgeFeaturedAttention:
                 self._h = None
         except Exception:
             pass
+
+
+@dataclass
+class DualSpaceConfig:
+    """DualSpaceConfig (crates/ruvector-attention/src/graph/dual_space.rs:30-50)."""
+    dim: int = 256
+    curvature: float = 1.0
+    euclidean_weight: float = 0.5
+    hyperbolic_weight: float = 0.5
+    temperature: float = 1.0
+
+
+class DualSpaceAttention:
+    """DualSpaceAttention::new (dual_space.rs:107-131: LCG seed 42 weights)."""
+
+    def __init__(self, config: DualSpaceConfig):
+        self.config = config
+        c = L.DualAttentionConfig(dim=config.dim, curvature=config.curvature,
+                                  euclidean_weight=config.euclidean_weight,
+                                  hyperbolic_weight=config.hyperbolic_weight, temperature=config.temperature)
+        h = C.c_void_p()
+        _check("rvx_dual_attention_create", C.byref(c), C.byref(h))
+        self._h = h
+
+    def dim(self) -> int:
+        return self.config.dim
+
+    def compute(self, query, keys: Sequence, values: Sequence) -> np.ndarray:
+        """Attention::compute (dual_space.rs:207-268)."""
+        q = L.f32c(query).reshape(-1)
+        if q.size != self.config.dim:
+            raise AttentionError(1, f"DimensionMismatch expected {self.config.dim} actual {q.size}")
+        n = len(keys)
+        if n == 0:
+            raise AttentionError(2, "Empty keys")
+        k = L.f32c(keys).reshape(n, -1)
+        v = L.f32c(values).reshape(len(values), -1)
+        vd = v.shape[1]
+        out = np.empty(vd, np.float32)
+        _check("rvx_dual_attention_compute", self._h, L.fptr(q), L.fptr(k), L.fptr(v), n, vd, L.fptr(out))
+        return out
+
+    def compute_with_mask(self, query, keys: Sequence, values: Sequence, mask=None) -> np.ndarray:
+        """compute_with_mask (dual_space.rs:271-291): keep the masked-in keys/values."""
+        if mask is None:
+            return self.compute(query, keys, values)
+        keep = [i for i, m in enumerate(mask) if m]
+        return self.compute(query, [keys[i] for i in keep], [values[i] for i in keep])
+
+    def forward_graph_device(self, x: Buffer, graph: Graph, y: Buffer) -> None:
+        """Every node as query, its CSR neighbours as keys = values."""
+        _check("rvx_dual_attention_forward_graph_device", self._h, graph.handle, x.handle, y.handle)
+
+    def __del__(self):
+        try:
+            if self._h:
+                L.call("rvx_dual_attention_destroy", self._h)
+                self._h = None
+        except Exception:
+            pass

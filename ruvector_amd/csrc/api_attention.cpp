@@ -17,6 +17,12 @@ struct rvx_edge_attention {
     DevMem d_wnode_x3;  // exact 3-way bf16 split of W_node (split-bf16 MFMA GEMM)
 };
 
+struct rvx_dual_attention {
+    rvx_dual_attention_config cfg{};
+    std::vector<float> w_euc, w_hyp, w_out;  // [dim][dim] = [out][in]
+    DevMem d_w[3], d_x3[3];                  // f32 and exact 3-way bf16 splits (split-bf16 GEMM)
+};
+
 namespace {
 
 void upload_vec(DevMem& d, const std::vector<float>& v) {
@@ -52,9 +58,135 @@ void transform(const rvx_edge_attention* a, const float* x, int64_t rows, float*
             nullptr, GemmEpilogue(), t, a->D, tag);
 }
 
+// C = X · W^T for one of the three DualSpaceAttention matrices (0 euc, 1 hyp, 2 out).
+void dsa_gemm(const rvx_dual_attention* a, int w, const float* x, int64_t rows, float* c, const char* tag) {
+    const int d = a->cfg.dim;
+    gemm_nt(rows, d, GemmOperand{x, d, a->d_w[w].as<float>(), d, d, a->d_x3[w].as<uint16_t>(), (int64_t)d * d},
+            nullptr, GemmEpilogue(), c, d, tag);
+}
+
+// te = x W_euc^T, th = project_to_ball(x W_hyp^T), nh = |th|^2 for `rows` rows.
+void dsa_transform(const rvx_dual_attention* a, const float* x, int64_t rows, float* te, float* th, float* nh) {
+    dsa_gemm(a, 0, x, rows, te, "dsa_transform");
+    dsa_gemm(a, 1, x, rows, th, "dsa_transform");
+    dsa_project_rows(th, rows, a->cfg.dim, a->cfg.curvature, nh);
+}
+
+DsaArgs dsa_args(const rvx_dual_attention* a) {
+    DsaArgs da;
+    da.dim = a->cfg.dim;
+    da.curvature = a->cfg.curvature;
+    da.euclidean_weight = a->cfg.euclidean_weight;
+    da.hyperbolic_weight = a->cfg.hyperbolic_weight;
+    da.temperature = a->cfg.temperature;
+    da.scale = 1.0f / std::sqrt((float)a->cfg.dim);  // DualSpaceAttention::new (dual_space.rs:109)
+    return da;
+}
+
 }  // namespace
 
 extern "C" {
+
+rvx_status rvx_dual_attention_create(const rvx_dual_attention_config* cfg, rvx_dual_attention** out) {
+    return guard([&] {
+        RVX_REQUIRE(cfg && out, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(cfg->dim > 0 && cfg->dim <= 1024, RVX_ERR_INVALID_PARAMETER, "dim must be in [1, 1024]");
+        auto a = std::make_unique<rvx_dual_attention>();
+        a->cfg = *cfg;
+        const int64_t d = cfg->dim;
+        // DualSpaceAttention::new (dual_space.rs:107-131): one LCG stream, seed 42
+        const float w_scale = std::sqrt(2.0f / (float)(d + d));
+        uint64_t seed = 42;
+        auto rnd = [&]() {
+            seed = seed * 6364136223846793005ull + 1ull;
+            return ((float)seed / (float)UINT64_MAX - 0.5f) * 2.0f * w_scale;
+        };
+        for (auto* w : {&a->w_euc, &a->w_hyp, &a->w_out}) {
+            w->resize(d * d);
+            for (auto& v : *w) v = rnd();
+        }
+        const std::vector<float>* ws[3] = {&a->w_euc, &a->w_hyp, &a->w_out};
+        for (int i = 0; i < 3; ++i) {
+            upload_vec(a->d_w[i], *ws[i]);
+            a->d_x3[i].reset(std::max<int64_t>(d * d, 1) * 6);
+            split_x3(a->d_w[i].as<float>(), d * d, a->d_x3[i].as<uint16_t>());
+        }
+        sync();
+        *out = a.release();
+    });
+}
+
+rvx_status rvx_dual_attention_destroy(rvx_dual_attention* a) {
+    return guard([&] { delete a; });
+}
+
+rvx_status rvx_dual_attention_compute(const rvx_dual_attention* a, const float* query, const float* keys,
+                                      const float* values, int32_t n, int32_t value_dim, float* out) {
+    return guard([&] {
+        RVX_REQUIRE(a && query && out, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(n > 0, RVX_ERR_INVALID_PARAMETER, "Empty keys");  // dual_space.rs:213-215
+        RVX_REQUIRE(keys && values && value_dim > 0 && value_dim <= 1024, RVX_ERR_INVALID_PARAMETER,
+                    "bad keys/values");
+        ComputeLock cl;
+        const int64_t d = a->cfg.dim;
+        float* dq = scratch_f32("dsa1_q", d);
+        float* dk = scratch_f32("dsa1_k", n * d);
+        float* dv = scratch_f32("dsa1_v", (int64_t)n * value_dim);
+        float* teq = scratch_f32("dsa1_teq", d);
+        float* thq = scratch_f32("dsa1_thq", d);
+        float* tek = scratch_f32("dsa1_tek", n * d);
+        float* thk = scratch_f32("dsa1_thk", n * d);
+        float* nh = scratch_f32("dsa1_nh", n + 1);
+        float* o1 = scratch_f32("dsa1_o1", std::max<int64_t>(value_dim, d));
+        float* o2 = scratch_f32("dsa1_o2", d);
+        auto* rp = (int64_t*)scratch_bytes("dsa1_rp", 16);
+        auto* col = (int32_t*)scratch_bytes("dsa1_col", (int64_t)n * 4);
+        std::vector<int64_t> hrp{0, n};
+        std::vector<int32_t> hcol(n);
+        for (int j = 0; j < n; ++j) hcol[j] = j;
+        RVX_HIP(hipMemcpyAsync(dq, query, (size_t)d * 4, hipMemcpyHostToDevice, stream()));
+        RVX_HIP(hipMemcpyAsync(dk, keys, (size_t)(n * d * 4), hipMemcpyHostToDevice, stream()));
+        RVX_HIP(hipMemcpyAsync(dv, values, (size_t)n * value_dim * 4, hipMemcpyHostToDevice, stream()));
+        RVX_HIP(hipMemcpyAsync(rp, hrp.data(), 16, hipMemcpyHostToDevice, stream()));
+        RVX_HIP(hipMemcpyAsync(col, hcol.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream()));
+        dsa_transform(a, dq, 1, teq, thq, nh + n);
+        dsa_transform(a, dk, n, tek, thk, nh);
+        DsaArgs da = dsa_args(a);
+        da.n = 1; da.value_dim = value_dim; da.rp = rp; da.col = col;
+        da.te_q = teq; da.th_q = thq; da.nh_q = nh + n;
+        da.te_k = tek; da.th_k = thk; da.nh_k = nh;
+        da.val = dv; da.ldv = value_dim; da.out = o1;
+        dual_space_attention(da);
+        const bool proj = value_dim == a->cfg.dim;  // dual_space.rs:263-267
+        if (proj) dsa_gemm(a, 2, o1, 1, o2, "dsa_out");
+        RVX_HIP(hipMemcpyAsync(out, proj ? o2 : o1, (size_t)value_dim * 4, hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
+rvx_status rvx_dual_attention_forward_graph_device(const rvx_dual_attention* a, const rvx_graph* g,
+                                                   const rvx_buffer* x, rvx_buffer* y) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(a && x && y, RVX_ERR_INVALID_PARAMETER, "null argument");
+        const int64_t d = a->cfg.dim, n = g->n;
+        RVX_REQUIRE(x->mem.bytes >= n * d * 4 && y->mem.bytes >= n * d * 4, RVX_ERR_DIMENSION_MISMATCH,
+                    "x / y smaller than n*dim");
+        ComputeLock cl;
+        float* te = scratch_f32("dsa_te", n * d);
+        float* th = scratch_f32("dsa_th", n * d);
+        float* nh = scratch_f32("dsa_nh", std::max<int64_t>(n, 1));
+        float* o1 = scratch_f32("dsa_o1", n * d);
+        dsa_transform(a, x->mem.as<float>(), n, te, th, nh);
+        DsaArgs da = dsa_args(a);
+        da.n = n; da.value_dim = (int)d; da.rp = g->row_ptr; da.col = g->col;
+        da.te_q = te; da.th_q = th; da.nh_q = nh;
+        da.te_k = te; da.th_k = th; da.nh_k = nh;
+        da.val = x->mem.as<float>(); da.ldv = d; da.out = o1;
+        dual_space_attention(da);
+        dsa_gemm(a, 2, o1, n, y->mem.as<float>(), "dsa_out");
+    });
+}
 
 rvx_status rvx_edge_attention_create(const rvx_edge_attention_config* cfg, rvx_edge_attention** out) {
     return guard([&] {

@@ -28,6 +28,26 @@ struct EfaArgs {
 };
 
 void edge_feat_attention(const EfaArgs& a);
+
+// DualSpaceAttention (crates/ruvector-attention/src/graph/dual_space.rs) over CSR
+// rows: query-side rows i (te_q / th_q / nh_q), key rows by col (te_k / th_k /
+// nh_k), values by col. te = x W_euclidean^T, th = project_to_ball(x W_hyperbolic^T),
+// nh = |th|^2. Isolated rows produce zeros.
+struct DsaArgs {
+    int64_t n = 0;
+    int dim = 0, value_dim = 0;
+    const int64_t* rp = nullptr;
+    const int32_t* col = nullptr;
+    const float* te_q = nullptr; const float* th_q = nullptr; const float* nh_q = nullptr;
+    const float* te_k = nullptr; const float* th_k = nullptr; const float* nh_k = nullptr;
+    const float* val = nullptr; int64_t ldv = 0;
+    float curvature = 1.0f, euclidean_weight = 0.5f, hyperbolic_weight = 0.5f, temperature = 1.0f, scale = 1.0f;
+    float* out = nullptr;     // [n][value_dim], value_dim <= 1024
+};
+void dual_space_attention(const DsaArgs& a);
+// project_to_ball (ruvector-attention hyperbolic/poincare.rs:121-132, eps 1e-5) of every
+// row in place, nh[r] = |row r|^2 after projection.
+void dsa_project_rows(float* t, int64_t rows, int dim, float curvature, float* nh);
 void differentiable_search(const float* q, int64_t nq, const float* cand, int C, int d, int k, float temperature,
                            float* sims, int64_t* out_idx, float* out_w, float* soft = nullptr);
 

@@ -215,4 +215,111 @@ void differentiable_search(const float* q, int64_t nq, const float* cand, int C,
     RVX_HIP(hipGetLastError());
 }
 
+
+namespace {
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// One wave per row: |row|, project_to_ball in place, |row|^2 after.
+__global__ __launch_bounds__(256) void k_dsa_ball(float* __restrict__ t, int64_t rows, int dim, float curvature,
+                                                 float* __restrict__ nh) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    float* x = t + r * dim;
+    float s = 0.0f;
+    for (int k = lane; k < dim; k += 64) s += x[k] * x[k];
+    s = wave_sum(s);
+    const float c = fabsf(curvature);
+    const float norm_x = sqrtf(s);
+    const float max_norm = (1.0f / sqrtf(c)) - 1e-5f;
+    if (norm_x >= max_norm) {
+        const float sc = max_norm / fmaxf(norm_x, 1e-7f);
+        float s2 = 0.0f;
+        for (int k = lane; k < dim; k += 64) {
+            const float v = sc * x[k];
+            x[k] = v;
+            s2 += v * v;
+        }
+        s = wave_sum(s2);
+    }
+    if (lane == 0) nh[r] = s;
+}
+
+// One wave per destination row: per-edge combined score (Euclidean dot * scale and
+// -poincare_dist, dual_space.rs:14-27, 160-168, 231-244; every lane holds it after
+// the wave reductions), stable_softmax (utils.rs:11-54) folded into one pass as a
+// running max with rescaled sums (non-finite scores weigh 0; no finite score ->
+// uniform weights), and the weighted sum of the value rows. value_dim <= 1024.
+constexpr int DSA_VPL = 16;  // value elements per lane
+__global__ __launch_bounds__(256) void k_dsa_rows(DsaArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const int64_t b = a.rp[i], e = a.rp[i + 1];
+    float* o = a.out + i * a.value_dim;
+    const float* teq = a.te_q + i * a.dim;
+    const float* thq = a.th_q + i * a.dim;
+    const float nq = a.nh_q[i];
+    const float c = fabsf(a.curvature);
+    float acc[DSA_VPL], plain[DSA_VPL];
+#pragma unroll
+    for (int t = 0; t < DSA_VPL; ++t) { acc[t] = 0.0f; plain[t] = 0.0f; }
+    float m = -INFINITY, sum = 0.0f;
+    for (int64_t p = b; p < e; ++p) {
+        const int64_t j = a.col[p];
+        const float* tek = a.te_k + j * a.dim;
+        const float* thk = a.th_k + j * a.dim;
+        float dot = 0.0f, diff = 0.0f;
+        for (int k = lane; k < a.dim; k += 64) {
+            dot += teq[k] * tek[k];
+            const float d = thq[k] - thk[k];
+            diff += d * d;
+        }
+        dot = wave_sum(dot);
+        diff = wave_sum(diff);
+        const float denom = fmaxf(1.0f - c * nq, 1e-7f) * fmaxf(1.0f - c * a.nh_k[j], 1e-7f);
+        const float arg = 1.0f + 2.0f * c * diff / denom;
+        const float hyp = -((1.0f / sqrtf(c)) * acoshf(fmaxf(arg, 1.0f)));
+        const float s = (a.euclidean_weight * (dot * a.scale) + a.hyperbolic_weight * hyp) / a.temperature;
+        const float* vr = a.val + j * a.ldv;
+        float w = 0.0f, r = 1.0f;
+        if (__builtin_isfinite(s)) {
+            if (s > m) { r = (m == -INFINITY) ? 0.0f : expf(m - s); m = s; w = 1.0f; }
+            else w = expf(s - m);
+        }
+        sum = sum * r + w;
+#pragma unroll
+        for (int t = 0; t < DSA_VPL; ++t) {
+            const int k = lane + 64 * t;
+            if (k < a.value_dim) {
+                const float v = vr[k];
+                acc[t] = acc[t] * r + w * v;
+                plain[t] = plain[t] + v;
+            }
+        }
+    }
+    const int64_t deg = e - b;
+    const bool uniform = m == -INFINITY || sum <= 1e-10f || !__builtin_isfinite(sum);
+#pragma unroll
+    for (int t = 0; t < DSA_VPL; ++t) {
+        const int k = lane + 64 * t;
+        if (k < a.value_dim) o[k] = deg == 0 ? 0.0f : uniform ? plain[t] * (1.0f / (float)deg) : acc[t] / sum;
+    }
+}
+}  // namespace
+
+void dsa_project_rows(float* t, int64_t rows, int dim, float curvature, float* nh) {
+    if (rows <= 0) return;
+    RVX_LAUNCH("dsa_ball", k_dsa_ball, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, t, rows, dim, curvature, nh);
+}
+
+void dual_space_attention(const DsaArgs& a) {
+    if (a.n <= 0) return;
+    RVX_LAUNCH("dsa_rows", k_dsa_rows, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, a);
+}
+
 }  // namespace rvx

@@ -54,6 +54,8 @@ _SIG = {
     "orc_cosine_similarity": (F32, [PF, PF, I64]),
     "orc_differentiable_search": (I32, [PF, PF, I32, I64, I32, F32, PI64, PF]),
     "orc_efa_init": (None, [I32, I32, I32, PF, PF, PF, PF, PF]),
+    "orc_dsa_init": (None, [I32, PF, PF, PF]),
+    "orc_dsa_compute": (I32, [I32, F32, F32, F32, F32, PF, PF, PF, PF, PF, PF, I32, I32, PF]),
     "orc_efa_compute": (I32, [I32, I32, I32, I32, F32, PF, PF, PF, PF, PF, PF, PF, PF, PF, I32, PF]),
     "orc_poincare_distance": (F32, [PF, PF, I64, F32]),
     "orc_hyp_new": (P, [I32, I32, I32, I32, I32, F32, F32, I32, U64]),
@@ -375,6 +377,29 @@ def efa_compute(node_dim, edge_dim, heads, query, keys, values, edges=None, conc
     out = np.empty(node_dim, np.float32)
     m = lib().orc_efa_compute(node_dim, edge_dim, heads, int(concat), slope, fp(wn), fp(we), fp(a_s), fp(a_d),
                               fp(a_e), fp(q), fp(k), fp(v), fp(e), n, fp(out))
+    return out[:m]
+
+
+def dsa_init(dim):
+    """DualSpaceAttention::new weights (dual_space.rs:107-131): w_euclidean, w_hyperbolic, w_out [dim][dim]."""
+    w = [np.empty(dim * dim, np.float32) for _ in range(3)]
+    lib().orc_dsa_init(dim, fp(w[0]), fp(w[1]), fp(w[2]))
+    return w
+
+
+def dsa_compute(dim, query, keys, values, curvature=1.0, euclidean_weight=0.5, hyperbolic_weight=0.5,
+                temperature=1.0):
+    """DualSpaceAttention::compute (dual_space.rs:207-268); None for empty keys (the reference's Err)."""
+    we, wh, wo = dsa_init(dim)
+    q = f32(query)
+    n = len(keys)
+    if n == 0:
+        return None
+    k = f32(keys).reshape(n, dim)
+    v = f32(values).reshape(n, -1)
+    out = np.empty(max(v.shape[1], dim), np.float32)
+    m = lib().orc_dsa_compute(dim, curvature, euclidean_weight, hyperbolic_weight, temperature, fp(we), fp(wh),
+                              fp(wo), fp(q), fp(k), fp(v), n, v.shape[1], fp(out))
     return out[:m]
 
 

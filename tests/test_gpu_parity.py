@@ -536,6 +536,68 @@ def test_edge_attention_graph_matches_per_node():
         assert_close(y[i], ref)
 
 
+@pytest.mark.parametrize("dim,n,vd,c,we,wh,t", [(64, 10, 64, 1.0, 0.5, 0.5, 1.0), (32, 5, 32, 0.5, 0.0, 1.0, 1.0),
+                                                 (32, 7, 20, 1.0, 1.0, 0.0, 0.5), (768, 24, 768, 1.0, 0.5, 0.5, 2.0)])
+def test_dual_space_attention_matches_oracle(dim, n, vd, c, we, wh, t):
+    """DualSpaceAttention::compute (dual_space.rs:207-268): GEMM projections, ball
+    projection, per-key scores, one-pass stable softmax, weighted values, output
+    projection (value_dim == dim only)."""
+    cfg = rv.DualSpaceConfig(dim=dim, curvature=c, euclidean_weight=we, hyperbolic_weight=wh, temperature=t)
+    att = rv.DualSpaceAttention(cfg)
+    # points well inside the ball: on its boundary (|u| -> 1/sqrt(c) - 1e-5 after
+    # project_to_ball) 1 - c|u|^2 ~ 2e-5 amplifies any rounding difference in |u|^2
+    # ~1e4-fold, so no f32 re-implementation meets 1e-5 there (see the boundary test)
+    q = O.fill_uniform(dim, 61 + dim, -0.05, 0.05)
+    keys = O.fill_uniform(n * dim, 62 + dim, -0.05, 0.05).reshape(n, dim)
+    vals = O.fill_uniform(n * vd, 63 + dim).reshape(n, vd)
+    got = att.compute(q, keys, vals)
+    ref = O.dsa_compute(dim, q, keys, vals, curvature=c, euclidean_weight=we, hyperbolic_weight=wh, temperature=t)
+    assert got.shape == ref.shape
+    assert_close(got, ref)
+    with pytest.raises(rv.RvxError):
+        att.compute(q, [], [])
+    masked = att.compute_with_mask(q, keys, vals, [i % 2 == 0 for i in range(n)])
+    assert_close(masked, O.dsa_compute(dim, q, keys[::2], vals[::2], curvature=c, euclidean_weight=we,
+                                       hyperbolic_weight=wh, temperature=t))
+
+
+def test_dual_space_attention_graph_matches_per_node():
+    dim, n, deg = 64, 60, 7
+    att = rv.DualSpaceAttention(rv.DualSpaceConfig(dim=dim))
+    x = O.fill_uniform(n * dim, 71, -0.1, 0.1).reshape(n, dim)
+    rp, col = O.random_csr(n, deg, 72)
+    keep = np.ones(n, bool)
+    keep[[3, 40]] = False  # isolated rows -> zeros
+    rp2 = np.concatenate([[0], np.cumsum(np.where(keep, deg, 0))]).astype(np.int64)
+    col2 = np.concatenate([col[i * deg:(i + 1) * deg] for i in range(n) if keep[i]]).astype(np.int32)
+    g = rv.Graph.from_csr(rp2, col2)
+    xb, yb = rv.Buffer.from_numpy(x), rv.Buffer(x.nbytes)
+    att.forward_graph_device(xb, g, yb)
+    y = yb.download(np.float32, x.shape)
+    assert np.all(y[3] == 0.0) and np.all(y[40] == 0.0)
+    for i in range(0, n, 5):
+        if not keep[i]:
+            continue
+        nb = col2[rp2[i]:rp2[i + 1]]
+        assert_close(y[i], O.dsa_compute(dim, x[i], x[nb], x[nb]))
+
+
+def test_dual_space_attention_ball_boundary():
+    """Inputs whose hyperbolic projections leave the ball take project_to_ball's
+    rescale branch (poincare.rs:121-132); there the Poincaré distance is
+    ill-conditioned (1 - c|u|^2 ~ 2e-5), so the bar is agreement to 2e-2 of the
+    output scale and the same ranking of keys by weight."""
+    dim, n = 64, 12
+    att = rv.DualSpaceAttention(rv.DualSpaceConfig(dim=dim))
+    q = O.fill_uniform(dim, 81, -3.0, 3.0)
+    keys = O.fill_uniform(n * dim, 82, -3.0, 3.0).reshape(n, dim)
+    vals = np.eye(n, dtype=np.float32)  # value_dim != dim: the output is the weight vector itself
+    got = att.compute(q, keys, vals)
+    ref = O.dsa_compute(dim, q, keys, vals)
+    assert rel_err(got, ref) < 2e-2
+    assert np.array_equal(np.argsort(-got, kind="stable")[:3], np.argsort(-ref, kind="stable")[:3])
+
+
 # ------------------------------------------------------------------ Poincaré
 def test_poincare_distance_matrix():
     d = 32

@@ -176,6 +176,43 @@ def test_edge_featured_lcg_init_first_value():
     assert wn[0] == np.float32(np.float32(r * np.float32(2.0)) * node_scale)
 
 
+# ---- crates/ruvector-attention/src/graph/dual_space.rs:296-411 --------------
+def test_dual_space_reference_cases():
+    # test_dual_space_basic, test_euclidean_dominant, test_hyperbolic_dominant
+    assert O.dsa_compute(64, [0.1] * 64, [[0.1] * 64] * 10, [[1.0] * 64] * 10).shape == (64,)
+    assert O.dsa_compute(32, [0.5] * 32, [[0.3] * 32] * 5, [[1.0] * 32] * 5, euclidean_weight=1.0,
+                         hyperbolic_weight=0.0).shape == (32,)
+    assert O.dsa_compute(32, [0.1] * 32, [[0.1] * 32] * 5, [[1.0] * 32] * 5, curvature=0.5, euclidean_weight=0.0,
+                         hyperbolic_weight=1.0).shape == (32,)
+    # empty keys: the reference's Err(InvalidConfig("Empty keys"))
+    assert O.dsa_compute(16, [0.5] * 16, [], []) is None
+
+
+def test_dual_space_temperature_and_identical_keys():
+    # test_temperature_scaling: both compute; identical keys -> uniform weights, so the
+    # pre-projection output is the values' mean and value_dim != dim skips the projection
+    k2 = [[0.8] * 16, [0.2] * 16]
+    v2 = [[1.0] * 16, [0.0] * 16]
+    lo = O.dsa_compute(16, [0.5] * 16, k2, v2, temperature=0.5)
+    hi = O.dsa_compute(16, [0.5] * 16, k2, v2, temperature=2.0)
+    assert lo.shape == hi.shape == (16,) and np.all(np.isfinite(lo)) and np.all(np.isfinite(hi))
+    vals = [[1.0, 2.0, 3.0], [3.0, 4.0, 5.0]]
+    out = O.dsa_compute(8, [0.2] * 8, [[0.3] * 8] * 2, vals)
+    assert np.allclose(out, [2.0, 3.0, 4.0], atol=1e-6)
+
+
+def test_dual_space_lcg_init():
+    we, wh, wo = O.dsa_init(4)
+    w_scale = np.float32(math.sqrt(np.float32(2.0) / np.float32(8)))
+    seed = 42
+    vals = []
+    for _ in range(3 * 16):
+        seed = (seed * 6364136223846793005 + 1) % (1 << 64)
+        r = np.float32(np.float32(seed) / np.float32(2.0 ** 64)) - np.float32(0.5)
+        vals.append(np.float32(np.float32(r * np.float32(2.0)) * w_scale))
+    assert np.array_equal(np.concatenate([we, wh, wo]), np.array(vals, np.float32))
+
+
 # ---- crates/ruvector-hyperbolic-hnsw/tests/math_tests.rs:84-130 ------------
 def test_poincare_metric_properties():
     rng = np.random.default_rng(1)
