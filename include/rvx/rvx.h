@@ -52,7 +52,9 @@ enum {
     RVX_METRIC_COSINE = 1,    /* Cosine     -> distance.rs:47-64  */
     RVX_METRIC_DOT = 2,       /* DotProduct -> distance.rs:68-80  */
     RVX_METRIC_L1 = 3,        /* Manhattan  -> distance.rs:84-86  */
-    RVX_METRIC_POINCARE = 4   /* poincare_distance (curvature c)  */
+    RVX_METRIC_POINCARE = 4,  /* poincare_distance (curvature c)  */
+    RVX_METRIC_HYP_L2 = 5     /* HyperbolicHnsw DistanceMetric::Euclidean: sqrt of fused_norms'
+                                 chunked |a-b|^2 (ruvector-hyperbolic-hnsw hnsw.rs:182-185) */
 };
 
 /* ------------------------------------------------------------------ */
@@ -429,7 +431,7 @@ rvx_status rvx_distance_matrix(int32_t metric, const float* q, int64_t nq, const
 /* (crates/ruvector-hyperbolic-hnsw/src/hnsw.rs:127-528, tangent.rs)   */
 /* ------------------------------------------------------------------ */
 typedef struct rvx_hyperbolic rvx_hyperbolic;
-typedef struct {                 /* HyperbolicHnswConfig (hnsw.rs:36-72), metric Poincaré */
+typedef struct {                 /* HyperbolicHnswConfig (hnsw.rs:36-72), metric Poincaré or Euclidean */
     int32_t dim;
     int32_t max_connections;     /* M, 16 */
     int32_t max_connections_0;   /* M0 at layer 0, 32 (<= 64) */
@@ -439,6 +441,7 @@ typedef struct {                 /* HyperbolicHnswConfig (hnsw.rs:36-72), metric
     float   curvature;           /* 1.0, > 0 */
     int32_t prune_factor;        /* 10: search_with_pruning keeps k * prune_factor (<= 128) */
     uint64_t seed;               /* level draws (the reference uses rand::random) */
+    int32_t metric;              /* RVX_METRIC_POINCARE (default) or RVX_METRIC_HYP_L2 (DistanceMetric::Euclidean) */
 } rvx_hyperbolic_config;
 /* HyperbolicHnswConfig::default() with dim = 0 (set it). */
 void rvx_hyperbolic_default_config(rvx_hyperbolic_config* cfg);

@@ -171,13 +171,14 @@ struct OHyp {
     int64_t entry = -1;
     int max_level = 0;
     bool has_cache = false;
+    bool euclid = false;                        // DistanceMetric::Euclidean (hnsw.rs:182-185)
     std::vector<float> centroid, tangent;       // tangent [n][d]
 
     const float* v(int64_t i) const { return data.data() + i * d; }
     float dist(const float* a, const float* b) const {
         float ds, na, nb;
         fused_norms(a, b, d, ds, na, nb);
-        return from_norms(ds, na, nb, c);
+        return euclid ? std::sqrt(ds) : from_norms(ds, na, nb, c);
     }
 };
 
@@ -301,6 +302,8 @@ void* orc_hyp_new(int32_t d, int32_t M, int32_t M0, int32_t efc, int32_t efs, fl
     return h;
 }
 void orc_hyp_free(void* hp) { delete static_cast<OHyp*>(hp); }
+// HyperbolicHnswConfig.metric: 0 Poincaré, 1 Euclidean (hnsw.rs:23-32, 173-185)
+void orc_hyp_set_metric(void* hp, int32_t euclid) { static_cast<OHyp*>(hp)->euclid = euclid != 0; }
 int64_t orc_hyp_len(void* hp) { return (int64_t)static_cast<OHyp*>(hp)->level.size(); }
 
 void orc_hyp_insert(void* hp, const float* vecs, int64_t n) {

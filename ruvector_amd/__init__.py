@@ -17,7 +17,7 @@ from .gnn import (GCNLayer, GnnError, GraphSAGELayer, RuvectorLayer, aggregate, 
                   differentiable_search_device,  # noqa: E402
                   differentiable_search_batch, hierarchical_forward)
 from .attention import DualSpaceAttention, DualSpaceConfig, EdgeFeaturedAttention, EdgeFeaturedConfig  # noqa: E402
-from .hyperbolic import (HyperbolicError, HyperbolicHnsw, HyperbolicHnswConfig,  # noqa: E402
+from .hyperbolic import (DualSpaceIndex, HyperbolicError, HyperbolicHnsw, HyperbolicHnswConfig,  # noqa: E402
                          ShardedHyperbolicHnsw)
 
 from .query import NeuralSearch, QueryMode, RuvectorQuery  # noqa: E402
@@ -29,6 +29,7 @@ __all__ = [
     "differentiable_search", "differentiable_search_batch", "hierarchical_forward", "EdgeFeaturedAttention",
     "DualSpaceAttention", "DualSpaceConfig",
     "EdgeFeaturedConfig", "HyperbolicError", "HyperbolicHnsw", "HyperbolicHnswConfig", "ShardedHyperbolicHnsw",
+    "DualSpaceIndex",
     "NeuralSearch", "QueryMode", "RuvectorQuery", "differentiable_search_device", "hnsw_last_search_stats", "scan_last_stats",
 ]
 __version__ = "0.1.0"

@@ -25,7 +25,7 @@ STATUS_NAMES = {
     6: "DeviceError", 7: "OutOfMemory", 8: "Unsupported", 9: "Serialization", 10: "CommError", 11: "NotFound",
 }
 
-METRIC_L2, METRIC_COSINE, METRIC_DOT, METRIC_L1, METRIC_POINCARE = 0, 1, 2, 3, 4
+METRIC_L2, METRIC_COSINE, METRIC_DOT, METRIC_L1, METRIC_POINCARE, METRIC_HYP_L2 = 0, 1, 2, 3, 4, 5
 INDEX_FLAT, INDEX_HNSW = 0, 1
 AGG_SUM, AGG_MEAN, AGG_MAX = 0, 1, 2
 SAGE_MEAN, SAGE_MAXPOOL, SAGE_LSTM = 0, 1, 2
@@ -59,7 +59,8 @@ class DualAttentionConfig(C.Structure):
 class HyperbolicConfig(C.Structure):
     _fields_ = [("dim", C.c_int32), ("max_connections", C.c_int32), ("max_connections_0", C.c_int32),
                 ("ef_construction", C.c_int32), ("ef_search", C.c_int32), ("level_mult", C.c_float),
-                ("curvature", C.c_float), ("prune_factor", C.c_int32), ("seed", C.c_uint64)]
+                ("curvature", C.c_float), ("prune_factor", C.c_int32), ("seed", C.c_uint64),
+                ("metric", C.c_int32)]
 
 
 class HnswGraph(C.Structure):

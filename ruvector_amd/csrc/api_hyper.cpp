@@ -80,7 +80,11 @@ void search_dev(const rvx_hyperbolic* h, const float* dq, int64_t nq, int k, int
         return;
     }
     if (mode == 1) {
-        poincare_topk(dq, nq, ix->vecs.as<float>(), ix->n, d, ix->curv, k, rd, rows);
+        if (ix->cfg.metric == RVX_METRIC_POINCARE)
+            poincare_topk(dq, nq, ix->vecs.as<float>(), ix->n, d, ix->curv, k, rd, rows);
+        else  // DistanceMetric::Euclidean: the same tiled scan, sqrt of the chunked |q-x|^2
+            scan_topk(RVX_METRIC_HYP_L2, dq, nullptr, nq, ix->vecs.as<float>(), nullptr, nullptr, ix->n, d, k, 0, rd,
+                      rows, "hyp_brute_force");
         if (counts) {
             std::vector<int32_t> c((size_t)nq, (int32_t)std::min<int64_t>(k, ix->n));
             RVX_HIP(hipMemcpyAsync(counts, c.data(), (size_t)nq * 4, hipMemcpyHostToDevice, stream()));
@@ -89,6 +93,8 @@ void search_dev(const rvx_hyperbolic* h, const float* dq, int64_t nq, int k, int
     } else if (mode == 2) {
         // search_with_pruning (hnsw.rs:440-483): tangent-space L2 scan of every
         // point, keep k * prune_factor, exact Poincaré re-rank
+        RVX_REQUIRE(ix->cfg.metric == RVX_METRIC_POINCARE, RVX_ERR_UNSUPPORTED,
+                    "search_with_pruning is implemented for the Poincaré metric");
         const int nc = (int)std::min<int64_t>((int64_t)k * h->cfg.prune_factor, ix->n);
         RVX_REQUIRE(nc <= SCAN_MAX_K, RVX_ERR_UNSUPPORTED, "k * prune_factor must be <= 128");
         float* qt = scratch_f32("hyp_qt", nq * d);
@@ -166,6 +172,8 @@ void check_cfg(const rvx_hyperbolic_config* c) {
                 RVX_ERR_INVALID_PARAMETER, "ef out of range");
     RVX_REQUIRE(c->curvature > 0.0f, RVX_ERR_INVALID_PARAMETER, "invalid curvature (must be > 0)");
     RVX_REQUIRE(c->level_mult > 0.0f && c->prune_factor >= 1, RVX_ERR_INVALID_PARAMETER, "bad level_mult / prune_factor");
+    RVX_REQUIRE(c->metric == RVX_METRIC_POINCARE || c->metric == RVX_METRIC_HYP_L2, RVX_ERR_UNSUPPORTED,
+                "HyperbolicHnsw metric must be Poincare or Euclidean");
 }
 
 }  // namespace
@@ -183,6 +191,7 @@ void rvx_hyperbolic_default_config(rvx_hyperbolic_config* c) {
     c->curvature = 1.0f;
     c->prune_factor = 10;
     c->seed = 0;
+    c->metric = RVX_METRIC_POINCARE;
 }
 
 rvx_status rvx_hyperbolic_create(const rvx_hyperbolic_config* cfg, rvx_hyperbolic** out) {
@@ -194,7 +203,7 @@ rvx_status rvx_hyperbolic_create(const rvx_hyperbolic_config* cfg, rvx_hyperboli
         rvx_index& ix = h->ix;
         ix.cfg.kind = RVX_INDEX_HNSW;
         ix.cfg.dim = cfg->dim;
-        ix.cfg.metric = RVX_METRIC_POINCARE;
+        ix.cfg.metric = cfg->metric;  // Poincaré or DistanceMetric::Euclidean (hnsw.rs:173-185)
         ix.cfg.m = cfg->max_connections;
         ix.cfg.ef_construction = cfg->ef_construction;
         ix.cfg.ef_search = cfg->ef_search;

@@ -88,6 +88,7 @@ template <int METRIC, bool Q_GLOBAL = false>
 __device__ __forceinline__ float row_dist(const float* __restrict__ qs, const float* __restrict__ x, int d, float qn,
                                           float xn, float curv = 1.0f) {
     if constexpr (METRIC == RVX_METRIC_POINCARE) return pdev::hyp_dist(qs, x, d, curv);
+    if constexpr (METRIC == RVX_METRIC_HYP_L2) return pdev::hyp_l2(qs, x, d);
     float acc = 0.0f;
     if ((d & 3) == 0) {
         acc = stream_acc<METRIC, Q_GLOBAL>(qs, x, d >> 2);

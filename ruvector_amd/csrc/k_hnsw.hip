@@ -55,7 +55,7 @@ __global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
     const int lane = threadIdx.x;
     const int ef = a.ef;
     const int ccap = ef + C_EXTRA;
-    constexpr bool COOP_OK = METRIC != RVX_METRIC_POINCARE;
+    constexpr bool COOP_OK = METRIC != RVX_METRIC_POINCARE && METRIC != RVX_METRIC_HYP_L2;
     const bool coop = COOP_OK && a.coop;
     unsigned char* wst = lds_raw;                                // [WD_LDS] distance stages (coop)
     float* qs = reinterpret_cast<float*>(lds_raw + (coop ? WD_LDS : 0));  // [d rounded to 4]
@@ -201,7 +201,7 @@ bool hnsw_coop(int metric, int d, int64_t rows) {
     // 0 off, 1 auto (tables past the per-CU translation reach), 2 always
     const int mode = env_int("RVX_HNSW_COOP", 1);  // read per launch: tests force both paths
     const int64_t min_bytes = (int64_t)env_int("RVX_HNSW_COOP_MIN_MB", 4096) << 20;
-    if (!mode || metric == RVX_METRIC_POINCARE || !wave_dist_ok(d)) return false;
+    if (!mode || metric == RVX_METRIC_POINCARE || metric == RVX_METRIC_HYP_L2 || !wave_dist_ok(d)) return false;
     return mode == 2 || rows * (int64_t)d * 4 >= min_bytes;
 }
 
@@ -236,6 +236,7 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_HYP_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     const char* t = tag ? tag : "hnsw_search";
@@ -245,6 +246,7 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         case RVX_METRIC_DOT: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, a); break;
         case RVX_METRIC_L1: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
         case RVX_METRIC_POINCARE: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_POINCARE>, dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_HYP_L2: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_HYP_L2>, dim3(nslots), dim3(64), lds, a); break;
         default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by HNSW search");
     }
     int st[32] = {0};

@@ -99,9 +99,9 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
             }
             float dd = INFINITY;
             bool coop = false;
-            if constexpr (METRIC != RVX_METRIC_POINCARE) coop = a.coop != 0;
+            if constexpr (METRIC != RVX_METRIC_POINCARE && METRIC != RVX_METRIC_HYP_L2) coop = a.coop != 0;
             if (coop) {
-                if constexpr (METRIC != RVX_METRIC_POINCARE) {
+                if constexpr (METRIC != RVX_METRIC_POINCARE && METRIC != RVX_METRIC_HYP_L2) {
                     if (__ballot(fresh)) {
                         const int row = fresh ? nid : -1;
                         const float dv = wave_dist<METRIC>(qs, a.x, a.d, row, qn,
@@ -338,6 +338,7 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
         hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_HYP_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     switch (metric) {
@@ -346,6 +347,9 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
         case RVX_METRIC_L1: RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
         case RVX_METRIC_POINCARE:
             RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_POINCARE>, dim3(nslots), dim3(64), lds, a);
+            break;
+        case RVX_METRIC_HYP_L2:
+            RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_HYP_L2>, dim3(nslots), dim3(64), lds, a);
             break;
         default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by the GPU HNSW build");
     }

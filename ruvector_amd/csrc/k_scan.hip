@@ -44,6 +44,7 @@ __device__ __forceinline__ float pair_finish(float acc, float qn, float xn, floa
     // Poincaré: acc = |q-x|^2 in fused_norms' chunked order, qn/xn = squared
     // norms in the same order (norm_squared == fused_norms' own norm sums)
     if (METRIC == RVX_METRIC_POINCARE) return pdev::from_norms(acc, qn, xn, curv);
+    if (METRIC == RVX_METRIC_HYP_L2) return sqrtf(acc);  // fused_norms' chunked |q-x|^2
     if (METRIC == RVX_METRIC_L2) return sqrtf(acc);
     if (METRIC == RVX_METRIC_DOT) return -acc;
     if (METRIC == RVX_METRIC_COSINE) return (qn > 1e-8f && xn > 1e-8f) ? 1.0f - acc / (qn * xn) : 1.0f;
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
                     for (int i = 0; i < 4; ++i)
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            if constexpr (METRIC == RVX_METRIC_POINCARE) {  // one 4-wide chunk of fused_norms
+                            if constexpr (METRIC == RVX_METRIC_POINCARE || METRIC == RVX_METRIC_HYP_L2) {  // one 4-wide chunk of fused_norms
                                 const float d0 = qv[i].x - xv[j].x, d1 = qv[i].y - xv[j].y;
                                 const float d2 = qv[i].z - xv[j].z, d3 = qv[i].w - xv[j].w;
                                 acc[i][j] = acc[i][j] + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
@@ -147,7 +148,7 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
                             }
                         }
                 }
-            } else if (METRIC == RVX_METRIC_POINCARE) {  // tail tile: whole chunks, then a sequential remainder
+            } else if (METRIC == RVX_METRIC_POINCARE || METRIC == RVX_METRIC_HYP_L2) {  // tail tile: whole chunks, then a sequential remainder
                 int kk = 0;
                 for (; kk + 4 <= kc; kk += 4) {
 #pragma unroll
@@ -966,6 +967,7 @@ void scan_topk_valu(int metric, const float* q, const float* qnorm, int64_t nq, 
         RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_HYP_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_done = true;
     }
     const dim3 grid((unsigned)qtiles, (unsigned)nchunks);
@@ -976,6 +978,7 @@ void scan_topk_valu(int metric, const float* q, const float* qnorm, int64_t nq, 
         case RVX_METRIC_DOT: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_DOT>, grid, dim3(256), lds, a); break;
         case RVX_METRIC_L1: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_L1>, grid, dim3(256), lds, a); break;
         case RVX_METRIC_POINCARE: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_POINCARE>, grid, dim3(256), lds, a); break;
+        case RVX_METRIC_HYP_L2: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_HYP_L2>, grid, dim3(256), lds, a); break;
         default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by the flat scan");
     }
     RVX_LAUNCH("scan_merge", k_merge_topk, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, part_d, part_i, nq,

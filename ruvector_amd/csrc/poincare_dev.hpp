@@ -69,6 +69,14 @@ __host__ __device__ inline float hyp_dist(const float* a, const float* b, int d,
     return from_norms(ds, na, nb, c);
 }
 
+// HyperbolicHnsw::distance for DistanceMetric::Euclidean (hnsw.rs:182-185):
+// sqrt of fused_norms' chunked |a-b|^2
+__host__ __device__ inline float hyp_l2(const float* a, const float* b, int d) {
+    float ds, na, nb;
+    fused3(a, b, d, ds, na, nb);
+    return sqrtf(ds);
+}
+
 // project_to_ball_inplace (:189-203)
 __host__ __device__ inline void project_inplace(float* x, int d, float c, float eps) {
     c = fmaxf(fabsf(c), EPS);

@@ -33,7 +33,8 @@ def _check(name, *args):
 
 @dataclass
 class HyperbolicHnswConfig:
-    """HyperbolicHnswConfig (hnsw.rs:36-72), Poincaré metric."""
+    """HyperbolicHnswConfig (hnsw.rs:36-72). metric: "poincare" (default) or "euclidean"
+    (DistanceMetric::Euclidean: sqrt of fused_norms' chunked |a-b|^2, hnsw.rs:182-185)."""
     max_connections: int = 16
     max_connections_0: int = 32
     ef_construction: int = 200
@@ -43,6 +44,7 @@ class HyperbolicHnswConfig:
     prune_factor: int = 10
     use_tangent_pruning: bool = True
     seed: int = 0
+    metric: str = "poincare"
 
 
 @dataclass(frozen=True)
@@ -70,7 +72,8 @@ class HyperbolicHnsw:
         cfg = L.HyperbolicConfig(dim=int(dim), max_connections=c.max_connections,
                                  max_connections_0=c.max_connections_0, ef_construction=c.ef_construction,
                                  ef_search=c.ef_search, level_mult=c.level_mult, curvature=c.curvature,
-                                 prune_factor=c.prune_factor, seed=c.seed)
+                                 prune_factor=c.prune_factor, seed=c.seed,
+                                 metric=L.METRIC_HYP_L2 if c.metric == "euclidean" else L.METRIC_POINCARE)
         h = C.c_void_p()
         _check("rvx_hyperbolic_create", C.byref(cfg), C.byref(h))
         self._h, self._dim = h, int(dim)
@@ -255,3 +258,49 @@ class ShardedHyperbolicHnsw:
     def search(self, query, k: int) -> List[Tuple[int, SearchResult]]:
         ids, d = self.search_batch(np.asarray(query, np.float32).reshape(1, -1), k)
         return [(int(i), SearchResult(int(i), float(x))) for i, x in zip(ids[0], d[0]) if i >= 0]
+
+
+class DualSpaceIndex:
+    """DualSpaceIndex (crates/ruvector-hyperbolic-hnsw/src/hnsw.rs:536-605): a Poincaré
+    HyperbolicHnsw (primary) and a Euclidean-metric twin over the same inserted vectors,
+    searched for 2k each and fused by reciprocal rank: score(id) = w / (rank_h + 1) +
+    (1 - w) / (rank_e + 1) in f32, highest first, then the top k re-scored with the
+    Poincaré distance of the raw query to the stored vector. Ties in the fused score
+    are ordered by first appearance (hyperbolic ranks, then Euclidean-only ids); the
+    reference leaves them in HashMap order."""
+
+    def __init__(self, curvature: float, fusion_weight: float, seed: int = 0):
+        self.hyperbolic = HyperbolicHnsw(HyperbolicHnswConfig(curvature=curvature, seed=seed))
+        self.euclidean = HyperbolicHnsw(HyperbolicHnswConfig(metric="euclidean", seed=seed))
+        self.fusion_weight = float(np.float32(min(max(fusion_weight, 0.0), 1.0)))
+
+    def insert(self, vector: Sequence[float]) -> int:
+        self.euclidean.insert(vector)
+        return self.hyperbolic.insert(vector)
+
+    def insert_batch(self, vectors) -> List[int]:
+        self.euclidean.insert_batch(vectors)
+        return self.hyperbolic.insert_batch(vectors)
+
+    def __len__(self) -> int:
+        return len(self.hyperbolic)
+
+    def search(self, query: Sequence[float], k: int) -> List[SearchResult]:
+        q = np.asarray(query, np.float32).reshape(-1)
+        hyp = self.hyperbolic.search(q, k * 2)
+        euc = self.euclidean.search(q, k * 2)
+        w = np.float32(self.fusion_weight)
+        scores = {}
+        for rank, r in enumerate(hyp):
+            scores[r.id] = np.float32(scores.get(r.id, np.float32(0.0)) + w * (np.float32(1.0) / np.float32(rank + 1)))
+        for rank, r in enumerate(euc):
+            scores[r.id] = np.float32(scores.get(r.id, np.float32(0.0)) +
+                                      (np.float32(1.0) - w) * (np.float32(1.0) / np.float32(rank + 1)))
+        top = sorted(scores.items(), key=lambda t: -t[1])[:k]
+        if not top:
+            return []
+        vecs = np.stack([self.hyperbolic.get_vector(i) for i, _ in top]).astype(np.float32)
+        dist = np.empty((1, len(top)), np.float32)
+        _check("rvx_distance_matrix", L.METRIC_POINCARE, L.fptr(q), 1, L.fptr(vecs), len(top), q.size,
+               float(self.hyperbolic.config.curvature), L.fptr(dist))
+        return [SearchResult(int(i), float(dd)) for (i, _), dd in zip(top, dist[0])]

@@ -69,6 +69,7 @@ _SIG = {
     "orc_hyp_centroid": (None, [P, PF]),
     "orc_hyp_search_pruning": (None, [P, PF, I64, I32, PI64, PF, I32]),
     "orc_hyp_set_curvature": (None, [P, F32]),
+    "orc_hyp_set_metric": (None, [P, I32]),
     "orc_hyp_export_sizes": (None, [P, PI64, PI32, PI64, PI64, PI64, PI64]),
     "orc_hyp_export": (None, [P, PU8, PI64, PI32, PI32, PI64, PI32]),
     "orc_hyp_from_graph": (P, [PF, I64, I32, I32, I32, I32, F32, I32, PU8, I64, I32, PI64, PI32, PI64, PI32, PI64,
@@ -461,6 +462,10 @@ class Hyp:
     def set_curvature(self, c):
         lib().orc_hyp_set_curvature(self._h, float(c))
 
+    def set_metric(self, metric):
+        """'poincare' or 'euclidean' (HyperbolicHnswConfig.metric, hnsw.rs:23-32)."""
+        lib().orc_hyp_set_metric(self._h, 1 if metric == "euclidean" else 0)
+
     def export(self):
         n, ml, ent, e0 = C.c_int64(), C.c_int32(), C.c_int64(), C.c_int64()
         uc = np.zeros(17, np.int64)
@@ -512,3 +517,22 @@ class Hyp:
             lib().orc_hyp_free(self._h)
         except Exception:
             pass
+
+
+def dual_space_search(hyp, euc, query, k, fusion_weight, curvature=1.0):
+    """DualSpaceIndex::search (crates/ruvector-hyperbolic-hnsw/src/hnsw.rs:573-605) over two
+    oracle Hyp indexes (Poincaré and Euclidean metric): 2k from each, f32 reciprocal-rank
+    fusion, highest score first (ties by first appearance), Poincaré distance of the raw
+    query to the stored vector. Returns [(id, distance)]."""
+    q = f32(query).reshape(1, -1)
+    hi, _, hc = hyp.search(q, 2 * k)
+    ei, _, ec = euc.search(q, 2 * k)
+    w = np.float32(min(max(fusion_weight, 0.0), 1.0))
+    scores = {}
+    for rank, i in enumerate(hi[0][:hc[0]]):
+        scores[int(i)] = np.float32(scores.get(int(i), np.float32(0.0)) + w * (np.float32(1.0) / np.float32(rank + 1)))
+    for rank, i in enumerate(ei[0][:ec[0]]):
+        scores[int(i)] = np.float32(scores.get(int(i), np.float32(0.0)) +
+                                    (np.float32(1.0) - w) * (np.float32(1.0) / np.float32(rank + 1)))
+    top = sorted(scores.items(), key=lambda t: -t[1])[:k]
+    return [(i, poincare_distance(q[0], hyp.get_vector(i), curvature)) for i, _ in top]

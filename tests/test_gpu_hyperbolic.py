@@ -163,3 +163,64 @@ def test_sharded_search_merges_like_the_reference():
     mi, md = rv.hyperbolic.merge_shard_results(parts, 5)
     assert recall(mi, ids) >= 0.95
     assert np.all(np.diff(dist, axis=1) >= 0)
+
+
+# ---- DistanceMetric::Euclidean and DualSpaceIndex (hnsw.rs:173-185, 536-605) ----
+def test_euclidean_metric_search_and_exact_scan_match_oracle():
+    n, d = 3000, 16
+    x = ball_points(n, d, 41)
+    o = O.Hyp(d, seed=3)
+    o.set_metric("euclidean")
+    o.insert(x)
+    h = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=3, metric="euclidean"))
+    h.insert_batch(x)
+    h.load_graph(o.export())
+    q = ball_points(150, d, 42)
+    for k, ef in ((10, 0), (5, 100)):
+        ids, dist, cnt = h.search_batch(q, k, ef)
+        rids, rd, rc = o.search(q, k, ef)
+        assert np.array_equal(cnt, rc) and np.array_equal(ids, rids) and close(dist, rd)
+    ids, dist, _ = h.brute_force(q, 10)
+    rids, rd = o.brute_force(q, 10)
+    assert np.array_equal(ids, rids) and close(dist, rd)
+    with pytest.raises(rv.HyperbolicError):  # tangent pruning is the Poincaré path
+        h.build_tangent_cache()
+        h.search_with_pruning_batch(q, 10)
+
+
+def test_euclidean_metric_gpu_build_recall():
+    n, d = 5000, 24
+    x = ball_points(n, d, 43)
+    q = ball_points(200, d, 44)
+    h = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=7, metric="euclidean"))
+    h.insert_batch(x)
+    o = O.Hyp(d, seed=7)
+    o.set_metric("euclidean")
+    o.insert(x)
+    gt, _ = o.brute_force(q, 10)
+    assert recall(gt, h.search_batch(q, 10)[0]) >= recall(gt, o.search(q, 10)[0]) - 0.02
+
+
+def test_dual_space_index_matches_oracle_fusion():
+    n, d, k = 2000, 16, 5
+    x = ball_points(n, d, 51)
+    dual = rv.DualSpaceIndex(curvature=1.0, fusion_weight=0.7, seed=2)
+    dual.insert_batch(x)
+    assert len(dual) == n
+    vecs = np.stack([dual.hyperbolic.get_vector(i) for i in range(n)])
+    oh = O.Hyp.from_graph(vecs, dual.hyperbolic.export_graph())
+    oe = O.Hyp.from_graph(vecs, dual.euclidean.export_graph())
+    oe.set_metric("euclidean")
+    for qi, qv in enumerate(ball_points(25, d, 52)):
+        got = dual.search(qv, k)
+        ref = O.dual_space_search(oh, oe, qv, k, 0.7)
+        assert [r.id for r in got] == [i for i, _ in ref], qi
+        assert close([r.distance for r in got], [dd for _, dd in ref])
+
+
+def test_dual_space_reference_case():  # hnsw.rs test_dual_space
+    dual = rv.DualSpaceIndex(1.0, 0.5)
+    for i in range(10):
+        dual.insert([0.1 * i, 0.05 * i])
+    res = dual.search([0.3, 0.15], 3)
+    assert len(res) == 3
