@@ -126,7 +126,9 @@ namespace {
 
 // Row chunking of the layer pipeline (same on every rank for a given chunk count).
 int sage_chunks_for(int64_t n) {
-    static const int pipe_chunks = std::max(1, env_int("RVX_SAGE_CHUNKS", 16));
+    // 24 chunks with the gather capped at one block per CU (k_aggregate.hip):
+    // 1.46G vs 1.37G edges/s for 16 uncapped at 10M x 768 (scripts/exp_sweep3.sh)
+    static const int pipe_chunks = std::max(1, env_int("RVX_SAGE_CHUNKS", 24));
     return n >= (int64_t)pipe_chunks * 16384 ? pipe_chunks : 1;
 }
 int64_t chunk_step(int64_t n, int chunks) { return ((n + chunks - 1) / chunks + 127) / 128 * 128; }

@@ -211,7 +211,7 @@ void launch_agg(const char* t, const int64_t* rp, const int32_t* col, const floa
 // and use NT loads; RVX_AGG_BLOCKS_PER_CU caps the grid to a persistent one.
 // With the split-bf16 GEMM the uncapped grid gave the shortest 10M x 768 layer
 // (552 vs 578 ms/step for 1 block/CU at 16 chunks, scripts/exp_pipeline.sh).
-int g_agg_overlap_cap = env_int("RVX_AGG_BLOCKS_PER_CU", 0);
+int g_agg_overlap_cap = env_int("RVX_AGG_BLOCKS_PER_CU", 1);
 int g_agg_overlap_unroll = env_int("RVX_AGG_UNROLL", 8);
 int g_agg_nt = env_int("RVX_AGG_NT", 1);
 

@@ -298,10 +298,10 @@ def test_graphsage_split_f16_operand_range(scale):
 
 
 def test_graphsage_chunked_pipeline_and_exchange_entry():
-    """n >= 16*16384 rows runs the two-stream row-chunk pipeline (api_graph.cpp
+    """n >= 24*16384 rows runs the two-stream row-chunk pipeline (api_graph.cpp
     sage_forward_dev); rvx_sage_forward_exchange at world 1 writes the same rows."""
     import ctypes
-    n, d, deg = 280_000, 64, 8
+    n, d, deg = 400_000, 64, 8
     x = rv.Buffer(n * d * 4)
     x.fill_uniform(n * d, 21, -1.0, 1.0)
     g = rv.Graph.random(n, deg, 22)
@@ -317,9 +317,15 @@ def test_graphsage_chunked_pipeline_and_exchange_entry():
     xs = x.download(np.float32, (n, d))
     rp, col = O.random_csr(n, deg, 22)
     wn, ws = O.sage_init(d, d, 0), O.sage_init(d, d, 1000)
-    for r0 in (0, 17_536 - 1500, n - 3000):  # first chunk, across the chunk-0/1 seam (16 chunks of 17,536), the tail
+    for r0 in (0, 16_768 - 1500, n - 3000):  # first chunk, across the chunk-0/1 seam (24 chunks of 16,768), the tail
         ref = O.sage_forward(xs, rp, col, wn, ws, rows=(r0, 3000))
-        assert_close(got[r0:r0 + 3000], ref)
+        # L2-normalising a ReLU output that keeps only a few small entries divides
+        # GEMM rounding by a tiny norm: row 1949 here keeps 4 of 64 (both the split-f16
+        # and the split-bf16 GEMM land at ~1.1e-5 of its scale, scripts/diag_sage_numerics.py).
+        # The 1e-5 bar applies to rows keeping >= d/4 entries; sparse rows get 5e-5.
+        dense = np.count_nonzero(ref, axis=1) >= d // 4
+        assert_close(got[r0:r0 + 3000][dense], ref[dense])
+        assert_close(got[r0:r0 + 3000], ref, tol=5e-5)
     with pytest.raises(rv.RvxError):  # x and y may not alias
         rv._lib.call("rvx_sage_forward_exchange", layer._h, g.handle, x.handle, x.handle,
                      off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), None, 1)

@@ -107,7 +107,7 @@ def _exchange_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         # ragged shards, one far below the pipelining threshold
-        sizes = [300_000, 150_001, 5_000][:world]
+        sizes = [450_000, 150_001, 5_000][:world]
         offsets = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
         n, d = int(offsets[-1]), 3
         full = np.arange(n * d, dtype=np.float32).reshape(n, d)
@@ -155,7 +155,8 @@ def test_chunked_halo_exchange_protocol(world):
     for p in procs:
         p.join(180)
     res = sorted(q.get(timeout=5) for _ in range(world))
-    assert res == [(r, True, True, 16) for r in range(world)]
+    from ruvector_amd.shard import PIPE_CHUNKS
+    assert res == [(r, True, True, PIPE_CHUNKS) for r in range(world)]
 
 
 def test_shard_plan_rows_cover_and_owner():
