@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """C4 benchmark: multi-layer ruvector-gnn RuvectorLayer stack +
-EdgeFeaturedAttention head over a graph, 1 GPU.
+EdgeFeaturedAttention head over a graph, one process per GPU (node-range shards,
+launched with torch.distributed.run for N>1; rows exchanged over RCCL p2p).
 
 Workload: N x 768 node table (N(0,1), seed 5), uniform random out-degree-32
 CSR (seed 6) with edge weights uniform [0,1) (seed 7) standing in for the HNSW
@@ -26,7 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0
-GEMM_PEAK_TFS = 2500.0 / 6  # split-bf16 MFMA ceiling in f32-equivalent FLOP/s (see bench.py)
+GEMM_PEAK_TFS = 2500.0 / 3  # split-f16 (3 f16 MFMA products per f32 FMA) ceiling, as in bench.py
 
 
 def main():
@@ -42,15 +43,39 @@ def main():
     p.add_argument("--no-cpu", action="store_true")
     a = p.parse_args()
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # host-side only: barrier, id broadcast, max
+        dist.init_process_group("gloo")
+
     import ruvector_amd as rv
     from ruvector_amd.attention import EdgeFeaturedAttention, EdgeFeaturedConfig
+    from ruvector_amd.shard import RcclComm, ShardPlan
 
+    rv.set_device(local)
     n, d, deg, H = a.nodes, a.dim, a.degree, a.dim
+    plan = ShardPlan(n, world)
+    r0, r1 = plan.rows(rank)
+    n_loc = r1 - r0
+    offsets = np.array([plan.rows(p)[0] for p in range(world)] + [n], dtype=np.int64)
+    comm = None
+    if world > 1:
+        uid = [RcclComm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = RcclComm(world, rank, uid[0])
+
+    # node-range shards: every rank holds the whole-table buffers but reads and
+    # writes only its own rows; its CSR rows (global column ids) and their slice
+    # of the edge-weight stream are generated in place, so the sharded job is
+    # the same graph as the 1-GPU one
     E = n * deg
     x = rv.Buffer(n * d * 4)
     x.fill_normal(n * d, 5)
-    g = rv.Graph.random(n, deg, 6, weight_seed=7)
-    ew = g._keep[2]  # [E][1] edge features = the edge weights
+    g = rv.Graph.random_shard(n, r0, n_loc, deg, 6, weight_seed=7)
+    ew = g._keep[2]  # [E_local][1] edge features = the edge weights
     layers = [rv.RuvectorLayer(d, H, a.heads, 0.0, seed=100 + i) for i in range(a.layers)]
     head = EdgeFeaturedAttention(EdgeFeaturedConfig(node_dim=H, edge_dim=1, num_heads=a.heads))
     bufs = [rv.Buffer(n * H * 4) for _ in range(2)]
@@ -60,25 +85,39 @@ def main():
     def step():
         src = x
         for i, layer in enumerate(layers):
-            layer.forward_graph_device(src, g, bufs[i % 2])
+            layer.forward_exchange(g, src, bufs[i % 2], offsets, comm)
             src = bufs[i % 2]
-        head.forward_graph_device(src, g, ew, out)
+        head.forward_exchange(g, src, ew, out, offsets, comm)
+
+    def barrier():
+        rv.synchronize()
+        if dist is not None:
+            dist.barrier()
 
     for _ in range(a.warmup):
         step()
-    rv.synchronize()
+    barrier()
     prof = rv.Profiler()
     with prof:
+        barrier()
         t0 = time.perf_counter()
         for _ in range(a.steps):
             step()
         rv.synchronize()
-        dt = (time.perf_counter() - t0) / a.steps
+        t1 = time.perf_counter()
+        barrier()
+    dt = (t1 - t0) / a.steps
     kern = prof.summary()
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    n_own = n_loc  # per-launch work below is this rank's rows
 
     # algorithmic work per layer
-    layer_flops = 2.0 * n * (d * H + 11 * H * H)
-    edge_bytes = E * (3 * 4 * H + 8) + n * (8 + 4 * H + 2 * 4 * H)
+    layer_flops = 2.0 * n_own * (d * H + 11 * H * H)
+    edge_bytes = n_own * deg * (3 * 4 * H + 8) + n_own * (8 + 4 * H + 2 * 4 * H)
     gemm_ms = sum(v["total_ms"] for k, v in kern.items() if k.startswith("gnn_gemm")) / a.steps / a.layers
     edge_ms = kern.get("gnn_edge_attention", {"total_ms": 0})["total_ms"] / a.steps / a.layers
     roof = {
@@ -93,21 +132,27 @@ def main():
     }
     line = {
         "metric": "GNN-layer edges/sec (RuvectorLayer stack + graph-attention head)",
-        "value": round(E * (a.layers + 1) / dt, 1), "unit": "edges/s", "n_gpus": 1, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "f32",
-        "config": {"workload": f"configs[3] stack on 1 GPU: {n} x {d}, {a.layers} x RuvectorLayer(h={a.heads}) + "
-                               "EdgeFeaturedAttention(8 heads, edge_dim 1)", "nodes": n, "degree": deg,
-                   "edges": E, "layers": a.layers},
+        "value": round(E * (a.layers + 1) / dt, 1), "unit": "edges/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "strong", "dtype": "f32",
+        "config": {"workload": f"configs[3] stack on {world} GPU(s): {n} x {d}, {a.layers} x RuvectorLayer(h={a.heads})"
+                               " + EdgeFeaturedAttention(8 heads, edge_dim 1)", "nodes": n, "degree": deg,
+                   "edges": E, "layers": a.layers, "parallelism": f"node-range x{world}",
+                   "exchange": "per layer: M|K|V rows (RuvectorLayer), T rows (attention head), "
+                               "one grouped RCCL p2p round each" if world > 1 else "none"},
         "data": "synthetic: X ~ N(0,1) seed 5; uniform random out-degree CSR seed 6; edge weights U[0,1) seed 7",
         "roofline": roof,
         "kernel_ms_per_step": {k: round(v["total_ms"] / a.steps, 3) for k, v in kern.items()},
     }
-    if not a.no_cpu:
-        line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, ew, layers[0], n, d, deg)
-    print(json.dumps(line), flush=True)
+    if rank == 0 and world == 1 and not a.no_cpu:
+        line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, ew, layers[0], n, d, deg, offsets)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
-def cpu_baseline(a, x_buf, g, ew_buf, layer, n, d, deg):
+def cpu_baseline(a, x_buf, g, ew_buf, layer, n, d, deg, offsets):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
     import ruvector_amd as rv
@@ -118,7 +163,7 @@ def cpu_baseline(a, x_buf, g, ew_buf, layer, n, d, deg):
     rp, col = O.random_csr(n, deg, 6)
     ew = O.fill_uniform(n * deg, 7, 0.0, 1.0)
     y1 = rv.Buffer(n * layer.hidden_dim * 4)
-    layer.forward_graph_device(x_buf, g, y1)
+    layer.forward_exchange(g, x_buf, y1, offsets)
     rows = 64
     t0 = time.perf_counter()
     O.rvl_forward_graph(W, x, rp, col, ew, rows=(0, rows), threads=threads)

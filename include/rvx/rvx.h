@@ -90,6 +90,9 @@ rvx_status rvx_buffer_zero(rvx_buffer* buf);
  *           crates/ruvector-bench/src/lib.rs:112-114)
  * random_csr: out-degree `deg` per node, col = h(seed, i*deg+t) mod N. */
 rvx_status rvx_fill_uniform(rvx_buffer* buf, int64_t n_floats, uint64_t seed, float lo, float hi);
+/* Elements [first, first+n_floats) of the rvx_fill_uniform(seed) stream (counter-based),
+ * so a node-range shard generates exactly its slice of the global edge weights. */
+rvx_status rvx_fill_uniform_at(rvx_buffer* buf, int64_t n_floats, uint64_t seed, int64_t first, float lo, float hi);
 rvx_status rvx_fill_normal(rvx_buffer* buf, int64_t n_floats, uint64_t seed);
 rvx_status rvx_normalize_rows(rvx_buffer* buf, int64_t rows, int32_t dim); /* L2, as hnsw_integration_test.rs:21-28 */
 rvx_status rvx_random_csr(int64_t n, int32_t deg, uint64_t seed, rvx_buffer* row_ptr_i64, rvx_buffer* col_i32);
@@ -268,6 +271,14 @@ rvx_status rvx_edge_attention_compute(const rvx_edge_attention* a, const float* 
 rvx_status rvx_edge_attention_forward_graph_device(const rvx_edge_attention* a, const rvx_graph* g,
                                                    const rvx_buffer* x, const rvx_buffer* edge_feat,
                                                    rvx_buffer* y);
+/* Node-range sharded form of the above (one process per GPU): g holds this rank's
+ * rows [offsets[rank], offsets[rank+1]) with global column ids, edge_feat its
+ * edges, x_full/y_full are whole-table [N][*] buffers of which only the owned
+ * rows are read/written. The transformed rows x W_node^T are exchanged once
+ * (one grouped RCCL p2p round); comm NULL = one process, offsets {0, N}. */
+rvx_status rvx_edge_attention_forward_exchange(const rvx_edge_attention* a, const rvx_graph* g,
+                                               const rvx_buffer* x_full, const rvx_buffer* edge_feat,
+                                               rvx_buffer* y_full, const int64_t* offsets, rvx_comm* comm);
 
 /* DualSpaceAttention (crates/ruvector-attention/src/graph/dual_space.rs:95-293):
  * Euclidean (scaled dot of x W_euclidean^T) and hyperbolic (-poincare_dist of

@@ -100,6 +100,7 @@ SIGNATURES = {
     "rvx_buffer_download": (None, [P, P, I64, I64]),
     "rvx_buffer_zero": (None, [P]),
     "rvx_fill_uniform": (None, [P, I64, U64, F32, F32]),
+    "rvx_fill_uniform_at": (None, [P, I64, U64, I64, F32, F32]),
     "rvx_fill_normal": (None, [P, I64, U64]),
     "rvx_normalize_rows": (None, [P, I64, I32]),
     "rvx_random_csr": (None, [I64, I32, U64, P, P]),
@@ -139,6 +140,7 @@ SIGNATURES = {
     "rvx_edge_attention_dim": (None, [P, PI32]),
     "rvx_edge_attention_compute": (None, [P, PF32, PF32, PF32, PF32, I32, PF32]),
     "rvx_edge_attention_forward_graph_device": (None, [P, P, P, P, P]),
+    "rvx_edge_attention_forward_exchange": (None, [P, P, P, P, P, PI64, P]),
     "rvx_dual_attention_create": (None, [C.POINTER(DualAttentionConfig), PP]),
     "rvx_dual_attention_destroy": (None, [P]),
     "rvx_dual_attention_compute": (None, [P, PF32, PF32, PF32, I32, I32, PF32]),

@@ -93,6 +93,15 @@ class EdgeFeaturedAttention:
         _check("rvx_edge_attention_forward_graph_device", self._h, graph.handle, x.handle,
                edge_features.handle if edge_features is not None else None, y.handle)
 
+    def forward_exchange(self, local_graph: Graph, x_full: Buffer, edge_features: Optional[Buffer], y_full: Buffer,
+                         offsets, comm=None) -> None:
+        """Node-range-sharded forward_graph_device (rvx_edge_attention_forward_exchange):
+        this rank's rows of y_full; the transformed rows travel to the peers over RCCL."""
+        off = np.ascontiguousarray(np.asarray(offsets, dtype=np.int64))
+        _check("rvx_edge_attention_forward_exchange", self._h, local_graph.handle, x_full.handle,
+               edge_features.handle if edge_features is not None else None, y_full.handle,
+               off.ctypes.data_as(C.POINTER(C.c_int64)), comm._h if comm is not None else None)
+
     def __del__(self):
         try:
             if self._h:

@@ -3,6 +3,7 @@
 #include <cmath>
 
 #include "attn.hpp"
+#include "comm.hpp"
 #include "gnn.hpp"
 #include "graph.hpp"
 #include "kernels.hpp"
@@ -301,6 +302,42 @@ rvx_status rvx_edge_attention_forward_graph_device(const rvx_edge_attention* a, 
         float* t = scratch_f32("efa_t", g->n * (int64_t)a->D);
         transform(a, x->mem.as<float>(), g->n, t, "efa_transform");
         run_efa(a, g->n, g->row_ptr, g->col, g->e, t, g->n, t, t, ef ? ef->mem.as<float>() : nullptr, y->mem.as<float>());
+    });
+}
+
+rvx_status rvx_edge_attention_forward_exchange(const rvx_edge_attention* a, const rvx_graph* g,
+                                               const rvx_buffer* x_full, const rvx_buffer* ef, rvx_buffer* y_full,
+                                               const int64_t* offsets, rvx_comm* comm) {
+    return guard([&] {
+        check_graph(g);
+        RVX_REQUIRE(a && x_full && y_full && offsets, RVX_ERR_INVALID_PARAMETER, "null argument");
+        const int world = comm_size(comm), me = comm_rank(comm);
+        for (int p = 0; p < world; ++p)
+            RVX_REQUIRE(offsets[p] >= 0 && offsets[p] <= offsets[p + 1], RVX_ERR_INVALID_PARAMETER,
+                        "offsets must be non-decreasing");
+        RVX_REQUIRE(offsets[me + 1] - offsets[me] == g->n, RVX_ERR_DIMENSION_MISMATCH,
+                    "graph rows differ from this rank's shard");
+        const int64_t N = offsets[world], o = offsets[me], D = a->D;
+        const int nd = a->cfg.node_dim;
+        const int od = a->cfg.concat_heads ? a->D : a->hd;
+        RVX_REQUIRE(x_full->mem.bytes >= N * nd * 4, RVX_ERR_DIMENSION_MISMATCH, "x_full smaller than N*node_dim");
+        RVX_REQUIRE(y_full->mem.bytes >= N * od * 4, RVX_ERR_DIMENSION_MISMATCH, "y_full smaller than N*out_dim");
+        RVX_REQUIRE(!ef || ef->mem.bytes >= g->e * a->cfg.edge_dim * 4, RVX_ERR_DIMENSION_MISMATCH,
+                    "edge features smaller than E*edge_dim");
+        ComputeLock cl;
+        // owned rows of T = x W_node^T into the whole table, every rank's rows to
+        // every peer, then the per-edge scores/softmax/aggregate on owned rows
+        // (queries T[o..o+n), keys = values = all of T by global column id)
+        float* t = scratch_f32("efa_t", N * D);
+        transform(a, x_full->mem.as<float>() + o * nd, g->n, t + o * D, "efa_transform");
+        if (world > 1) {
+            ProfScope ps("efa_halo_exchange");
+            std::vector<int64_t> rows(world);
+            for (int p = 0; p < world; ++p) rows[p] = offsets[p + 1] - offsets[p];
+            comm_exchange_rows(comm, t, D, offsets, rows.data(), stream());
+        }
+        run_efa(a, g->n, g->row_ptr, g->col, g->e, t + o * D, N, t, t, ef ? ef->mem.as<float>() : nullptr,
+                y_full->mem.as<float>() + o * od);
     });
 }
 

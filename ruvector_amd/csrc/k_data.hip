@@ -127,6 +127,12 @@ void fill_uniform(float* p, int64_t n, uint64_t seed, float lo, float hi) {
                        hi - lo);
     RVX_HIP(hipGetLastError());
 }
+void fill_uniform_at(float* p, int64_t n, uint64_t seed, int64_t first, float lo, float hi) {
+    ProfScope ps("fill_uniform");
+    hipLaunchKernelGGL(k_fill_uniform, dim3(grid_for(n, 256)), dim3(256), 0, stream(), p, n,
+                       splitmix64(seed) + (uint64_t)first, lo, hi - lo);
+    RVX_HIP(hipGetLastError());
+}
 void fill_normal(float* p, int64_t n, uint64_t seed) {
     ProfScope ps("fill_normal");
     hipLaunchKernelGGL(k_fill_normal, dim3(grid_for(n, 256)), dim3(256), 0, stream(), p, n, splitmix64(seed));
@@ -170,6 +176,13 @@ rvx_status rvx_fill_uniform(rvx_buffer* buf, int64_t n, uint64_t seed, float lo,
     return guard([&] {
         RVX_REQUIRE(buf && n >= 0 && n * 4 <= buf->mem.bytes, RVX_ERR_INVALID_PARAMETER, "buffer too small");
         fill_uniform(buf->mem.as<float>(), n, seed, lo, hi);
+    });
+}
+rvx_status rvx_fill_uniform_at(rvx_buffer* buf, int64_t n, uint64_t seed, int64_t first, float lo, float hi) {
+    return guard([&] {
+        RVX_REQUIRE(buf && n >= 0 && first >= 0 && n * 4 <= buf->mem.bytes, RVX_ERR_INVALID_PARAMETER,
+                    "buffer too small");
+        fill_uniform_at(buf->mem.as<float>(), n, seed, first, lo, hi);
     });
 }
 rvx_status rvx_fill_normal(rvx_buffer* buf, int64_t n, uint64_t seed) {

@@ -66,6 +66,10 @@ class Buffer:
     def fill_uniform(self, n: int, seed: int, lo: float = -1.0, hi: float = 1.0) -> None:
         L.call("rvx_fill_uniform", self._h, int(n), int(seed), float(lo), float(hi))
 
+    def fill_uniform_at(self, n: int, seed: int, first: int, lo: float = -1.0, hi: float = 1.0) -> None:
+        """Elements [first, first+n) of the fill_uniform(seed) stream."""
+        L.call("rvx_fill_uniform_at", self._h, int(n), int(seed), int(first), float(lo), float(hi))
+
     def fill_normal(self, n: int, seed: int) -> None:
         L.call("rvx_fill_normal", self._h, int(n), int(seed))
 

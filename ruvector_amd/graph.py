@@ -67,16 +67,22 @@ class Graph:
         return cls(h, keep=(rp, col) if w is None else (rp, col, w))
 
     @classmethod
-    def random_shard(cls, num_nodes_total: int, row_begin: int, num_rows: int, degree: int, seed: int) -> "Graph":
-        """Rows [row_begin, row_begin+num_rows) of Graph.random(num_nodes_total, ...), global column ids."""
+    def random_shard(cls, num_nodes_total: int, row_begin: int, num_rows: int, degree: int, seed: int,
+                     weight_seed: Optional[int] = None) -> "Graph":
+        """Rows [row_begin, row_begin+num_rows) of Graph.random(num_nodes_total, ...), global column ids
+        (with weight_seed, the same rows' slice of the global edge-weight stream)."""
         rp = Buffer((num_rows + 1) * 8)
         col = Buffer(max(num_rows * degree * 4, 4))
         L.call("rvx_random_csr_shard", int(num_nodes_total), int(row_begin), int(num_rows), int(degree), int(seed),
                rp.handle, col.handle)
+        w = None
+        if weight_seed is not None:
+            w = Buffer(max(num_rows * degree * 4, 4))
+            w.fill_uniform_at(num_rows * degree, weight_seed, row_begin * degree, 0.0, 1.0)
         h = C.c_void_p()
-        L.call("rvx_graph_from_device_csr", int(num_rows), int(num_rows * degree), rp.handle, col.handle, None,
-               C.byref(h))
-        return cls(h, keep=(rp, col))
+        L.call("rvx_graph_from_device_csr", int(num_rows), int(num_rows * degree), rp.handle, col.handle,
+               w.handle if w is not None else None, C.byref(h))
+        return cls(h, keep=(rp, col) if w is None else (rp, col, w))
 
     def destroy(self):
         if self._h:

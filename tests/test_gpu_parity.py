@@ -542,6 +542,44 @@ def test_edge_attention_graph_matches_per_node():
         assert_close(y[i], ref)
 
 
+def test_edge_attention_forward_exchange_entry():
+    """rvx_edge_attention_forward_exchange (node-range-sharded head: owned rows of
+    T = x W_node^T into the whole table, p2p exchange, per-edge attention on owned
+    rows) at world 1 writes the same bits as forward_graph_device."""
+    node_dim, heads, n, deg = 64, 4, 3000, 6
+    att = rv.EdgeFeaturedAttention(rv.EdgeFeaturedConfig(node_dim=node_dim, edge_dim=1, num_heads=heads))
+    x = O.fill_uniform(n * node_dim, 28).reshape(n, node_dim)
+    rp, col = O.random_csr(n, deg, 29)
+    ef = O.fill_uniform(n * deg, 30, 0.0, 1.0)
+    g = rv.Graph.from_csr(rp, col)
+    xb, eb = rv.Buffer.from_numpy(x), rv.Buffer.from_numpy(ef)
+    y_ref, y = rv.Buffer(x.nbytes), rv.Buffer(x.nbytes)
+    att.forward_graph_device(xb, g, eb, y_ref)
+    att.forward_exchange(g, xb, eb, y, [0, n])
+    got = y.download(np.float32, x.shape)
+    assert np.array_equal(got, y_ref.download(np.float32, x.shape))
+    i = 11
+    nb = col[rp[i]:rp[i + 1]]
+    assert_close(got[i], O.efa_compute(node_dim, 1, heads, x[i], x[nb], x[nb], ef[rp[i]:rp[i + 1]].reshape(-1, 1)))
+    with pytest.raises(rv.RvxError):
+        att.forward_exchange(g, xb, eb, y, [0, n + 1])
+
+
+def test_random_shard_weights_are_the_global_slice():
+    """Graph.random_shard(weight_seed) generates exactly its rows' slice of the
+    global column ids and edge-weight stream (counter-based generator), so a
+    sharded benchmark runs the same graph as the 1-GPU one."""
+    n, deg = 10_007, 5
+    full = rv.Graph.random(n, deg, 6, weight_seed=7)
+    col_f = full._keep[1].download(np.int32, (n * deg,))
+    w_f = full._keep[2].download(np.float32, (n * deg,))
+    assert np.array_equal(w_f, O.fill_uniform(n * deg, 7, 0.0, 1.0))
+    for r0, nr in [(0, 3000), (3000, 4000), (7000, 3007)]:
+        sh = rv.Graph.random_shard(n, r0, nr, deg, 6, weight_seed=7)
+        assert np.array_equal(sh._keep[1].download(np.int32, (nr * deg,)), col_f[r0 * deg:(r0 + nr) * deg])
+        assert np.array_equal(sh._keep[2].download(np.float32, (nr * deg,)), w_f[r0 * deg:(r0 + nr) * deg])
+
+
 @pytest.mark.parametrize("dim,n,vd,c,we,wh,t", [(64, 10, 64, 1.0, 0.5, 0.5, 1.0), (32, 5, 32, 0.5, 0.0, 1.0, 1.0),
                                                  (32, 7, 20, 1.0, 1.0, 0.0, 0.5), (768, 24, 768, 1.0, 0.5, 0.5, 2.0)])
 def test_dual_space_attention_matches_oracle(dim, n, vd, c, we, wh, t):
