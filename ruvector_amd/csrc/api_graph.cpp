@@ -146,14 +146,23 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
     // sample_neighbors subset (graphsage.rs:92-102, k_sample.hip)
     g = sampled_graph(g, l->num_samples);
     const int64_t n = g->n;
-    float* agg = scratch_f32("sage_agg", n * (int64_t)l->in);
     const int a = (l->aggregator == RVX_SAGE_MAXPOOL) ? AGG_MAX : AGG_MEAN;
     // split-f16 dual GEMM when the shapes allow it: the gather also emits the
-    // per-row operand scale over the aggregate and self rows
-    const bool h2 = l->wn_h2.p && l->in <= 1024 && ((uintptr_t)x & 15) == 0 &&
-                    gemm_h2_ok(std::max<int64_t>(n, 1), l->out, GemmOperand{agg, l->in, nullptr, l->in, l->in},
-                               nullptr) &&
-                    gemm_h2_ok(std::max<int64_t>(n, 1), l->out, GemmOperand{x, l->in, nullptr, l->in, l->in}, nullptr);
+    // per-row operand scale over the aggregate and self rows, and (h2p) the
+    // scaled [aggregate | self] operand itself as two f16 planes, so the GEMM
+    // k-loop does no conversion work
+    const int64_t plane = (int64_t)l->in * l->out;
+    const GemmOperand w0{nullptr, 2 * l->in, nullptr, l->in, l->in, nullptr, 0, l->wn_h2.as<_Float16>(), 0, nullptr};
+    const int64_t a_plane = std::max<int64_t>(n, 1) * 2 * l->in;
+    const bool h2p = l->wn_h2.p && l->in <= 1024 && l->in % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
+                     gemm_h2p_ok(std::max<int64_t>(n, 1), l->out, 2 * l->in, a_plane, w0, &w0);
+    float* agg = h2p ? nullptr : scratch_f32("sage_agg", n * (int64_t)l->in);
+    _Float16* aplanes = h2p ? (_Float16*)scratch_bytes("sage_aplanes", a_plane * 2 * 2) : nullptr;
+    const bool h2 = h2p || (l->wn_h2.p && l->in <= 1024 && ((uintptr_t)x & 15) == 0 &&
+                            gemm_h2_ok(std::max<int64_t>(n, 1), l->out,
+                                       GemmOperand{agg, l->in, nullptr, l->in, l->in}, nullptr) &&
+                            gemm_h2_ok(std::max<int64_t>(n, 1), l->out, GemmOperand{x, l->in, nullptr, l->in, l->in},
+                                       nullptr));
     float* scale = h2 ? scratch_f32("sage_scale", std::max<int64_t>(n, 1)) : nullptr;
     GemmEpilogue ep;
     ep.epi = GEMM_EPI_RELU;
@@ -175,15 +184,24 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         if (chunks > 1) {
             StreamScope on_aux(d.aux);
             aggregate_rows(g->row_ptr + r0, g->col, nullptr, rows, x, l->in, a, /*empty_fill zeros*/ 0, 0,
-                           agg + r0 * l->in, "sage_aggregate", /*overlapped*/ true,
-                           x + (row_offset + r0) * l->in, h2 ? scale + r0 : nullptr);
+                           h2p ? nullptr : agg + r0 * l->in, "sage_aggregate", /*overlapped*/ true,
+                           x + (row_offset + r0) * l->in, h2 ? scale + r0 : nullptr,
+                           h2p ? aplanes + r0 * 2 * l->in : nullptr, a_plane);
             RVX_HIP(hipEventRecord(ev[c], d.aux));
             RVX_HIP(hipStreamWaitEvent(d.stream, ev[c], 0));
         } else {
             aggregate_rows(g->row_ptr, g->col, nullptr, n, x, l->in, a, 0, 0, agg, "sage_aggregate", false,
-                           x + row_offset * l->in, scale);
+                           x + row_offset * l->in, scale, aplanes, a_plane);
         }
-        const int64_t plane = (int64_t)l->in * l->out;
+        if (h2p) {
+            GemmOperand s0{nullptr, 2 * l->in, nullptr, l->in, l->in};
+            gemm_nt_h2p(rows, l->out, aplanes + r0 * 2 * l->in, 2 * l->in, a_plane, s0, l->wn_h2.as<_Float16>(), &s0,
+                        l->ws_h2.as<_Float16>(), scale + r0, l->w_inv.as<float>(), ep, y + r0 * l->out, l->out,
+                        "sage_gemm");
+            if (l->normalize) normalize_rows(y + r0 * l->out, rows, l->out, true, "sage_normalize");
+            if (hook) hook(c, r0, rows);
+            continue;
+        }
         GemmOperand s0{agg + r0 * l->in, l->in, l->wn_t.as<float>(), l->in, l->in, l->wn_x3.as<uint16_t>(), plane};
         GemmOperand s1{x + (row_offset + r0) * l->in, l->in, l->ws_t.as<float>(), l->in, l->in,
                        l->ws_x3.as<uint16_t>(), plane};

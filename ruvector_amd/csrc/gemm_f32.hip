@@ -49,6 +49,8 @@ struct GemmArgs {
     // inverse scale of B, and the two f16 planes of each B
     const float* a_scale; const float* b_inv;
     const _Float16* B0h; const _Float16* B1h; int64_t B0h_plane, B1h_plane;
+    // pre-split A (gemm_nt_h2p): f16 planes [2][M][lda] written by the producer
+    const _Float16* A0h; const _Float16* A1h; int64_t Ah_plane;
 };
 
 __device__ __forceinline__ float epi_apply(int epi, float v) {
@@ -947,6 +949,190 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
     }
 }
 
+// Pre-split variant ("h2p") of the split-f16 GEMM: the producer (the SAGE
+// gather, aggregate_rows with planes) already wrote A*a_scale as two f16
+// planes with the same round-to-nearest split as split_h2_pair, so the k-loop
+// is LDS-DMA fills and MFMAs only. A and B tiles share one layout (2 planes x
+// rows x 64 B, 16-B chunks XOR-swizzled by (row>>2)&3). WM waves along M
+// (32 rows each) x 128 columns; an NST-stage ring: step t waits only for its
+// own DMAs (counted vmcnt), one raw barrier, then refills the stage step t-1
+// read, so NST-1 steps of fills stay in flight across the MFMAs. Every output
+// element sees the same MFMA chain as h2g: the results are bit-identical.
+template <int V>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(V >= 0 && V < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((V & 15) | ((V >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+template <bool DUAL, int WM, int NST>
+__global__ __launch_bounds__(64 * WM, WM == 4 && NST == 2 ? 2 : 1) void gemm_nt_h2p(GemmArgs g, int epi) {
+    constexpr int BM = 32 * WM;
+    constexpr int APL = BM * 64;               // one f16 A plane of a BM x 32 tile
+    constexpr int BPL = XB_PLANE;              // one f16 B plane of a 128 x 32 tile
+    constexpr int STG = 2 * APL + 2 * BPL;
+    constexpr int NA = 4;                      // A DMA pieces per wave (2 planes x BM/16 rows / WM)
+    constexpr int NBP = 16 / WM;               // B DMA pieces per wave
+    constexpr int F = NA + NBP;                // DMAs per thread per step
+    extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
+
+    const int64_t nwg = g.nblocks;
+    const int64_t bid = blockIdx.x;
+    const int64_t xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+    const int64_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    const int64_t tm = wgid / g.tiles_n;
+    const int tn = (int)(wgid % g.tiles_n);
+    const int64_t m0 = tm * BM;
+    const int n0 = tn * XBN;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, lh = lane >> 5;
+
+    const int nk0 = g.K0 / 32;
+    const int nsteps = nk0 + (DUAL ? g.K1 / 32 : 0);
+    auto sw = [](int row) { return (row >> 2) & 3; };
+
+    uint32_t a_off[2][NA], b_off[2][NBP];
+    const char* a_base[2];
+    const char* b_base[2];
+#pragma unroll
+    for (int ph = 0; ph < (DUAL ? 2 : 1); ++ph) {
+        const _Float16* A = ph ? g.A1h : g.A0h;
+        const _Float16* B = ph ? g.B1h : g.B0h;
+        const int64_t lda = ph ? g.lda1 : g.lda0, ldb = ph ? g.ldb1 : g.ldb0, bpl = ph ? g.B1h_plane : g.B0h_plane;
+        a_base[ph] = reinterpret_cast<const char*>(A + m0 * lda);
+        b_base[ph] = reinterpret_cast<const char*>(B + (int64_t)n0 * ldb);
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {  // piece: plane piece / (BM/16), rows 16 * (piece % (BM/16))
+            const int piece = NA * wave + j;
+            const int row = 16 * (piece % (BM / 16)) + (lane >> 2);
+            const int chunk = (lane & 3) ^ sw(row);
+            const int64_t ra = std::min<int64_t>(m0 + row, g.M - 1) - m0;
+            a_off[ph][j] = (uint32_t)(((piece / (BM / 16)) * g.Ah_plane + ra * lda + 8 * chunk) * 2);
+        }
+#pragma unroll
+        for (int j = 0; j < NBP; ++j) {
+            const int piece = NBP * wave + j;
+            const int row = 16 * (piece & 7) + (lane >> 2);
+            const int chunk = (lane & 3) ^ sw(row);
+            const int64_t rb = std::min<int64_t>(n0 + row, (int64_t)g.N - 1) - n0;
+            b_off[ph][j] = (uint32_t)(((piece >> 3) * bpl + rb * ldb + 8 * chunk) * 2);
+        }
+    }
+
+    auto fill = [&](int t, unsigned char* base) {
+        const int ph = (DUAL && t >= nk0) ? 1 : 0;
+        const int k0 = (t - (ph ? nk0 : 0)) * 32;
+        const char* ab = a_base[ph] + (int64_t)k0 * 2;
+        const char* bb = b_base[ph] + (int64_t)k0 * 2;
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+            const int piece = NA * wave + j;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(ab + a_off[ph][j]),
+                (__attribute__((address_space(3))) void*)(base + (piece / (BM / 16)) * APL + (piece % (BM / 16)) * 1024),
+                16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < NBP; ++j) {
+            const int piece = NBP * wave + j;
+            __builtin_amdgcn_global_load_lds(
+                (const void*)(bb + b_off[ph][j]),
+                (__attribute__((address_space(3))) void*)(base + 2 * APL + (piece >> 3) * BPL + (piece & 7) * 1024),
+                16, 0, 0);
+        }
+    };
+    auto x_sw = [&](int row, int chunk) { return row * 64 + ((chunk ^ sw(row)) << 4); };
+
+    f32x16 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[j][e] = 0.0f;
+
+    int a_rd[2], b_rd[2][4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        a_rd[s] = x_sw(wave * 32 + lr, 2 * s + lh);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) b_rd[s][ni] = 2 * APL + x_sw(ni * 32 + lr, 2 * s + lh);
+    }
+
+    auto compute = [&](const unsigned char* __restrict__ cur) {
+        f16x8 af[2][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) af[s][p] = *reinterpret_cast<const f16x8*>(cur + a_rd[s] + p * APL);
+        u32x4 bq[2][2];
+#pragma unroll
+        for (int p = 0; p < 2; ++p) bq[0][p] = *reinterpret_cast<const u32x4*>(cur + b_rd[0][0] + p * BPL);
+#pragma unroll
+        for (int gi = 0; gi < 8; ++gi) {
+            const int s = gi >> 2, ni = gi & 3;
+            if (gi + 1 < 8) {
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+                    bq[(gi + 1) & 1][p] =
+                        *reinterpret_cast<const u32x4*>(cur + b_rd[(gi + 1) >> 2][(gi + 1) & 3] + p * BPL);
+            }
+            f16x8 bf[2];
+#pragma unroll
+            for (int p = 0; p < 2; ++p) bf[p] = __builtin_bit_cast(f16x8, bq[gi & 1][p]);
+            acc[ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[s][1], bf[0], acc[ni], 0, 0, 0);
+            acc[ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[s][0], bf[1], acc[ni], 0, 0, 0);
+            acc[ni] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[s][0], bf[0], acc[ni], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    // ring: steps 0..NST-2 in flight before the loop
+#pragma unroll
+    for (int f = 0; f < NST - 1; ++f)
+        if (f < nsteps) fill(f, xsm + f * STG);
+    int st = 0, fst = NST - 1;
+    for (int t = 0; t < nsteps; ++t) {
+        const int later = min(NST - 2, nsteps - t - 1);  // steps after t already issued
+        if (NST >= 4 && later >= 2) wait_vmcnt<(NST >= 4 ? 2 * F : 0)>();
+        else if (NST >= 3 && later >= 1) wait_vmcnt<(NST >= 3 ? F : 0)>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // every wave's share of step t landed; step t-1's stage is free
+        asm volatile("" ::: "memory");
+        if (t + NST - 1 < nsteps) fill(t + NST - 1, xsm + fst * STG);
+        compute(xsm + st * STG);
+        st = st == NST - 1 ? 0 : st + 1;
+        fst = fst == NST - 1 ? 0 : fst + 1;
+    }
+
+    float rinv[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int64_t row = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        rinv[e] = row < g.M ? 1.0f / g.a_scale[row] : 0.0f;
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+        const int col = n0 + ni * 32 + lr;
+        if (col >= g.N) continue;
+        const float cinv = g.b_inv[col];
+        float b = 0.0f;
+        if (g.bias0) b = g.bias0[col];
+        if (g.bias1) b += g.bias1[col];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int64_t row = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+            if (row < g.M) {
+                float v = (acc[ni][e] * rinv[e]) * cinv;
+                if (g.alpha != 1.0f) v *= g.alpha;
+                if (g.bias0 || g.bias1) v += b;
+                if (g.addend) v += g.addend[row * g.ld_add + col];
+                g.C[row * g.ldc + col] = epi_apply(epi, v);
+            }
+        }
+    }
+}
+
 // B rows n of one or two [N][K] matrices: common scale t_n, f16 planes of each
 // (plane stride N*K), inv[n] = 1 / t_n. One wave per row.
 __global__ __launch_bounds__(256) void k_split_h2_rows(const float* __restrict__ B0, const float* __restrict__ B1,
@@ -1126,6 +1312,65 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
     const char* t = tag ? tag : "gemm_nt_h2";
     if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)g.nblocks), dim3(256), lds, g, ep.epi);
     else RVX_LAUNCH(t, gemm_nt_h2g<false>, dim3((unsigned)g.nblocks), dim3(256), lds, g, ep.epi);
+}
+
+bool gemm_h2p_ok(int64_t M, int N, int64_t lda, int64_t a_plane, const GemmOperand& s0, const GemmOperand* s1) {
+    // read per call so tests cover every path; RVX_GEMM_H2=0 turns off both split-f16 kernels
+    // (opt-in: no faster than h2g in the 10M x 768 layer, which runs power-capped at ~1.9 GHz in every
+    // tiling tried, scripts/exp_h2p.sh)
+    if (!env_int("RVX_GEMM_H2P", 0) || !env_int("RVX_GEMM_H2", 1) || M <= 0 || N <= 0) return false;
+    const int64_t lim = (int64_t)1 << 31;
+    auto ok = [&](const GemmOperand& o) {
+        const int64_t plane = o.Bh_plane ? o.Bh_plane : (int64_t)o.ldb * N;
+        return o.K % 32 == 0 && o.ldb % 8 == 0 && (plane + (int64_t)XBN * o.ldb) * 2 < lim;
+    };
+    return lda % 8 == 0 && (a_plane + 256 * lda) * 2 < lim && ok(s0) && (!s1 || ok(*s1));
+}
+
+void gemm_nt_h2p(int64_t M, int N, const _Float16* Ah, int64_t lda, int64_t a_plane, const GemmOperand& s0,
+                 const _Float16* B0h, const GemmOperand* s1, const _Float16* B1h, const float* a_scale,
+                 const float* b_inv, const GemmEpilogue& ep, float* C, int64_t ldc, const char* tag) {
+    if (M <= 0 || N <= 0) return;
+    RVX_REQUIRE(gemm_h2p_ok(M, N, lda, a_plane, s0, s1) && aligned16(Ah), RVX_ERR_INVALID_SHAPE,
+                "shape not supported by the pre-split f16 GEMM");
+    GemmArgs g{};
+    g.addend = ep.addend;
+    g.ld_add = ep.ld_addend;
+    g.A0h = Ah; g.lda0 = lda; g.ldb0 = s0.ldb; g.K0 = s0.K; g.Ah_plane = a_plane;
+    g.B0h = B0h; g.B0h_plane = s0.Bh_plane ? s0.Bh_plane : (int64_t)N * s0.ldb;
+    if (s1) {
+        g.A1h = Ah + s0.K; g.lda1 = lda; g.ldb1 = s1->ldb; g.K1 = s1->K; g.B1h = B1h;
+        g.B1h_plane = s1->Bh_plane ? s1->Bh_plane : (int64_t)N * s1->ldb;
+    }
+    g.bias0 = ep.bias0; g.bias1 = ep.bias1; g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.alpha = ep.alpha;
+    g.a_scale = a_scale; g.b_inv = b_inv;
+    // RVX_GEMM_H2P_CFG: 0 = 128x128, 2 stages, 2 blocks/CU; 1 = 256x128, 3 stages; 2 = 128x128, 3 stages;
+    // 3 = 256x128, 2 stages (one block of 8 or 4 waves per CU for 1-3)
+    const int cfg = env_int("RVX_GEMM_H2P_CFG", 0);
+    const int bm = (cfg == 1 || cfg == 3) ? 256 : 128;
+    g.tiles_n = (N + XBN - 1) / XBN;
+    g.nblocks = ((M + bm - 1) / bm) * g.tiles_n;
+    RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
+    const char* t = tag ? tag : "gemm_nt_h2p";
+#define RVX_H2P(WM, NST)                                                                                           \
+    do {                                                                                                           \
+        constexpr int lds = NST * (2 * 32 * WM * 64 + 2 * XB_PLANE);                                               \
+        static bool attr = false;                                                                                  \
+        if (!attr) {                                                                                               \
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2p<true, WM, NST>,                                   \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds));                         \
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2p<false, WM, NST>,                                  \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds));                         \
+            attr = true;                                                                                           \
+        }                                                                                                          \
+        if (s1) RVX_LAUNCH(t, (gemm_nt_h2p<true, WM, NST>), dim3((unsigned)g.nblocks), dim3(64 * WM), lds, g, ep.epi); \
+        else RVX_LAUNCH(t, (gemm_nt_h2p<false, WM, NST>), dim3((unsigned)g.nblocks), dim3(64 * WM), lds, g, ep.epi); \
+    } while (0)
+    if (cfg == 1) RVX_H2P(8, 3);
+    else if (cfg == 2) RVX_H2P(4, 3);
+    else if (cfg == 3) RVX_H2P(8, 2);
+    else RVX_H2P(4, 2);
+#undef RVX_H2P
 }
 
 namespace {

@@ -32,6 +32,20 @@ __device__ __forceinline__ float4 agg_op(float4 a, float4 v) {
 __device__ __forceinline__ float4 scale4(float4 v, float w) { return make_float4(v.x * w, v.y * w, v.z * w, v.w * w); }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+// v*t as f16 hi = rn(v*t) at p[0..3] and lo = rn(v*t - hi) at p[pstride..]
+__device__ __forceinline__ void split_store4(float4 v, float t, _Float16* p, int64_t pstride) {
+    const float x[4] = {v.x * t, v.y * t, v.z * t, v.w * t};
+    f16x4 hi, lo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        hi[i] = (_Float16)x[i];
+        lo[i] = (_Float16)(x[i] - (float)hi[i]);
+    }
+    *reinterpret_cast<f16x4*>(p) = hi;
+    *reinterpret_cast<f16x4*>(p + pstride) = lo;
+}
 // Gathered rows are touched once per edge at random, so they never hit in L2
 // on a large table; NT loads keep them from evicting the working set of a
 // GEMM running beside the gather.
@@ -51,7 +65,8 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
                                                       const float* __restrict__ wts, int64_t n,
                                                       const float* __restrict__ x, int dim, int empty_fill,
                                                       int post_scale, float* __restrict__ out,
-                                                      const float* __restrict__ self_x, float* __restrict__ row_scale) {
+                                                      const float* __restrict__ self_x, float* __restrict__ row_scale,
+                                                      _Float16* __restrict__ planes, int64_t pstride) {
     const int lane = threadIdx.x & 63;
     // grid-stride over rows: the grid may be capped (persistent) so the gather
     // leaves CU slots to a concurrently running GEMM
@@ -121,17 +136,33 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
     if (row_scale) {  // split-f16 GEMM operand scale over this row's aggregate and self rows
         float m = 0.0f;
         const float* sp = self_x + row * dim + 4 * lane;
+        float4 sv[NV];
 #pragma unroll
         for (int j = 0; j < NV; ++j)
             if (active[j]) {
                 const float4 v = *reinterpret_cast<const float4*>(sp + 256 * j);
+                sv[j] = v;
                 m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
                 if (cnt_total > 0)
                     m = fmaxf(m, fmaxf(fmaxf(fabsf(acc[j].x), fabsf(acc[j].y)), fmaxf(fabsf(acc[j].z), fabsf(acc[j].w))));
             }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-        if (lane == 0) row_scale[row] = h2_scale_dev(m);
+        const float t = h2_scale_dev(m);
+        if (lane == 0) row_scale[row] = t;
+        if (planes) {
+            // the GEMM operand itself: [aggregate | self] * t split into two f16
+            // planes, rounding exactly as the in-GEMM split (split_h2_pair)
+            _Float16* p0 = planes + row * 2 * dim + 4 * lane;
+#pragma unroll
+            for (int j = 0; j < NV; ++j)
+                if (active[j]) {
+                    const float4 a = cnt_total > 0 ? acc[j] : make_float4(0, 0, 0, 0);
+                    split_store4(a, t, p0 + 256 * j, pstride);
+                    split_store4(sv[j], t, p0 + dim + 256 * j, pstride);
+                }
+            continue;
+        }
     }
     if (cnt_total == 0) {
         const float* self = x + row * dim + 4 * lane;
@@ -177,22 +208,24 @@ __global__ __launch_bounds__(256) void k_aggregate_scalar(const int64_t* rp, con
 template <int AGG, bool W>
 void launch_agg(const char* t, const int64_t* rp, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
                 int empty_fill, int post_scale, float* out, int cap_per_cu, bool deep, bool nt, const float* self_x,
-                float* row_scale) {
+                float* row_scale, _Float16* planes, int64_t pstride) {
     int64_t blocks = (n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
     if (cap_per_cu > 0) blocks = std::min<int64_t>(blocks, (int64_t)cap_per_cu * device().num_cus);
     const dim3 grid((unsigned)blocks), block(256);
     const bool vec = (dim % 4 == 0) && (((uintptr_t)x & 15) == 0) && (((uintptr_t)out & 15) == 0);
+    RVX_REQUIRE(!planes || (vec && row_scale && self_x && empty_fill == 0), RVX_ERR_INVALID_SHAPE,
+                "planes need the vector gather with zero-filled empty rows");
 #define RVX_AGG_VEC(NV)                                                                                          \
     do {                                                                                                         \
         if (deep && nt)                                                                                        \
             RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 8, true>), grid, block, 0, rp, col, w, n, x, dim,         \
-                       empty_fill, post_scale, out, self_x, row_scale);                                          \
+                       empty_fill, post_scale, out, self_x, row_scale, planes, pstride);                         \
         else if (deep)                                                                                           \
             RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 8>), grid, block, 0, rp, col, w, n, x, dim, empty_fill,   \
-                       post_scale, out, self_x, row_scale);                                                      \
+                       post_scale, out, self_x, row_scale, planes, pstride);                                     \
         else                                                                                                     \
             RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 4>), grid, block, 0, rp, col, w, n, x, dim, empty_fill,   \
-                       post_scale, out, self_x, row_scale);                                                      \
+                       post_scale, out, self_x, row_scale, planes, pstride);                                     \
     } while (0)
     if (vec && dim <= 256) RVX_AGG_VEC(1);
     else if (vec && dim <= 512) RVX_AGG_VEC(2);
@@ -217,7 +250,7 @@ int g_agg_nt = env_int("RVX_AGG_NT", 1);
 
 void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
                     int agg, int empty_fill, int post_scale, float* out, const char* tag, bool overlapped,
-                    const float* self_x, float* row_scale) {
+                    const float* self_x, float* row_scale, _Float16* planes, int64_t plane_stride) {
     if (n <= 0) return;
     static const int standalone_deep = env_int("RVX_AGG_STANDALONE_DEEP", 0);  // experiment knob
     const int cap = overlapped ? g_agg_overlap_cap : 0;
@@ -227,12 +260,12 @@ void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, 
     const char* t = tag ? tag : "aggregate";
     const bool W = w != nullptr;
     switch (agg) {
-        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale)
-                        : launch_agg<AGG_SUM, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale); break;
-        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale)
-                         : launch_agg<AGG_MEAN, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale); break;
-        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale)
-                        : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale); break;
+        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride)
+                        : launch_agg<AGG_SUM, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride); break;
+        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride)
+                         : launch_agg<AGG_MEAN, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride); break;
+        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride)
+                        : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride); break;
         default: fail(RVX_ERR_INVALID_PARAMETER, "unknown aggregator");
     }
 }

@@ -45,6 +45,13 @@ bool gemm_h2_ok(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1);
 void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
                 const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
                 int64_t ldc, const char* tag);
+// Pre-split A (gemm_nt_h2p): Ah holds A*a_scale as f16 planes [2][M][lda]
+// (plane stride a_plane), phase 0 in columns [0, s0.K), phase 1 (s1) in
+// [s0.K, s0.K + s1->K); s0/s1 give K and the B planes as for gemm_nt_h2.
+bool gemm_h2p_ok(int64_t M, int N, int64_t lda, int64_t a_plane, const GemmOperand& s0, const GemmOperand* s1);
+void gemm_nt_h2p(int64_t M, int N, const _Float16* Ah, int64_t lda, int64_t a_plane, const GemmOperand& s0,
+                 const _Float16* B0h, const GemmOperand* s1, const _Float16* B1h, const float* a_scale,
+                 const float* b_inv, const GemmEpilogue& ep, float* C, int64_t ldc, const char* tag);
 // gemm_nt_h2 when every operand carries f16 planes and the shapes allow it
 // (per-row A scales computed here, row_scale_h2), else gemm_nt.
 void gemm_auto(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, const GemmEpilogue& ep, float* C,
@@ -76,6 +83,9 @@ enum { AGG_SUM = 0, AGG_MEAN = 1, AGG_MAX = 2 };
 void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, int64_t n, const float* x,
                     int dim, int agg, int empty_fill, int post_scale, float* out, const char* tag,
                     bool overlapped = false,  // true: runs beside a GEMM (capped grid)
-                    const float* self_x = nullptr, float* row_scale = nullptr);
+                    const float* self_x = nullptr, float* row_scale = nullptr,
+                    // with row_scale: write [aggregate | self] * row_scale as f16 planes
+                    // [2][n][2*dim] (plane stride plane_stride) instead of out
+                    _Float16* planes = nullptr, int64_t plane_stride = 0);
 
 }  // namespace rvx

@@ -276,6 +276,27 @@ def test_graphsage_split_f16_gemm(monkeypatch, in_f, out_f, n):
     assert_close(layer.forward_graph(x, g), ref)
 
 
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("in_f,out_f,n,deg", [(768, 768, 600, 9), (96, 232, 1000, 5), (64, 130, 257, 0),
+                                               (32, 32, 129, 3)])
+def test_graphsage_presplit_operand(monkeypatch, in_f, out_f, n, deg, cfg):
+    """The gather writing the scaled [aggregate | self] operand as f16 planes
+    (gemm_nt_h2p) gives the same bits as the in-GEMM split (gemm_nt_h2g), and
+    the oracle's values, for every tile/ring configuration (RVX_GEMM_H2P_CFG);
+    deg 0 covers all-empty neighbourhoods."""
+    monkeypatch.setenv("RVX_GEMM_H2P_CFG", cfg)
+    x = O.fill_uniform(n * in_f, 70 + n).reshape(n, in_f)
+    rp, col = O.random_csr(n, deg, 71)
+    g = rv.Graph.from_csr(rp, col)
+    layer = rv.GraphSAGELayer(in_f, out_f, num_samples=max(deg, 1))
+    monkeypatch.setenv("RVX_GEMM_H2P", "0")
+    y0 = layer.forward_graph(x, g)
+    monkeypatch.setenv("RVX_GEMM_H2P", "1")  # opt-in path
+    y = layer.forward_graph(x, g)
+    assert np.array_equal(y, y0)
+    assert_close(y, O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0))
+
+
 @pytest.mark.parametrize("scale", [1e-30, 1e-8, 1e12, 1e15])
 def test_graphsage_split_f16_operand_range(scale):
     """Power-of-two operand scaling keeps f16 in range for any f32 magnitude:
