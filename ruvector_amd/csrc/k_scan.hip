@@ -417,29 +417,38 @@ __global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs
     // with the chunk XOR-swizzled by (row >> 2) & 3 on the source address, so
     // the fragment reads below are bank-conflict free.
     int prow[2], pchunk[2];
-    int64_t qsrc[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         prow[j] = 16 * (2 * wave + j) + (lane >> 2);
         pchunk[j] = (lane & 3) ^ ((prow[j] >> 2) & 3);
-        qsrc[j] = min(q0 + prow[j], a.nq - 1) * a.d + pchunk[j] * 8;
     }
     const int nk = a.d / FK;
     const int64_t ntile = r_end > r_beg ? (r_end - r_beg + FR - 1) / FR : 0;
     const int64_t iters = ntile * nk;
-    const _Float16* fa[2];  // source rows of the tile being filled
-    const _Float16* fq[2] = {a.qh + qsrc[0], a.qh + qsrc[1]};
-    auto fill_tile = [&](int64_t t) {
+    // DMA sources as a wave-uniform base plus 32-bit per-lane offsets (rows past
+    // the end clamp to the last row), so a k-step's fill is address-add free:
+    // SGPR base + k, VGPR offset (the tile offsets change once per tile)
+    const char* qbase = reinterpret_cast<const char*>(a.qh + q0 * a.d);
+    uint32_t qoff[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fa[j] = a.xh + (min(t + prow[j], r_end - 1) - a.row0) * a.d + pchunk[j] * 8;
+    for (int j = 0; j < 2; ++j)
+        qoff[j] = (uint32_t)(((int64_t)min<int64_t>(prow[j], a.nq - 1 - q0) * a.d + pchunk[j] * 8) * 2);
+    struct TileSrc { const char* base; uint32_t off[2]; };
+    auto tile_src = [&](int64_t t) {  // t = first row of a tile in [r_beg, r_end)
+        TileSrc ts;
+        ts.base = reinterpret_cast<const char*>(a.xh + (t - a.row0) * a.d);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            ts.off[j] = (uint32_t)(((int64_t)min<int64_t>(prow[j], r_end - 1 - t) * a.d + pchunk[j] * 8) * 2);
+        return ts;
     };
-    auto fill = [&](int k0, unsigned char* dst) {
+    auto fill = [&](const TileSrc& ts, int k0, unsigned char* dst) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-            __builtin_amdgcn_global_load_lds((const void*)(fa[j] + k0),
+            __builtin_amdgcn_global_load_lds((const void*)(ts.base + k0 * 2 + ts.off[j]),
                                              (__attribute__((address_space(3))) void*)(dst + (2 * wave + j) * 1024),
                                              16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)(fq[j] + k0),
+            __builtin_amdgcn_global_load_lds((const void*)(qbase + k0 * 2 + qoff[j]),
                                              (__attribute__((address_space(3))) void*)(dst + FR * 64 +
                                                                                       (2 * wave + j) * 1024),
                                              16, 0, 0);
@@ -536,41 +545,35 @@ __global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs
         }
     };
 
-    // Ring of F_NSTAGE stages: step it reads stage it % 3 while the DMA of
-    // steps it+1 and it+2 is in flight. Each wave issues 4 DMAs per step, so
-    // vmcnt(4) retires its share of step it; the raw barrier then publishes
-    // every wave's share (barriers do not drain VMEM; __syncthreads would).
-    // The tile epilogue's own barriers drain the ring once per 128-row tile.
-    float2 pre = make_float2(NAN, 0.0f);
-    int64_t rt = r_beg, frt = r_beg;  // current tile; tile of the next fill
-    int kt = 0, fkt = 0;              // k-step of the current step; of the next fill
-    int st = 0, fst = 0;              // ring stage of the current step; of the next fill
-    auto advance_fill = [&]() {
-        if (++fkt == nk) { fkt = 0; frt += FR; fill_tile(frt); }
-        fst = fst == F_NSTAGE - 1 ? 0 : fst + 1;
-    };
+    // Ring of F_NSTAGE stages: step it reads stage it % F_NSTAGE while the DMA
+    // of the next F_NSTAGE-1 steps is in flight. Each wave issues 4 DMAs per
+    // step, so vmcnt(4 * later) retires its share of step it; the raw barrier
+    // then publishes every wave's share (barriers do not drain VMEM;
+    // __syncthreads would). Tiles are the outer loop and k-steps the inner one
+    // (unrolled by F_NSTAGE when nk is a multiple of it, so ring stages and LDS
+    // read offsets are constants): per-tile work stays out of the k-loop. The
+    // tile epilogue's own barriers drain the ring once per 128-row tile.
     __syncthreads();  // list init visible before the first epilogue
-    fill_tile(frt);
-    for (int64_t f = 0; f < F_NSTAGE - 1 && f < iters; ++f) {
-        fill(fkt * FK, fsm + fst * F_STAGE);
-        advance_fill();
-    }
-    for (int64_t it = 0; it < iters; ++it) {
-        {  // retire step it: later steps already issued may stay in flight (4 DMAs each)
-            const int64_t later = min((int64_t)F_NSTAGE - 2, iters - it - 1);
-            if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+    TileSrc cur_src = tile_src(r_beg);
+    TileSrc nxt_src = cur_src;
+#pragma unroll
+    for (int f = 0; f < F_NSTAGE - 1; ++f)
+        if (f < iters) fill(f < nk ? cur_src : tile_src(r_beg + (f / nk) * FR), (f % nk) * FK, fsm + f * F_STAGE);
+
+    // one k-step: global step it, ring stage st (fill stage fst = st - 1 mod F_NSTAGE)
+    auto kstep = [&](int64_t it, int64_t rt, int kt, int st) {
+        const int64_t later = min((int64_t)F_NSTAGE - 2, iters - it - 1);
+        if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (it + F_NSTAGE - 1 < iters) {  // the stage read in step it-1: every wave is past that read
-            fill(fkt * FK, fsm + fst * F_STAGE);
-            advance_fill();
-        }
-        if (kt == 0 && tid < FR) {  // the tile's row constants, consumed by its epilogue
-            const int64_t row = rt + tid;
-            pre = row < r_end ? a.xc[row - a.row0] : make_float2(NAN, 0.0f);
+            const int fk = kt + F_NSTAGE - 1;
+            const int fst = st == 0 ? F_NSTAGE - 1 : st - 1;
+            if (fk < nk) fill(cur_src, fk * FK, fsm + fst * F_STAGE);
+            else if (fk < 2 * nk) fill(nxt_src, (fk - nk) * FK, fsm + fst * F_STAGE);
+            else fill(tile_src(rt + (fk / nk) * FR), (fk % nk) * FK, fsm + fst * F_STAGE);  // d < 64
         }
         const unsigned char* cur = fsm + st * F_STAGE;
 #pragma unroll
@@ -587,21 +590,36 @@ __global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs
                 for (int fn = 0; fn < 2; ++fn)
                     acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
         }
-#ifdef RVX_ABLATE_EPI
-        if (kt == nk - 1 && it + 1 == iters) {
-#else
-        if (kt == nk - 1) {
-#endif
-            epilogue(rt, pre);
+    };
+
+    const bool unrolled = nk % F_NSTAGE == 0;  // every tile starts on ring stage 0
+    int st = 0;
+    int64_t it = 0;
+    for (int64_t rt = r_beg; rt < r_end; rt += FR) {
+        // the tile's row constants, consumed by its epilogue
+        const float2 pre = (tid < FR && rt + tid < r_end) ? a.xc[rt + tid - a.row0] : make_float2(NAN, 0.0f);
+        if (rt + FR < r_end) nxt_src = tile_src(rt + FR);
+        if (unrolled) {
+            for (int kt = 0; kt < nk; kt += F_NSTAGE, it += F_NSTAGE)
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+                for (int u = 0; u < F_NSTAGE; ++u) kstep(it + u, rt, kt + u, u);
+        } else {
+            for (int kt = 0; kt < nk; ++kt, ++it) {
+                kstep(it, rt, kt, st);
+                st = st == F_NSTAGE - 1 ? 0 : st + 1;
+            }
         }
-        if (++kt == nk) { kt = 0; rt += FR; }
-        st = st == F_NSTAGE - 1 ? 0 : st + 1;
+#ifdef RVX_ABLATE_EPI
+        if (rt + FR >= r_end)
+#endif
+        epilogue(rt, pre);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+        cur_src = nxt_src;
     }
     __syncthreads();
 
