@@ -338,18 +338,28 @@ typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int FQ = 128, FR = 128, FK = 32;  // queries x rows per tile, K per stage
+#ifndef RVX_SCAN_WIDE
+#define RVX_SCAN_WIDE 1  // 256 x 256 tiles, 8 waves, one block per CU (0: 128 x 128, 4 waves, two blocks)
+#endif
 #ifndef RVX_SCAN_FKP
 #define RVX_SCAN_FKP 16
 #define RVX_SCAN_FCB 8
 #define RVX_SCAN_NSTAGE 3
-#define RVX_SCAN_BLOCKS 2
+#define RVX_SCAN_BLOCKS (RVX_SCAN_WIDE ? 1 : 2)
 #endif
+// Waves 2 (rows) x F_WQ (queries); each wave F_FM x 2 accumulators of 32 x 32
+// (rows x queries). Each wave DMAs 2 row pieces and 2 query pieces (16 rows x
+// 64 B each) per k-step, so FR = FQ = 32 x waves. The wide tile halves the
+// L2->LDS bytes per MFMA of the 128 x 128 one (the filter is L2-bound there).
+constexpr int F_WQ = RVX_SCAN_WIDE ? 4 : 2, F_FM = RVX_SCAN_WIDE ? 4 : 2;
+constexpr int F_THREADS = 64 * 2 * F_WQ;
+constexpr int FQ = 64 * F_WQ, FR = 64 * F_FM, FK = 32;  // queries x rows per tile, K per stage
+static_assert(FQ == FR && FR == 32 * F_THREADS / 64, "DMA pieces assume FR = FQ = 32 x waves");
 constexpr int FKP = RVX_SCAN_FKP;           // list length per (query, split)
 constexpr int FCB = RVX_SCAN_FCB;           // candidate slots per query per merge round
 constexpr int F_STAGE = (FR + FQ) * FK * 2;  // 16 KB: f16 rows then f16 queries, 64 B per row
 constexpr int F_NSTAGE = RVX_SCAN_NSTAGE;   // LDS-DMA ring: F_NSTAGE - 1 k-steps in flight across the barrier
-constexpr int F_LDS = F_NSTAGE * F_STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 8;  // 74.5 KB: 2 blocks / CU
+constexpr int F_LDS = F_NSTAGE * F_STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 8;  // 74.5 KB (2 blocks / CU) or 149 KB (wide)
 constexpr int F_MAXE = 16;                  // rerank: list entries per lane (nsplit_total * FKP <= 64 * F_MAXE)
 
 struct FilterArgs {
@@ -373,7 +383,7 @@ __device__ __forceinline__ float approx_value(float acc, float xi, float qi, flo
 __device__ __forceinline__ bool lt_vr(float v, int r, float bv, int br) { return v < bv || (v == bv && r < br); }
 
 template <int METRIC>
-__global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs a) {
+__global__ __launch_bounds__(F_THREADS, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
     float* best_v = reinterpret_cast<float*>(fsm + F_NSTAGE * F_STAGE);  // [FQ][FKP] ascending (v, row)
     int32_t* best_r = reinterpret_cast<int32_t*>(best_v + FQ * FKP);
@@ -396,7 +406,7 @@ __global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs
 
     float2* rowc = reinterpret_cast<float2*>(ovf + 4);              // [FR] current tile's row constants
 
-    for (int i = tid; i < FQ * FKP; i += 256) { best_v[i] = INFINITY; best_r[i] = -1; }
+    for (int i = tid; i < FQ * FKP; i += F_THREADS) { best_v[i] = INFINITY; best_r[i] = -1; }
     if (tid < FQ) { cand_n[tid] = 0; thr[tid] = INFINITY; fillc[tid] = 0; }
     if (tid < 2) ovf[tid] = 0;
 
@@ -454,20 +464,24 @@ __global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs
                                              16, 0, 0);
         }
     };
-    int a_rd[2][2], b_rd[2][2];
+    constexpr int WROWS = 32 * F_FM;  // rows per wave
+    int a_rd[F_FM][2], b_rd[2][2];
+#pragma unroll
+    for (int f = 0; f < F_FM; ++f) {
+        const int ra = wm * WROWS + f * 32 + lr;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) a_rd[f][ks] = ra * 64 + (((2 * ks + lh) ^ ((ra >> 2) & 3)) << 4);
+    }
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
-        const int ra = wm * 64 + f * 32 + lr, rb = wn * 64 + f * 32 + lr;
+        const int rb = wn * 64 + f * 32 + lr;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            a_rd[f][ks] = ra * 64 + (((2 * ks + lh) ^ ((ra >> 2) & 3)) << 4);
-            b_rd[f][ks] = FR * 64 + rb * 64 + (((2 * ks + lh) ^ ((rb >> 2) & 3)) << 4);
-        }
+        for (int ks = 0; ks < 2; ++ks) b_rd[f][ks] = FR * 64 + rb * 64 + (((2 * ks + lh) ^ ((rb >> 2) & 3)) << 4);
     }
 
-    f32x16 acc[2][2];
+    f32x16 acc[F_FM][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < F_FM; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -483,10 +497,10 @@ __global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs
         if (tid < FR) rowc[tid] = pre;
         __syncthreads();
 #pragma unroll
-        for (int fm = 0; fm < 2; ++fm)
+        for (int fm = 0; fm < F_FM; ++fm)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                const float2 c = rowc[wm * 64 + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh];
+                const float2 c = rowc[wm * WROWS + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh];
                 const bool rv = !__builtin_isnan(c.x);  // past the split, or deleted
                 const float xs = (METRIC == RVX_METRIC_L2) ? c.y : 0.0f;
                 const float xn = (METRIC == RVX_METRIC_COSINE) ? c.y : 0.0f;
@@ -502,7 +516,7 @@ __global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs
                 const int ql = wn * 64 + fn * 32 + lr;
                 const float t = thr[ql];
 #pragma unroll
-                for (int fm = 0; fm < 2; ++fm)
+                for (int fm = 0; fm < F_FM; ++fm)
 #pragma unroll
                     for (int e = 0; e < 16; ++e) {
                         const float v = acc[fm][fn][e];
@@ -511,7 +525,7 @@ __global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs
                         if (slot < FCB) {
                             cand_v[ql * FCB + slot] = v;
                             cand_r[ql * FCB + slot] =
-                                (int32_t)(rt + wm * 64 + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh);
+                                (int32_t)(rt + wm * WROWS + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh);
                             acc[fm][fn][e] = INFINITY;
                         } else {
                             ovf[round & 1] = 1;
@@ -578,14 +592,15 @@ __global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs
         const unsigned char* cur = fsm + st * F_STAGE;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            h16x8 af[2], bf[2];
+            h16x8 af[F_FM], bf[2];
 #pragma unroll
-            for (int f = 0; f < 2; ++f) {
+            for (int f = 0; f < F_FM; ++f)
                 af[f] = __builtin_bit_cast(h16x8, *reinterpret_cast<const u32x4*>(cur + a_rd[f][ks]));
-                bf[f] = __builtin_bit_cast(h16x8, *reinterpret_cast<const u32x4*>(cur + b_rd[f][ks]));
-            }
 #pragma unroll
-            for (int fm = 0; fm < 2; ++fm)
+            for (int f = 0; f < 2; ++f)
+                bf[f] = __builtin_bit_cast(h16x8, *reinterpret_cast<const u32x4*>(cur + b_rd[f][ks]));
+#pragma unroll
+            for (int fm = 0; fm < F_FM; ++fm)
 #pragma unroll
                 for (int fn = 0; fn < 2; ++fn)
                     acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
@@ -614,7 +629,7 @@ __global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs
 #endif
         epilogue(rt, pre);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < F_FM; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -623,7 +638,7 @@ __global__ __launch_bounds__(256, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs
     }
     __syncthreads();
 
-    for (int i = tid; i < FQ * FKP; i += 256) {
+    for (int i = tid; i < FQ * FKP; i += F_THREADS) {
         const int64_t qg = q0 + i / FKP;
         if (qg >= a.nq) continue;
         const int64_t o = (qg * a.nsplit_total + a.split0 + sl) * FKP + (i % FKP);
@@ -874,9 +889,9 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
                       part_v, part_r};
         const dim3 grid((unsigned)(qtiles * s_c));
         switch (metric) {
-            case RVX_METRIC_L2: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_L2>, grid, dim3(256), F_LDS, fa); break;
-            case RVX_METRIC_COSINE: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_COSINE>, grid, dim3(256), F_LDS, fa); break;
-            default: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_DOT>, grid, dim3(256), F_LDS, fa); break;
+            case RVX_METRIC_L2: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_L2>, grid, dim3(F_THREADS), F_LDS, fa); break;
+            case RVX_METRIC_COSINE: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_COSINE>, grid, dim3(F_THREADS), F_LDS, fa); break;
+            default: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_DOT>, grid, dim3(F_THREADS), F_LDS, fa); break;
         }
     }
     RerankArgs ra{q, qnorm, qc, x, xnorm, nq, d, k, nsplit_total, part_v, part_r, max_bits, id_offset, out_d, out_i,
