@@ -45,7 +45,10 @@ __device__ __forceinline__ float finish_dist(float acc, float qn, float xn) {
 // accumulates (one load at a time would expose a memory round trip per 16 B
 // of a 3 KB row). Q_GLOBAL: the other operand is a stored row too (pair_dist)
 // and is streamed the same way; otherwise it is read at use (LDS).
-constexpr int ROW_BATCH = 8;  // float4s per batch
+#ifndef RVX_ROW_BATCH
+#define RVX_ROW_BATCH 8
+#endif
+constexpr int ROW_BATCH = RVX_ROW_BATCH;  // float4s per batch
 
 template <int METRIC, bool Q_GLOBAL>
 __device__ __forceinline__ float stream_acc(const float* __restrict__ qs, const float* __restrict__ x, int n4) {

@@ -50,7 +50,10 @@ struct SearchArgs {
 };
 
 template <int METRIC>
-__global__ __launch_bounds__(64) void k_hnsw_search(SearchArgs a) {
+#ifndef RVX_HNSW_WPE
+#define RVX_HNSW_WPE
+#endif
+__global__ __launch_bounds__(64) RVX_HNSW_WPE void k_hnsw_search(SearchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int lane = threadIdx.x;
     const int ef = a.ef;
