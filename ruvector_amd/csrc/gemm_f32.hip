@@ -772,14 +772,13 @@ __device__ __forceinline__ void split_h2_pair(float a0, float a1, float sc, unsi
 }
 
 template <bool DUAL>
-__global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
+__device__ __forceinline__ void h2g_tile(const GemmArgs& g, int epi, int64_t bid) {
     constexpr int XA = 128 * 128;             // f32 A tile bytes per stage
     constexpr int STG = XA + 2 * XB_PLANE;    // 32 KB stage
     constexpr int NB = 4;                     // B DMA pieces per wave (2 planes x 8 pieces)
     extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
 
     const int64_t nwg = g.nblocks;
-    const int64_t bid = blockIdx.x;
     const int64_t xcd = bid % 8, q = nwg / 8, r = nwg % 8;
     const int64_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
     const int64_t tm = wgid / g.tiles_n;
@@ -1133,6 +1132,16 @@ __global__ __launch_bounds__(64 * WM, WM == 4 && NST == 2 ? 2 : 1) void gemm_nt_
     }
 }
 
+// One tile per block, or (grid capped below the tile count, RVX_GEMM_CAP) a
+// persistent grid striding over the tiles in XCD-mapped order.
+template <bool DUAL>
+__global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
+    for (int64_t b = blockIdx.x; b < g.nblocks; b += gridDim.x) {
+        h2g_tile<DUAL>(g, epi, b);
+        if (b + gridDim.x < g.nblocks) __syncthreads();  // LDS stages are reused by the next tile
+    }
+}
+
 // B rows n of one or two [N][K] matrices: common scale t_n, f16 planes of each
 // (plane stride N*K), inv[n] = 1 / t_n. One wave per row.
 __global__ __launch_bounds__(256) void k_split_h2_rows(const float* __restrict__ B0, const float* __restrict__ B1,
@@ -1310,8 +1319,13 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
         attr = true;
     }
     const char* t = tag ? tag : "gemm_nt_h2";
-    if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)g.nblocks), dim3(256), lds, g, ep.epi);
-    else RVX_LAUNCH(t, gemm_nt_h2g<false>, dim3((unsigned)g.nblocks), dim3(256), lds, g, ep.epi);
+    // RVX_GEMM_CAP > 0: persistent grid of that many blocks per CU (a multiple of 8
+    // blocks, so a block keeps its XCD across the tiles it strides over)
+    const int cap = env_int("RVX_GEMM_CAP", 2);  // 2 = every resident slot, no block turnover (scripts/exp_gemm_cap.sh)
+    int64_t grid = g.nblocks;
+    if (cap > 0) grid = std::min<int64_t>(grid, ((int64_t)cap * device().num_cus + 7) / 8 * 8);
+    if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
+    else RVX_LAUNCH(t, gemm_nt_h2g<false>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
 }
 
 bool gemm_h2p_ok(int64_t M, int N, int64_t lda, int64_t a_plane, const GemmOperand& s0, const GemmOperand* s1) {
