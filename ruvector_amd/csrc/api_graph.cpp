@@ -207,7 +207,8 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
                        l->ws_x3.as<uint16_t>(), plane};
         if (h2)
             gemm_nt_h2(rows, l->out, s0, l->wn_h2.as<_Float16>(), &s1, l->ws_h2.as<_Float16>(), scale + r0,
-                       l->w_inv.as<float>(), ep, y + r0 * l->out, l->out, "sage_gemm");
+                       l->w_inv.as<float>(), ep, y + r0 * l->out, l->out, "sage_gemm",
+                       chunks > 1 ? env_int("RVX_SAGE_GEMM_CAP", 2) : -1);
         else
             gemm_nt(rows, l->out, s0, &s1, ep, y + r0 * l->out, l->out, "sage_gemm");
         if (l->normalize) normalize_rows(y + r0 * l->out, rows, l->out, true, "sage_normalize");

@@ -1294,7 +1294,7 @@ bool gemm_h2_ok(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1) 
 
 void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
                 const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
-                int64_t ldc, const char* tag) {
+                int64_t ldc, const char* tag, int persist) {
     if (M <= 0 || N <= 0) return;
     GemmArgs g{};
     g.addend = ep.addend;
@@ -1319,9 +1319,12 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
         attr = true;
     }
     const char* t = tag ? tag : "gemm_nt_h2";
-    // RVX_GEMM_CAP > 0: persistent grid of that many blocks per CU (a multiple of 8
-    // blocks, so a block keeps its XCD across the tiles it strides over)
-    const int cap = env_int("RVX_GEMM_CAP", 2);  // 2 = every resident slot, no block turnover (scripts/exp_gemm_cap.sh)
+    // persistent grid of `cap` blocks per CU (a multiple of 8 blocks, so a block
+    // keeps its XCD across the tiles it strides over). The overlapped GraphSAGE
+    // GEMM asks for 2 (every resident slot, no block turnover beside the gather:
+    // +2% per step, scripts/exp_gemm_cap.sh); standalone GEMMs are 6-13% faster
+    // with one block per tile (C4 layer GEMMs), so that stays the default.
+    const int cap = persist >= 0 ? persist : env_int("RVX_GEMM_CAP", 0);
     int64_t grid = g.nblocks;
     if (cap > 0) grid = std::min<int64_t>(grid, ((int64_t)cap * device().num_cus + 7) / 8 * 8);
     if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);

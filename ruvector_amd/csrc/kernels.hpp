@@ -42,9 +42,10 @@ void split_x3(const float* src, int64_t n, uint16_t* dst);
 // (powers of two from aggregate_rows' row_scale), B given as two f16 planes
 // ([2][N][K], from split_h2_rows) with b_inv[n] its inverse column scale.
 bool gemm_h2_ok(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1);
+// persist: blocks per CU of a persistent grid (0 = one block per tile; -1 = RVX_GEMM_CAP, default 0)
 void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
                 const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
-                int64_t ldc, const char* tag);
+                int64_t ldc, const char* tag, int persist = -1);
 // Pre-split A (gemm_nt_h2p): Ah holds A*a_scale as f16 planes [2][M][lda]
 // (plane stride a_plane), phase 0 in columns [0, s0.K), phase 1 (s1) in
 // [s0.K, s0.K + s1->K); s0/s1 give K and the B planes as for gemm_nt_h2.

@@ -1,4 +1,4 @@
-# Interleaved repeats: persistent split-f16 GEMM grid (RVX_GEMM_CAP blocks per CU) beside the gather, 10M x 768 GraphSAGE.
+# Interleaved repeats: persistent split-f16 GEMM grid (RVX_SAGE_GEMM_CAP blocks per CU) beside the gather, 10M x 768 GraphSAGE.
 set -u
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
@@ -10,6 +10,6 @@ import json,sys; d=json.loads(sys.stdin.read()); k=d.get('kernel_ms',{})
 print(round(d['value']/1e6), 'Medges/s', d['ms_per_step'], 'ms', {n: v for n, v in k.items() if 'gemm' in n or 'agg' in n})"
 }
 for rep in 1 2 3; do
-  run cap0_$rep RVX_GEMM_CAP=0
-  run cap2_$rep RVX_GEMM_CAP=2
+  run cap0_$rep RVX_SAGE_GEMM_CAP=0
+  run cap2_$rep RVX_SAGE_GEMM_CAP=2
 done
