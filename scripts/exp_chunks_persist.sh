@@ -1,0 +1,17 @@
+# Interleaved repeats: row-chunk count with the persistent overlapped GEMM (10M x 768 GraphSAGE).
+set -u
+cd "${GRAFT_REPO_ROOT}"
+mkdir -p gpurun_out
+run() {
+  local label=$1; shift
+  env "$@" timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu --no-hnsw --no-scan > gpurun_out/sw_$label.log 2>&1 || { tail -5 gpurun_out/sw_$label.log; exit 1; }
+  echo -n "$label: "; tail -1 gpurun_out/sw_$label.log | python -c "
+import json,sys; d=json.loads(sys.stdin.read()); k=d.get('kernel_ms',{})
+print(round(d['value']/1e6), 'Medges/s', d['ms_per_step'], 'ms', {n: v for n, v in k.items() if 'gemm' in n or 'agg' in n})"
+}
+for rep in 1 2; do
+  run c16_$rep RVX_SAGE_CHUNKS=16
+  run c24_$rep RVX_SAGE_CHUNKS=24
+  run c32_$rep RVX_SAGE_CHUNKS=32
+  run c48_$rep RVX_SAGE_CHUNKS=48
+done
