@@ -29,7 +29,8 @@ def run(n=10_000_000, d=768, nq=10_000, k=10, metric_name="l2", cpu_queries=16, 
         x_seed=5):
     """xb: an HBM-resident [n][d] f32 table to search (default: N(0,1) rows, seed x_seed)."""
     import ruvector_amd as rv
-    metric = {"l2": rv.DistanceMetric.Euclidean, "cosine": rv.DistanceMetric.Cosine}[metric_name]
+    metric = {"l2": rv.DistanceMetric.Euclidean, "cosine": rv.DistanceMetric.Cosine,
+              "dot": rv.DistanceMetric.DotProduct}[metric_name]
     if xb is None:
         xb = rv.Buffer(n * d * 4)
         xb.fill_normal(n * d, x_seed)

@@ -338,28 +338,32 @@ typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-#ifndef RVX_SCAN_WIDE
-#define RVX_SCAN_WIDE 1  // 256 x 256 tiles, 8 waves, one block per CU (0: 128 x 128, 4 waves, two blocks)
-#endif
 #ifndef RVX_SCAN_FKP
 #define RVX_SCAN_FKP 16
 #define RVX_SCAN_FCB 8
 #define RVX_SCAN_NSTAGE 3
-#define RVX_SCAN_BLOCKS (RVX_SCAN_WIDE ? 1 : 2)
 #endif
-// Waves 2 (rows) x F_WQ (queries); each wave F_FM x 2 accumulators of 32 x 32
-// (rows x queries). Each wave DMAs 2 row pieces and 2 query pieces (16 rows x
-// 64 B each) per k-step, so FR = FQ = 32 x waves. The wide tile halves the
-// L2->LDS bytes per MFMA of the 128 x 128 one (the filter is L2-bound there).
-constexpr int F_WQ = RVX_SCAN_WIDE ? 4 : 2, F_FM = RVX_SCAN_WIDE ? 4 : 2;
-constexpr int F_THREADS = 64 * 2 * F_WQ;
-constexpr int FQ = 64 * F_WQ, FR = 64 * F_FM, FK = 32;  // queries x rows per tile, K per stage
-static_assert(FQ == FR && FR == 32 * F_THREADS / 64, "DMA pieces assume FR = FQ = 32 x waves");
+constexpr int FK = 32;                      // K per stage
 constexpr int FKP = RVX_SCAN_FKP;           // list length per (query, split)
 constexpr int FCB = RVX_SCAN_FCB;           // candidate slots per query per merge round
-constexpr int F_STAGE = (FR + FQ) * FK * 2;  // 16 KB: f16 rows then f16 queries, 64 B per row
 constexpr int F_NSTAGE = RVX_SCAN_NSTAGE;   // LDS-DMA ring: F_NSTAGE - 1 k-steps in flight across the barrier
-constexpr int F_LDS = F_NSTAGE * F_STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 8;  // 74.5 KB (2 blocks / CU) or 149 KB (wide)
+// Tile shapes. Waves 2 (rows) x WQ (queries); each wave FM x 2 accumulators of
+// 32 x 32 (rows x queries). Each wave DMAs 2 row pieces and 2 query pieces (16
+// rows x 64 B each) per k-step, so FR = FQ = 32 x waves.
+//   WIDE: 256 x 256, 8 waves, one block per CU (149 KB LDS) — half the L2->LDS
+//         bytes per MFMA; taken for d >= 512 (10M x 768: 78.6 -> 64.3 ms per launch)
+//   else: 128 x 128, 4 waves, two blocks per CU (74.5 KB) — shorter tile
+//         epilogues for short rows (100k x 128: 3.8 vs 5.7 ms)
+template <bool WIDE>
+struct FCfg {
+    static constexpr int WQ = WIDE ? 4 : 2, FM = WIDE ? 4 : 2;
+    static constexpr int THREADS = 64 * 2 * WQ;
+    static constexpr int FQ = 64 * WQ, FR = 64 * FM;
+    static constexpr int STAGE = (FR + FQ) * FK * 2;  // f16 rows then f16 queries, 64 B per row
+    static constexpr int LDS = F_NSTAGE * STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 8;
+    static constexpr int BLOCKS = WIDE ? 1 : 2;
+    static_assert(FQ == FR && FR == 32 * THREADS / 64, "DMA pieces assume FR = FQ = 32 x waves");
+};
 constexpr int F_MAXE = 16;                  // rerank: list entries per lane (nsplit_total * FKP <= 64 * F_MAXE)
 
 struct FilterArgs {
@@ -382,8 +386,10 @@ __device__ __forceinline__ float approx_value(float acc, float xi, float qi, flo
 
 __device__ __forceinline__ bool lt_vr(float v, int r, float bv, int br) { return v < bv || (v == bv && r < br); }
 
-template <int METRIC>
-__global__ __launch_bounds__(F_THREADS, RVX_SCAN_BLOCKS) void k_scan_filter(FilterArgs a) {
+template <int METRIC, bool WIDE>
+__global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_scan_filter(FilterArgs a) {
+    using Cf = FCfg<WIDE>;
+    constexpr int FQ = Cf::FQ, FR = Cf::FR, F_STAGE = Cf::STAGE, F_FM = Cf::FM, F_THREADS = Cf::THREADS;
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
     float* best_v = reinterpret_cast<float*>(fsm + F_NSTAGE * F_STAGE);  // [FQ][FKP] ascending (v, row)
     int32_t* best_r = reinterpret_cast<int32_t*>(best_v + FQ * FKP);
@@ -844,6 +850,12 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     const int mode = env_int("RVX_SCAN_MFMA", 1);  // 0 off, 1 auto, 2 force (tests); read per call
     if (mode == 0) return false;
     if (metric != RVX_METRIC_L2 && metric != RVX_METRIC_COSINE && metric != RVX_METRIC_DOT) return false;
+    // tile shape: RVX_SCAN_WIDE 0/1 forces it (tests), else 256^2 for d >= 512
+    const int wide_env = env_int("RVX_SCAN_WIDE", -1);
+    const bool wide = wide_env >= 0 ? wide_env != 0 : d >= 512;
+    const int FR = wide ? FCfg<true>::FR : FCfg<false>::FR, FQ = wide ? FCfg<true>::FQ : FCfg<false>::FQ;
+    const int F_LDS = wide ? FCfg<true>::LDS : FCfg<false>::LDS;
+    const int F_THREADS = wide ? FCfg<true>::THREADS : FCfg<false>::THREADS;
     if (d % FK != 0 || k > FKP || n >= ((int64_t)1 << 31) - FR || nq <= 0 || n <= 0) return false;
     if (metric == RVX_METRIC_COSINE && (!qnorm || !xnorm)) return false;
     if (mode == 1 && (nq < 256 || n < 65536)) return false;
@@ -874,9 +886,11 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
 
     static bool attr = false;
     if (!attr) {
-        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS));
-        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS));
-        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, F_LDS));
+#define RVX_FILTER_ATTR(M, W) \
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<M, W>, hipFuncAttributeMaxDynamicSharedMemorySize, FCfg<W>::LDS))
+        RVX_FILTER_ATTR(RVX_METRIC_L2, true); RVX_FILTER_ATTR(RVX_METRIC_COSINE, true); RVX_FILTER_ATTR(RVX_METRIC_DOT, true);
+        RVX_FILTER_ATTR(RVX_METRIC_L2, false); RVX_FILTER_ATTR(RVX_METRIC_COSINE, false); RVX_FILTER_ATTR(RVX_METRIC_DOT, false);
+#undef RVX_FILTER_ATTR
         attr = true;
     }
     const bool cos = metric == RVX_METRIC_COSINE;
@@ -888,10 +902,19 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
         FilterArgs fa{xh, xc, qh, qc, nq, c0, c1, d, rows_per_split, (int)(c * s_c), (int)qtiles, nsplit_total,
                       part_v, part_r};
         const dim3 grid((unsigned)(qtiles * s_c));
-        switch (metric) {
-            case RVX_METRIC_L2: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_L2>, grid, dim3(F_THREADS), F_LDS, fa); break;
-            case RVX_METRIC_COSINE: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_COSINE>, grid, dim3(F_THREADS), F_LDS, fa); break;
-            default: RVX_LAUNCH("scan_filter", k_scan_filter<RVX_METRIC_DOT>, grid, dim3(F_THREADS), F_LDS, fa); break;
+        const dim3 blk((unsigned)F_THREADS);
+        if (wide) {
+            switch (metric) {
+                case RVX_METRIC_L2: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, true>), grid, blk, F_LDS, fa); break;
+                case RVX_METRIC_COSINE: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, true>), grid, blk, F_LDS, fa); break;
+                default: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, true>), grid, blk, F_LDS, fa); break;
+            }
+        } else {
+            switch (metric) {
+                case RVX_METRIC_L2: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, false>), grid, blk, F_LDS, fa); break;
+                case RVX_METRIC_COSINE: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, false>), grid, blk, F_LDS, fa); break;
+                default: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, false>), grid, blk, F_LDS, fa); break;
+            }
         }
     }
     RerankArgs ra{q, qnorm, qc, x, xnorm, nq, d, k, nsplit_total, part_v, part_r, max_bits, id_offset, out_d, out_i,

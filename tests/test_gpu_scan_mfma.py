@@ -46,6 +46,28 @@ def test_forced_filter_bit_exact(monkeypatch, metric, name, k):
     assert np.array_equal(dist, rd)
 
 
+@pytest.mark.parametrize("wide", ["0", "1"])
+@pytest.mark.parametrize("metric,name", METRICS)
+@pytest.mark.parametrize("d", [32, 96, 256, 768])
+def test_tile_shapes_bit_exact(monkeypatch, wide, metric, name, d):
+    """Both filter tile shapes (128^2 and 256^2, RVX_SCAN_WIDE) at depths that take
+    the ring's unrolled k-loop (d/32 a multiple of 3), the generic one, and d < 64
+    (fills two tiles ahead); ragged row and query counts."""
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    monkeypatch.setenv("RVX_SCAN_WIDE", wide)
+    n, nq = 9001, 300
+    x = normal(n, d, 50 + d)
+    q = normal(nq, d, 51 + d)
+    ids, dist = flat(x, metric).brute_force_array(q, 10)
+    st = rv.scan_last_stats()
+    # a query whose split list fills below its k-th value + 2 eps cannot be proven
+    # complete and is re-run on the VALU scan (cosine's eps window is wide at this n)
+    assert st["mfma"] == nq and st["fallback"] <= 3, st
+    rids, rd = O.flat_search(x, q, 10, name)
+    assert np.array_equal(ids.astype(np.int64), rids)
+    assert np.array_equal(dist, rd)
+
+
 @pytest.mark.parametrize("metric,name", METRICS)
 def test_chunked_conversion_and_flat_search(monkeypatch, metric, name):
     monkeypatch.setenv("RVX_SCAN_MFMA", "2")
