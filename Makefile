@@ -14,6 +14,11 @@ LDFLAGS  := -shared --offload-arch=$(ARCH) -L/opt/rocm/lib -lamdhip64 -lrccl -Wl
 SRCS := $(wildcard $(CSRC)/*.cpp) $(wildcard $(CSRC)/*.hip)
 OBJS := $(patsubst $(CSRC)/%,$(BUILD)/%.o,$(SRCS))
 HDRS := $(wildcard $(CSRC)/*.hpp) include/rvx/rvx.h
+# Binary provenance: sha256 over every source the library is built from (sorted
+# paths, contents concatenated), compiled into rvx_version(); ruvector_amd
+# recomputes it from the shipped sources and refuses a stale librvx.so.
+PROV := $(sort $(SRCS) $(HDRS))
+SRC_HASH = $(shell cat $(PROV) | sha256sum | cut -c1-16)
 
 LIB := ruvector_amd/librvx.so
 
@@ -22,6 +27,11 @@ all: $(LIB) oracle
 $(BUILD)/%.o: $(CSRC)/% $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+# runtime.cpp carries the source hash, so it rebuilds whenever any source changes
+$(BUILD)/runtime.cpp.o: $(CSRC)/runtime.cpp $(SRCS) $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DRVX_SRC_HASH=\"$(SRC_HASH)\" -x hip -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) $(LDFLAGS) -o $@ $(OBJS)

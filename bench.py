@@ -182,6 +182,7 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+        "gemm_dtype": "split-f16x3" if GEMM_H2 else "split-bf16x6" if GEMM_X3 else "fp32",
         "gemm": GEMM_DESC,
         "data": "synthetic: X ~ N(0,1) Box-Muller on device (seed 3); uniform random out-degree CSR (seed 4); "
                 "GraphSAGE deterministic init (graphsage.rs:56-78)",
@@ -197,7 +198,9 @@ def main():
     }
 
     if rank == 0 and world == 1 and not a.no_cpu:
-        line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, tables[0], n_tot, d, deg)
+        line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, tables, n_tot, d, deg, layers)
+    if world == 1:
+        line["gemm_paths"] = gemm_alternatives(g, x, tables[0], off_ptr, d, deg)
     if not a.no_scan:
         del tables, g
         line["exact_scan"] = scan_leg(a, x, n_tot, d, rank, world, dist)
@@ -280,13 +283,49 @@ def attach_pmc_traffic(rls, cfg):
             r["traffic_source"] = "rocprofv3 --pmc (HBM bytes per launch; MFMA-bound kernel)"
 
 
-def cpu_baseline(a, x_buf, g, h1_buf, n, d, deg):
-    """Oracle (reference algorithm, C++) on a bounded sample of layer-1 rows;
-    h1_buf holds the GPU's layer-1 output of the last timed step."""
+def gemm_alternatives(g, x, y, off_ptr, d, deg):
+    """One GraphSAGE layer (layer 1 of the bench, same graph and input) with each GEMM
+    path, to put the default split-f16x3 timing beside the split-bf16 (exact 3-way
+    bf16 split, 6 products) and FP32-MFMA ones: ms per layer, averaged over 2 runs
+    after one warm-up. Default path first so the three numbers come from one box state."""
+    import ruvector_amd as rv
+    layer = rv.GraphSAGELayer(d, d, num_samples=deg)
+    out = {}
+    for name, env in (("split-f16x3", {}), ("split-bf16x6", {"RVX_GEMM_H2": "0"}),
+                      ("fp32-mfma", {"RVX_GEMM_H2": "0", "RVX_GEMM_X3": "0"})):
+        old = {k: os.environ.get(k) for k in ("RVX_GEMM_H2", "RVX_GEMM_X3")}
+        os.environ.update(env)
+        try:
+            ts = []
+            for i in range(3):
+                rv.synchronize()
+                t0 = time.perf_counter()
+                rv._lib.call("rvx_sage_forward_exchange", layer._h, g.handle, x.handle, y.handle, off_ptr, None, 0)
+                rv.synchronize()
+                if i:
+                    ts.append(time.perf_counter() - t0)
+            out[name] = {"layer_ms": round(sum(ts) / len(ts) * 1e3, 2)}
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    return out
+
+
+def cpu_baseline(a, x_buf, g, tables, n, d, deg, layers):
+    """Oracle (reference algorithm, C++) on a bounded sample of layer-1 rows, plus
+    per-layer parity of every layer: tables[i] holds the GPU's layer-(i+1) output of
+    the last timed step; layer i+1 > 1 is checked on rows 0..8191 from the GPU's own
+    layer-i rows (gathered from HBM), so each layer is compared on its actual input.
+    The reference's GraphSAGE (graphsage.rs:105-115 linear_transform) is plain Rust
+    loops with sequential f32 sums, so the scalar-order oracle is its CPU speed."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
+    from benchutil import host_threads
 
-    threads = min(16, os.cpu_count() or 1)
+    threads, tinfo = host_threads()
     x = x_buf.download(np.float32, (n, d))
     rp, col = O.random_csr(n, deg, 4)
     wn, ws = O.sage_init(d, d, 0), O.sage_init(d, d, 1000)
@@ -298,12 +337,25 @@ def cpu_baseline(a, x_buf, g, h1_buf, n, d, deg):
     t0 = time.perf_counter()
     ref = O.sage_forward(x, rp, col, wn, ws, rows=(0, rows), threads=threads)
     dt = time.perf_counter() - t0
-    got = h1_buf.download(np.float32, (rows, d))
+    del x
+    got = tables[0].gather_rows(n, d, np.arange(rows))
     err = float(np.max(np.abs(got.astype(np.float64) - ref)) / max(float(np.max(np.abs(ref))), 1e-30))
-    cpu = {"value": round(rows * deg / dt, 1), "unit": "edges/s", "cores": threads, "kind": "port",
-           "sample": f"oracle GraphSAGE-mean layer 1 (graphsage.rs:118-187 restated, AVX2, {threads} threads) on "
-                     f"rows 0..{rows} of the same {n} x {d} graph, {dt:.1f} s"}
-    parity = {"rows": rows, "max_rel_err": err, "tol": 1e-5, "ok": err <= 1e-5}
+    del got, ref
+    cpu = {"value": round(rows * deg / dt, 1), "unit": "edges/s", "cores": threads, "kind": "port", "host": tinfo,
+           "sample": f"oracle GraphSAGE-mean layer 1 (graphsage.rs:118-187 restated in the reference's scalar order, "
+                     f"{threads} threads) on rows 0..{rows} of the same {n} x {d} graph, {dt:.1f} s"}
+    per_layer = [{"layer": 1, "rows": rows, "max_rel_err": err, "input": "x"}]
+    r2 = min(n, 8192)
+    for li in range(1, layers):
+        need = np.unique(np.concatenate([np.arange(r2), col[:rp[r2]]]))
+        h = tables[(li - 1) % 2].gather_rows(n, d, need)
+        ref = O.sage_forward(h, rp[:r2 + 1], np.searchsorted(need, col[:rp[r2]]).astype(np.int32), wn, ws,
+                             rows=(0, r2), threads=threads)
+        got = tables[li % 2].gather_rows(n, d, np.arange(r2))
+        e = float(np.max(np.abs(got.astype(np.float64) - ref)) / max(float(np.max(np.abs(ref))), 1e-30))
+        per_layer.append({"layer": li + 1, "rows": r2, "max_rel_err": e, "input": f"GPU layer-{li} rows"})
+    worst = max(p["max_rel_err"] for p in per_layer)
+    parity = {"rows": rows, "max_rel_err": worst, "tol": 1e-5, "ok": worst <= 1e-5, "per_layer": per_layer}
     return cpu, parity
 
 

@@ -90,14 +90,16 @@ def run(n, d, nq, m, efc, efs, k, metric_name, seed_base=1, cpu=False, cpu_secon
         q = qb.download(np.float32, (nq, d))
         h = O.Hnsw(d, metric_name, m=m, ef_construction=efc, seed=seed_base)
         t0 = time.perf_counter()
-        h.insert(x, threads=min(16, os.cpu_count() or 1))
+        from benchutil import host_threads
+        bt, _ = host_threads()
+        h.insert(x, threads=bt)
         cb = time.perf_counter() - t0
         cs = []
         for ef in efs:
-            cids, _, _ = h.search(q[:2000], k, ef, threads=min(16, os.cpu_count() or 1))
+            cids, _, _ = h.search(q[:2000], k, ef, threads=bt)
             rec = float(np.mean([len(set(a.tolist()) & set(b.tolist())) / k for a, b in zip(gt[:2000].astype(np.int64), cids)]))
             cs.append({"ef": ef, "recall": round(rec, 4)})
-        out["cpu_build"] = {"build_s": round(cb, 2), "threads": min(16, os.cpu_count() or 1), "sweep_2k_queries": cs}
+        out["cpu_build"] = {"build_s": round(cb, 2), "threads": bt, "sweep_2k_queries": cs}
         log(f"cpu build {cb:.1f} s; recall {cs}")
     pick = best or (max(sweep, key=lambda s: s["recall"]) if sweep else None)  # CPU leg at recall >= 0.95 if reached
     if cpu and pick:
@@ -106,19 +108,34 @@ def run(n, d, nq, m, efc, efs, k, metric_name, seed_base=1, cpu=False, cpu_secon
         x = xb.download(np.float32, (n, d))
         q = qb.download(np.float32, (nq, d))
         h = O.Hnsw.from_graph(x, idx.export_graph(), metric_name)
-        threads = min(16, os.cpu_count() or 1)
-        sample = min(nq, 500)
-        t0 = time.perf_counter()
-        h.search(q[:sample], k, pick["ef"], threads=threads)
-        dt = time.perf_counter() - t0
-        sample = int(min(nq, max(sample, sample * cpu_seconds / max(dt, 1e-3))))
-        t0 = time.perf_counter()
-        cids, _, _ = h.search(q[:sample], k, pick["ef"], threads=threads)
-        dt = time.perf_counter() - t0
+        from benchutil import host_threads
+        threads, tinfo = host_threads()
+
+        def timed(fast, target):
+            O.lib().orc_hnsw_set_fast(h._h, int(fast))
+            m = min(nq, 500)
+            t0 = time.perf_counter()
+            h.search(q[:m], k, pick["ef"], threads=threads)
+            dt = time.perf_counter() - t0
+            m = int(min(nq, max(m, m * target / max(dt, 1e-3))))
+            t0 = time.perf_counter()
+            r = h.search(q[:m], k, pick["ef"], threads=threads)[0]
+            return m, time.perf_counter() - t0, r
+
+        # fast mode: SIMD distances as the default SimSIMD build (kind "simd", the ratio's baseline)
+        fm, fdt, _ = timed(True, cpu_seconds)
+        # reference scalar order on the same graph (the parity oracle: ids must equal the GPU's)
+        sample, dt, cids = timed(False, cpu_seconds / 2)
         gpu_ids = idx.search_array(q[:sample], k, pick["ef"])[0].astype(np.int64)
-        out["cpu_baseline"] = {"value": round(sample / dt, 1), "unit": "queries/s", "cores": threads, "kind": "port",
-                               "sample": f"oracle hnsw_rs search_filter on the same graph, {sample} queries, "
-                                         f"ef={pick['ef']} (recall {pick['recall']})",
+        width = O.lib().orc_simd_width()
+        out["cpu_baseline"] = {"value": round(fm / fdt, 1), "unit": "queries/s", "cores": threads, "kind": "simd",
+                               "host": tinfo,
+                               "sample": f"hnsw_rs search_filter (hnsw.rs:1475-1570 restated) on the same graph with "
+                                         f"AVX{'-512' if width == 512 else '2'} FMA distances, {fm} queries, "
+                                         f"ef={pick['ef']} (recall {pick['recall']}), {threads} threads, {fdt:.1f} s",
+                               "scalar_order": {"value": round(sample / dt, 1), "kind": "port",
+                                                "sample": f"same search in the reference's scalar distance order, "
+                                                          f"{sample} queries, {dt:.1f} s"},
                                "gpu_qps_same_ef": pick["qps"]}
         out["cpu_gpu_ids_equal"] = bool(np.array_equal(cids, gpu_ids))
     return out

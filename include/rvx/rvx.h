@@ -82,6 +82,10 @@ void*      rvx_buffer_device_ptr(rvx_buffer* buf);
 rvx_status rvx_buffer_upload(rvx_buffer* buf, const void* src, int64_t bytes, int64_t offset);
 rvx_status rvx_buffer_download(const rvx_buffer* buf, void* dst, int64_t bytes, int64_t offset);
 rvx_status rvx_buffer_zero(rvx_buffer* buf);
+/* Rows ids[0..n) of a [rows][dim] f32 table to host out [n][dim] (one device gather per
+ * 256 MB; parity checks and stored-row export). Errors: IndexError for an id outside [0, rows). */
+rvx_status rvx_buffer_gather_rows_f32(const rvx_buffer* table, int64_t rows, int32_t dim, const int64_t* ids,
+                                     int64_t n, float* out);
 
 /* Synthetic data generators (device side; the integer stream is shared with
  * oracle/oracle.cpp so the CPU baseline sees identical inputs).
@@ -237,6 +241,19 @@ rvx_status rvx_gnn_forward_star_device(const rvx_layer* l, const rvx_buffer* nod
                                        int64_t table_rows, const rvx_buffer* cand_ids, int32_t c,
                                        const rvx_buffer* weights, rvx_buffer* out);
 
+/* hierarchical_forward (crates/ruvector-gnn/src/search.rs:105-162) for nq queries at once,
+ * all in HBM. Walks zip(levels, layers): level s (level_rows[s] rows of the current
+ * embedding dim, row-major; 0 rows = skipped) gives differentiable_search top-min(5, rows)
+ * at temperature 1 over ALL its rows, the soft-weighted row sum agg, combined =
+ * (cur + agg) / 2, then cur = layers[s]->forward(combined, top rows, top weights).
+ * q [nq][dim] -> out [nq][*out_dim] (out_dim = last applied layer's hidden_dim, or dim).
+ * Errors: DimensionMismatch when a layer's input_dim differs from the embedding dim
+ * (the reference asserts in cosine_similarity, search.rs:5). Replaces the per-query
+ * Rust call; the reference has no batched form. */
+rvx_status rvx_hierarchical_forward_device(const rvx_layer* const* layers, int32_t n_layers,
+                                           const rvx_buffer* const* levels, const int64_t* level_rows,
+                                           int32_t n_levels, const rvx_buffer* q, int64_t nq, int32_t dim,
+                                           rvx_buffer* out, int32_t* out_dim);
 /* differentiable_search (crates/ruvector-gnn/src/search.rs:56-94), batched:
  * q [nq][d], cand [nq][c][d] -> idx [nq][k] (int64, -1 padded), w [nq][k]. */
 rvx_status rvx_differentiable_search_batch(const float* q, int64_t nq, const float* cand, int32_t c,
@@ -510,6 +527,26 @@ rvx_status rvx_comm_destroy(rvx_comm* c);
  * recv [nranks*rows][cols] (rank-major), on the library stream. */
 rvx_status rvx_comm_allgather_f32(rvx_comm* c, const rvx_buffer* send, int64_t count, rvx_buffer* recv);
 rvx_status rvx_comm_allreduce_max_f64(rvx_comm* c, double* value);
+
+/* Host-staged transport (tests and hosts without RCCL peers, e.g. several ranks
+ * sharing one GPU): behind the same row exchange the *_forward_exchange entry
+ * points use, each round stages this rank's rows in host memory and calls
+ * `fn(user, send, send_bytes, recv, recv_bytes)` once: send this rank's block to
+ * every peer and fill recv[p] (recv_bytes[p] bytes; recv[me] is NULL) from peer p.
+ * Returns 0 on success. Collectives (all-gather, all-reduce) need RCCL. */
+typedef int32_t (*rvx_host_exchange_fn)(void* user, const void* send, int64_t send_bytes, void* const* recv,
+                                        const int64_t* recv_bytes);
+rvx_status rvx_comm_init_host(int32_t nranks, int32_t rank, rvx_host_exchange_fn fn, void* user, rvx_comm** out);
+
+/* The p2p round plan of the node-range exchange that the
+ * *_forward_exchange entry points run: kind 0 = GraphSAGE (rvx_sage_forward_exchange:
+ * the owned rows in row chunks, one round per chunk after that chunk's GEMM; every
+ * rank uses the chunk count of the largest shard), kind 1 = RuvectorLayer / edge
+ * attention tables (one round per table, whole shards). offsets [world+1]. With
+ * r0 == NULL only *n_rounds is written; else r0/rows [n_rounds][world]: in round c
+ * rank p ships rows [r0, r0+rows) (rows may be 0). Host-only: no device work. */
+rvx_status rvx_exchange_plan(int32_t kind, const int64_t* offsets, int32_t world, int32_t* n_rounds, int64_t* r0,
+                             int64_t* rows);
 
 #ifdef __cplusplus
 }

@@ -19,6 +19,8 @@
 // hnsw_rs 0.3.3 is vendored (patches/hnsw_rs) and followed line by line,
 // except that its entropy-seeded level generator is replaced by a seeded one
 // and heap ties (unordered in the reference) are ordered by point id.
+#include <immintrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -75,6 +77,89 @@ struct CandMin {  // min-heap on (d, id)
 };
 
 enum { M_L2 = 0, M_COS = 1, M_DOT = 2, M_L1 = 3 };
+
+// ---- CPU-baseline "fast mode" (SURVEY.md §8d): SIMD distances like the
+// reference's default SimSIMD build / simd_intrinsics.rs:196-... (AVX-512 or
+// AVX2 FMA, 16/8-lane partial sums, horizontal reduction). NOT the reference
+// order: used only to time the CPU baseline (bench cpu_baseline legs,
+// kind "simd"); parity always uses orc_distance.
+
+__attribute__((target("avx512f"))) void simd3_512(const float* a, const float* b, int64_t d, int metric, float* o) {
+    __m512 s0 = _mm512_setzero_ps(), s1 = _mm512_setzero_ps(), s2 = _mm512_setzero_ps();
+    int64_t i = 0;
+    for (; i + 16 <= d; i += 16) {
+        const __m512 x = _mm512_loadu_ps(a + i), y = _mm512_loadu_ps(b + i);
+        if (metric == M_L2) {
+            const __m512 t = _mm512_sub_ps(x, y);
+            s0 = _mm512_fmadd_ps(t, t, s0);
+        } else if (metric == M_L1) {
+            s0 = _mm512_add_ps(s0, _mm512_abs_ps(_mm512_sub_ps(x, y)));
+        } else {
+            s0 = _mm512_fmadd_ps(x, y, s0);
+            if (metric == M_COS) { s1 = _mm512_fmadd_ps(x, x, s1); s2 = _mm512_fmadd_ps(y, y, s2); }
+        }
+    }
+    if (i < d) {
+        const __mmask16 m = (__mmask16)((1u << (d - i)) - 1);
+        const __m512 x = _mm512_maskz_loadu_ps(m, a + i), y = _mm512_maskz_loadu_ps(m, b + i);
+        if (metric == M_L2) { const __m512 t = _mm512_sub_ps(x, y); s0 = _mm512_fmadd_ps(t, t, s0); }
+        else if (metric == M_L1) s0 = _mm512_add_ps(s0, _mm512_abs_ps(_mm512_sub_ps(x, y)));
+        else {
+            s0 = _mm512_fmadd_ps(x, y, s0);
+            if (metric == M_COS) { s1 = _mm512_fmadd_ps(x, x, s1); s2 = _mm512_fmadd_ps(y, y, s2); }
+        }
+    }
+    o[0] = _mm512_reduce_add_ps(s0);
+    o[1] = _mm512_reduce_add_ps(s1);
+    o[2] = _mm512_reduce_add_ps(s2);
+}
+
+__attribute__((target("avx2,fma"))) float hsum256(__m256 v) {
+    const __m128 lo = _mm256_castps256_ps128(v), hi = _mm256_extractf128_ps(v, 1);
+    __m128 s = _mm_add_ps(lo, hi);
+    s = _mm_add_ps(s, _mm_movehl_ps(s, s));
+    s = _mm_add_ss(s, _mm_shuffle_ps(s, s, 1));
+    return _mm_cvtss_f32(s);
+}
+
+__attribute__((target("avx2,fma"))) void simd3_256(const float* a, const float* b, int64_t d, int metric, float* o) {
+    __m256 s0 = _mm256_setzero_ps(), s1 = _mm256_setzero_ps(), s2 = _mm256_setzero_ps();
+    const __m256 absm = _mm256_castsi256_ps(_mm256_set1_epi32(0x7fffffff));
+    int64_t i = 0;
+    for (; i + 8 <= d; i += 8) {
+        const __m256 x = _mm256_loadu_ps(a + i), y = _mm256_loadu_ps(b + i);
+        if (metric == M_L2) { const __m256 t = _mm256_sub_ps(x, y); s0 = _mm256_fmadd_ps(t, t, s0); }
+        else if (metric == M_L1) s0 = _mm256_add_ps(s0, _mm256_and_ps(absm, _mm256_sub_ps(x, y)));
+        else {
+            s0 = _mm256_fmadd_ps(x, y, s0);
+            if (metric == M_COS) { s1 = _mm256_fmadd_ps(x, x, s1); s2 = _mm256_fmadd_ps(y, y, s2); }
+        }
+    }
+    float r0 = hsum256(s0), r1 = hsum256(s1), r2 = hsum256(s2);
+    for (; i < d; ++i) {
+        if (metric == M_L2) { const float t = a[i] - b[i]; r0 += t * t; }
+        else if (metric == M_L1) r0 += std::fabs(a[i] - b[i]);
+        else { r0 += a[i] * b[i]; if (metric == M_COS) { r1 += a[i] * a[i]; r2 += b[i] * b[i]; } }
+    }
+    o[0] = r0; o[1] = r1; o[2] = r2;
+}
+
+const bool g_avx512 = __builtin_cpu_supports("avx512f");
+
+float fast_distance(const float* a, const float* b, int64_t d, int metric) {
+    float s[3];
+    if (g_avx512) simd3_512(a, b, d, metric, s);
+    else simd3_256(a, b, d, metric, s);
+    switch (metric) {
+        case M_L2: return (float)std::sqrt((double)s[0]);  // distance.rs:30-32 (SimSIMD sqeuclidean)
+        case M_COS: {
+            const float den = std::sqrt(s[1]) * std::sqrt(s[2]);
+            return den > 0.0f ? 1.0f - s[0] / den : 1.0f;
+        }
+        case M_DOT: return -s[0];
+        default: return s[0];
+    }
+}
 
 // ndarray numeric_util::unrolled_dot
 float unrolled_dot(const float* x, const float* y, int64_t len) {
@@ -189,6 +274,47 @@ void orc_flat_search(const float* base, int64_t n, int64_t d, int32_t metric, co
     });
 }
 
+// FlatIndex::search CPU baseline in fast mode (SIMD distances, all threads over
+// row blocks like rayon's par_iter over the vectors, flat.rs:39-49; per-block
+// top-k merged). Queries go in batches of 16 so each row is read once per batch.
+void orc_flat_search_fast(const float* base, int64_t n, int64_t d, int32_t metric, const float* q, int64_t nq, int32_t k,
+                          int64_t* out_ids, float* out_d, int32_t nthreads) {
+    const int64_t QB = 16, RB = 8192;
+    for (int64_t q0 = 0; q0 < nq; q0 += QB) {
+        const int64_t nb = std::min(QB, nq - q0);
+        const int64_t blocks = (n + RB - 1) / RB;
+        std::vector<std::vector<Cand>> part((size_t)blocks * nb);
+        pfor(blocks, nthreads, [&](int64_t bi) {
+            const int64_t r0 = bi * RB, r1 = std::min(n, r0 + RB);
+            std::vector<std::priority_queue<Cand, std::vector<Cand>, CandMax>> heap(nb);
+            for (int64_t j = r0; j < r1; ++j)
+                for (int64_t t = 0; t < nb; ++t) {
+                    const Cand c{fast_distance(q + (q0 + t) * d, base + j * d, d, metric), j};
+                    auto& h = heap[t];
+                    if ((int)h.size() < k) h.push(c);
+                    else if (cand_less(c, h.top())) { h.pop(); h.push(c); }
+                }
+            for (int64_t t = 0; t < nb; ++t) {
+                auto& v = part[(size_t)(bi * nb + t)];
+                while (!heap[t].empty()) { v.push_back(heap[t].top()); heap[t].pop(); }
+            }
+        });
+        for (int64_t t = 0; t < nb; ++t) {
+            std::vector<Cand> all;
+            for (int64_t bi = 0; bi < blocks; ++bi) {
+                const auto& v = part[(size_t)(bi * nb + t)];
+                all.insert(all.end(), v.begin(), v.end());
+            }
+            const int64_t kk = std::min<int64_t>(k, (int64_t)all.size());
+            std::partial_sort(all.begin(), all.begin() + kk, all.end(), cand_less);
+            for (int64_t s2 = 0; s2 < k; ++s2) {
+                out_ids[(q0 + t) * k + s2] = s2 < kk ? all[s2].id : -1;
+                out_d[(q0 + t) * k + s2] = s2 < kk ? all[s2].d : INFINITY;
+            }
+        }
+    }
+}
+
 }  // extern "C"
 
 // ============================================================ hnsw_rs 0.3.3
@@ -212,7 +338,10 @@ struct OHnsw {
 
     OHnsw() : count_at_level(17) {}
     const float* v(int64_t i) const { return data.data() + i * d; }
-    float dist(const float* a, int64_t j) const { return orc_distance(a, v(j), d, metric); }
+    bool fast = false;  // CPU-baseline SIMD distances (not the reference order)
+    float dist(const float* a, int64_t j) const {
+        return fast ? fast_distance(a, v(j), d, metric) : orc_distance(a, v(j), d, metric);
+    }
 };
 
 // LayerGenerator::generate (hnsw.rs:358-369): floor(-ln(U) / ln(M)), redrawn
@@ -275,7 +404,7 @@ std::vector<Cand> select_neighbours(const OHnsw& h, const std::vector<Cand>& can
         if (!nbv.empty()) {
             const float* ev = h.v(e.id);
             for (const Cand& dd : nbv)
-                if (orc_distance(ev, h.v(dd.id), h.d, h.metric) <= e.d) { insert = false; break; }
+                if (h.dist(ev, dd.id) <= e.d) { insert = false; break; }
         }
         if (insert) nbv.push_back(e);
     }
@@ -360,6 +489,10 @@ void* orc_hnsw_new(int64_t d, int32_t metric, int32_t m, int32_t ef_c, int32_t m
 }
 
 void orc_hnsw_free(void* hp) { delete static_cast<OHnsw*>(hp); }
+
+// CPU-baseline fast mode: SIMD distances for build and search (bench only).
+void orc_hnsw_set_fast(void* hp, int32_t on) { static_cast<OHnsw*>(hp)->fast = on != 0; }
+int32_t orc_simd_width() { return g_avx512 ? 512 : 256; }
 
 // Sequential add_batch (index/hnsw.rs:314-319) for nthreads <= 1, otherwise
 // Hnsw::parallel_insert (hnsw.rs:1212-1218) semantics.
@@ -912,6 +1045,39 @@ int32_t orc_differentiable_search(const float* q, const float* cand, int32_t c, 
     });
     for (int t = 0; t < kk; ++t) { idx[t] = iw[t].first; w[t] = iw[t].second; }
     return kk;
+}
+
+// hierarchical_forward (search.rs:105-162) for one query: zip(levels, layers);
+// an empty level is skipped; top-min(5, rows) at temperature 1; agg accumulated
+// in top-k order (search.rs:133-140); combined = (cur + agg) / 2; then
+// RuvectorLayer::forward(combined, top rows, top weights). out has room for the
+// largest dim; returns the output dim.
+int32_t orc_hierarchical_forward(const orc_rvl* const* layers, int32_t n_layers, const float* const* levels,
+                                 const int64_t* level_rows, int32_t n_levels, const float* q, int32_t dim, float* out) {
+    std::vector<float> cur(q, q + dim);
+    const int steps = std::min(n_layers, n_levels);
+    for (int s = 0; s < steps; ++s) {
+        const int64_t rows = level_rows[s];
+        if (rows == 0) continue;
+        const int64_t d = (int64_t)cur.size();
+        const float* emb = levels[s];
+        const int k = (int)std::min<int64_t>(5, rows);
+        std::vector<int64_t> idx(k);
+        std::vector<float> w(k);
+        const int kk = orc_differentiable_search(cur.data(), emb, (int32_t)rows, d, k, 1.0f, idx.data(), w.data());
+        std::vector<float> agg(d, 0.0f);
+        for (int t = 0; t < kk; ++t)
+            for (int64_t i = 0; i < d; ++i) agg[i] += w[t] * emb[idx[t] * d + i];
+        std::vector<float> combined(d);
+        for (int64_t i = 0; i < d; ++i) combined[i] = (cur[i] + agg[i]) / 2.0f;
+        std::vector<float> nbrs((size_t)kk * d);
+        for (int t = 0; t < kk; ++t) std::memcpy(&nbrs[(size_t)t * d], emb + idx[t] * d, d * 4);
+        std::vector<float> y(layers[s]->H);
+        orc_rvl_forward_one(layers[s], combined.data(), nbrs.data(), kk, w.data(), kk, y.data());
+        cur.swap(y);
+    }
+    std::memcpy(out, cur.data(), cur.size() * 4);
+    return (int32_t)cur.size();
 }
 
 // ============================================================ edge_featured.rs

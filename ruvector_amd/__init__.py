@@ -15,12 +15,14 @@ from .core import (DistanceMetric, FlatIndex, HnswConfig, HnswIndex, RuvectorErr
                    batch_distances, distance, distance_matrix, hnsw_last_search_stats, scan_last_stats)
 from .gnn import (GCNLayer, GnnError, GraphSAGELayer, RuvectorLayer, aggregate, differentiable_search,
                   differentiable_search_device,  # noqa: E402
-                  differentiable_search_batch, hierarchical_forward)
+                  differentiable_search_batch, hierarchical_forward, hierarchical_forward_batch,
+                  hierarchical_forward_device)
 from .attention import DualSpaceAttention, DualSpaceConfig, EdgeFeaturedAttention, EdgeFeaturedConfig  # noqa: E402
 from .hyperbolic import (DualSpaceIndex, HyperbolicError, HyperbolicHnsw, HyperbolicHnswConfig,  # noqa: E402
                          ShardedHyperbolicHnsw)
 
 from .query import NeuralSearch, QueryMode, RuvectorQuery  # noqa: E402
+from .vector_db import DbOptions, SearchQuery, VectorDB, VectorEntry  # noqa: E402
 
 __all__ = [
     "RvxError", "Buffer", "Profiler", "device_count", "device_info", "set_device", "synchronize", "Graph",
@@ -30,6 +32,6 @@ __all__ = [
     "DualSpaceAttention", "DualSpaceConfig",
     "EdgeFeaturedConfig", "HyperbolicError", "HyperbolicHnsw", "HyperbolicHnswConfig", "ShardedHyperbolicHnsw",
     "DualSpaceIndex",
-    "NeuralSearch", "QueryMode", "RuvectorQuery", "differentiable_search_device", "hnsw_last_search_stats", "scan_last_stats",
+    "NeuralSearch", "QueryMode", "RuvectorQuery", "DbOptions", "SearchQuery", "VectorDB", "VectorEntry", "differentiable_search_device", "hnsw_last_search_stats", "scan_last_stats",
 ]
 __version__ = "0.1.0"

@@ -98,6 +98,7 @@ SIGNATURES = {
     "rvx_buffer_device_ptr": (P, [P]),
     "rvx_buffer_upload": (None, [P, P, I64, I64]),
     "rvx_buffer_download": (None, [P, P, I64, I64]),
+    "rvx_buffer_gather_rows_f32": (None, [P, I64, I32, P, I64, P]),
     "rvx_buffer_zero": (None, [P]),
     "rvx_fill_uniform": (None, [P, I64, U64, F32, F32]),
     "rvx_fill_uniform_at": (None, [P, I64, U64, I64, F32, F32]),
@@ -132,6 +133,7 @@ SIGNATURES = {
     "rvx_gnn_forward_exchange": (None, [P, P, P, P, PI64, P]),
     "rvx_differentiable_search_batch": (None, [PF32, I64, PF32, I32, I32, I32, F32, PI64, PF32]),
     "rvx_gnn_forward_star_device": (None, [P, P, I64, P, I64, P, I32, P, P]),
+    "rvx_hierarchical_forward_device": (None, [P, I32, P, P, I32, P, I64, I32, P, P]),
     "rvx_hnsw_last_search_stats": (None, [PI64, PI64, PI64]),
     "rvx_scan_last_stats": (None, [PI64, PI64, PI64]),
     "rvx_differentiable_search_device": (None, [P, I64, P, I64, P, I32, I32, I32, F32, P, P, P]),
@@ -188,6 +190,8 @@ SIGNATURES = {
     "rvx_profile_query": (None, [C.c_char_p, C.POINTER(C.c_double), PI64]),
     "rvx_profile_names": (None, [C.c_char_p, SZ]),
     "rvx_comm_unique_id": (None, [C.POINTER(C.c_uint8)]),
+    "rvx_comm_init_host": (None, [I32, I32, P, P, P]),
+    "rvx_exchange_plan": (None, [I32, P, I32, P, P, P]),
     "rvx_comm_init": (None, [C.POINTER(C.c_uint8), I32, I32, PP]),
     "rvx_comm_destroy": (None, [P]),
     "rvx_comm_allgather_f32": (None, [P, P, I64, P]),
@@ -198,8 +202,33 @@ _lib = None
 _lock = threading.Lock()
 
 
+CSRC_DIR = os.path.join(_HERE, "csrc")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "rvx", "rvx.h")
+
+
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) over the library's sources, the same files
+    and order as the Makefile's SRC_HASH: sorted paths of csrc/*.cpp, *.hip,
+    *.hpp and include/rvx/rvx.h, contents concatenated."""
+    import hashlib
+    names = [f"ruvector_amd/csrc/{f}" for f in os.listdir(CSRC_DIR)
+             if f.endswith((".cpp", ".hip", ".hpp"))] + ["include/rvx/rvx.h"]
+    root = os.path.dirname(_HERE)
+    h = hashlib.sha256()
+    for rel in sorted(names):
+        with open(os.path.join(root, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def built_hash(lib) -> str:
+    v = lib.rvx_version().decode()
+    return v.rsplit(" src ", 1)[-1] if " src " in v else "unknown"
+
+
 def load() -> C.CDLL:
-    """Load librvx.so (raises loudly if it was not built)."""
+    """Load librvx.so (raises loudly if it was not built, or if it was built
+    from other sources than the ones shipped beside it)."""
     global _lib
     with _lock:
         if _lib is not None:
@@ -209,6 +238,15 @@ def load() -> C.CDLL:
                 f"{LIB_PATH} is missing: build the HIP extension first "
                 "(python -c 'import __graft_entry__ as g; g.build()'). There is no CPU fallback.")
         lib = C.CDLL(LIB_PATH)
+        lib.rvx_version.restype = C.c_char_p
+        lib.rvx_version.argtypes = []
+        if (not os.environ.get("RVX_LIB") and os.environ.get("RVX_ALLOW_STALE") != "1"
+                and os.path.isdir(CSRC_DIR)):
+            want, got = source_hash(), built_hash(lib)
+            if want != got:
+                raise ImportError(
+                    f"{LIB_PATH} was built from sources {got}, the tree holds {want}: rebuild it "
+                    "(python -c 'import __graft_entry__ as g; g.build()').")
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = I32 if res is None else res

@@ -332,9 +332,8 @@ rvx_status rvx_edge_attention_forward_exchange(const rvx_edge_attention* a, cons
         transform(a, x_full->mem.as<float>() + o * nd, g->n, t + o * D, "efa_transform");
         if (world > 1) {
             ProfScope ps("efa_halo_exchange");
-            std::vector<int64_t> rows(world);
-            for (int p = 0; p < world; ++p) rows[p] = offsets[p + 1] - offsets[p];
-            comm_exchange_rows(comm, t, D, offsets, rows.data(), stream());
+            for (const ExchangeRound& r : exchange_plan(PLAN_WHOLE, offsets, world))
+                comm_exchange_rows(comm, t, D, r.r0.data(), r.rows.data(), stream());
         }
         run_efa(a, g->n, g->row_ptr, g->col, g->e, t + o * D, N, t, t, ef ? ef->mem.as<float>() : nullptr,
                 y_full->mem.as<float>() + o * od);

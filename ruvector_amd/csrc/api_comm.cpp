@@ -10,8 +10,10 @@
 using namespace rvx;
 
 struct rvx_comm {
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr;  // RCCL transport
     int nranks = 0, rank = 0;
+    rvx_host_exchange_fn host_fn = nullptr;  // host-staged transport (rvx_comm_init_host)
+    void* host_user = nullptr;
 };
 
 #define RVX_NCCL(expr)                                                                         \
@@ -27,9 +29,43 @@ namespace rvx {
 int comm_rank(const rvx_comm* c) { return c ? c->rank : 0; }
 int comm_size(const rvx_comm* c) { return c ? c->nranks : 1; }
 
+namespace {
+// Host-staged round: wait for the rows on `s`, copy this rank's block to host,
+// let the host transport move every block, copy the peers' blocks back.
+void host_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int64_t* r0, const int64_t* rows,
+                        hipStream_t s) {
+    const int me = c->rank, w = c->nranks;
+    RVX_HIP(hipStreamSynchronize(s));
+    std::vector<float> send((size_t)std::max<int64_t>(rows[me] * row_elems, 1));
+    if (rows[me] > 0)
+        RVX_HIP(hipMemcpy(send.data(), table + r0[me] * row_elems, (size_t)(rows[me] * row_elems * 4),
+                          hipMemcpyDeviceToHost));
+    std::vector<std::vector<float>> recv(w);
+    std::vector<void*> rptr(w, nullptr);
+    std::vector<int64_t> rbytes(w, 0);
+    for (int p = 0; p < w; ++p) {
+        if (p == me) continue;
+        rbytes[p] = rows[p] * row_elems * 4;
+        recv[p].resize((size_t)std::max<int64_t>(rows[p] * row_elems, 1));
+        rptr[p] = recv[p].data();
+    }
+    const int32_t rc = c->host_fn(c->host_user, send.data(), rows[me] * row_elems * 4, rptr.data(), rbytes.data());
+    RVX_REQUIRE(rc == 0, RVX_ERR_COMM, "host transport failed with status " + std::to_string(rc));
+    for (int p = 0; p < w; ++p)
+        if (p != me && rows[p] > 0)
+            RVX_HIP(hipMemcpyAsync(table + r0[p] * row_elems, recv[p].data(), (size_t)rbytes[p],
+                                   hipMemcpyHostToDevice, s));
+    RVX_HIP(hipStreamSynchronize(s));  // recv blocks are host temporaries
+}
+}  // namespace
+
 void comm_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int64_t* r0, const int64_t* rows,
                         hipStream_t s) {
     if (!c || c->nranks <= 1) return;
+    if (c->host_fn) {
+        host_exchange_rows(c, table, row_elems, r0, rows, s);
+        return;
+    }
     const int me = c->rank;
     RVX_NCCL(ncclGroupStart());
     for (int k = 1; k < c->nranks; ++k) {
@@ -70,6 +106,19 @@ rvx_status rvx_comm_init(const uint8_t id[RVX_COMM_ID_BYTES], int32_t nranks, in
     });
 }
 
+rvx_status rvx_comm_init_host(int32_t nranks, int32_t rank, rvx_host_exchange_fn fn, void* user, rvx_comm** out) {
+    return guard([&] {
+        RVX_REQUIRE(fn && out && nranks > 0 && rank >= 0 && rank < nranks, RVX_ERR_INVALID_PARAMETER,
+                    "bad host comm args");
+        auto c = std::make_unique<rvx_comm>();
+        c->nranks = nranks;
+        c->rank = rank;
+        c->host_fn = fn;
+        c->host_user = user;
+        *out = c.release();
+    });
+}
+
 rvx_status rvx_comm_destroy(rvx_comm* c) {
     return guard([&] {
         if (c && c->comm) ncclCommDestroy(c->comm);
@@ -80,6 +129,7 @@ rvx_status rvx_comm_destroy(rvx_comm* c) {
 rvx_status rvx_comm_allgather_f32(rvx_comm* c, const rvx_buffer* send, int64_t count, rvx_buffer* recv) {
     return guard([&] {
         RVX_REQUIRE(c && send && recv && count >= 0, RVX_ERR_INVALID_PARAMETER, "bad all-gather args");
+        RVX_REQUIRE(c->comm, RVX_ERR_UNSUPPORTED, "all-gather needs the RCCL transport");
         RVX_REQUIRE(send->mem.bytes >= count * 4 && recv->mem.bytes >= count * 4 * c->nranks, RVX_ERR_INVALID_PARAMETER,
                     "all-gather buffers too small");
         ProfScope ps("rccl_allgather");
@@ -90,6 +140,7 @@ rvx_status rvx_comm_allgather_f32(rvx_comm* c, const rvx_buffer* send, int64_t c
 rvx_status rvx_comm_allreduce_max_f64(rvx_comm* c, double* value) {
     return guard([&] {
         RVX_REQUIRE(c && value, RVX_ERR_INVALID_PARAMETER, "null argument");
+        RVX_REQUIRE(c->comm, RVX_ERR_UNSUPPORTED, "all-reduce needs the RCCL transport");
         double* d = (double*)scratch_bytes("comm_scalar", 8);
         RVX_HIP(hipMemcpyAsync(d, value, 8, hipMemcpyHostToDevice, stream()));
         RVX_NCCL(ncclAllReduce(d, d, 1, ncclFloat64, ncclMax, c->comm, stream()));

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstring>
 
+#include "attn.hpp"
 #include "comm.hpp"
 #include "gnn.hpp"
 #include "graph.hpp"
@@ -284,6 +285,38 @@ void forward_dev(const rvx_layer* l, int64_t n, const int64_t* rp, const int32_t
     phase2_dev(l, rows_out, rp, col, max_deg, w, wmode, M, KV, 0, y);
 }
 
+// RuvectorLayer::forward(nodes[i], table[ids[i*c .. i*c+c)], weights[i*c ..]) for
+// every i < nq (ids outside [0, trows) are absent neighbours; weights nullable =
+// empty edge-weight slice): one star graph over [nodes | gathered rows].
+void star_forward(const rvx_layer* l, const float* nodes, int64_t nq, const float* table, int64_t table_rows,
+                  const int64_t* ids, int c, const float* weights, float* out) {
+    const int64_t in = l->in;
+    const int64_t n = nq + nq * (int64_t)c;
+    RVX_REQUIRE(n < ((int64_t)1 << 31), RVX_ERR_INVALID_SHAPE, "star table exceeds int32 neighbour ids");
+    float* T = scratch_f32("rvs_t", n * in);
+    auto* deg = (int32_t*)scratch_bytes("rvs_deg", nq * 4);
+    auto* drp = (int64_t*)scratch_bytes("rvs_rp", (nq + 1) * 8);
+    auto* dcol = (int32_t*)scratch_bytes("rvs_col", std::max<int64_t>(nq * c, 1) * 4);
+    float* dw = weights ? scratch_f32("rvs_w", std::max<int64_t>(nq * c, 1)) : nullptr;
+    star_gather(nodes, nq, table, table_rows, ids, c, (int)in, T);
+    // row_ptr: prefix sum of the per-node valid-candidate counts on the host
+    star_degrees(ids, nq, c, table_rows, deg);
+    std::vector<int32_t> hdeg(nq);
+    std::vector<int64_t> hrp(nq + 1, 0);
+    RVX_HIP(hipMemcpyAsync(hdeg.data(), deg, (size_t)nq * 4, hipMemcpyDeviceToHost, stream()));
+    sync();
+    int64_t max_deg = 0;
+    for (int64_t i = 0; i < nq; ++i) {
+        hrp[i + 1] = hrp[i] + hdeg[i];
+        max_deg = std::max<int64_t>(max_deg, hdeg[i]);
+    }
+    RVX_HIP(hipMemcpyAsync(drp, hrp.data(), (size_t)(nq + 1) * 8, hipMemcpyHostToDevice, stream()));
+    star_csr(ids, weights, nq, c, table_rows, drp, dcol, dw);
+    // weights absent -> aggregate_messages returns zeros (layer.rs:427-429): wmode 0
+    forward_dev(l, n, drp, dcol, max_deg, dw, weights ? 2 : 0, T, out, nq);
+    sync();  // hrp / hdeg are host temporaries
+}
+
 }  // namespace
 
 extern "C" {
@@ -454,32 +487,66 @@ rvx_status rvx_gnn_forward_star_device(const rvx_layer* l, const rvx_buffer* nod
         RVX_REQUIRE(!weights || weights->mem.bytes >= nq * (int64_t)c * 4, RVX_ERR_DIMENSION_MISMATCH,
                     "weights smaller than nq*c");
         RVX_REQUIRE(out->mem.bytes >= nq * H * 4, RVX_ERR_DIMENSION_MISMATCH, "out smaller than nq*hidden_dim");
-        const int64_t n = nq + nq * (int64_t)c;
-        RVX_REQUIRE(n < ((int64_t)1 << 31), RVX_ERR_INVALID_SHAPE, "star table exceeds int32 neighbour ids");
         ComputeLock cl;
-        const int64_t* ids = cand_ids->mem.as<int64_t>();
-        float* T = scratch_f32("rvs_t", n * in);
-        auto* deg = (int32_t*)scratch_bytes("rvs_deg", nq * 4);
-        auto* drp = (int64_t*)scratch_bytes("rvs_rp", (nq + 1) * 8);
-        auto* dcol = (int32_t*)scratch_bytes("rvs_col", std::max<int64_t>(nq * c, 1) * 4);
-        float* dw = weights ? scratch_f32("rvs_w", std::max<int64_t>(nq * c, 1)) : nullptr;
-        star_gather(nodes->mem.as<float>(), nq, table->mem.as<float>(), table_rows, ids, c, (int)in, T);
-        // row_ptr: prefix sum of the per-node valid-candidate counts on the host
-        star_degrees(ids, nq, c, table_rows, deg);
-        std::vector<int32_t> hdeg(nq);
-        std::vector<int64_t> hrp(nq + 1, 0);
-        RVX_HIP(hipMemcpyAsync(hdeg.data(), deg, (size_t)nq * 4, hipMemcpyDeviceToHost, stream()));
-        sync();
-        int64_t max_deg = 0;
-        for (int64_t i = 0; i < nq; ++i) {
-            hrp[i + 1] = hrp[i] + hdeg[i];
-            max_deg = std::max<int64_t>(max_deg, hdeg[i]);
+        star_forward(l, nodes->mem.as<float>(), nq, table->mem.as<float>(), table_rows, cand_ids->mem.as<int64_t>(), c,
+                     weights ? weights->mem.as<float>() : nullptr, out->mem.as<float>());
+    });
+}
+
+rvx_status rvx_hierarchical_forward_device(const rvx_layer* const* layers, int32_t n_layers,
+                                           const rvx_buffer* const* levels, const int64_t* level_rows,
+                                           int32_t n_levels, const rvx_buffer* q, int64_t nq, int32_t dim,
+                                           rvx_buffer* out, int32_t* out_dim) {
+    return guard([&] {
+        RVX_REQUIRE(q && out && out_dim && nq >= 0 && dim > 0 && n_layers >= 0 && n_levels >= 0,
+                    RVX_ERR_INVALID_PARAMETER, "bad arguments");
+        RVX_REQUIRE((n_layers == 0 || layers) && (n_levels == 0 || (levels && level_rows)), RVX_ERR_INVALID_PARAMETER,
+                    "null layer or level arrays");
+        RVX_REQUIRE(q->mem.bytes >= nq * (int64_t)dim * 4, RVX_ERR_DIMENSION_MISMATCH, "q smaller than nq*dim");
+        // zip(layer_embeddings, gnn_layers) (search.rs:117-119): the shorter list bounds the walk
+        const int steps = std::min(n_layers, n_levels);
+        int64_t d = dim, dmax = dim;
+        for (int s = 0; s < steps; ++s) {
+            RVX_REQUIRE(layers[s], RVX_ERR_INVALID_PARAMETER, "null layer");
+            RVX_REQUIRE(level_rows[s] >= 0 && level_rows[s] < ((int64_t)1 << 31), RVX_ERR_INVALID_PARAMETER,
+                        "bad level size");
+            if (level_rows[s] == 0) continue;  // empty level: skipped (search.rs:121-123)
+            RVX_REQUIRE(levels[s], RVX_ERR_INVALID_PARAMETER, "null level buffer");
+            // cosine_similarity asserts equal lengths (search.rs:5); Linear needs input_dim
+            RVX_REQUIRE(layers[s]->in == d, RVX_ERR_DIMENSION_MISMATCH,
+                        "layer " + std::to_string(s) + " input_dim " + std::to_string(layers[s]->in) +
+                            " != embedding dim " + std::to_string(d));
+            RVX_REQUIRE(levels[s]->mem.bytes >= level_rows[s] * d * 4, RVX_ERR_DIMENSION_MISMATCH,
+                        "level buffer smaller than rows*dim");
+            d = layers[s]->H;
+            dmax = std::max(dmax, d);
         }
-        RVX_HIP(hipMemcpyAsync(drp, hrp.data(), (size_t)(nq + 1) * 8, hipMemcpyHostToDevice, stream()));
-        star_csr(ids, weights ? weights->mem.as<float>() : nullptr, nq, c, table_rows, drp, dcol, dw);
-        // weights absent -> aggregate_messages returns zeros (layer.rs:427-429): wmode 0
-        forward_dev(l, n, drp, dcol, max_deg, dw, weights ? 2 : 0, T, out->mem.as<float>(), nq);
-        sync();  // hrp / hdeg are host temporaries
+        RVX_REQUIRE(out->mem.bytes >= nq * d * 4, RVX_ERR_DIMENSION_MISMATCH, "out smaller than nq*out_dim");
+        *out_dim = (int32_t)d;
+        if (nq == 0) return;
+        ComputeLock cl;
+        float* cur_buf[2] = {scratch_f32("hier_a", nq * dmax), scratch_f32("hier_b", nq * dmax)};
+        float* comb = scratch_f32("hier_comb", nq * dmax);
+        const float* cur = q->mem.as<float>();
+        int ping = 0;
+        d = dim;
+        for (int s = 0; s < steps; ++s) {
+            const int64_t C = level_rows[s];
+            if (C == 0) continue;
+            const int k = (int)std::min<int64_t>(5, C);  // 5.min(embeddings.len()) (search.rs:128)
+            const float* table = levels[s]->mem.as<float>();
+            float* sims = scratch_f32("hier_sims", nq * C);
+            auto* idx = (int64_t*)scratch_bytes("hier_idx", nq * k * 8);
+            float* w = scratch_f32("hier_w", nq * k);
+            differentiable_search(cur, nq, table, (int)C, (int)d, k, 1.0f, sims, idx, w, nullptr, true);
+            hier_combine(cur, nq, table, (int)d, idx, w, k, comb);
+            float* nxt = cur_buf[ping];
+            ping ^= 1;
+            star_forward(layers[s], comb, nq, table, C, idx, k, w, nxt);
+            cur = nxt;
+            d = layers[s]->H;
+        }
+        RVX_HIP(hipMemcpyAsync(out->mem.p, cur, (size_t)(nq * d * 4), hipMemcpyDeviceToDevice, stream()));
     });
 }
 
@@ -517,10 +584,10 @@ rvx_status rvx_gnn_forward_exchange(const rvx_layer* l, const rvx_graph* g, cons
         phase1_dev(l, g->n, x_full->mem.as<float>() + o * l->in, M + o * H, KV + o * 2 * H);
         if (world > 1) {
             ProfScope ps("gnn_halo_exchange");
-            std::vector<int64_t> rows(world);
-            for (int p = 0; p < world; ++p) rows[p] = offsets[p + 1] - offsets[p];
-            comm_exchange_rows(comm, M, H, offsets, rows.data(), stream());
-            comm_exchange_rows(comm, KV, 2 * H, offsets, rows.data(), stream());
+            for (const ExchangeRound& r : exchange_plan(PLAN_WHOLE, offsets, world)) {
+                comm_exchange_rows(comm, M, H, r.r0.data(), r.rows.data(), stream());
+                comm_exchange_rows(comm, KV, 2 * H, r.r0.data(), r.rows.data(), stream());
+            }
         }
         phase2_dev(l, g->n, g->row_ptr, g->col, g->max_deg, g->w, 1, M, KV, o, y_full->mem.as<float>() + o * H);
     });

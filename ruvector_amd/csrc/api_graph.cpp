@@ -43,6 +43,45 @@ void check_graph(const rvx_graph* g) {
     RVX_REQUIRE(g && g->row_ptr && (g->e == 0 || g->col), RVX_ERR_INVALID_PARAMETER, "null graph");
 }
 
+// Row chunking of the layer pipeline (same on every rank for a given chunk count).
+int sage_chunks_for(int64_t n) {
+    // 24 chunks with the gather capped at one block per CU (k_aggregate.hip):
+    // 1.46G vs 1.37G edges/s for 16 uncapped at 10M x 768 (scripts/exp_sweep3.sh)
+    const int pipe_chunks = std::max(1, env_int("RVX_SAGE_CHUNKS", 24));
+    return n >= (int64_t)pipe_chunks * 16384 ? pipe_chunks : 1;
+}
+int64_t chunk_step(int64_t n, int chunks) { return ((n + chunks - 1) / chunks + 127) / 128 * 128; }
+
+std::vector<ExchangeRound> exchange_plan(int kind, const int64_t* offsets, int world) {
+    std::vector<ExchangeRound> plan;
+    if (kind == PLAN_WHOLE) {
+        ExchangeRound r;
+        for (int p = 0; p < world; ++p) {
+            r.r0.push_back(offsets[p]);
+            r.rows.push_back(offsets[p + 1] - offsets[p]);
+        }
+        plan.push_back(r);
+        return plan;
+    }
+    // every rank uses the chunk count of the largest shard, so the p2p rounds
+    // pair up (a shard with fewer real chunks sends empty ones)
+    int64_t maxn = 0;
+    for (int p = 0; p < world; ++p) maxn = std::max(maxn, offsets[p + 1] - offsets[p]);
+    const int chunks = sage_chunks_for(maxn);
+    for (int c = 0; c < chunks; ++c) {
+        ExchangeRound r;
+        for (int p = 0; p < world; ++p) {
+            const int64_t np = offsets[p + 1] - offsets[p];
+            const int64_t st = chunk_step(np, chunks);
+            const int64_t b = std::min(np, (int64_t)c * st);
+            r.r0.push_back(offsets[p] + b);
+            r.rows.push_back(std::min(st, np - b));
+        }
+        plan.push_back(r);
+    }
+    return plan;
+}
+
 namespace {
 
 // Finish a graph once row_ptr/col are on the device and a host row_ptr is known.
@@ -124,14 +163,6 @@ struct rvx_gcn_layer {
 
 namespace {
 
-// Row chunking of the layer pipeline (same on every rank for a given chunk count).
-int sage_chunks_for(int64_t n) {
-    // 24 chunks with the gather capped at one block per CU (k_aggregate.hip):
-    // 1.46G vs 1.37G edges/s for 16 uncapped at 10M x 768 (scripts/exp_sweep3.sh)
-    static const int pipe_chunks = std::max(1, env_int("RVX_SAGE_CHUNKS", 24));
-    return n >= (int64_t)pipe_chunks * 16384 ? pipe_chunks : 1;
-}
-int64_t chunk_step(int64_t n, int chunks) { return ((n + chunks - 1) / chunks + 127) / 128 * 128; }
 
 // Called on the host after chunk c's launches are queued (rows [r0, r0+rows)
 // of y, possibly empty); the chunk's output is complete at that point of the
@@ -436,27 +467,16 @@ rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g
             sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me]);
             return;
         }
-        // every rank uses the chunk count of the largest shard, so the p2p
-        // rounds pair up (a shard with fewer real chunks sends empty ones)
-        int64_t maxn = 0;
-        for (int p = 0; p < world; ++p) maxn = std::max(maxn, offsets[p + 1] - offsets[p]);
-        const int chunks = sage_chunks_for(maxn);
+        const std::vector<ExchangeRound> plan = exchange_plan(PLAN_SAGE, offsets, world);
+        const int chunks = (int)plan.size();
         Device& d = device();
         hipEvent_t* ev = pipeline_events(2 * chunks + 2) + chunks + 1;
-        std::vector<int64_t> r0(world), rows(world);
         auto hook = [&](int c, int64_t, int64_t) {
-            for (int p = 0; p < world; ++p) {
-                const int64_t np = offsets[p + 1] - offsets[p];
-                const int64_t st = chunk_step(np, chunks);
-                const int64_t b = std::min(np, (int64_t)c * st);
-                r0[p] = offsets[p] + b;
-                rows[p] = std::min(st, np - b);
-            }
             RVX_HIP(hipEventRecord(ev[c], d.stream));
             RVX_HIP(hipStreamWaitEvent(d.xfer, ev[c], 0));
             StreamScope on_xfer(d.xfer);
             ProfScope ps("halo_exchange");
-            comm_exchange_rows(comm, y, l->out, r0.data(), rows.data(), d.xfer);
+            comm_exchange_rows(comm, y, l->out, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
         };
         sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], chunks, hook);
         RVX_HIP(hipEventRecord(ev[chunks], d.xfer));
@@ -512,6 +532,26 @@ rvx_status rvx_gcn_forward(const rvx_gcn_layer* l, const rvx_graph* g, int32_t u
         gcn_forward_dev(l, g, use_w != 0, dx, dy);
         RVX_HIP(hipMemcpyAsync(y, dy, (size_t)(n * l->out * 4), hipMemcpyDeviceToHost, stream()));
         sync();
+    });
+}
+
+rvx_status rvx_exchange_plan(int32_t kind, const int64_t* offsets, int32_t world, int32_t* n_rounds, int64_t* r0,
+                             int64_t* rows) {
+    return guard([&] {
+        RVX_REQUIRE(offsets && n_rounds && world > 0 && (kind == PLAN_SAGE || kind == PLAN_WHOLE),
+                    RVX_ERR_INVALID_PARAMETER, "bad plan arguments");
+        for (int p = 0; p < world; ++p)
+            RVX_REQUIRE(offsets[p] >= 0 && offsets[p] <= offsets[p + 1], RVX_ERR_INVALID_PARAMETER,
+                        "offsets must be non-decreasing");
+        const std::vector<ExchangeRound> plan = exchange_plan(kind, offsets, world);
+        *n_rounds = (int32_t)plan.size();
+        if (!r0) return;
+        RVX_REQUIRE(rows, RVX_ERR_INVALID_PARAMETER, "null rows");
+        for (size_t c = 0; c < plan.size(); ++c)
+            for (int p = 0; p < world; ++p) {
+                r0[c * world + p] = plan[c].r0[p];
+                rows[c * world + p] = plan[c].rows[p];
+            }
     });
 }
 

@@ -17,6 +17,8 @@
 #include <string>
 
 #include "common.hpp"
+#include "gnn.hpp"
+#include "graph.hpp"
 #include "index.hpp"
 
 namespace rvx {
@@ -202,6 +204,29 @@ rvx_status rvx_index_export_rows(const rvx_index* ix, int64_t row0, int64_t coun
         if (vecs) ix->vecs.download(vecs, count * d * 4, row0 * d * 4);
         if (ids) std::copy(ix->ids.begin() + row0, ix->ids.begin() + row0 + count, ids);
         if (deleted) std::copy(ix->deleted_h.begin() + row0, ix->deleted_h.begin() + row0 + count, deleted);
+    });
+}
+
+rvx_status rvx_buffer_gather_rows_f32(const rvx_buffer* table, int64_t rows, int32_t dim, const int64_t* ids,
+                                     int64_t n, float* out) {
+    return guard([&] {
+        RVX_REQUIRE(table && dim > 0 && rows >= 0 && n >= 0 && (n == 0 || (ids && out)), RVX_ERR_INVALID_PARAMETER,
+                    "bad arguments");
+        RVX_REQUIRE(table->mem.bytes >= rows * (int64_t)dim * 4, RVX_ERR_DIMENSION_MISMATCH,
+                    "table smaller than rows*dim");
+        for (int64_t i = 0; i < n; ++i)
+            RVX_REQUIRE(ids[i] >= 0 && ids[i] < rows, RVX_ERR_INDEX, "row id out of range");
+        ComputeLock cl;
+        const int64_t step = std::max<int64_t>(1, std::min<int64_t>(n, ((int64_t)256 << 20) / ((int64_t)dim * 4)));
+        auto* dids = (int64_t*)scratch_bytes("gather_ids", step * 8);
+        float* dst = scratch_f32("gather_rows", step * dim);
+        for (int64_t r0 = 0; r0 < n; r0 += step) {
+            const int64_t m = std::min(step, n - r0);
+            RVX_HIP(hipMemcpyAsync(dids, ids + r0, (size_t)m * 8, hipMemcpyHostToDevice, stream()));
+            star_gather(nullptr, 1, table->mem.as<float>(), rows, dids, (int)m, dim, dst);
+            RVX_HIP(hipMemcpyAsync(out + r0 * dim, dst, (size_t)(m * dim * 4), hipMemcpyDeviceToHost, stream()));
+            rvx::sync();
+        }
     });
 }
 

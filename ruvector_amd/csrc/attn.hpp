@@ -48,7 +48,14 @@ void dual_space_attention(const DsaArgs& a);
 // project_to_ball (ruvector-attention hyperbolic/poincare.rs:121-132, eps 1e-5) of every
 // row in place, nh[r] = |row r|^2 after projection.
 void dsa_project_rows(float* t, int64_t rows, int dim, float curvature, float* nh);
+// differentiable_search (search.rs:56-94) for nq queries: candidates of query i
+// are cand[i*C .. i*C+C) rows, or all C rows of one shared table (shared_table).
+// out_idx/out_w [nq][k] (idx -1 past min(k, C)); soft (nullable) [nq][C].
 void differentiable_search(const float* q, int64_t nq, const float* cand, int C, int d, int k, float temperature,
-                           float* sims, int64_t* out_idx, float* out_w, float* soft = nullptr);
+                           float* sims, int64_t* out_idx, float* out_w, float* soft = nullptr,
+                           bool shared_table = false);
+// hierarchical_forward's combine step (search.rs:132-148): comb = (cur + sum_t w_t table[idx_t]) / 2.
+void hier_combine(const float* cur, int64_t nq, const float* table, int d, const int64_t* idx, const float* w, int k,
+                  float* comb);
 
 }  // namespace rvx

@@ -1,5 +1,7 @@
 // comm.hpp — internal RCCL helpers shared by the layer drivers.
 #pragma once
+#include <vector>
+
 #include "common.hpp"
 
 struct rvx_comm;
@@ -16,5 +18,15 @@ int comm_size(const rvx_comm* c);
 // round moves all peers' chunks concurrently.
 void comm_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int64_t* r0, const int64_t* rows,
                         hipStream_t s);
+
+// Exchange round plan (rvx_exchange_plan): plan[c] = {r0[p], rows[p]} of round c.
+enum { PLAN_SAGE = 0, PLAN_WHOLE = 1 };
+struct ExchangeRound {
+    std::vector<int64_t> r0, rows;
+};
+std::vector<ExchangeRound> exchange_plan(int kind, const int64_t* offsets, int world);
+// Row chunks of a GraphSAGE layer pipeline over n rows (same on every rank).
+int sage_chunks_for(int64_t n);
+int64_t chunk_step(int64_t n, int chunks);
 
 }  // namespace rvx

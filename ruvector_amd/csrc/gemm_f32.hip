@@ -1216,7 +1216,7 @@ void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, con
     if (s1) fast = fast && (s1->K % 4 == 0) && (s1->lda % 4 == 0) && (s1->ldb % 4 == 0) && aligned16(s1->A) &&
                    aligned16(s1->B);
     const char* t = tag ? tag : "gemm_nt";
-    static const int x3_mode = env_int("RVX_GEMM_X3", 1);
+    const int x3_mode = env_int("RVX_GEMM_X3", 1);  // read per call: bench times every GEMM path
     bool x3 = fast && x3_mode && s0.Bx3 && (s0.K % 8 == 0) && (s0.ldb % 8 == 0);
     if (s1) x3 = x3 && s1->Bx3 && (s1->K % 8 == 0) && (s1->ldb % 8 == 0);
     if (x3) {

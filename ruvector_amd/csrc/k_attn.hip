@@ -133,19 +133,32 @@ __global__ __launch_bounds__(256) void k_edge_feat_out(EfaArgs a) {
 }
 
 // ---- differentiable_search -------------------------------------------------
-__global__ __launch_bounds__(64) void k_diff_search(const float* q, int64_t nq, const float* cand, int C, int d, int k,
-                                                    float temperature, float* sims, int64_t* out_idx, float* out_w,
-                                                    float* soft) {
+// One wave per query. cand rows of query qi start at cand + qi * cand_q_stride
+// (stride C*d: per-query candidate lists; 0: one table shared by every query,
+// hierarchical_forward's layer embeddings). Lanes split the candidates for the
+// similarities, the max (order-free), the exps and the divisions; the softmax
+// denominator is summed by lane 0 in candidate order (search.rs:41 `.sum()`),
+// so every weight is the reference's value. The top-k (stable descending sort,
+// search.rs:80-88) is k rounds of a wave arg-max under (weight desc, index asc).
+__device__ __forceinline__ bool ds_better(float w, int j, float bw, int bj) {
+    return bj < 0 || w > bw || (w == bw && j < bj);
+}
+
+__global__ __launch_bounds__(64) void k_diff_search(const float* q, int64_t nq, const float* cand,
+                                                    int64_t cand_q_stride, int C, int d, int k, float temperature,
+                                                    float* sims, int64_t* out_idx, float* out_w, float* soft) {
     const int lane = threadIdx.x;
     const int64_t qi = blockIdx.x;
     if (qi >= nq) return;
     const float* qv = q + qi * d;
+    const float* cq = cand + qi * cand_q_stride;
     float* s = sims + qi * C;
     double qn2 = 0.0;
     for (int c = 0; c < d; ++c) qn2 = qn2 + (double)qv[c] * (double)qv[c];
     const float na = (float)sqrt(qn2);
+    float mx = -INFINITY;
     for (int j = lane; j < C; j += 64) {
-        const float* cv = cand + (qi * C + j) * (int64_t)d;
+        const float* cv = cq + (int64_t)j * d;
         float dot = 0.0f;
         double n2 = 0.0;
         for (int c = 0; c < d; ++c) {
@@ -153,36 +166,70 @@ __global__ __launch_bounds__(64) void k_diff_search(const float* q, int64_t nq, 
             n2 = n2 + (double)cv[c] * (double)cv[c];
         }
         const float nb = (float)sqrt(n2);
-        s[j] = (na == 0.0f || nb == 0.0f) ? 0.0f : dot / (na * nb);
+        const float sim = (na == 0.0f || nb == 0.0f) ? 0.0f : dot / (na * nb);
+        s[j] = sim;
+        mx = fmaxf(mx, sim);
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    // softmax with temperature (search.rs:29-44)
+    for (int j = lane; j < C; j += 64) s[j] = expf((s[j] - mx) / temperature);
     __builtin_amdgcn_wave_barrier();
     __threadfence_block();
-    if (lane != 0) return;
-    // softmax with temperature (search.rs:29-44)
-    float mx = -INFINITY;
-    for (int j = 0; j < C; ++j) mx = fmaxf(mx, s[j]);
     float sum = 0.0f;
-    for (int j = 0; j < C; ++j) { const float e = expf((s[j] - mx) / temperature); s[j] = e; sum = sum + e; }
-    sum = fmaxf(sum, 1e-10f);
-    for (int j = 0; j < C; ++j) s[j] = s[j] / sum;
-    if (soft)
-        for (int j = 0; j < C; ++j) soft[qi * C + j] = s[j];
-    // stable sort by weight descending (ties keep index order), take k
+    if (lane == 0) {
+        for (int j = 0; j < C; ++j) sum = sum + s[j];
+        sum = fmaxf(sum, 1e-10f);
+    }
+    sum = __shfl(sum, 0);
+    for (int j = lane; j < C; j += 64) {
+        const float w = s[j] / sum;
+        s[j] = w;
+        if (soft) soft[qi * C + j] = w;
+    }
+    if (k == 0) return;
+    // stable sort by weight descending (ties keep index order), take k; NaN
+    // weights (no order in partial_cmp) are never taken
     const int kk = min(k, C);
     for (int t = 0; t < k; ++t) {
-        if (t >= kk) { out_idx[qi * k + t] = -1; out_w[qi * k + t] = 0.0f; continue; }
-        int best = -1;
+        int bj = -1;
         float bw = 0.0f;
-        for (int j = 0; j < C; ++j) {
-            if (s[j] != s[j] && best < 0) continue;  // NaN weights sort as equal; skip
-            const float w = s[j];
-            if (w == -INFINITY) continue;
-            if (best < 0 || w > bw) { best = j; bw = w; }
+        if (t < kk)
+            for (int j = lane; j < C; j += 64) {
+                const float w = s[j];
+                if (w != w || w == -INFINITY) continue;  // NaN or consumed
+                if (ds_better(w, j, bw, bj)) { bj = j; bw = w; }
+            }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int oj = __shfl_xor(bj, o);
+            const float ow = __shfl_xor(bw, o);
+            if (oj >= 0 && ds_better(ow, oj, bw, bj)) { bj = oj; bw = ow; }
         }
-        if (best < 0) { out_idx[qi * k + t] = -1; out_w[qi * k + t] = 0.0f; continue; }
-        out_idx[qi * k + t] = best;
-        out_w[qi * k + t] = bw;
-        s[best] = -INFINITY;  // consumed
+        if (lane == 0) {
+            out_idx[qi * k + t] = bj;
+            out_w[qi * k + t] = bj < 0 ? 0.0f : bw;
+        }
+        if (bj >= 0 && (bj & 63) == lane) s[bj] = -INFINITY;  // consumed (owner lane rereads it)
+    }
+}
+
+// hierarchical_forward's combine (search.rs:132-148): agg = sum_t w_t * row(idx_t)
+// accumulated in top-k order from 0, combined = (cur + agg) / 2. Lanes over
+// columns, one block per query.
+__global__ __launch_bounds__(256) void k_hier_combine(const float* cur, int64_t nq, const float* table, int d,
+                                                      const int64_t* idx, const float* w, int k, float* comb) {
+    const int64_t qi = blockIdx.x;
+    if (qi >= nq) return;
+    for (int c = threadIdx.x; c < d; c += blockDim.x) {
+        float agg = 0.0f;
+        for (int t = 0; t < k; ++t) {
+            const int64_t j = idx[qi * k + t];
+            if (j < 0) continue;
+            const float p = w[qi * k + t] * table[j * d + c];
+            agg = agg + p;
+        }
+        comb[qi * d + c] = (cur[qi * d + c] + agg) / 2.0f;
     }
 }
 
@@ -207,12 +254,16 @@ void edge_feat_attention(const EfaArgs& a) {
 }
 
 void differentiable_search(const float* q, int64_t nq, const float* cand, int C, int d, int k, float temperature,
-                           float* sims, int64_t* out_idx, float* out_w, float* soft) {
+                           float* sims, int64_t* out_idx, float* out_w, float* soft, bool shared_table) {
     if (nq <= 0) return;
-    ProfScope ps("differentiable_search");
-    hipLaunchKernelGGL(k_diff_search, dim3((unsigned)nq), dim3(64), 0, stream(), q, nq, cand, C, d, k, temperature, sims,
-                       out_idx, out_w, soft);
-    RVX_HIP(hipGetLastError());
+    RVX_LAUNCH("differentiable_search", k_diff_search, dim3((unsigned)nq), dim3(64), 0, q, nq, cand,
+               shared_table ? (int64_t)0 : (int64_t)C * d, C, d, k, temperature, sims, out_idx, out_w, soft);
+}
+
+void hier_combine(const float* cur, int64_t nq, const float* table, int d, const int64_t* idx, const float* w, int k,
+                  float* comb) {
+    if (nq <= 0) return;
+    RVX_LAUNCH("hier_combine", k_hier_combine, dim3((unsigned)nq), dim3(256), 0, cur, nq, table, d, idx, w, k, comb);
 }
 
 

@@ -180,7 +180,12 @@ int32_t rvx_last_error(char* buf, size_t len) {
     return (int32_t)m.size();
 }
 
-const char* rvx_version(void) { return "rvx 0.1.0 (gfx950)"; }
+#ifndef RVX_SRC_HASH
+#define RVX_SRC_HASH "unknown"
+#endif
+// "rvx <version> (gfx950) src <hash>": the hash is sha256 over the library's
+// sources (Makefile SRC_HASH), checked against the shipped tree on import.
+const char* rvx_version(void) { return "rvx 0.2.0 (gfx950) src " RVX_SRC_HASH; }
 
 rvx_status rvx_device_count(int32_t* count) {
     return guard([&] {

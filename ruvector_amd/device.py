@@ -54,6 +54,15 @@ class Buffer:
         a = np.ascontiguousarray(a)
         L.call("rvx_buffer_upload", self._h, a.ctypes.data_as(C.c_void_p), a.nbytes, offset)
 
+    def gather_rows(self, rows: int, dim: int, ids) -> np.ndarray:
+        """Rows `ids` of this buffer viewed as a [rows][dim] f32 table (device gather)."""
+        ids = np.ascontiguousarray(ids, dtype=np.int64).reshape(-1)
+        out = np.empty((ids.size, dim), np.float32)
+        if ids.size:
+            L.call("rvx_buffer_gather_rows_f32", self._h, int(rows), int(dim), ids.ctypes.data_as(C.c_void_p),
+                   ids.size, out.ctypes.data_as(C.c_void_p))
+        return out
+
     def download(self, dtype, shape, offset: int = 0) -> np.ndarray:
         out = np.empty(shape, dtype=dtype)
         if out.nbytes:

@@ -238,22 +238,49 @@ def differentiable_search(query, candidate_embeddings, k: int, temperature: floa
     return [int(i) for i in idx[0]], [float(x) for x in w[0]]
 
 
+def hierarchical_forward_device(q: Buffer, nq: int, dim: int, levels: Sequence[Tuple[Buffer, int]],
+                                gnn_layers: Sequence[RuvectorLayer], out: Buffer) -> int:
+    """hierarchical_forward (search.rs:105-162) for nq queries resident in HBM:
+    levels[s] = (buffer, rows) of level s's embeddings. Returns the output dim."""
+    nl, nv = len(gnn_layers), len(levels)
+    lay = (C.c_void_p * max(nl, 1))(*[l._h.value if isinstance(l._h, C.c_void_p) else l._h for l in gnn_layers])
+    lev = (C.c_void_p * max(nv, 1))(*[b.handle.value if isinstance(b.handle, C.c_void_p) else b.handle
+                                      for b, _ in levels])
+    rows = np.ascontiguousarray([int(r) for _, r in levels] or [0], dtype=np.int64)
+    od = C.c_int32(0)
+    _check("rvx_hierarchical_forward_device", lay, nl, lev, L.i64ptr(rows), nv, q.handle, int(nq), int(dim),
+           out.handle, C.byref(od))
+    return od.value
+
+
+def hierarchical_forward_batch(queries: np.ndarray, layer_embeddings: Sequence[np.ndarray],
+                               gnn_layers: Sequence[RuvectorLayer]) -> np.ndarray:
+    """hierarchical_forward for a batch of queries [nq][d] over shared layer embeddings
+    (one device pass per level; see rvx_hierarchical_forward_device)."""
+    q = L.f32c(queries)
+    if q.ndim == 1:
+        q = q[None]
+    nq, d = q.shape
+    levels, keep, dd = [], [], d
+    for s, emb in enumerate(layer_embeddings[:len(gnn_layers)]):
+        e = L.f32c(emb).reshape(len(emb), -1) if len(emb) else np.zeros((0, dd), np.float32)
+        if len(e) and e.shape[1] != dd:
+            raise GnnError(1, f"level {s} embeddings have dim {e.shape[1]}, expected {dd}")
+        b = Buffer.from_numpy(e)
+        keep.append(b)
+        levels.append((b, len(e)))
+        if len(e):
+            dd = gnn_layers[s].hidden_dim
+    out_dim = max([d] + [l.hidden_dim for l in gnn_layers])
+    qb, ob = Buffer.from_numpy(q), Buffer(max(nq * out_dim * 4, 4))
+    od = hierarchical_forward_device(qb, nq, d, levels, gnn_layers, ob)
+    return ob.download(np.float32, (nq, od))
+
+
 def hierarchical_forward(query, layer_embeddings: Sequence[Sequence[Sequence[float]]],
                          gnn_layers: Sequence[RuvectorLayer]) -> np.ndarray:
-    """hierarchical_forward (search.rs:105-162)."""
+    """hierarchical_forward (search.rs:105-162) for one query (the reference signature)."""
     cur = L.f32c(query).reshape(-1)
     if len(layer_embeddings) == 0 or len(gnn_layers) == 0:
         return cur
-    for embeddings, layer in zip(layer_embeddings, gnn_layers):
-        if len(embeddings) == 0:
-            continue
-        emb = L.f32c(embeddings)
-        idx, w = differentiable_search(cur, emb, min(5, len(emb)), 1.0)
-        agg = np.zeros_like(cur)
-        for i, wt in zip(idx, w):
-            row = emb[i]
-            for c in range(min(len(row), len(agg))):
-                agg[c] = np.float32(agg[c] + np.float32(wt) * row[c])
-        combined = ((cur + agg) / np.float32(2.0)).astype(np.float32)
-        cur = layer.forward(combined, [emb[i] for i in idx], w)
-    return cur
+    return hierarchical_forward_batch(cur[None], layer_embeddings, gnn_layers)[0]

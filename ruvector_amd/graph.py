@@ -51,6 +51,21 @@ class Graph:
         return cls(h)
 
     @classmethod
+    def shard_from_csr(cls, row_ptr, col, num_nodes_total: int, edge_weights=None) -> "Graph":
+        """A node-range shard: CSR rows of this rank's destination nodes whose column
+        ids are GLOBAL node ids in [0, num_nodes_total) (the *_forward_exchange layout)."""
+        rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+        cl = np.ascontiguousarray(col, dtype=np.int32)
+        if cl.size and (int(cl.min()) < 0 or int(cl.max()) >= num_nodes_total):
+            raise L.RvxError(3, "column index out of range")
+        rpb, clb = Buffer.from_numpy(rp), Buffer.from_numpy(cl if cl.size else np.zeros(1, np.int32))
+        wb = None if edge_weights is None else Buffer.from_numpy(L.f32c(edge_weights))
+        h = C.c_void_p()
+        L.call("rvx_graph_from_device_csr", len(rp) - 1, int(rp[-1]), rpb.handle, clb.handle,
+               wb.handle if wb is not None else None, C.byref(h))
+        return cls(h, keep=(rpb, clb) if wb is None else (rpb, clb, wb))
+
+    @classmethod
     def random(cls, num_nodes: int, degree: int, seed: int, weight_seed: Optional[int] = None) -> "Graph":
         """Uniform random out-degree CSR generated on the device (SURVEY §8d C2);
         with weight_seed, edge weights uniform [0, 1) from the same generator."""

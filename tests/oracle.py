@@ -37,6 +37,9 @@ _SIG = {
     "orc_flat_search": (None, [PF, I64, I64, I32, PU8, PF, I64, I32, PI64, PF, I32]),
     "orc_hnsw_new": (P, [I64, I32, I32, I32, I32, U64]),
     "orc_hnsw_free": (None, [P]),
+    "orc_hnsw_set_fast": (None, [P, I32]),
+    "orc_simd_width": (I32, []),
+    "orc_flat_search_fast": (None, [PF, I64, I64, I32, PF, I64, I32, PI64, PF, I32]),
     "orc_hnsw_insert": (None, [P, PF, I64, I32]),
     "orc_hnsw_search": (None, [P, PF, I64, I32, I32, PI64, PF, PI32, I32]),
     "orc_hnsw_export_sizes": (None, [P, PI64, PI32, PI64, PI64, PI64, PI64]),
@@ -53,6 +56,7 @@ _SIG = {
     "orc_rvl_forward_graph": (None, [C.POINTER(Rvl), PF, I64, PI64, PI32, PF, I64, I64, PF, I32]),
     "orc_cosine_similarity": (F32, [PF, PF, I64]),
     "orc_differentiable_search": (I32, [PF, PF, I32, I64, I32, F32, PI64, PF]),
+    "orc_hierarchical_forward": (I32, [P, I32, P, PI64, I32, PF, I32, PF]),
     "orc_efa_init": (None, [I32, I32, I32, PF, PF, PF, PF, PF]),
     "orc_dsa_init": (None, [I32, PF, PF, PF]),
     "orc_dsa_compute": (I32, [I32, F32, F32, F32, F32, PF, PF, PF, PF, PF, PF, I32, I32, PF]),
@@ -357,6 +361,20 @@ def differentiable_search(q, cand, k, temperature):
     w = np.empty(max(k, 1), np.float32)
     n = lib().orc_differentiable_search(fp(q), fp(cand) if c else None, c, q.size, k, temperature, ip64(idx), fp(w))
     return idx[:n], w[:n]
+
+
+def hierarchical_forward(q, levels, weights):
+    """hierarchical_forward (search.rs:105-162), one query; levels: list of [rows][dim]
+    arrays, weights: list of RvlWeights (zip of the two)."""
+    q = f32(q).reshape(-1)
+    nl, nv = len(weights), len(levels)
+    lv = [f32(np.asarray(e, np.float32).reshape(len(e), -1)) if len(e) else np.zeros((0, 1), np.float32) for e in levels]
+    lay = (C.c_void_p * max(nl, 1))(*[C.cast(C.byref(W.s), C.c_void_p).value for W in weights])
+    lev = (C.c_void_p * max(nv, 1))(*[e.ctypes.data if e.size else None for e in lv])
+    rows = np.ascontiguousarray([len(e) for e in lv] or [0], dtype=np.int64)
+    out = np.empty(max([q.size] + [W.H for W in weights]), np.float32)
+    n = lib().orc_hierarchical_forward(lay, nl, lev, ip64(rows), nv, fp(q), q.size, fp(out))
+    return out[:n].copy()
 
 
 def efa_init(node_dim, edge_dim, heads):

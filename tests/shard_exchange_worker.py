@@ -1,0 +1,111 @@
+"""One rank of tests/test_gpu_shard_exchange.py (not collected by pytest).
+
+Runs the three C++ node-range exchange entry points with world > 1 — all ranks
+share GPU 0 over the host-staged transport (rvx_comm_init_host; RCCL refuses
+two ranks on one device) — and compares with the 1-process forward:
+
+  * rvx_sage_forward_exchange, 2 layers: after layer 1 EVERY row of the table
+    (owned rows + the rows received from each peer, round by round) must equal
+    the unsharded layer bit for bit; layer 2's owned rows likewise;
+  * rvx_gnn_forward_exchange (RuvectorLayer, M|K|V exchange): owned rows;
+  * rvx_edge_attention_forward_exchange (T exchange): owned rows.
+
+usage: shard_exchange_worker.py WORLD RANK PORT OUT_JSON OFFSETS(comma-separated)
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    world, rank, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    offsets = np.array([int(v) for v in sys.argv[5].split(",")], np.int64)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RVX_SAGE_CHUNKS"] = "3"  # several exchange rounds at test size (>= 3 x 16384 rows per shard)
+    import ctypes as C
+
+    import torch.distributed as dist
+
+    import oracle as O
+    import ruvector_amd as rv
+    from ruvector_amd.attention import EdgeFeaturedAttention, EdgeFeaturedConfig
+    from ruvector_amd.shard import PLAN_SAGE, HostComm, exchange_plan
+
+    from datetime import timedelta
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=90))
+    res = {"rank": rank}
+    try:
+        rv.set_device(0)
+        comm = HostComm(world, rank)
+        N = int(offsets[-1])
+        o0, o1 = int(offsets[rank]), int(offsets[rank + 1])
+        off_p = offsets.ctypes.data_as(C.POINTER(C.c_int64))
+        one = np.array([0, N], np.int64)
+        one_p = one.ctypes.data_as(C.POINTER(C.c_int64))
+        res["rounds"] = len(exchange_plan(PLAN_SAGE, offsets))
+
+        # ---- GraphSAGE (chunked rounds overlapped with the layer pipeline)
+        d, deg = 32, 6
+        x = O.fill_uniform(N * d, 81).reshape(N, d)
+        rp, col = O.random_csr(N, deg, 82)
+        g_full = rv.Graph.from_csr(rp, col)
+        g_loc = rv.Graph.shard_from_csr(rp[o0:o1 + 1] - rp[o0], col[rp[o0]:rp[o1]], N)
+        layer = rv.GraphSAGELayer(d, d, num_samples=deg)
+        xb = rv.Buffer.from_numpy(x)
+        y1, y2, r1, r2 = (rv.Buffer(N * d * 4) for _ in range(4))
+        for b in (y1, y2):
+            b.upload(np.full((N, d), np.nan, np.float32))  # unreceived rows would stay NaN
+        call = rv._lib.call
+        call("rvx_sage_forward_exchange", layer._h, g_loc.handle, xb.handle, y1.handle, off_p, comm._h, 1)
+        call("rvx_sage_forward_exchange", layer._h, g_loc.handle, y1.handle, y2.handle, off_p, comm._h, 0)
+        call("rvx_sage_forward_exchange", layer._h, g_full.handle, xb.handle, r1.handle, one_p, None, 0)
+        call("rvx_sage_forward_exchange", layer._h, g_full.handle, r1.handle, r2.handle, one_p, None, 0)
+        a1, b1 = y1.download(np.float32, (N, d)), r1.download(np.float32, (N, d))
+        a2, b2 = y2.download(np.float32, (N, d)), r2.download(np.float32, (N, d))
+        res["sage_layer1_all_rows_equal"] = bool(np.array_equal(a1, b1))
+        res["sage_layer1_halo_rows"] = int(N - (o1 - o0))
+        res["sage_layer2_owned_equal"] = bool(np.array_equal(a2[o0:o1], b2[o0:o1]))
+        ref = O.sage_forward(x, rp, col, O.sage_init(d, d, 0), O.sage_init(d, d, 1000), rows=(o0, min(o1 - o0, 500)))
+        res["sage_layer1_vs_oracle"] = float(np.max(np.abs(a1[o0:o0 + len(ref)] - ref)) / np.max(np.abs(ref)))
+
+        # ---- RuvectorLayer (M|K|V exchange) and the attention head (T exchange)
+        n2 = int(offsets[-1])
+        H, heads, deg2 = 64, 4, 5
+        xg = O.fill_uniform(n2 * H, 83).reshape(n2, H)
+        rp2, col2 = O.random_csr(n2, deg2, 84)
+        ew = O.fill_uniform(len(col2), 85, 0.0, 1.0)
+        gf = rv.Graph.from_csr(rp2, col2, ew)
+        gl = rv.Graph.shard_from_csr(rp2[o0:o1 + 1] - rp2[o0], col2[rp2[o0]:rp2[o1]], n2, ew[rp2[o0]:rp2[o1]])
+        rl = rv.RuvectorLayer(H, H, heads, 0.0, seed=7)
+        xgb = rv.Buffer.from_numpy(xg)
+        ys, yr = rv.Buffer(n2 * H * 4), rv.Buffer(n2 * H * 4)
+        rl.forward_exchange(gl, xgb, ys, offsets, comm)
+        rl.forward_graph_device(xgb, gf, yr)
+        res["gnn_owned_equal"] = bool(np.array_equal(ys.download(np.float32, (n2, H))[o0:o1],
+                                                     yr.download(np.float32, (n2, H))[o0:o1]))
+        att = EdgeFeaturedAttention(EdgeFeaturedConfig(node_dim=H, edge_dim=1, num_heads=heads))
+        efl, eff = rv.Buffer.from_numpy(ew[rp2[o0]:rp2[o1]].copy()), rv.Buffer.from_numpy(ew)
+        zs, zr = rv.Buffer(n2 * H * 4), rv.Buffer(n2 * H * 4)
+        att.forward_exchange(gl, yr, efl, zs, offsets, comm)
+        att.forward_graph_device(yr, gf, eff, zr)
+        res["efa_owned_equal"] = bool(np.array_equal(zs.download(np.float32, (n2, H))[o0:o1],
+                                                     zr.download(np.float32, (n2, H))[o0:o1]))
+        rv.synchronize()
+    except Exception as e:  # reported to the test, not swallowed
+        import traceback
+        res["error"] = f"{e!r}\n{traceback.format_exc()}"
+    finally:
+        with open(out, "w") as f:
+            json.dump(res, f)
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

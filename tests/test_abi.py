@@ -55,3 +55,13 @@ def test_graft_entry_exposes_build_and_smoke():
     m = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(m)
     assert callable(m.build) and callable(m.smoke)
+
+
+def test_library_built_from_shipped_sources():
+    """Binary provenance: rvx_version() carries the sha256 of the sources the
+    library was built from (Makefile SRC_HASH); it must equal the hash of the
+    tree's csrc + header, so a stale prebuilt librvx.so cannot run unnoticed."""
+    from ruvector_amd import _lib
+    lib = _lib.load()
+    assert _lib.built_hash(lib) == _lib.source_hash()
+    assert len(_lib.source_hash()) == 16

@@ -520,10 +520,79 @@ def test_differentiable_search_matches_oracle():
     assert i[0] == 0 and len(w) == 2
 
 
-def test_hierarchical_forward_shape():
-    layer = rv.RuvectorLayer(2, 2, 1, 0.0)
+def test_differentiable_search_ties_and_many_candidates():
+    """Wave-parallel top-k (k_attn.hip k_diff_search): 1000 candidates with exact
+    duplicates (equal weights keep index order, search.rs:80-82) and k > C."""
+    nq, c, d = 8, 1000, 32
+    q = O.fill_uniform(nq * d, 41).reshape(nq, d)
+    base = O.fill_uniform(nq * 250 * d, 42).reshape(nq, 250, d)
+    cand = np.ascontiguousarray(np.concatenate([base, base[:, ::-1], base, base[:, :1].repeat(250, 1)], axis=1))
+    idx, w = rv.differentiable_search_batch(q, cand, 16, 0.05)
+    for i in range(nq):
+        ri, rw = O.differentiable_search(q[i], cand[i], 16, 0.05)
+        assert np.array_equal(idx[i], ri)
+        assert_close(w[i], rw, 1e-6)
+    small = np.ascontiguousarray(cand[:, :3])
+    idx, w = rv.differentiable_search_batch(q, small, 5, 1.0)
+    assert idx.shape == (nq, 3)
+    for i in range(nq):
+        assert np.array_equal(idx[i], O.differentiable_search(q[i], small[i], 5, 1.0)[0])
+
+
+def test_hierarchical_forward_reference_case():
+    layer, W, _ = _layer_and_weights(2, 2, 1, 0.0)
     out = rv.hierarchical_forward([1.0, 0.0], [[[1.0, 0.0], [0.0, 1.0]]], [layer])
-    assert out.shape == (2,)
+    assert out.shape == (2,)  # search.rs:227-245
+    assert_close(out, O.hierarchical_forward([1.0, 0.0], [[[1.0, 0.0], [0.0, 1.0]]], [W]))
+
+
+@pytest.mark.parametrize("case", ["one", "three", "empty_level", "few_candidates", "zip_short", "wide"])
+def test_hierarchical_forward_batch_matches_oracle(case):
+    """Batched device hierarchical_forward (rvx_hierarchical_forward_device) vs the
+    oracle's per-query restatement of search.rs:105-162, 1..3 levels, dims changing
+    across layers, empty levels, fewer than 5 candidates."""
+    nq = 48
+    if case == "wide":
+        dims, rows = [768, 768], [2000]
+    elif case == "one":
+        dims, rows = [32, 32], [200]
+    elif case == "three":
+        dims, rows = [32, 48, 64, 32], [300, 40, 9]
+    elif case == "empty_level":
+        dims, rows = [32, 32, 16], [0, 50]      # layer 0 skipped with its level
+    elif case == "few_candidates":
+        dims, rows = [16, 24, 24], [3, 1]
+    else:  # zip_short: more layers than levels
+        dims, rows = [16, 16, 16], [20]
+    layers, ws = [], []
+    for s in range(len(dims) - 1):
+        heads = 8 if dims[s + 1] % 8 == 0 else 4
+        l, W, _ = _layer_and_weights(dims[s], dims[s + 1], heads, 0.0, seed=20 + s)
+        layers.append(l)
+        ws.append(W)
+    if case == "empty_level":  # level 1 pairs with layer 1 whose input is the query dim
+        l, W, _ = _layer_and_weights(32, 16, 4, 0.0, seed=30)
+        layers[1], ws[1] = l, W
+    levels = []
+    dcur = dims[0]
+    for s, r in enumerate(rows):
+        levels.append(O.fill_uniform(r * dcur, 50 + s).reshape(r, dcur) if r else np.zeros((0, dcur), np.float32))
+        if r:
+            dcur = ws[s].H
+    q = O.fill_uniform(nq * dims[0], 60).reshape(nq, dims[0])
+    got = rv.hierarchical_forward_batch(q, levels, layers)
+    ref = np.stack([O.hierarchical_forward(q[i], levels, ws) for i in range(nq)])
+    assert got.shape == ref.shape
+    assert_close(got, ref)
+    one = rv.hierarchical_forward(q[3], levels, layers)
+    assert np.array_equal(one, got[3])
+
+
+def test_hierarchical_forward_dimension_mismatch():
+    l, _, _ = _layer_and_weights(8, 8, 2, 0.0)
+    with pytest.raises(rv.GnnError) as e:
+        rv.hierarchical_forward_batch(np.zeros((2, 4), np.float32), [np.ones((3, 4), np.float32)], [l])
+    assert e.value.kind == "DimensionMismatch"
 
 
 # ------------------------------------------------------------------ graph attention

@@ -154,6 +154,38 @@ def test_ruvector_layer_no_neighbors_is_layernorm():
     assert abs(float(np.mean(out))) < 1e-5  # LayerNorm test (layer.rs:471-480)
 
 
+# ---- crates/ruvector-gnn/src/search.rs:227-245 (test_hierarchical_forward) ----
+def test_hierarchical_forward_len():
+    W = O.RvlWeights(_layer_json(2, 2, 1, 0.0))
+    out = O.hierarchical_forward([1.0, 0.0], [[[1.0, 0.0], [0.0, 1.0]]], [W])
+    assert out.shape == (2,) and np.all(np.isfinite(out))
+
+
+def test_hierarchical_forward_walk_rules():
+    """search.rs:109-111: no levels or no layers -> the query itself; :121-123 an empty
+    level skips its paired layer; zip bounds the walk by the shorter list; one level
+    equals the composition differentiable_search -> combine -> forward by hand."""
+    W1, W2 = O.RvlWeights(_layer_json(4, 6, 2, 0.0, 1)), O.RvlWeights(_layer_json(6, 4, 2, 0.0, 2))
+    q = np.array([0.3, -1.0, 0.5, 2.0], np.float32)
+    emb1 = O.fill_uniform(7 * 4, 3).reshape(7, 4)
+    emb2 = O.fill_uniform(3 * 6, 4).reshape(3, 6)
+    assert np.array_equal(O.hierarchical_forward(q, [], [W1]), q)
+    assert np.array_equal(O.hierarchical_forward(q, [emb1], []), q)
+    one = O.hierarchical_forward(q, [emb1], [W1])
+    idx, w = O.differentiable_search(q, emb1, 5, 1.0)
+    agg = np.zeros(4, np.float32)
+    for i, wt in zip(idx, w):
+        agg = (agg + np.float32(wt) * emb1[i]).astype(np.float32)
+    comb = ((q + agg) / np.float32(2.0)).astype(np.float32)
+    assert np.array_equal(one, O.rvl_forward_one(W1, comb, emb1[idx], w))
+    assert np.array_equal(O.hierarchical_forward(q, [emb1, emb2], [W1]), one)  # zip stops at 1
+    two = O.hierarchical_forward(q, [emb1, emb2], [W1, W2])
+    assert two.shape == (4,)
+    # empty first level: W1 skipped, level 2 (dim 6) cannot pair with a dim-4 query
+    skip = O.hierarchical_forward(q, [np.zeros((0, 4), np.float32), emb1], [W2, W1])
+    assert np.array_equal(skip, one)
+
+
 # ---- crates/ruvector-attention/src/graph/edge_featured.rs:327-393 ----------
 def test_edge_featured_attention_len():
     out = O.efa_compute(64, 16, 4, [0.5] * 64, [[0.3] * 64] * 10, [[1.0] * 64] * 10, [[0.2] * 16] * 10)

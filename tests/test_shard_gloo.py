@@ -170,3 +170,61 @@ def test_shard_plan_rows_cover_and_owner():
         for node in range(0, n, max(1, n // 97)):
             r = p.owner(node)
             assert spans[r][0] <= node < spans[r][1]
+
+
+# ---- the C++ round plan and the host-staged transport (no GPU needed) --------
+@pytest.mark.parametrize("offsets", [[0, 1000], [0, 500, 1001], [0, 60000, 100000, 150001],
+                                     [0, 400000, 800000], [0, 393216 * 2, 393216 * 2 + 5, 393216 * 3]])
+def test_exchange_plan_matches_mirror(offsets):
+    """rvx_exchange_plan (the plan rvx_sage_forward_exchange runs, api_graph.cpp
+    exchange_plan) equals the Python mirror shard.exchange_rounds; the whole-shard
+    plan of the RuvectorLayer / attention exchange is one round of full shards."""
+    from ruvector_amd import shard
+    assert shard.exchange_plan(shard.PLAN_SAGE, offsets) == shard.exchange_rounds(offsets)
+    whole = shard.exchange_plan(shard.PLAN_WHOLE, offsets)
+    assert whole == [[(offsets[p], offsets[p + 1] - offsets[p]) for p in range(len(offsets) - 1)]]
+    # every rank's rows are covered exactly once across the rounds
+    for p in range(len(offsets) - 1):
+        got = [r for rnd in shard.exchange_plan(shard.PLAN_SAGE, offsets) for r in [rnd[p]] if r[1]]
+        covered = np.concatenate([np.arange(a, a + n) for a, n in got]) if got else np.zeros(0, np.int64)
+        assert np.array_equal(covered, np.arange(offsets[p], offsets[p + 1]))
+
+
+def _host_comm_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import ctypes as C
+    import torch.distributed as dist
+    from ruvector_amd.shard import HostComm
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = HostComm(world, rank)
+        sizes = [3 + 2 * p if p != 1 else 0 for p in range(world)]  # rank 1 sends nothing
+        send = np.full(max(sizes[rank], 1), 10.0 * rank + 1, np.float32)
+        recv = [np.zeros(max(sizes[p], 1), np.float32) for p in range(world)]
+        ptrs = (C.c_void_p * world)(*[None if p == rank else recv[p].ctypes.data for p in range(world)])
+        nbytes = (C.c_int64 * world)(*[0 if p == rank else sizes[p] * 4 for p in range(world)])
+        rc = comm._fn(None, send.ctypes.data, sizes[rank] * 4, ptrs, nbytes)
+        ok = rc == 0 and all(np.all(recv[p][:sizes[p]] == 10.0 * p + 1) for p in range(world) if p != rank)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_transport_moves_every_block(world):
+    """HostComm's exchange callback (the host-staged transport behind rvx_comm_init_host)
+    delivers each rank's block to every peer, ragged and empty blocks included."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_host_comm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(res[r] for r in range(world)), res
