@@ -51,6 +51,8 @@ struct GemmArgs {
     const _Float16* B0h; const _Float16* B1h; int64_t B0h_plane, B1h_plane;
     // pre-split A (gemm_nt_h2p): f16 planes [2][M][lda] written by the producer
     const _Float16* A0h; const _Float16* A1h; int64_t Ah_plane;
+    // persistent split-f16 GEMM: per-XCD tile counters (stride 32 words), zeroed per launch
+    unsigned* queue;
 };
 
 __device__ __forceinline__ float epi_apply(int epi, float v) {
@@ -771,16 +773,21 @@ __device__ __forceinline__ void split_h2_pair(float a0, float a1, float sc, unsi
     w2 = (unsigned)__builtin_bit_cast(unsigned short, l0) | ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
 }
 
+// XCD x (= block id % 8: workgroups are dealt round-robin over the 8 XCDs)
+// owns the contiguous tile range [xcd_first(x), xcd_first(x) + xcd_count(x)).
+__device__ __forceinline__ int64_t xcd_first(int64_t nwg, int64_t xcd) {
+    const int64_t q = nwg / 8, r = nwg % 8;
+    return xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+}
+__device__ __forceinline__ int64_t xcd_count(int64_t nwg, int64_t xcd) { return nwg / 8 + (xcd < nwg % 8 ? 1 : 0); }
+
 template <bool DUAL>
-__device__ __forceinline__ void h2g_tile(const GemmArgs& g, int epi, int64_t bid) {
+__device__ __forceinline__ void h2g_tile(const GemmArgs& g, int epi, int64_t wgid) {
     constexpr int XA = 128 * 128;             // f32 A tile bytes per stage
     constexpr int STG = XA + 2 * XB_PLANE;    // 32 KB stage
     constexpr int NB = 4;                     // B DMA pieces per wave (2 planes x 8 pieces)
     extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
 
-    const int64_t nwg = g.nblocks;
-    const int64_t xcd = bid % 8, q = nwg / 8, r = nwg % 8;
-    const int64_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
     const int64_t tm = wgid / g.tiles_n;
     const int tn = (int)(wgid % g.tiles_n);
     const int64_t m0 = tm * 128;
@@ -1133,11 +1140,31 @@ __global__ __launch_bounds__(64 * WM, WM == 4 && NST == 2 ? 2 : 1) void gemm_nt_
 }
 
 // One tile per block, or (grid capped below the tile count, RVX_GEMM_CAP) a
-// persistent grid striding over the tiles in XCD-mapped order.
+// persistent grid. Persistent blocks drain their XCD's tile range through a
+// per-XCD atomic counter (g.queue, zeroed before the launch): tiles are taken
+// in row-tile-major order as blocks free up, so the column tiles of one
+// 128-row A tile start within a few tile-grabs of each other on one XCD and
+// share the A rows through its L2 (a static stride lets the blocks drift
+// apart and every column tile re-fetches A from HBM). Every block reaches the
+// counter's end, so the grid always drains.
 template <bool DUAL>
 __global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
+    if (g.queue) {
+        __shared__ int64_t s_t;
+        const int64_t xcd = blockIdx.x % 8;
+        const int64_t first = xcd_first(g.nblocks, xcd), cnt = xcd_count(g.nblocks, xcd);
+        for (;;) {
+            if (threadIdx.x == 0) s_t = (int64_t)atomicAdd(g.queue + 32 * xcd, 1u);
+            __syncthreads();
+            const int64_t t = s_t;
+            if (t >= cnt) break;
+            h2g_tile<DUAL>(g, epi, first + t);
+            __syncthreads();  // LDS stages and s_t are reused by the next tile
+        }
+        return;
+    }
     for (int64_t b = blockIdx.x; b < g.nblocks; b += gridDim.x) {
-        h2g_tile<DUAL>(g, epi, b);
+        h2g_tile<DUAL>(g, epi, xcd_first(g.nblocks, b % 8) + b / 8);
         if (b + gridDim.x < g.nblocks) __syncthreads();  // LDS stages are reused by the next tile
     }
 }
@@ -1327,6 +1354,10 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
     const int cap = persist >= 0 ? persist : env_int("RVX_GEMM_CAP", 0);
     int64_t grid = g.nblocks;
     if (cap > 0) grid = std::min<int64_t>(grid, ((int64_t)cap * device().num_cus + 7) / 8 * 8);
+    if (grid < g.nblocks && grid % 8 == 0 && env_int("RVX_GEMM_QUEUE", 1)) {
+        g.queue = (unsigned*)scratch_bytes("gemm_h2_queue", 8 * 32 * 4);
+        RVX_HIP(hipMemsetAsync(g.queue, 0, 8 * 32 * 4, stream()));
+    }
     if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
     else RVX_LAUNCH(t, gemm_nt_h2g<false>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
 }
