@@ -207,7 +207,9 @@ int64_t search_layer_single(const OHyp& h, const float* q, int64_t entry, int l)
     return current;
 }
 
-std::vector<R> search_layer(const OHyp& h, const float* q, int64_t entry, int ef, int l) {
+// lex_stop (the query path): the stop test compares (d, id) pairs, as the GPU
+// search does (oracle.cpp search_layer); differs only on exact distance ties.
+std::vector<R> search_layer(const OHyp& h, const float* q, int64_t entry, int ef, int l, bool lex_stop = false) {
     const float ed = h.dist(q, h.v(entry));
     std::unordered_set<int64_t> visited{entry};
     std::priority_queue<R, std::vector<R>, RMin> cand;
@@ -217,7 +219,8 @@ std::vector<R> search_layer(const OHyp& h, const float* q, int64_t entry, int ef
     while (!cand.empty()) {
         const R cur = cand.top();
         cand.pop();
-        if (cur.d > res.top().d && (int)res.size() >= ef) break;
+        const R& f = res.top();
+        if ((cur.d > f.d || (lex_stop && cur.d == f.d && cur.id > f.id)) && (int)res.size() >= ef) break;
         for (int64_t nb : h.conn[cur.id][l]) {
             if (!visited.insert(nb).second) continue;
             const float dd = h.dist(q, h.v(nb));
@@ -330,7 +333,7 @@ void orc_hyp_search(void* hp, const float* q, int64_t nq, int32_t k, int32_t ef_
         int64_t current = h.entry;
         for (int l = h.max_level; l >= 1; --l) current = search_layer_single(h, x.data(), current, l);
         const int ef = std::max(ef_arg > 0 ? ef_arg : h.efs, k);
-        std::vector<R> r = search_layer(h, x.data(), current, ef, 0);
+        std::vector<R> r = search_layer(h, x.data(), current, ef, 0, /*lex_stop=*/true);
         const int take = std::min<int>(k, (int)r.size());
         for (int s = 0; s < take; ++s) { oi[s] = r[s].id; od[s] = r[s].d; }
         if (counts) counts[qi] = take;

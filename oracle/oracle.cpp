@@ -362,7 +362,11 @@ std::vector<Cand> copy_list(const OHnsw& h, int64_t p, int l) {
 }
 
 // search_layer (hnsw.rs:913-1055), no filter. Returns R sorted ascending.
-std::vector<Cand> search_layer(const OHnsw& h, const float* q, int64_t ep, int ef, int layer) {
+// lex_stop (the query path, Hnsw::search): stop when the popped candidate is
+// beyond R's farthest in the (d, id) order rather than by distance alone — the
+// two differ only on an exact distance tie with the farthest, where the
+// reference's heap order is unspecified; the GPU search uses this rule.
+std::vector<Cand> search_layer(const OHnsw& h, const float* q, int64_t ep, int ef, int layer, bool lex_stop = false) {
     std::vector<Cand> out;
     if (h.count_at_level[layer].load() == 0) return out;  // points_by_layer[layer].is_empty()
     std::priority_queue<Cand, std::vector<Cand>, CandMax> R;
@@ -376,7 +380,7 @@ std::vector<Cand> search_layer(const OHnsw& h, const float* q, int64_t ep, int e
         const Cand c = C.top();
         C.pop();
         const Cand f = R.top();
-        if (c.d > f.d) break;  // -(c.dist_to_ref) > f.dist_to_ref -> return
+        if (c.d > f.d || (lex_stop && c.d == f.d && c.id > f.id)) break;  // -(c.dist_to_ref) > f.dist_to_ref -> return
         const std::vector<Cand> lst = copy_list(h, c.id, layer);
         for (const Cand& e : lst) {
             if (!visited.insert(e.id).second) continue;
@@ -542,7 +546,7 @@ void orc_hnsw_search(void* hp, const float* q, int64_t nq, int32_t k, int32_t ef
         const int ef = std::max(ef_arg, k);
         int layer_to_search = 0;
         while (layer_to_search < 16 && h.count_at_level[layer_to_search].load() == 0) ++layer_to_search;
-        const std::vector<Cand> r = search_layer(h, qv, pivot, ef, layer_to_search);
+        const std::vector<Cand> r = search_layer(h, qv, pivot, ef, layer_to_search, /*lex_stop=*/true);
         const int last = std::min<int64_t>(std::min(k, ef), (int64_t)r.size());
         for (int s = 0; s < last; ++s) { oi[s] = r[s].id; od[s] = r[s].d; }
         if (out_n) out_n[qi] = last;

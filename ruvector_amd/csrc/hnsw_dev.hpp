@@ -13,7 +13,8 @@ namespace rvx {
 namespace hnswdev {
 
 constexpr int VCAP_MIN = 32768;  // visited-set slots per query (power of two), grown with ef
-constexpr int C_EXTRA = 128; // candidate capacity = ef + C_EXTRA
+constexpr int C_EXTRA = 128; // candidate capacity = ef + C_EXTRA (builder)
+constexpr int ID_MASK = 0x7FFFFFFF;  // node ids; bit 31 is the search's expanded flag
 
 // One float4 step of the reference's scalar accumulation (distance.rs:34-85).
 template <int METRIC>
@@ -312,6 +313,73 @@ __device__ __forceinline__ void merge_sorted(float* ad, int* ai, int n, const fl
     __builtin_amdgcn_wave_barrier();
 }
 
+// Exact sequential admission decisions of one expansion's fresh neighbours
+// (lanes in fmask, in lane order) against a register window of R's largest
+// <= 64 entries (lane wn-1 = the max): each admission inserts into the window
+// (or below it) and pops the window max when |R| > ef, which reproduces the
+// exact sequence of farthest values. Returns the admitted lane mask; r = |R|
+// after the batch. R ids may carry the search's expanded flag in bit 31
+// (masked off here).
+__device__ __forceinline__ unsigned long long decide_batch(unsigned long long fmask, float dd, int nid, int ef,
+                                                           const float* rd, const int* ri, int rs, int& r, int lane) {
+    int wn = min(rs, 64);
+    int below = rs - wn;
+    float wd = INFINITY; int wi = INT_MAX;
+    if (lane < wn) { wd = rd[below + lane]; wi = ri[below + lane] & ID_MASK; }
+    r = rs;
+    unsigned long long adm = 0ull;
+    unsigned long long todo = fmask;
+    while (todo) {
+        const int src = __ffsll((long long)todo) - 1;
+        todo &= todo - 1;
+        const float ed = __shfl(dd, src);
+        const int eid = __shfl(nid, src);
+        const float fd = __shfl(wd, wn - 1);  // current farthest of R
+        if (!(ed < fd || r < ef)) continue;
+        adm |= 1ull << src;
+        r += 1;
+        const float w0d = __shfl(wd, 0);
+        const int w0i = __shfl(wi, 0);
+        if (below == 0 || !lt_de(ed, eid, w0d, w0i)) {
+            if (wn == 64) {  // keep 64: the smallest window entry moves below
+                wd = __shfl_down(wd, 1); wi = __shfl_down(wi, 1);
+                if (lane == 63) { wd = INFINITY; wi = INT_MAX; }
+                wn = 63; below += 1;
+            }
+            const int pos = __popcll(__ballot(lane < wn && lt_de(wd, wi, ed, eid)));
+            const float ud = __shfl_up(wd, 1);
+            const int ui = __shfl_up(wi, 1);
+            if (lane > pos && lane <= wn) { wd = ud; wi = ui; }
+            if (lane == pos) { wd = ed; wi = eid; }
+            wn += 1;
+        } else {
+            below += 1;
+        }
+        if (r > ef) {  // pop the farthest
+            if (lane == wn - 1) { wd = INFINITY; wi = INT_MAX; }
+            wn -= 1; r -= 1;
+        }
+    }
+    return adm;
+}
+
+// The admitted lanes' (d, id) sorted ascending into the scratch (sd, si)[0..na).
+__device__ __forceinline__ int sort_batch(unsigned long long adm, float dd, int nid, float* sd, int* si, int lane) {
+    const int na = __popcll(adm);
+    if (na == 0) return 0;
+    const bool mine = (adm >> lane) & 1ull;
+    int rank = 0;
+    for (unsigned long long t = adm; t; t &= t - 1) {
+        const int o = __ffsll((long long)t) - 1;
+        const float od = __shfl(dd, o);
+        const int oi = __shfl(nid, o);
+        rank += lt_de(od, oi, dd, nid) ? 1 : 0;
+    }
+    if (mine) { sd[rank] = dd; si[rank] = nid; }
+    __builtin_amdgcn_wave_barrier();
+    return na;
+}
+
 __device__ bool admit_batch(bool fresh, float dd, int nid, int ef, int ccap, float* rd, int* ri, int& rs, float* cd,
                             int* ci, int& cs, float* sd, int* si, int lane) {
     const unsigned long long fmask = __ballot(fresh);
@@ -350,58 +418,10 @@ __device__ bool admit_batch(bool fresh, float dd, int nid, int ef, int ccap, flo
         }
         return true;
     }
-    // 1. decisions against the window of R's largest entries
-    int wn = min(rs, 64);
-    int below = rs - wn;
-    float wd = INFINITY; int wi = INT_MAX;
-    if (lane < wn) { wd = rd[below + lane]; wi = ri[below + lane]; }
     int r = rs;
-    unsigned long long adm = 0ull;
-    unsigned long long todo = fmask;
-    while (todo) {
-        const int src = __ffsll((long long)todo) - 1;
-        todo &= todo - 1;
-        const float ed = __shfl(dd, src);
-        const int eid = __shfl(nid, src);
-        const float fd = __shfl(wd, wn - 1);  // current farthest of R
-        if (!(ed < fd || r < ef)) continue;
-        adm |= 1ull << src;
-        r += 1;
-        const float w0d = __shfl(wd, 0);
-        const int w0i = __shfl(wi, 0);
-        if (below == 0 || !lt_de(ed, eid, w0d, w0i)) {
-            if (wn == 64) {  // keep 64: the smallest window entry moves below
-                wd = __shfl_down(wd, 1); wi = __shfl_down(wi, 1);
-                if (lane == 63) { wd = INFINITY; wi = INT_MAX; }
-                wn = 63; below += 1;
-            }
-            const int pos = __popcll(__ballot(lane < wn && lt_de(wd, wi, ed, eid)));
-            const float ud = __shfl_up(wd, 1);
-            const int ui = __shfl_up(wi, 1);
-            if (lane > pos && lane <= wn) { wd = ud; wi = ui; }
-            if (lane == pos) { wd = ed; wi = eid; }
-            wn += 1;
-        } else {
-            below += 1;
-        }
-        if (r > ef) {  // pop the farthest
-            if (lane == wn - 1) { wd = INFINITY; wi = INT_MAX; }
-            wn -= 1; r -= 1;
-        }
-    }
-    const int na = __popcll(adm);
+    const unsigned long long adm = decide_batch(fmask, dd, nid, ef, rd, ri, rs, r, lane);
+    const int na = sort_batch(adm, dd, nid, sd, si, lane);
     if (na == 0) return true;
-    // 2. the admitted batch sorted ascending into the scratch
-    const bool mine = (adm >> lane) & 1ull;
-    int rank = 0;
-    for (unsigned long long t = adm; t; t &= t - 1) {
-        const int o = __ffsll((long long)t) - 1;
-        const float od = __shfl(dd, o);
-        const int oi = __shfl(nid, o);
-        rank += lt_de(od, oi, dd, nid) ? 1 : 0;
-    }
-    if (mine) { sd[rank] = dd; si[rank] = nid; }
-    __builtin_amdgcn_wave_barrier();
     merge_sorted(rd, ri, rs, sd, si, na, r, /*asc=*/true, lane);
     rs = r;
     // C is descending: the same batch reversed
@@ -413,6 +433,59 @@ __device__ bool admit_batch(bool fresh, float dd, int nid, int ef, int ccap, flo
     merge_sorted(cd, ci, cs, sd, si, na, cs + na, /*asc=*/false, lane);
     cs += na;
     return true;
+}
+
+// ---- search: R only ---------------------------------------------------------
+// The search keeps no candidate array: a candidate that is not in R is at or
+// beyond R's farthest in the (d, id) order and, R's farthest never growing
+// once |R| = ef, would end the search when popped, so "pop the nearest
+// candidate" is "take the nearest unexpanded entry of R" (bit 31 of its id
+// marks it expanded) and "stop" is "none left". That is search_layer's loop
+// (hnsw.rs:913-1055) with the stop test comparing (d, id) pairs, which only
+// differs from the reference's distance-only test on an exact distance tie
+// with R's farthest (the reference's heaps leave tie order unspecified).
+
+// R's rank of (d, id): entries of R (ascending, flagged ids) ordered before it
+__device__ __forceinline__ int rank_in_r(const float* rd, const int* ri, int n, float d, int id) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (lt_de(rd[mid], ri[mid] & ID_MASK, d, id)) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// Merge the ascending batch (sd, si)[0..na) into R (rd, ri)[0..n), keeping the
+// first nkeep entries. Each batch entry finds its rank in R by binary search;
+// R entry j moves right by #{batch entries ranked <= j}, a constant over every
+// 64-entry chunk that holds no batch rank, so only chunks at or after the
+// first rank move and each costs one ballot. Returns the first batch rank
+// (entries before it did not move).
+__device__ __forceinline__ int merge_into_r(float* rd, int* ri, int n, const float* sd, const int* si, int na, int nkeep,
+                                            int lane) {
+    float bd = 0.f; int bi = 0, rk = INT_MAX;
+    if (lane < na) { bd = sd[lane]; bi = si[lane]; rk = rank_in_r(rd, ri, n, bd, bi); }
+    const int first = __shfl(rk, 0);
+    __builtin_amdgcn_wave_barrier();
+    for (int base = ((n - 1) / 64) * 64; base >= 0 && base + 63 >= first; base -= 64) {
+        const int j = base + lane;
+        // batch entries ranked at or before the chunk, and those inside it
+        int shift = __popcll(__ballot(lane < na && rk <= base));
+        unsigned long long in = __ballot(lane < na && rk > base && rk <= base + 63);
+        while (in) {
+            const int b = __ffsll((long long)in) - 1;
+            in &= in - 1;
+            shift += (j >= __shfl(rk, b)) ? 1 : 0;
+        }
+        float vd = 0.f; int vi = 0;
+        if (j < n) { vd = rd[j]; vi = ri[j]; }
+        __builtin_amdgcn_wave_barrier();
+        if (j < n && j + shift < nkeep) { rd[j + shift] = vd; ri[j + shift] = vi; }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane < na && lane + rk < nkeep) { rd[lane + rk] = bd; ri[lane + rk] = bi; }
+    __builtin_amdgcn_wave_barrier();
+    return first;
 }
 
 // distance between two stored rows, reference scalar order (distance.rs)

@@ -14,14 +14,17 @@
 // Distances use the reference's scalar accumulation order (see k_scan.hip), so
 // on the same graph the returned ids and distances are bit-exact. The
 // reference orders heap ties by distance only (:272-296); here ties are
-// broken by node id in both heaps (a measure-zero difference on real data).
+// broken by node id, and the stop test compares (d, id) pairs (a measure-zero
+// difference on real data; the oracle's search uses the same rule).
 //
-// Per query: result set R as an ascending sorted array (farthest last) and the
-// candidate set C as a descending sorted array (nearest last) in LDS, updated
-// once per expansion by admit_batch (hnsw_dev.hpp: exact sequential decisions
-// in registers, then one merge per array); the visited set is an open-addressing
-// hash in a per-wave global scratch slot (32K entries, CAS-claimed by all
-// lanes at once); neighbour distances are computed one row per lane.
+// Per query: the result set R as an ascending sorted array (farthest last) in
+// LDS, each id's bit 31 marking an expanded entry; there is no candidate
+// array — the nearest candidate is the nearest unexpanded entry of R
+// (hnsw_dev.hpp merge_into_r). One expansion's fresh neighbours are admitted
+// by exact sequential decisions in registers (decide_batch) and ONE merge
+// into R whose cost grows with the entries behind the first insertion only.
+// The visited set is an open-addressing hash in a per-wave global scratch slot
+// (CAS-claimed by all lanes at once); neighbour distances are one row per lane.
 #include <cstring>
 
 #include "common.hpp"
@@ -42,7 +45,7 @@ struct SearchArgs {
     int nslots;
     unsigned vcap;
     float* out_d; int64_t* out_i; int32_t* out_n;  // [nq][k]
-    int* status;       // set to 1 on candidate overflow
+    int* status;       // unused (the R-only search cannot overflow)
     unsigned long long* stats;  // [2]: distance evaluations, layer-0 expansions (per launch)
     float curv;        // Poincaré curvature
     int hyper;         // HyperbolicHnsw::search semantics (see below)
@@ -57,17 +60,14 @@ __global__ __launch_bounds__(64) RVX_HNSW_WPE void k_hnsw_search(SearchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int lane = threadIdx.x;
     const int ef = a.ef;
-    const int ccap = ef + C_EXTRA;
     constexpr bool COOP_OK = METRIC != RVX_METRIC_POINCARE && METRIC != RVX_METRIC_HYP_L2;
     const bool coop = COOP_OK && a.coop;
     unsigned char* wst = lds_raw;                                // [WD_LDS] distance stages (coop)
     float* qs = reinterpret_cast<float*>(lds_raw + (coop ? WD_LDS : 0));  // [d rounded to 4]
     const int dq = (a.d + 3) & ~3;
     float* rd = qs + dq;                                        // R dist [ef+1]
-    int* ri = reinterpret_cast<int*>(rd + ef + 1);              // R id
-    float* cd = reinterpret_cast<float*>(ri + ef + 1);          // C dist [ccap]
-    int* ci = reinterpret_cast<int*>(cd + ccap);                // C id
-    float* sdb = reinterpret_cast<float*>(ci + ccap);           // admitted batch [64]
+    int* ri = reinterpret_cast<int*>(rd + ef + 1);              // R id | expanded flag (bit 31)
+    float* sdb = reinterpret_cast<float*>(ri + ef + 1);         // admitted batch [64]
     int* sib = reinterpret_cast<int*>(sdb + 64);
 
     unsigned long long* vis = a.visited + (int64_t)blockIdx.x * a.vcap;
@@ -142,25 +142,31 @@ __global__ __launch_bounds__(64) RVX_HNSW_WPE void k_hnsw_search(SearchArgs a) {
             } while (moved && a.hyper);
         }
 
-        // ---- layer 0: search_layer (:913-1055)
-        int rs = 0, cs = 0;
-        bool overflow = false;
+        // ---- layer 0: search_layer (:913-1055) over R alone (hnsw_dev.hpp
+        // merge_into_r): expand the nearest unexpanded entry of R until none is left
+        int rs = 1;
         {
             const float d0 = dist_of(pivot);
             if (lane == 0) {
-                rd[0] = d0; ri[0] = pivot; cd[0] = d0; ci[0] = pivot;
+                rd[0] = d0; ri[0] = pivot;
                 visit_claim(vis, vmask, qtag, pivot);
             }
-            rs = 1; cs = 1;
             __threadfence_block();
             __builtin_amdgcn_wave_barrier();
         }
-        while (cs > 0 && !overflow) {
-            const float c_d = cd[cs - 1];
-            const int c_id = ci[cs - 1];
-            cs -= 1;
-            // -(c.dist) > f.dist -> return; HyperbolicHnsw also needs |R| >= ef (hnsw.rs:357-361)
-            if (c_d > rd[rs - 1] && (!a.hyper || rs >= ef)) break;
+        int scan = 0;  // every entry of R before `scan` is expanded
+        for (;;) {
+            int at = -1;
+            for (int b0 = scan; b0 < rs; b0 += 64) {
+                const unsigned long long m = __ballot(b0 + lane < rs && ri[b0 + lane] >= 0);
+                if (m) { at = b0 + __ffsll((long long)m) - 1; break; }
+            }
+            if (at < 0) break;
+            const int c_id = ri[at];
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) ri[at] = c_id | INT_MIN;
+            __builtin_amdgcn_wave_barrier();
+            scan = at + 1;
             const int64_t b = a.g.rp0[c_id], e = a.g.rp0[c_id + 1];
             n_expand += 1;
             for (int64_t c0 = b; c0 < e; c0 += 64) {
@@ -171,21 +177,25 @@ __global__ __launch_bounds__(64) RVX_HNSW_WPE void k_hnsw_search(SearchArgs a) {
                     nid = a.g.col0[p];
                     fresh = visit_claim(vis, vmask, qtag, nid);
                 }
-                float dd = INFINITY;
-                if (__ballot(fresh)) dd = dist_lane(fresh ? nid : -1);
+                const unsigned long long fmask = __ballot(fresh);
+                if (!fmask) continue;
+                const float dd = dist_lane(fresh ? nid : -1);
+                n_dist += (unsigned long long)__popcll(fmask);
                 // admission in neighbour order (hnsw.rs:1004-1046), batched exactly
-                n_dist += (unsigned long long)__popcll(__ballot(fresh));
-                if (!admit_batch(fresh, dd, nid, ef, ccap, rd, ri, rs, cd, ci, cs, sdb, sib, lane)) overflow = true;
-                if (overflow) break;
+                int r = rs;
+                const unsigned long long adm = decide_batch(fmask, dd, nid, ef, rd, ri, rs, r, lane);
+                const int na = sort_batch(adm, dd, nid, sdb, sib, lane);
+                if (na == 0) continue;
+                scan = min(scan, merge_into_r(rd, ri, rs, sdb, sib, na, r, lane));
+                rs = r;
             }
         }
-        if (overflow && lane == 0) atomicExch(a.status, 1);
 
         // ---- output: ascending, first min(k, ef, |R|)
         const int take = min(a.k, rs);
         for (int s = lane; s < a.k; s += 64) {
             a.out_d[qi * a.k + s] = s < take ? rd[s] : INFINITY;
-            a.out_i[qi * a.k + s] = s < take ? (int64_t)ri[s] : (int64_t)-1;
+            a.out_i[qi * a.k + s] = s < take ? (int64_t)(ri[s] & ID_MASK) : (int64_t)-1;
         }
         if (lane == 0) a.out_n[qi] = take;
         __builtin_amdgcn_wave_barrier();
@@ -210,7 +220,7 @@ bool hnsw_coop(int metric, int d, int64_t rows) {
 
 size_t hnsw_search_lds(int d, int ef, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)WD_LDS : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)(ef + C_EXTRA) * 8 + 64 * 8;
+    return (coop ? (size_t)WD_LDS : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 8;
 }
 
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
@@ -260,7 +270,6 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     g_search_stats.n_dist = (int64_t)tally[0];
     g_search_stats.n_expand = (int64_t)tally[1];
     g_search_stats.nq = nq;
-    RVX_REQUIRE(st[0] == 0, RVX_ERR_INDEX, "HNSW candidate list overflow (pathological distance ties)");
 }
 
 }  // namespace rvx

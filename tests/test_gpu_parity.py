@@ -175,6 +175,39 @@ def test_hnsw_search_bit_exact_on_same_graph(metric):
         assert np.array_equal(dist, rd)
 
 
+def test_hnsw_search_large_ef_bit_exact():
+    # ef far above the graph degree (R-only search: long merges, many expansions)
+    x, h, g, idx = _hnsw_pair(6000, 32, "l2", 8, 60, 11)
+    q = O.fill_uniform(64 * 32, 12).reshape(64, 32)
+    for k, ef in ((10, 1500), (100, 3000)):
+        ids, dist, cnt = idx.search_array(q, k, ef)
+        rids, rd, rc = h.search(q, k, ef)
+        assert np.array_equal(cnt, rc)
+        assert np.array_equal(ids.astype(np.int64)[:, :k], rids)
+        assert np.array_equal(dist, rd)
+
+
+def test_hnsw_search_tie_heavy_bit_exact():
+    # 3000 points on 12 distinct vectors: hundreds of exact distance ties at R's
+    # farthest (the round-1 candidate list overflowed here and raised RVX_ERR_INDEX);
+    # ids and distances equal the oracle's (d, id)-ordered search on the same graph
+    n, d = 3000, 16
+    base = O.fill_uniform(12 * d, 21).reshape(12, d)
+    x = np.ascontiguousarray(base[np.arange(n) % 12])
+    h = O.Hnsw(d, "l2", m=8, ef_construction=40, seed=3)
+    h.insert(x, threads=1)
+    idx = rv.HnswIndex(d, rv.DistanceMetric.Euclidean, rv.HnswConfig(m=8, ef_construction=40, ef_search=100))
+    idx.add_array(x, np.arange(n, dtype=np.uint64))
+    idx.load_graph(h.export())
+    q = np.ascontiguousarray(np.concatenate([base[:4], O.fill_uniform(4 * d, 22).reshape(4, d)]))
+    for k, ef in ((10, 50), (40, 400)):
+        ids, dist, cnt = idx.search_array(q, k, ef)
+        rids, rd, rc = h.search(q, k, ef)
+        assert np.array_equal(cnt, rc)
+        assert np.array_equal(ids.astype(np.int64)[:, :k], rids)
+        assert np.array_equal(dist, rd)
+
+
 def test_hnsw_layer0_export_matches_graph():
     x, h, g, idx = _hnsw_pair(500, 16, "l2", 8, 40, 9)
     rp, col, dist = idx.layer0()
