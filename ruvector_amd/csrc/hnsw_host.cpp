@@ -155,8 +155,8 @@ void hnsw_install(rvx_index* ix, HostGraph&& hg) {
 void hnsw_insert_range(rvx_index* ix, int64_t first, int64_t count) {
     RVX_REQUIRE(ix->build_valid, RVX_ERR_UNSUPPORTED,
                 "adding vectors to an HNSW index whose graph was loaded with rvx_index_load_graph is not supported");
-    RVX_REQUIRE(ix->hyper ? (ix->cfg.m <= 64 && ix->m0 <= 64) : ix->cfg.m <= 32, RVX_ERR_UNSUPPORTED,
-                "GPU HNSW construction supports lists of <= 64 neighbours");
+    RVX_REQUIRE(ix->hyper ? (ix->cfg.m <= 64 && ix->m0 <= 128) : ix->cfg.m <= 64, RVX_ERR_UNSUPPORTED,
+                "GPU HNSW construction supports layer-0 lists of <= 128 and upper lists of <= 64 neighbours");
     RVX_REQUIRE(ix->cfg.metric != RVX_METRIC_DOT, RVX_ERR_INVALID_PARAMETER, "DotProduct cannot be used with HNSW");
     if (count <= 0) return;
     const int M = ix->cfg.m, C0 = ix->hyper ? ix->m0 : 2 * M, max_layer = std::min(16, ix->cfg.dim);

@@ -34,6 +34,8 @@ namespace rvx {
 namespace {
 using namespace hnswdev;
 
+constexpr int MAX_C0 = 128;  // layer-0 list capacity (2M for hnsw_rs: M <= 64)
+
 struct BuildArgs {
     BuildGraph G;
     const float* x; const float* xnorm; int d;
@@ -44,7 +46,6 @@ struct BuildArgs {
     unsigned long long* visited; int nslots; unsigned vcap;
     int* rev_head; int* rev_next; int* rev_key; float* rev_d; int* rev_src;  // reverse-edge chains
     int rev_cap;  // records per batch point
-    int* status;
     float curv;  // Poincaré curvature
     int hyper;   // HyperbolicHnsw::insert rules
     int coop;    // wave-cooperative LDS-staged distances in the layer searches
@@ -69,23 +70,34 @@ __device__ __forceinline__ int list_key(const BuildGraph& G, int p, int l) {  //
 }
 
 // search_layer (hnsw.rs:913-1055) at layer l from ep; R left ascending in (rd, ri), returns |R|.
+// R-only form (hnsw_dev.hpp merge_into_r, as the query kernel k_hnsw.hip): the
+// nearest candidate is the nearest unexpanded entry of R (id bit 31 = expanded);
+// the flags are cleared before returning.
 template <int METRIC>
 __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn, int ep, float d_ep, int ef, int l,
-                                  unsigned long long* vis, unsigned vmask, unsigned long long tag, float* rd, int* ri, float* cd,
-                                  int* ci, int ccap, float* sdb, int* sib, unsigned char* wst, int lane, bool& overflow) {
+                                  unsigned long long* vis, unsigned vmask, unsigned long long tag, float* rd, int* ri,
+                                  float* sdb, int* sib, unsigned char* wst, int lane) {
     if (!((a.nonempty_mask >> l) & 1u)) return 0;  // points_by_layer[layer].is_empty()
-    int rs = 1, cs = 1;
+    int rs = 1;
     if (lane == 0) {
-        rd[0] = d_ep; ri[0] = ep; cd[0] = d_ep; ci[0] = ep;
+        rd[0] = d_ep; ri[0] = ep;
         visit_claim(vis, vmask, tag, ep);
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
-    while (cs > 0 && !overflow) {
-        const float c_d = cd[cs - 1];
-        const int c_id = ci[cs - 1];
-        cs -= 1;
-        if (c_d > rd[rs - 1]) break;
+    int scan = 0;
+    for (;;) {
+        int at = -1;
+        for (int b0 = scan; b0 < rs; b0 += 64) {
+            const unsigned long long m = __ballot(b0 + lane < rs && ri[b0 + lane] >= 0);
+            if (m) { at = b0 + __ffsll((long long)m) - 1; break; }
+        }
+        if (at < 0) break;
+        const int c_id = ri[at];
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) ri[at] = c_id | INT_MIN;
+        __builtin_amdgcn_wave_barrier();
+        scan = at + 1;
         const int* nbi;
         const float* nbd;
         const int cnt = list_get(a.G, c_id, l, &nbi, &nbd);
@@ -97,27 +109,33 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
                 nid = nbi[p];
                 fresh = visit_claim(vis, vmask, tag, nid);
             }
+            const unsigned long long fmask = __ballot(fresh);
+            if (!fmask) continue;
             float dd = INFINITY;
             bool coop = false;
             if constexpr (METRIC != RVX_METRIC_POINCARE && METRIC != RVX_METRIC_HYP_L2) coop = a.coop != 0;
             if (coop) {
                 if constexpr (METRIC != RVX_METRIC_POINCARE && METRIC != RVX_METRIC_HYP_L2) {
-                    if (__ballot(fresh)) {
-                        const int row = fresh ? nid : -1;
-                        const float dv = wave_dist<METRIC>(qs, a.x, a.d, row, qn,
-                                                           (METRIC == RVX_METRIC_COSINE && fresh) ? a.xnorm[nid] : 0.0f,
-                                                           wst, lane);
-                        if (fresh) dd = dv;
-                    }
+                    const int row = fresh ? nid : -1;
+                    const float dv = wave_dist<METRIC>(qs, a.x, a.d, row, qn,
+                                                       (METRIC == RVX_METRIC_COSINE && fresh) ? a.xnorm[nid] : 0.0f,
+                                                       wst, lane);
+                    if (fresh) dd = dv;
                 }
             } else if (fresh) {
                 dd = row_dist<METRIC>(qs, a.x + (int64_t)nid * a.d, a.d, qn,
                                       METRIC == RVX_METRIC_COSINE ? a.xnorm[nid] : 0.0f, a.curv);
             }
-            if (!admit_batch(fresh, dd, nid, ef, ccap, rd, ri, rs, cd, ci, cs, sdb, sib, lane)) overflow = true;
-            if (overflow) break;
+            int r = rs;
+            const unsigned long long adm = decide_batch(fmask, dd, nid, ef, rd, ri, rs, r, lane);
+            const int na = sort_batch(adm, dd, nid, sdb, sib, lane);
+            if (na == 0) continue;
+            scan = min(scan, merge_into_r(rd, ri, rs, sdb, sib, na, r, lane));
+            rs = r;
         }
     }
+    for (int i = lane; i < rs; i += 64) ri[i] &= ID_MASK;
+    __builtin_amdgcn_wave_barrier();
     return rs;
 }
 
@@ -126,20 +144,16 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int lane = threadIdx.x;
     const int ef = a.ef_c;
-    const int ccap = ef + C_EXTRA;
     const int dq = (a.d + 3) & ~3;
     unsigned char* wst = lds_raw;  // [WD_LDS] distance stages (coop)
     float* qs = reinterpret_cast<float*>(lds_raw + (a.coop ? WD_LDS : 0));
     float* rd = qs + dq;
     int* ri = reinterpret_cast<int*>(rd + ef + 1);
-    float* cd = reinterpret_cast<float*>(ri + ef + 1);
-    int* ci = reinterpret_cast<int*>(cd + ccap);
-    float* sd = reinterpret_cast<float*>(ci + ccap);  // selected [64]
-    int* si = reinterpret_cast<int*>(sd + 64);
+    float* sd = reinterpret_cast<float*>(ri + ef + 1);  // selected [MAX_C0] (search: admitted batch [64])
+    int* si = reinterpret_cast<int*>(sd + MAX_C0);
     unsigned long long* vis = a.visited + (int64_t)blockIdx.x * a.vcap;
     const unsigned vmask = a.vcap - 1;
     unsigned epoch = 0;
-    bool overflow = false;
 
     for (int b = blockIdx.x; b < a.batch_n; b += a.nslots) {
         const int p = (int)(a.batch_begin + b);
@@ -157,8 +171,8 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
         // 1. greedy descent, ef = 1 (hnsw.rs:1105-1146)
         for (int l = a.entry_level; l >= lev + 1; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
-            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, 1, l, vis, vmask, tag, rd, ri, cd, ci, ccap, sd,
-                                                      si, wst, lane, overflow);
+            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, 1, l, vis, vmask, tag, rd, ri, sd, si, wst,
+                                                      lane);
             if (rs > 0 && rd[0] < d_ep) { ep = ri[0]; d_ep = rd[0]; }
         }
         // 2. layers lev .. 0 (hnsw.rs:1149-1196); HyperbolicHnsw inserts at
@@ -166,8 +180,8 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
         const int ltop = a.hyper ? min(lev, a.entry_level) : lev;
         for (int l = ltop; l >= 0; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
-            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, ef, l, vis, vmask, tag, rd, ri, cd, ci, ccap, sd,
-                                                      si, wst, lane, overflow);
+            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, ef, l, vis, vmask, tag, rd, ri, sd, si, wst,
+                                                      lane);
             if (rs == 0) continue;
             const int nb_conn = l == 0 ? a.G.C0 : a.G.M;
             int ss = 0;
@@ -181,8 +195,8 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
                     const int e = ri[t];
                     const float de = rd[t];
                     bool bad = false;
-                    if (lane < ss) {
-                        const int s = si[lane];
+                    for (int j = lane; j < ss && !bad; j += 64) {
+                        const int s = si[j];
                         const float dse = row_dist<METRIC>(a.x + (int64_t)e * a.d, a.x + (int64_t)s * a.d, a.d,
                                                            METRIC == RVX_METRIC_COSINE ? a.xnorm[e] : 0.0f,
                                                            METRIC == RVX_METRIC_COSINE ? a.xnorm[s] : 0.0f, a.curv);
@@ -232,7 +246,6 @@ __global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
         }
         for (int i = rec + lane; i < a.rev_cap; i += 64) a.rev_key[rbase + i] = -1;
     }
-    if (overflow && lane == 0) atomicExch(a.status, 1);
 }
 
 // One wave per list that received reverse edges (the record that found the
@@ -268,28 +281,33 @@ __global__ __launch_bounds__(256) void k_build_merge(BuildArgs a, int nrec) {
             cap = a.G.M;
         }
         int cnt = *cntp;
-        // lane j holds element j of the sorted list (cap <= 64)
-        float md = lane < cnt ? ds[lane] : INFINITY;
-        int mi = lane < cnt ? ids[lane] : INT_MAX;
+        // lane j holds elements j and 64 + j of the sorted list (cap <= 128)
+        float md = lane < cnt ? ds[lane] : INFINITY, md1 = 64 + lane < cnt ? ds[64 + lane] : INFINITY;
+        int mi = lane < cnt ? ids[lane] : INT_MAX, mi1 = 64 + lane < cnt ? ids[64 + lane] : INT_MAX;
         int steps = 0;
         for (int h = a.rev_head[key]; h >= 0 && h < nrec && steps < nrec; h = a.rev_next[h], ++steps) {
             const float d = a.rev_d[h];
             const int id = a.rev_src[h];
-            if (__ballot(mi == id) != 0ull) continue;  // already present
+            if (__ballot(mi == id || mi1 == id) != 0ull) continue;  // already present
             if (cnt == cap) {
-                const float ld = __shfl(md, cap - 1);
-                const int li2 = __shfl(mi, cap - 1);
+                const float ld = cap <= 64 ? __shfl(md, cap - 1) : __shfl(md1, cap - 65);
+                const int li2 = cap <= 64 ? __shfl(mi, cap - 1) : __shfl(mi1, cap - 65);
                 if (!lt(d, id, ld, li2)) continue;
             }
-            const bool before = lane < cnt && lt(md, mi, d, id);
-            const int pos = __popcll(__ballot(before));
-            const float upd = __shfl_up(md, 1);
-            const int upi = __shfl_up(mi, 1);
+            const int pos = __popcll(__ballot(lane < cnt && lt(md, mi, d, id))) +
+                            __popcll(__ballot(64 + lane < cnt && lt(md1, mi1, d, id)));
+            const float cd = __shfl(md, 63);  // element 63 moves to 64
+            const int ci = __shfl(mi, 63);
+            const float upd = __shfl_up(md, 1), upd1 = __shfl_up(md1, 1);
+            const int upi = __shfl_up(mi, 1), upi1 = __shfl_up(mi1, 1);
             if (lane > pos) { md = upd; mi = upi; }
             if (lane == pos) { md = d; mi = id; }
+            if (64 + lane > pos) { md1 = lane == 0 ? cd : upd1; mi1 = lane == 0 ? ci : upi1; }
+            if (64 + lane == pos) { md1 = d; mi1 = id; }
             cnt = min(cnt + 1, cap);
         }
         if (lane < cnt) { ds[lane] = md; ids[lane] = mi; }
+        if (64 + lane < cnt) { ds[64 + lane] = md1; ids[64 + lane] = mi1; }
         if (lane == 0) { *cntp = cnt; a.rev_head[key] = -1; }
     }
 }
@@ -298,14 +316,15 @@ __global__ __launch_bounds__(256) void k_build_merge(BuildArgs a, int nrec) {
 
 size_t build_lds_bytes(int d, int ef, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)WD_LDS : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)(ef + C_EXTRA) * 8 + 64 * 8;
+    return (coop ? (size_t)WD_LDS : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)MAX_C0 * 8;
 }
 
 void build_insert_batch(const BuildGraph& G, int metric, const float* x, const float* xnorm, int d,
                         int64_t batch_begin, int batch_n, int entry, int entry_level, unsigned nonempty_mask, int ef_c,
                         BuildScratch& s, float curv, int hyper) {
     if (batch_n <= 0) return;
-    RVX_REQUIRE(G.C0 <= 64 && G.M <= 64, RVX_ERR_UNSUPPORTED, "GPU HNSW build supports lists of <= 64 neighbours");
+    RVX_REQUIRE(G.C0 <= MAX_C0 && G.M <= 64, RVX_ERR_UNSUPPORTED,
+                "GPU HNSW build supports layer-0 lists of <= 128 and upper lists of <= 64 neighbours");
     RVX_REQUIRE(ef_c >= 1 && ef_c <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER, "ef_construction out of range");
     const unsigned vcap = visited_capacity(ef_c);
     const int nslots = (int)std::min<int64_t>(std::min(batch_n, 8192),
@@ -327,9 +346,7 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     a.rev_head = s.rev_head;
     a.rev_cap = rev_cap;
     a.nslots = nslots;
-    a.status = (int*)scratch_bytes("build_status", 256);
     RVX_HIP(hipMemsetAsync(a.visited, 0, (size_t)nslots * vcap * 8, stream()));
-    RVX_HIP(hipMemsetAsync(a.status, 0, 4, stream()));
     const size_t lds = build_lds_bytes(d, ef_c, a.coop != 0);
     RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");
     static bool attr = false;
@@ -355,10 +372,7 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     }
     const int waves = (int)((nrec + 63) / 64);
     RVX_LAUNCH("hnsw_build_merge", k_build_merge, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, a, (int)nrec);
-    int st = 0;
-    RVX_HIP(hipMemcpyAsync(&st, a.status, 4, hipMemcpyDeviceToHost, stream()));
     sync();
-    RVX_REQUIRE(st == 0, RVX_ERR_INDEX, "HNSW build candidate list overflow (pathological distance ties)");
 }
 
 }  // namespace rvx

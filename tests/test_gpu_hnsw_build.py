@@ -75,6 +75,37 @@ def test_recall_matches_cpu_build():
         assert r_gpu >= r_cpu - 0.02, (ef, r_gpu, r_cpu)
 
 
+@pytest.mark.parametrize("m", [48, 64])
+def test_wide_lists_recall_and_invariants(m):
+    # M up to 64 (layer-0 lists of 2M = 128: two list elements per lane in the
+    # reverse-edge merge, selection over two chunks of selected points)
+    n, d, efc = 12000, 32, 120
+    x = O.fill_uniform(n * d, 17).reshape(n, d)
+    q = O.fill_uniform(200 * d, 18).reshape(200, d)
+    gt, _ = O.flat_search(x, q, 10, "l2")
+    idx = build_gpu(x, "l2", m, efc, seed=6, chunks=2)
+    g = idx.export_graph()
+    rp, col = g["row_ptr0"], g["col0"]
+    deg = np.diff(rp)
+    assert deg.max() <= 2 * m and deg.max() > 64  # lists past one wave's width exist
+    for i in range(0, n, 97):
+        nb = col[rp[i]:rp[i + 1]]
+        assert i not in nb.tolist() and len(set(nb.tolist())) == len(nb)
+        dd = np.sqrt(np.sum((x[nb] - x[i]) ** 2, 1))
+        assert np.all(np.diff(dd) >= -1e-5)  # sorted by distance to the owner
+    h = O.Hnsw(d, "l2", m=m, ef_construction=efc, seed=6)
+    h.insert(x, threads=16)
+    for ef in (20, 64):
+        r_gpu = recall(gt, idx.search_array(q, 10, ef)[0].astype(np.int64))
+        r_cpu = recall(gt, h.search(q, 10, ef)[0])
+        assert r_gpu >= r_cpu - 0.02, (ef, r_gpu, r_cpu)
+    # GPU search on the GPU-built graph = the oracle's search of the same graph
+    ref = O.Hnsw.from_graph(x, g, "l2")
+    ids, dist, _ = idx.search_array(q, 10, 64)
+    rids, rd, _ = ref.search(q, 10, 64)
+    assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd)
+
+
 def test_reference_recall_thresholds():
     # hnsw_integration_test.rs:57-118 (100 vectors, m16 ef_c100 ef_s200, >= 0.90) and :122-185 (1k, >= 0.95)
     for n, m, efc, thr in ((100, 16, 100, 0.90), (1000, 32, 200, 0.95)):
