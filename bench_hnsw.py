@@ -16,6 +16,8 @@ import time
 
 import numpy as np
 
+import benchutil
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -40,8 +42,9 @@ def run(n, d, nq, m, efc, efs, k, metric_name, seed_base=1, cpu=False, cpu_secon
     idx = rv.HnswIndex(d, metric, rv.HnswConfig(m=m, ef_construction=efc, ef_search=100), seed=seed_base)
     rv.synchronize()
     t0 = time.perf_counter()
-    rv._lib.call("rvx_index_add_batch_device", idx.handle, xb.handle, n, 0)
-    rv.synchronize()
+    with benchutil.heartbeat(f"building {n}x{d}", log=log):
+        rv._lib.call("rvx_index_add_batch_device", idx.handle, xb.handle, n, 0)
+        rv.synchronize()
     build_s = time.perf_counter() - t0
     log(f"build {n}x{d} M={m} ef_c={efc}: {build_s:.2f} s")
 

@@ -26,3 +26,30 @@ def host_threads():
     n = min(x for x in (aff, quota, share) if x)
     return n, {"threads": n, "nproc": os.cpu_count(), "affinity": aff, "cgroup_quota": quota,
                "omp_num_threads": share}
+
+
+class heartbeat:
+    """Print a progress line every `every` seconds while a long native call runs
+    (ctypes releases the GIL), so a supervisor that watches output sees life."""
+
+    def __init__(self, label, every=30.0, log=None):
+        import sys
+        import threading
+        self.label, self.every = label, every
+        self.log = log or (lambda s: print(s, file=sys.stderr, flush=True))
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        import time
+        t0 = time.perf_counter()
+        while not self._stop.wait(self.every):
+            self.log(f"... {self.label}: {time.perf_counter() - t0:.0f} s")
+
+    def __enter__(self):
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._t.join()
