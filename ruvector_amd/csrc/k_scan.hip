@@ -364,7 +364,7 @@ struct FCfg {
     static constexpr int BLOCKS = WIDE ? 1 : 2;
     static_assert(FQ == FR && FR == 32 * THREADS / 64, "DMA pieces assume FR = FQ = 32 x waves");
 };
-constexpr int F_MAXE = 16;                  // rerank: list entries per lane (nsplit_total * FKP <= 64 * F_MAXE)
+constexpr int F_MAXE = 32;                  // rerank: list entries per lane (nsplit_total * FKP <= 64 * F_MAXE)
 
 struct FilterArgs {
     // per-row constants {1/scale (NaN for a deleted row), |x|^2 (L2, dot) or the
@@ -381,7 +381,8 @@ __device__ __forceinline__ float approx_value(float acc, float xi, float qi, flo
     const float dot = (acc * xi) * qi;  // undo the power-of-two scales (exact)
     if (METRIC == RVX_METRIC_L2) return (xs + qs) - 2.0f * dot;
     if (METRIC == RVX_METRIC_DOT) return -dot;
-    return (qn > 1e-8f && xn > 1e-8f) ? 1.0f - dot / (qn * xn) : 1.0f;
+    // a degenerate norm gives 1; the 0 * dot keeps an invalid row's / padding query's NaN
+    return (qn > 1e-8f && xn > 1e-8f) ? 1.0f - dot / (qn * xn) : 1.0f + 0.0f * dot;
 }
 
 __device__ __forceinline__ bool lt_vr(float v, int r, float bv, int br) { return v < bv || (v == bv && r < br); }
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
         qv_[fn] = qg < a.nq;
         const int64_t qc = min(qg, a.nq - 1);
         const float2 c = a.qc[qc];
-        qi_[fn] = c.x;
+        qi_[fn] = qv_[fn] ? c.x : __builtin_nanf("");  // padding query: every v is NaN
         qs_[fn] = (METRIC == RVX_METRIC_L2) ? c.y : 0.0f;
         qn_[fn] = (METRIC == RVX_METRIC_COSINE) ? c.y : 0.0f;
     }
@@ -499,6 +500,13 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     // offered or rejected value becomes INF. Slots per query per round are
     // bounded (FCB), so rounds repeat with the tightened thresholds until no
     // offer overflowed (thresholds only fall, so a rejection is final).
+    // Invalid rows (past the split, deleted: 1/scale = NaN) and padding queries
+    // (qi_ = NaN) give v = NaN, which no threshold test admits. A value is
+    // tested with one compare whose lane mask is the uniform branch condition,
+    // so the common case (no lane below its threshold) costs the compare and a
+    // scalar branch; offered values are marked in a per-lane bit mask (rounds
+    // repeat while some query's candidate slots overflowed), rejected ones need
+    // no mark (thresholds only fall, so a rejection is final).
     auto epilogue = [&](int64_t rt, float2 pre) {
         if (tid < FR) rowc[tid] = pre;
         __syncthreads();
@@ -507,15 +515,14 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const float2 c = rowc[wm * WROWS + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh];
-                const bool rv = !__builtin_isnan(c.x);  // past the split, or deleted
                 const float xs = (METRIC == RVX_METRIC_L2) ? c.y : 0.0f;
                 const float xn = (METRIC == RVX_METRIC_COSINE) ? c.y : 0.0f;
 #pragma unroll
                 for (int fn = 0; fn < 2; ++fn)
-                    acc[fm][fn][e] = (rv && qv_[fn])
-                                         ? approx_value<METRIC>(acc[fm][fn][e], c.x, qi_[fn], xs, qs_[fn], xn, qn_[fn])
-                                         : INFINITY;
+                    acc[fm][fn][e] = approx_value<METRIC>(acc[fm][fn][e], c.x, qi_[fn], xs, qs_[fn], xn, qn_[fn]);
             }
+        static_assert(F_FM * 16 <= 64, "offered-value mask holds one bit per (fm, e)");
+        uint64_t offered[2] = {0ull, 0ull};  // per fn: values already handed to the list
         for (int round = 0;; ++round) {
 #pragma unroll
             for (int fn = 0; fn < 2; ++fn) {
@@ -526,13 +533,16 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
 #pragma unroll
                     for (int e = 0; e < 16; ++e) {
                         const float v = acc[fm][fn][e];
-                        if (!(v < t)) { acc[fm][fn][e] = INFINITY; continue; }
+                        const uint64_t bit = 1ull << (fm * 16 + e);
+                        const bool pass = v < t && !(offered[fn] & bit);
+                        if (!__ballot(pass)) continue;
+                        if (!pass) continue;
                         const int slot = atomicAdd(&cand_n[ql], 1);
                         if (slot < FCB) {
                             cand_v[ql * FCB + slot] = v;
                             cand_r[ql * FCB + slot] =
                                 (int32_t)(rt + wm * WROWS + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh);
-                            acc[fm][fn][e] = INFINITY;
+                            offered[fn] |= bit;
                         } else {
                             ovf[round & 1] = 1;
                         }
@@ -867,8 +877,22 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     const int64_t qtiles = (nq + FQ - 1) / FQ;
     const int64_t max_splits = 64 * F_MAXE / FKP;  // rerank capacity
     if (nchunks > max_splits || qtiles > 65535) return false;
-    int64_t s_c = std::max<int64_t>(1, std::min<int64_t>((2048 + qtiles - 1) / qtiles, max_splits / nchunks));
-    s_c = std::min<int64_t>(s_c, std::max<int64_t>(1, chunk_rows / (8 * FR)));  // >= 8 tiles per split
+    // splits per chunk: a block streams one split's tiles for one query tile, and
+    // resident blocks run in waves (one per CU for the 256^2 tile, two for 128^2).
+    // Time ~ waves(s) x (tiles per split + warm-up), the warm-up being the early
+    // tiles of a split whose still-empty lists admit most values (~8 tiles'
+    // worth): 10M x 768 / 10k queries takes 32 splits per chunk (1280 blocks =
+    // 5 full waves, not 640 = 2.5), 100k x 128 takes 6 (one wave).
+    const int64_t slots = (int64_t)device().num_cus * (wide ? 1 : 2);
+    const int64_t tiles = (chunk_rows + FR - 1) / FR;
+    const int64_t s_max = std::max<int64_t>(1, std::min<int64_t>(max_splits / nchunks, tiles / 8));
+    int64_t s_c = 1;
+    double best_t = 1e300;
+    for (int64_t s = 1; s <= s_max; ++s) {
+        const int64_t waves = (qtiles * s + slots - 1) / slots;
+        const double t = (double)waves * ((double)tiles / (double)s + 8.0);
+        if (t < best_t * (1.0 - 1e-9)) { best_t = t; s_c = s; }
+    }
     int64_t rows_per_split = ((chunk_rows + s_c - 1) / s_c + FR - 1) / FR * FR;
     s_c = (chunk_rows + rows_per_split - 1) / rows_per_split;
     const int nsplit_total = (int)(nchunks * s_c);
