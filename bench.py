@@ -8,7 +8,9 @@ out-degree-32 CSR, 2-layer ruvector-gnn GraphSAGE-mean forward
 (crates/ruvector-postgres/src/gnn/graphsage.rs:118-187) with the reference's
 deterministic weights. A step = one full 2-layer forward over every node.
 
-Multi-GPU (one process per GPU, torch.distributed.run): the 10M nodes are
+Multi-GPU (one process per GPU, launched by torch.distributed.run; the
+processes themselves use no torch: RCCL id over a TCP rendezvous, barriers and
+the max-over-ranks clock as RCCL all-reduces): the 10M nodes are
 split into contiguous node-id ranges (strong scaling). The input node table is
 resident on every GPU; each layer writes its owned rows of the next table and
 ships them to every peer over RCCL p2p (xGMI) chunk by chunk while the
@@ -77,13 +79,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # host-side only: barrier, id broadcast, max
-        dist.init_process_group("gloo")
-
     import ruvector_amd as rv
-    from ruvector_amd.shard import RcclComm, ShardPlan
+    from ruvector_amd.shard import REDUCE_MAX, RcclComm, ShardPlan
 
     rv.set_device(local)
     n_tot, d, deg, layers = a.nodes, a.dim, a.degree, a.layers
@@ -93,11 +90,9 @@ def main():
     offsets = np.array([plan.rows(p)[0] for p in range(world)] + [n_tot], dtype=np.int64)
     off_ptr = offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
 
-    comm = None
-    if world > 1:
-        uid = [RcclComm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = RcclComm(world, rank, uid[0])
+    # RCCL communicator: id over a stdlib TCP rendezvous, barriers and the
+    # max-over-ranks clock as RCCL all-reduces (no other collective library)
+    comm = RcclComm.from_env() if world > 1 else None
 
     # ---- inputs resident in HBM: the node table (same on every GPU), this
     # rank's CSR rows (global column ids), two full tables for layer outputs
@@ -118,8 +113,8 @@ def main():
 
     def barrier():
         rv.synchronize()
-        if dist is not None:
-            dist.barrier()
+        if comm is not None:
+            comm.barrier()
 
     for _ in range(a.warmup):
         step()
@@ -135,11 +130,8 @@ def main():
         barrier()
     elapsed = t1 - t0
     kern = prof.summary()
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if comm is not None:
+        elapsed = comm.allreduce([elapsed], REDUCE_MAX)[0]
 
     edges_per_step = n_tot * deg * layers
     value = edges_per_step * a.steps / elapsed
@@ -203,17 +195,17 @@ def main():
         line["gemm_paths"] = gemm_alternatives(g, x, tables[0], off_ptr, d, deg)
     if not a.no_scan:
         del tables, g
-        line["exact_scan"] = scan_leg(a, x, n_tot, d, rank, world, dist)
+        line["exact_scan"] = scan_leg(a, x, n_tot, d, rank, world, comm)
     if not a.no_hnsw:
         del x
-        line["hnsw"] = hnsw_leg(a, rank, world, dist)
+        line["hnsw"] = hnsw_leg(a, rank, world, comm)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.barrier()
 
 
-def hnsw_leg(a, rank, world, dist):
+def hnsw_leg(a, rank, world, comm):
     """Second half of the metric: HNSW queries/s at recall@10 >= 0.95 on
     BASELINE configs[0] (C1: 100k x 128, M=32, ef_c=200, 10k queries). The index
     is a replica per GPU (search does not shard), built on the GPU; each rank
@@ -222,20 +214,16 @@ def hnsw_leg(a, rank, world, dist):
     res = bench_hnsw.run(100_000, 128, 10_000, 32, 200, [300, 400, 600, 800], 10, "l2",
                          cpu=(rank == 0 and world == 1 and not a.no_cpu), log=lambda s: None)
     qps = res["qps_at_recall95"] or 0.0
-    if dist is not None:
-        import torch
-        t = torch.tensor([qps, res["build_s"]], dtype=torch.float64)
-        lo = t.clone()
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-        res["per_gpu_min_qps"] = float(lo[0])
-        qps = float(t[0])
+    if comm is not None:
+        from ruvector_amd.shard import REDUCE_MIN
+        res["per_gpu_min_qps"] = comm.allreduce([qps], REDUCE_MIN)[0]
+        qps = comm.allreduce([qps])[0]
     res["value"] = round(qps, 1)
     res["unit"] = "queries/s (recall@10 >= 0.95, replicas summed over GPUs)"
     return res
 
 
-def scan_leg(a, x, n, d, rank, world, dist):
+def scan_leg(a, x, n, d, rank, world, comm):
     """Queries/s at recall@10 >= 0.95 on the metric's 10M x 768 table itself: on N(0,1)
     768-d rows the reference's HNSW parameters (M=32, ef_c=200) do not reach recall 0.95
     at 10M (profiles/r01_c3_10m.json; the GPU-built graph's recall equals the oracle
@@ -248,11 +236,8 @@ def scan_leg(a, x, n, d, rank, world, dist):
     res = bench_scan.run(n, d, 10_000, 10, "l2", cpu_queries=(16 if rank == 0 and world == 1 and not a.no_cpu else 0),
                          valu=False, log=lambda s: None, xb=x, x_seed=3)
     qps = res["mfma"]["qps"]
-    if dist is not None:
-        import torch
-        t = torch.tensor([qps], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        qps = float(t[0])
+    if comm is not None:
+        qps = comm.allreduce([qps])[0]
     res["value"] = round(qps, 1)
     res["unit"] = "queries/s (recall@10 = 1.0, exact; replicas summed over GPUs)"
     return res

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """C4 benchmark: multi-layer ruvector-gnn RuvectorLayer stack +
 EdgeFeaturedAttention head over a graph, one process per GPU (node-range shards,
-launched with torch.distributed.run for N>1; rows exchanged over RCCL p2p).
+launched with torch.distributed.run for N>1 — the processes use no torch; rows exchanged over RCCL p2p).
 
 Workload: N x 768 node table (N(0,1), seed 5), uniform random out-degree-32
 CSR (seed 6) with edge weights uniform [0,1) (seed 7) standing in for the HNSW
@@ -46,14 +46,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # host-side only: barrier, id broadcast, max
-        dist.init_process_group("gloo")
-
     import ruvector_amd as rv
     from ruvector_amd.attention import EdgeFeaturedAttention, EdgeFeaturedConfig
-    from ruvector_amd.shard import RcclComm, ShardPlan
+    from ruvector_amd.shard import REDUCE_MAX, RcclComm, ShardPlan
 
     rv.set_device(local)
     n, d, deg, H = a.nodes, a.dim, a.degree, a.dim
@@ -61,11 +56,7 @@ def main():
     r0, r1 = plan.rows(rank)
     n_loc = r1 - r0
     offsets = np.array([plan.rows(p)[0] for p in range(world)] + [n], dtype=np.int64)
-    comm = None
-    if world > 1:
-        uid = [RcclComm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = RcclComm(world, rank, uid[0])
+    comm = RcclComm.from_env() if world > 1 else None  # TCP rendezvous for the RCCL id
 
     # node-range shards: every rank holds the whole-table buffers but reads and
     # writes only its own rows; its CSR rows (global column ids) and their slice
@@ -91,8 +82,8 @@ def main():
 
     def barrier():
         rv.synchronize()
-        if dist is not None:
-            dist.barrier()
+        if comm is not None:
+            comm.barrier()
 
     for _ in range(a.warmup):
         step()
@@ -108,11 +99,8 @@ def main():
         barrier()
     dt = (t1 - t0) / a.steps
     kern = prof.summary()
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    if comm is not None:
+        dt = comm.allreduce([dt], REDUCE_MAX)[0]
     n_own = n_loc  # per-launch work below is this rank's rows
 
     # algorithmic work per layer
@@ -147,9 +135,8 @@ def main():
         line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, ew, layers[0], n, d, deg, offsets)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.barrier()
 
 
 def cpu_baseline(a, x_buf, g, ew_buf, layer, n, d, deg, offsets):

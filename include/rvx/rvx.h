@@ -527,6 +527,14 @@ rvx_status rvx_comm_destroy(rvx_comm* c);
  * recv [nranks*rows][cols] (rank-major), on the library stream. */
 rvx_status rvx_comm_allgather_f32(rvx_comm* c, const rvx_buffer* send, int64_t count, rvx_buffer* recv);
 rvx_status rvx_comm_allreduce_max_f64(rvx_comm* c, double* value);
+/* Host scalars reduced over every rank (sum / max / min), in place; also the
+ * bench's barrier and its max-over-ranks clock, so no launcher-side collective
+ * library is needed (the unique id travels over a TCP rendezvous,
+ * ruvector_amd.shard.rendezvous_unique_id). */
+#define RVX_REDUCE_SUM 0
+#define RVX_REDUCE_MAX 1
+#define RVX_REDUCE_MIN 2
+rvx_status rvx_comm_allreduce_f64(rvx_comm* c, double* values, int32_t count, int32_t op);
 
 /* Host-staged transport (tests and hosts without RCCL peers, e.g. several ranks
  * sharing one GPU): behind the same row exchange the *_forward_exchange entry

@@ -149,4 +149,19 @@ rvx_status rvx_comm_allreduce_max_f64(rvx_comm* c, double* value) {
     });
 }
 
+rvx_status rvx_comm_allreduce_f64(rvx_comm* c, double* values, int32_t count, int32_t op) {
+    return guard([&] {
+        RVX_REQUIRE(c && values && count >= 0, RVX_ERR_INVALID_PARAMETER, "bad all-reduce args");
+        RVX_REQUIRE(op >= RVX_REDUCE_SUM && op <= RVX_REDUCE_MIN, RVX_ERR_INVALID_PARAMETER, "unknown reduce op");
+        RVX_REQUIRE(c->comm, RVX_ERR_UNSUPPORTED, "all-reduce needs the RCCL transport");
+        if (count == 0) return;
+        const ncclRedOp_t rop = op == RVX_REDUCE_SUM ? ncclSum : op == RVX_REDUCE_MAX ? ncclMax : ncclMin;
+        double* d = (double*)scratch_bytes("comm_scalars", (int64_t)count * 8);
+        RVX_HIP(hipMemcpyAsync(d, values, (size_t)count * 8, hipMemcpyHostToDevice, stream()));
+        RVX_NCCL(ncclAllReduce(d, d, (size_t)count, ncclFloat64, rop, c->comm, stream()));
+        RVX_HIP(hipMemcpyAsync(values, d, (size_t)count * 8, hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
 }  // extern "C"

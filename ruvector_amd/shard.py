@@ -7,7 +7,9 @@ whole graph for HNSW-like topologies); HNSW shards merge per-shard top-k.
 
 The exchange is pluggable so the same driver runs over RCCL on MI355X
 (RcclComm, device buffers, librvx) and over torch.distributed gloo in the
-CPU tests (tests/test_shard_gloo.py).
+CPU tests (tests/test_shard_gloo.py). The product side needs no collective
+library of its own: the RCCL id travels over a stdlib TCP rendezvous
+(rendezvous_unique_id) and barriers / clock maxima are RCCL all-reduces.
 """
 from __future__ import annotations
 
@@ -108,8 +110,57 @@ def exchange_plan(kind: int, offsets: Sequence[int]) -> List[List[Tuple[int, int
     return [[(int(r0[c, p]), int(rows[c, p])) for p in range(world)] for c in range(n.value)]
 
 
+def rendezvous_unique_id(rank: int, world: int, make_id: Callable[[], bytes], addr: str = None, port: int = None,
+                         timeout: float = 300.0) -> bytes:
+    """Hand rank 0's communicator id to every rank over plain TCP (no launcher
+    collective library): rank 0 serves `make_id()` on (MASTER_ADDR,
+    MASTER_PORT + 17) to each of the world-1 peers, which connect with retry.
+    The offset keeps clear of the launcher's own store on MASTER_PORT."""
+    import os
+    import socket
+    import time
+    if world <= 1:
+        return make_id()
+    addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = (port if port is not None else int(os.environ.get("MASTER_PORT", "29500"))) + 17
+    if rank == 0:
+        uid = make_id()
+        with socket.create_server((addr, port), reuse_port=False) as srv:
+            srv.settimeout(timeout)
+            for _ in range(world - 1):
+                conn, _a = srv.accept()
+                with conn:
+                    conn.sendall(len(uid).to_bytes(4, "little") + uid)
+        return uid
+    deadline = time.monotonic() + timeout
+    while True:
+        try:
+            with socket.create_connection((addr, port), timeout=10.0) as conn:
+                buf = b""
+                while len(buf) < 4 or len(buf) < 4 + int.from_bytes(buf[:4], "little"):
+                    chunk = conn.recv(4096)
+                    if not chunk:
+                        raise ConnectionError("rendezvous closed early")
+                    buf += chunk
+                return buf[4:4 + int.from_bytes(buf[:4], "little")]
+        except (ConnectionRefusedError, ConnectionError, socket.timeout, OSError):
+            if time.monotonic() > deadline:
+                raise
+            time.sleep(0.2)
+
+
+REDUCE_SUM, REDUCE_MAX, REDUCE_MIN = 0, 1, 2
+
+
 class RcclComm:
     """RCCL communicator of librvx (one per process/GPU)."""
+
+    @classmethod
+    def from_env(cls) -> "RcclComm":
+        """One communicator over the launcher's RANK / WORLD_SIZE, id by rendezvous_unique_id."""
+        import os
+        world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+        return cls(world, rank, rendezvous_unique_id(rank, world, cls.unique_id))
 
     def __init__(self, world: int, rank: int, unique_id: bytes):
         arr = (C.c_uint8 * L.COMM_ID_BYTES).from_buffer_copy(unique_id)
@@ -130,6 +181,15 @@ class RcclComm:
         v = C.c_double(value)
         L.call("rvx_comm_allreduce_max_f64", self._h, C.byref(v))
         return v.value
+
+    def allreduce(self, values: Sequence[float], op: int = REDUCE_SUM) -> List[float]:
+        arr = (C.c_double * len(values))(*[float(v) for v in values])
+        L.call("rvx_comm_allreduce_f64", self._h, arr, len(values), int(op))
+        return list(arr)
+
+    def barrier(self) -> None:
+        """Every rank's library stream drained and every rank arrived."""
+        self.allreduce([0.0])
 
     def __del__(self):
         try:

@@ -228,3 +228,36 @@ def test_host_transport_moves_every_block(world):
     for p in ps:
         p.join(timeout=60)
     assert all(res[r] for r in range(world)), res
+
+
+def _rdv_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    from ruvector_amd.shard import rendezvous_unique_id
+    made = []
+
+    def make():
+        made.append(1)
+        return bytes(range(128))[::-1] + b"rank0"
+
+    uid = rendezvous_unique_id(rank, world, make, addr="127.0.0.1", port=port, timeout=60.0)
+    q.put((rank, uid, len(made)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tcp_rendezvous_hands_rank0_id_to_every_rank(world):
+    """bench.py's multi-GPU bootstrap without torch.distributed: rank 0's RCCL id
+    (here a stand-in byte string) reaches every rank over the stdlib TCP
+    rendezvous; only rank 0 makes an id."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rdv_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    ids = {uid for _, uid, _ in got}
+    assert len(ids) == 1 and next(iter(ids)).endswith(b"rank0")
+    assert sorted(m for _, _, m in got) == [0] * (world - 1) + [1]
