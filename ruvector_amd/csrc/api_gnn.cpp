@@ -108,6 +108,7 @@ struct rvx_layer {
     // device: weights [out][in] (the GEMM's K-contiguous B) with their exact
     // 3-way bf16 splits for the split-bf16 MFMA GEMM; biases and norm f32
     DevWeight d_wmsg, d_wqkv, d_wo, d_wagg, d_wzr, d_uzr, d_wh, d_uh;
+    DevWeight d_wkT;  // folded attention: per head W_k,h^T as [heads][H][hd] (rows heads*H, cols hd)
     DevMem d_bmsg, d_bqkv, d_bo, d_bagg, d_bwzr, d_buzr, d_bwh, d_buh, d_gamma, d_beta;
 };
 
@@ -142,6 +143,14 @@ void upload_layer(rvx_layer* l) {
     const int64_t H = l->H;
     l->d_wmsg.upload(l->w_msg.w, H, l->in); upload(l->d_bmsg, l->w_msg.b);
     l->d_wqkv.upload(cat({&l->q.w, &l->k.w, &l->v.w}), 3 * H, H); upload(l->d_bqkv, cat({&l->q.b, &l->k.b, &l->v.b}));
+    {
+        const int64_t hd = l->hd, heads = l->heads;
+        std::vector<float> wkt((size_t)(H * H));
+        for (int64_t h = 0; h < heads; ++h)
+            for (int64_t c = 0; c < H; ++c)
+                for (int64_t d = 0; d < hd; ++d) wkt[(size_t)((h * H + c) * hd + d)] = l->k.w[(size_t)((h * hd + d) * H + c)];
+        l->d_wkT.upload(wkt, heads * H, hd);
+    }
     l->d_wo.upload(l->o.w, H, H); upload(l->d_bo, l->o.b);
     l->d_wagg.upload(l->w_agg.w, H, H); upload(l->d_bagg, l->w_agg.b);
     l->d_wzr.upload(cat({&l->w_z.w, &l->w_r.w}), 2 * H, H); l->d_uzr.upload(cat({&l->u_z.w, &l->u_r.w}), 2 * H, H);
@@ -209,12 +218,27 @@ void put_linear(std::string& s, const HostLinear& l) {
 // n_out (< 0: n): phase 2 runs for rows [0, n_out) only — the star form, whose
 // rows past n_out are neighbour-only (they feed phase 1's M and K|V); rp and y
 // then need only n_out + 1 / n_out rows.
-// Phase 1 for `rows` rows: M = w_msg(x) and K|V = M·[W_k;W_v]^T.
+// Folded attention (gnn.hpp EdgeFoldArgs): K|V are never formed, the edges
+// read M alone and a sharded layer exchanges H columns per row instead of 3H
+// (SURVEY.md §8e). RVX_GNN_FOLD: 0 (default) off, 1 the multi-rank exchange
+// path, 2 every batched forward. Opt-in: on one GPU at 2M x 768 / 8 heads the
+// folded layer is 1.5x slower (edge kernel 2 x 120 -> 220 ms per layer: eight
+// full-wave score reductions per edge and M read twice; the eight K = 96 qt
+// GEMMs 51 ms), which the 3x smaller exchange (7/8 x N x 2H x 4 B less per
+// GPU and layer) only repays on a slow or contended interconnect. Read per call.
+bool use_fold(const rvx_layer* l, bool exchange_multi) {
+    const int mode = env_int("RVX_GNN_FOLD", 0);
+    if (!edge_fold_ok(l->H, l->heads)) return false;
+    return mode == 2 || (mode == 1 && exchange_multi);
+}
+
+// Phase 1 for `rows` rows: M = w_msg(x) and (KV non-null) K|V = M·[W_k;W_v]^T.
 void phase1_dev(const rvx_layer* l, int64_t rows, const float* x, float* M, float* KV) {
     const int64_t H = l->H;
     GemmEpilogue ep;
     ep.bias0 = l->d_bmsg.as<float>();
     gemm_auto(rows, (int)H, l->d_wmsg.op(x, l->in), nullptr, ep, M, H, "gnn_gemm_msg");
+    if (!KV) return;
     ep = GemmEpilogue();
     ep.bias0 = l->d_bqkv.as<float>() + H;
     gemm_auto(rows, (int)(2 * H), l->d_wqkv.op(M, H, H), nullptr, ep, KV, 2 * H, "gnn_gemm_kv");
@@ -223,11 +247,17 @@ void phase1_dev(const rvx_layer* l, int64_t rows, const float* x, float* M, floa
 // Phase 2 for destination rows [0, rows_out) of rp: neighbours index the whole
 // M / KV tables (global ids), the destination rows themselves are rows
 // self_off + r of them; y receives rows_out rows.
+// KV == nullptr: folded attention (qt / u tables of heads*H floats per row, so
+// the row chunk is capped at 128k rows).
 void phase2_dev(const rvx_layer* l, int64_t rows_out, const int64_t* rp, const int32_t* col, int64_t max_deg,
                 const float* w, int wmode, const float* M, const float* KV, int64_t self_off, float* y) {
-    const int64_t H = l->H;
-    const int64_t CHUNK = std::max<int64_t>(4096, env_int("RVX_GNN_CHUNK_ROWS", 1 << 20));  // read per call
+    const int64_t H = l->H, heads = l->heads, hd = l->hd;
+    const bool fold = KV == nullptr;
+    int64_t CHUNK = std::max<int64_t>(4096, env_int("RVX_GNN_CHUNK_ROWS", 1 << 20));  // read per call
+    if (fold) CHUNK = std::min<int64_t>(CHUNK, 1 << 17);
     const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(rows_out, CHUNK));
+    float* QT = fold ? scratch_f32("rvl_qt", chunk * heads * H) : nullptr;
+    float* U = fold ? scratch_f32("rvl_u", chunk * heads * H) : nullptr;
     float* Q = scratch_f32("rvl_q", chunk * H);
     float* S1 = scratch_f32("rvl_s1", chunk * 2 * H);
     float* S2 = scratch_f32("rvl_s2", chunk * H);
@@ -242,12 +272,31 @@ void phase2_dev(const rvx_layer* l, int64_t rows_out, const int64_t* rp, const i
         ep.bias0 = l->d_bqkv.as<float>();
         gemm_auto(rows, (int)H, l->d_wqkv.op(Mc, H, 0), nullptr, ep, Q, H, "gnn_gemm_q");
 
-        EdgeArgs ea;
-        ea.n = rows; ea.H = (int)H; ea.heads = l->heads; ea.hd = l->hd; ea.G = edge_group_lanes((int)H, l->heads);
-        ea.rp = rp + r0; ea.col = col; ea.w = w; ea.wmode = w ? wmode : 0;
-        ea.q = Q; ea.ldq = H; ea.k = KV; ea.v = KV + H; ea.ldkv = 2 * H; ea.m = M;
-        ea.scores = scores; ea.att = S2; ea.wagg = S3;
-        edge_attention(ea);
+        if (fold) {
+            // qt_h = W_k,h^T q_h (one GEMM per head), edges over m_j, att_h = W_v,h u_h + b_v,h
+            for (int64_t h = 0; h < heads; ++h)
+                gemm_auto(rows, (int)H, l->d_wkT.op(Q + h * hd, H, h * H), nullptr, GemmEpilogue(), QT + h * H,
+                          heads * H, "gnn_gemm_qt");
+            EdgeFoldArgs fa;
+            fa.n = rows; fa.H = (int)H; fa.heads = (int)heads; fa.hd = (int)hd;
+            fa.rp = rp + r0; fa.col = col; fa.w = w; fa.wmode = w ? wmode : 0;
+            fa.q = Q; fa.bk = l->d_bqkv.as<float>() + H; fa.qt = QT; fa.m = M;
+            fa.scores = scores; fa.u = U; fa.wagg = S3;
+            edge_attention_fold(fa);
+            for (int64_t h = 0; h < heads; ++h) {
+                ep = GemmEpilogue();
+                ep.bias0 = l->d_bqkv.as<float>() + 2 * H + h * hd;
+                gemm_auto(rows, (int)hd, l->d_wqkv.op(U + h * H, heads * H, 2 * H + h * hd), nullptr, ep, S2 + h * hd, H,
+                          "gnn_gemm_att");
+            }
+        } else {
+            EdgeArgs ea;
+            ea.n = rows; ea.H = (int)H; ea.heads = l->heads; ea.hd = l->hd; ea.G = edge_group_lanes((int)H, l->heads);
+            ea.rp = rp + r0; ea.col = col; ea.w = w; ea.wmode = w ? wmode : 0;
+            ea.q = Q; ea.ldq = H; ea.k = KV; ea.v = KV + H; ea.ldkv = 2 * H; ea.m = M;
+            ea.scores = scores; ea.att = S2; ea.wagg = S3;
+            edge_attention(ea);
+        }
 
         ep = GemmEpilogue();
         ep.bias0 = l->d_bo.as<float>();
@@ -280,7 +329,7 @@ void forward_dev(const rvx_layer* l, int64_t n, const int64_t* rp, const int32_t
     const int64_t H = l->H;
     const int64_t rows_out = n_out < 0 ? n : std::min(n_out, n);
     float* M = scratch_f32("rvl_m", n * H);
-    float* KV = scratch_f32("rvl_kv", n * 2 * H);
+    float* KV = use_fold(l, false) ? nullptr : scratch_f32("rvl_kv", n * 2 * H);
     phase1_dev(l, n, x, M, KV);
     phase2_dev(l, rows_out, rp, col, max_deg, w, wmode, M, KV, 0, y);
 }
@@ -576,17 +625,19 @@ rvx_status rvx_gnn_forward_exchange(const rvx_layer* l, const rvx_graph* g, cons
         RVX_REQUIRE(x_full->mem.bytes >= N * l->in * 4, RVX_ERR_DIMENSION_MISMATCH, "x_full smaller than N*input_dim");
         RVX_REQUIRE(y_full->mem.bytes >= N * H * 4, RVX_ERR_DIMENSION_MISMATCH, "y_full smaller than N*hidden_dim");
         ComputeLock cl;
-        // phase 1 on the owned rows, straight into the whole-table M and K|V,
-        // then every rank's rows of both tables to every peer (one grouped
-        // p2p round each on the library stream), then phase 2 on owned rows
+        // phase 1 on the owned rows, straight into the whole-table M (and,
+        // unfolded, K|V), then every rank's rows to every peer (one grouped p2p
+        // round per table on the library stream), then phase 2 on owned rows.
+        // Folded (RVX_GNN_FOLD=1/2) only M travels: H columns per row, not 3H.
+        const bool fold = use_fold(l, world > 1);
         float* M = scratch_f32("rvl_m", N * H);
-        float* KV = scratch_f32("rvl_kv", N * 2 * H);
-        phase1_dev(l, g->n, x_full->mem.as<float>() + o * l->in, M + o * H, KV + o * 2 * H);
+        float* KV = fold ? nullptr : scratch_f32("rvl_kv", N * 2 * H);
+        phase1_dev(l, g->n, x_full->mem.as<float>() + o * l->in, M + o * H, KV ? KV + o * 2 * H : nullptr);
         if (world > 1) {
             ProfScope ps("gnn_halo_exchange");
             for (const ExchangeRound& r : exchange_plan(PLAN_WHOLE, offsets, world)) {
                 comm_exchange_rows(comm, M, H, r.r0.data(), r.rows.data(), stream());
-                comm_exchange_rows(comm, KV, 2 * H, r.r0.data(), r.rows.data(), stream());
+                if (KV) comm_exchange_rows(comm, KV, 2 * H, r.r0.data(), r.rows.data(), stream());
             }
         }
         phase2_dev(l, g->n, g->row_ptr, g->col, g->max_deg, g->w, 1, M, KV, o, y_full->mem.as<float>() + o * H);

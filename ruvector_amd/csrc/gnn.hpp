@@ -40,6 +40,29 @@ struct FinishArgs {
 };
 
 void edge_attention(const EdgeArgs& a);
+
+// Folded attention (RuvectorLayer exchanging M only): with
+// k_j = W_k m_j + b_k and v_j = W_v m_j + b_v, per destination i and head h
+//   score_ij,h = (qt_i,h · m_j + q_i,h · b_k,h) / sqrt(hd),  qt_i,h = W_k,h^T q_i,h
+//   u_i,h      = sum_j a_ij,h m_j            (att_i,h = W_v,h u_i,h + b_v,h)
+// so the edges read m_j alone. qt: [n][heads][H]; u: [n][heads][H].
+struct EdgeFoldArgs {
+    int64_t n = 0;
+    int H = 0, heads = 0, hd = 0;
+    const int64_t* rp = nullptr;
+    const int32_t* col = nullptr;
+    const float* w = nullptr;
+    int wmode = 0;
+    const float* q = nullptr;    // [n][H]  (for q_h · b_k,h)
+    const float* bk = nullptr;   // [H]
+    const float* qt = nullptr;   // [n][heads][H]
+    const float* m = nullptr;    // [N][H]
+    float* scores = nullptr;     // [chunk edges][heads] scratch
+    float* u = nullptr;          // [n][heads][H]
+    float* wagg = nullptr;       // [n][H]
+};
+bool edge_fold_ok(int H, int heads);
+void edge_attention_fold(const EdgeFoldArgs& a);
 int edge_group_lanes(int H, int heads);  // 0 when the grouped kernel does not apply
 void mul_rows(const float* r, int64_t ldr, const float* h, float* out, int64_t n, int H);
 void gru_finish(const FinishArgs& a);

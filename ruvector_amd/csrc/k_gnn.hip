@@ -161,6 +161,155 @@ __global__ __launch_bounds__(256) void k_edge_attn_generic(EdgeArgs a) {
     }
 }
 
+// Folded attention (gnn.hpp EdgeFoldArgs), one wave per destination: lane owns
+// columns [lane*CPL, lane*CPL+CPL) of every head's qt / u rows and of m_j, so
+// an edge reads one H-float row. Scores: per head a lane partial over its
+// columns + a full-wave tree; softmax per head in edge order (one lane per
+// head: max, exp, sum, e/sum as layer.rs:196-199); u_h and the weighted
+// message aggregate in edge order.
+constexpr int FOLD_MAXH = 8;
+
+template <int CPL>
+__device__ __forceinline__ void ld_cols(const float* p, float (&v)[CPL]) {
+    if constexpr (CPL % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < CPL; c += 4) {
+            const float4 t = ld4(p + c);
+            v[c] = t.x; v[c + 1] = t.y; v[c + 2] = t.z; v[c + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) v[c] = p[c];
+    }
+}
+template <int CPL>
+__device__ __forceinline__ void st_cols(float* p, const float (&v)[CPL]) {
+    if constexpr (CPL % 4 == 0) {
+#pragma unroll
+        for (int c = 0; c < CPL; c += 4) *reinterpret_cast<float4*>(p + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
+    } else {
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) p[c] = v[c];
+    }
+}
+__device__ __forceinline__ float wave_sum(float p) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o);
+    return p;
+}
+
+template <int CPL>
+__global__ __launch_bounds__(256) void k_edge_attn_fold(EdgeFoldArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const int H = a.H, heads = a.heads, hd = a.hd;
+    const int c0 = lane * CPL;
+    const int64_t beg = a.rp[i], end = a.rp[i + 1];
+    const int deg = (int)(end - beg);
+    float* scores = a.scores - a.rp[0] * heads;  // chunk-relative edge slots
+    float* urow = a.u + i * (int64_t)heads * H + c0;
+    float zero[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) zero[c] = 0.0f;
+    if (deg == 0) {
+        for (int h = 0; h < heads; ++h) st_cols<CPL>(urow + (int64_t)h * H, zero);
+        st_cols<CPL>(a.wagg + i * H + c0, zero);
+        return;
+    }
+    // q_h · b_k,h per head (the key bias folded out of the edge loop)
+    float cb[FOLD_MAXH];
+    {
+        float qv[CPL], bv[CPL];
+        ld_cols<CPL>(a.q + i * H + c0, qv);
+        ld_cols<CPL>(a.bk + c0, bv);
+#pragma unroll
+        for (int h = 0; h < FOLD_MAXH; ++h) {
+            float p = 0.0f;
+            if (h < heads) {
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) p = ((c0 + c) / hd == h) ? p + qv[c] * bv[c] : p;
+                p = wave_sum(p);
+            }
+            cb[h] = p;
+        }
+    }
+    const float scale = sqrtf((float)hd);
+    float mx[FOLD_MAXH];
+    {
+        float qt[FOLD_MAXH][CPL];
+#pragma unroll
+        for (int h = 0; h < FOLD_MAXH; ++h) {
+            if (h < heads) ld_cols<CPL>(a.qt + i * (int64_t)heads * H + (int64_t)h * H + c0, qt[h]);
+            mx[h] = -INFINITY;
+        }
+        // pass 1: scores
+        for (int64_t e = beg; e < end; ++e) {
+            float mv[CPL];
+            ld_cols<CPL>(a.m + (int64_t)a.col[e] * H + c0, mv);
+#pragma unroll
+            for (int h = 0; h < FOLD_MAXH; ++h) {
+                if (h >= heads) continue;
+                float p = 0.0f;
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) p = p + qt[h][c] * mv[c];
+                const float s = (wave_sum(p) + cb[h]) / scale;
+                mx[h] = fmaxf(mx[h], s);
+                if (lane == h) scores[e * heads + h] = s;
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
+    // pass 2: lane h < heads runs head h's softmax in edge order
+    if (lane < heads) {
+        float m_h = mx[0];
+#pragma unroll
+        for (int h = 1; h < FOLD_MAXH; ++h)
+            if (lane == h) m_h = mx[h];
+        float sum = 0.0f;
+        for (int64_t e = beg; e < end; ++e) {
+            const float ex = expf(scores[e * heads + lane] - m_h);
+            scores[e * heads + lane] = ex;
+            sum = sum + ex;
+        }
+        sum = fmaxf(sum, 1e-10f);
+        for (int64_t e = beg; e < end; ++e) scores[e * heads + lane] = scores[e * heads + lane] / sum;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence_block();
+    // pass 3: u_h = sum_j a_jh m_j and the weighted message aggregate
+    float u[FOLD_MAXH][CPL], agg[CPL];
+#pragma unroll
+    for (int h = 0; h < FOLD_MAXH; ++h)
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) u[h][c] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) agg[c] = 0.0f;
+    float wsum = 0.0f;
+    if (a.wmode == 1) wsum = row_weight_sum(a.w, beg, end);
+    for (int64_t e = beg; e < end; ++e) {
+        float mv[CPL];
+        ld_cols<CPL>(a.m + (int64_t)a.col[e] * H + c0, mv);
+#pragma unroll
+        for (int h = 0; h < FOLD_MAXH; ++h) {
+            if (h >= heads) continue;
+            const float wt = scores[e * heads + h];
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) u[h][c] = u[h][c] + wt * mv[c];
+        }
+        if (a.wmode != 0) {
+            const float ww = norm_weight(a.wmode, a.w, e, wsum, deg);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) agg[c] = agg[c] + ww * mv[c];
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < FOLD_MAXH; ++h)
+        if (h < heads) st_cols<CPL>(urow + (int64_t)h * H, u[h]);
+    st_cols<CPL>(a.wagg + i * H + c0, agg);
+}
+
 __global__ void k_mul(const float* r, int64_t ldr, const float* h, float* out, int64_t n, int H) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= n * H) return;
@@ -216,6 +365,31 @@ void edge_attention(const EdgeArgs& a) {
     else if (aligned && a.H % 64 == 0 && a.G > 0 && a.H / 64 == 12) RVX_LAUNCH(t, k_edge_attn_grouped<12>, grid, block, 0, a);
     else if (aligned && a.H % 64 == 0 && a.G > 0 && a.H / 64 == 16) RVX_LAUNCH(t, k_edge_attn_grouped<16>, grid, block, 0, a);
     else RVX_LAUNCH(t, k_edge_attn_generic, grid, block, 0, a);
+}
+
+bool edge_fold_ok(int H, int heads) {
+    if (H % 64 != 0 || heads <= 0 || heads > FOLD_MAXH || H % heads != 0) return false;
+    const int cpl = H / 64;
+    return cpl == 1 || cpl == 2 || cpl == 4 || cpl == 8 || cpl == 12 || cpl == 16;
+}
+
+void edge_attention_fold(const EdgeFoldArgs& a) {
+    if (a.n <= 0) return;
+    RVX_REQUIRE(edge_fold_ok(a.H, a.heads), RVX_ERR_UNSUPPORTED, "folded attention needs H % 64 == 0, heads <= 8");
+    const bool aligned = (((uintptr_t)a.q | (uintptr_t)a.qt | (uintptr_t)a.m | (uintptr_t)a.u | (uintptr_t)a.wagg |
+                           (uintptr_t)a.bk) & 15) == 0;
+    const int cpl = a.H / 64;
+    RVX_REQUIRE(aligned || cpl % 4 != 0, RVX_ERR_INVALID_PARAMETER, "folded attention operands must be 16-B aligned");
+    const dim3 grid((unsigned)((a.n + 3) / 4)), block(256);
+    const char* t = "gnn_edge_attention";
+    switch (cpl) {
+        case 1: RVX_LAUNCH(t, k_edge_attn_fold<1>, grid, block, 0, a); break;
+        case 2: RVX_LAUNCH(t, k_edge_attn_fold<2>, grid, block, 0, a); break;
+        case 4: RVX_LAUNCH(t, k_edge_attn_fold<4>, grid, block, 0, a); break;
+        case 8: RVX_LAUNCH(t, k_edge_attn_fold<8>, grid, block, 0, a); break;
+        case 12: RVX_LAUNCH(t, k_edge_attn_fold<12>, grid, block, 0, a); break;
+        default: RVX_LAUNCH(t, k_edge_attn_fold<16>, grid, block, 0, a); break;
+    }
 }
 
 int edge_group_lanes(int H, int heads) {

@@ -86,10 +86,19 @@ def main():
         rl = rv.RuvectorLayer(H, H, heads, 0.0, seed=7)
         xgb = rv.Buffer.from_numpy(xg)
         ys, yr = rv.Buffer(n2 * H * 4), rv.Buffer(n2 * H * 4)
-        rl.forward_exchange(gl, xgb, ys, offsets, comm)
-        rl.forward_graph_device(xgb, gf, yr)
-        res["gnn_owned_equal"] = bool(np.array_equal(ys.download(np.float32, (n2, H))[o0:o1],
-                                                     yr.download(np.float32, (n2, H))[o0:o1]))
+        # M|K|V exchange (RVX_GNN_FOLD=0, default) and the folded M-only
+        # exchange (forced on for the 1-process reference too)
+        for mode, key in (("0", "gnn_owned_equal"), ("2", "gnn_fold_owned_equal")):
+            os.environ["RVX_GNN_FOLD"] = mode
+            rl.forward_exchange(gl, xgb, ys, offsets, comm)
+            rl.forward_graph_device(xgb, gf, yr)
+            res[key] = bool(np.array_equal(ys.download(np.float32, (n2, H))[o0:o1],
+                                           yr.download(np.float32, (n2, H))[o0:o1]))
+        os.environ.pop("RVX_GNN_FOLD")
+        W = O.RvlWeights(json.loads(rl.to_json()))
+        ref = O.rvl_forward_graph(W, xg, rp2, col2, ew, rows=(o0, min(o1 - o0, 300)))
+        got = ys.download(np.float32, (n2, H))[o0:o0 + len(ref)]
+        res["gnn_fold_vs_oracle"] = float(np.max(np.abs(got - ref)) / np.max(np.abs(ref)))
         att = EdgeFeaturedAttention(EdgeFeaturedConfig(node_dim=H, edge_dim=1, num_heads=heads))
         efl, eff = rv.Buffer.from_numpy(ew[rp2[o0]:rp2[o1]].copy()), rv.Buffer.from_numpy(ew)
         zs, zr = rv.Buffer(n2 * H * 4), rv.Buffer(n2 * H * 4)

@@ -507,6 +507,39 @@ def test_ruvector_forward_graph_matches_oracle(monkeypatch, hidden, heads, h2):
     assert_close(y, ref)
 
 
+@pytest.mark.parametrize("hidden,heads,deg", [(64, 4, 12), (128, 8, 7), (768, 8, 32), (256, 2, 5)])
+def test_ruvector_forward_graph_folded_attention(monkeypatch, hidden, heads, deg):
+    """Folded attention (RVX_GNN_FOLD=2; the default of the multi-rank exchange,
+    SURVEY.md §8e): no K|V tables, scores = (W_k,h^T q_h) . m_j + q_h . b_k,h,
+    att_h = W_v,h (sum_j a_jh m_j) + b_v,h — the edges read M alone. Same layer
+    (incl. isolated rows and nonzero biases) within 1e-5 of the oracle's
+    per-pair K/V evaluation, and of the unfolded GPU path."""
+    n = 300
+    layer, W, js = _layer_and_weights(hidden, hidden, heads, 0.1, seed=11)
+    # nonzero attention biases so the folded b_k / b_v terms are exercised
+    for name in ("q_linear", "k_linear", "v_linear"):
+        b = js["attention"][name]["bias"]
+        b["data"] = [float(v) for v in O.fill_uniform(len(b["data"]), 90 + len(name), -0.5, 0.5)]
+    layer = rv.RuvectorLayer.from_json(json.dumps(js))
+    W = O.RvlWeights(js)
+    x = O.fill_uniform(n * hidden, 14).reshape(n, hidden)
+    rng = np.random.default_rng(deg)
+    degs = rng.integers(0, 2 * deg, n)
+    degs[::17] = 0  # isolated rows: LayerNorm(M_i)
+    rp = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
+    col = rng.integers(0, n, int(rp[-1])).astype(np.int32)
+    ew = O.fill_uniform(len(col), 16, 0.0, 1.0)
+    g = rv.Graph.from_csr(rp, col, ew)
+    monkeypatch.setenv("RVX_GNN_FOLD", "0")
+    y0 = layer.forward_graph(x, g)
+    monkeypatch.setenv("RVX_GNN_FOLD", "2")
+    y = layer.forward_graph(x, g)
+    ref = O.rvl_forward_graph(W, x, rp, col, ew)
+    assert_close(y, ref)
+    assert_close(y, y0)
+    print(f"H {hidden} h {heads}: folded vs oracle {rel_err(y, ref):.2e}, unfolded vs oracle {rel_err(y0, ref):.2e}")
+
+
 def test_ruvector_forward_graph_row_chunks(monkeypatch):
     """Phase 2 of the batched layer runs in row chunks (api_gnn.cpp forward_dev):
     chunk seams, the chunk-relative score slots and isolated rows in a later

@@ -55,4 +55,5 @@ def test_exchange_entry_points_multi_rank(offsets, tmp_path):
         assert r["sage_layer2_owned_equal"], r
         assert r["sage_layer1_vs_oracle"] <= 1e-5, r
         assert r["gnn_owned_equal"], r
+        assert r["gnn_fold_owned_equal"] and r["gnn_fold_vs_oracle"] <= 1e-5, r
         assert r["efa_owned_equal"], r
