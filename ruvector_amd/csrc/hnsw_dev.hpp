@@ -51,7 +51,7 @@ __device__ __forceinline__ float finish_dist(float acc, float qn, float xn) {
 #endif
 constexpr int ROW_BATCH = RVX_ROW_BATCH;  // float4s per batch
 
-template <int METRIC, bool Q_GLOBAL>
+template <int METRIC, bool Q_GLOBAL, int RB = ROW_BATCH>
 __device__ __forceinline__ float stream_acc(const float* __restrict__ qs, const float* __restrict__ x, int n4) {
     const float4* r = reinterpret_cast<const float4*>(x);
     const float4* qq = reinterpret_cast<const float4*>(qs);
@@ -60,26 +60,26 @@ __device__ __forceinline__ float stream_acc(const float* __restrict__ qs, const 
     // use (a guarded load would sit in its own block and the waitcnt pass would
     // fall back to vmcnt(0), serialising the row again); the last prefetch
     // re-reads a batch already in cache instead of branching.
-    const int nfull = n4 / (2 * ROW_BATCH) * (2 * ROW_BATCH);
+    const int nfull = n4 / (2 * RB) * (2 * RB);
     if (nfull > 0) {
-        float4 xa[ROW_BATCH], xb[ROW_BATCH], qa[Q_GLOBAL ? ROW_BATCH : 1], qb[Q_GLOBAL ? ROW_BATCH : 1];
+        float4 xa[RB], xb[RB], qa[Q_GLOBAL ? RB : 1], qb[Q_GLOBAL ? RB : 1];
         auto load = [&](float4* xv, float4* qv, int base) {
 #pragma unroll
-            for (int j = 0; j < ROW_BATCH; ++j) {
+            for (int j = 0; j < RB; ++j) {
                 xv[j] = r[base + j];
                 if constexpr (Q_GLOBAL) qv[j] = qq[base + j];
             }
         };
         auto run = [&](const float4* xv, const float4* qv, int base) {
 #pragma unroll
-            for (int j = 0; j < ROW_BATCH; ++j) acc = acc4<METRIC>(acc, Q_GLOBAL ? qv[j] : qq[base + j], xv[j]);
+            for (int j = 0; j < RB; ++j) acc = acc4<METRIC>(acc, Q_GLOBAL ? qv[j] : qq[base + j], xv[j]);
         };
         load(xa, qa, 0);
-        for (int base = 0; base < nfull; base += 2 * ROW_BATCH) {
-            load(xb, qb, base + ROW_BATCH);
+        for (int base = 0; base < nfull; base += 2 * RB) {
+            load(xb, qb, base + RB);
             run(xa, qa, base);
-            load(xa, qa, base + 2 * ROW_BATCH < nfull ? base + 2 * ROW_BATCH : base);
-            run(xb, qb, base + ROW_BATCH);
+            load(xa, qa, base + 2 * RB < nfull ? base + 2 * RB : base);
+            run(xb, qb, base + RB);
         }
     }
     for (int k = nfull; k < n4; ++k) acc = acc4<METRIC>(acc, qq[k], r[k]);
@@ -88,14 +88,14 @@ __device__ __forceinline__ float stream_acc(const float* __restrict__ qs, const 
 
 // curv: the Poincaré curvature (RVX_METRIC_POINCARE only: HyperbolicHnsw::distance,
 // fused norms + poincare_distance_from_norms, hnsw.rs:173-180)
-template <int METRIC, bool Q_GLOBAL = false>
+template <int METRIC, bool Q_GLOBAL = false, int RB = ROW_BATCH>
 __device__ __forceinline__ float row_dist(const float* __restrict__ qs, const float* __restrict__ x, int d, float qn,
                                           float xn, float curv = 1.0f) {
     if constexpr (METRIC == RVX_METRIC_POINCARE) return pdev::hyp_dist(qs, x, d, curv);
     if constexpr (METRIC == RVX_METRIC_HYP_L2) return pdev::hyp_l2(qs, x, d);
     float acc = 0.0f;
     if ((d & 3) == 0) {
-        acc = stream_acc<METRIC, Q_GLOBAL>(qs, x, d >> 2);
+        acc = stream_acc<METRIC, Q_GLOBAL, RB>(qs, x, d >> 2);
     } else {
         for (int k = 0; k < d; ++k) {
             const float q = qs[k], v = x[k];

@@ -52,11 +52,10 @@ struct SearchArgs {
     int coop;          // wave-cooperative LDS-staged distances (hnsw_dev.hpp wave_dist)
 };
 
-template <int METRIC>
-#ifndef RVX_HNSW_WPE
-#define RVX_HNSW_WPE
-#endif
-__global__ __launch_bounds__(64) RVX_HNSW_WPE void k_hnsw_search(SearchArgs a) {
+// RB: float4s per streamed row batch of the per-lane distances (hnsw_dev.hpp
+// stream_acc).
+template <int METRIC, int RB>
+__device__ __forceinline__ void search_body(const SearchArgs& a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int lane = threadIdx.x;
     const int ef = a.ef;
@@ -81,7 +80,7 @@ __global__ __launch_bounds__(64) RVX_HNSW_WPE void k_hnsw_search(SearchArgs a) {
         __builtin_amdgcn_wave_barrier();
         const float qn = (METRIC == RVX_METRIC_COSINE) ? a.qnorm[qi] : 0.0f;
         auto dist_of = [&](int node) {
-            return row_dist<METRIC>(qs, a.x + (int64_t)node * a.d, a.d,
+            return row_dist<METRIC, false, RB>(qs, a.x + (int64_t)node * a.d, a.d,
                                     qn, METRIC == RVX_METRIC_COSINE ? a.xnorm[node] : 0.0f, a.curv);
         };
         // every lane calls; node < 0: no row (INFINITY)
@@ -206,6 +205,22 @@ __global__ __launch_bounds__(64) RVX_HNSW_WPE void k_hnsw_search(SearchArgs a) {
     }
 }
 
+#ifndef RVX_HNSW_WPE
+#define RVX_HNSW_WPE
+#endif
+template <int METRIC>
+__global__ __launch_bounds__(64) RVX_HNSW_WPE void k_hnsw_search(SearchArgs a) {
+    search_body<METRIC, ROW_BATCH>(a);
+}
+// Short rows (d <= 256, per-lane distances): 4-float4 row batches and at least
+// 4 waves per SIMD (117 VGPRs instead of 167 -> 3 waves). C1 100k x 128, ef 600:
+// 334k vs 302k QPS; at d = 768 the deeper batches win (1M x 768 ef 800: 52.9k
+// vs 47.3k), so they keep the default kernel (scripts/exp_hnsw_occupancy.sh).
+template <int METRIC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_hnsw_search_short(SearchArgs a) {
+    search_body<METRIC, 4>(a);
+}
+
 }  // namespace
 
 SearchStats g_search_stats;
@@ -250,9 +265,22 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_HYP_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search_short<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search_short<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search_short<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search_short<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     const char* t = tag ? tag : "hnsw_search";
+    const bool short_rows = !coop && d <= 256 && env_int("RVX_HNSW_SHORT", 1);  // read per call: tests cover both
+    if (short_rows && metric != RVX_METRIC_POINCARE && metric != RVX_METRIC_HYP_L2) {
+        switch (metric) {
+            case RVX_METRIC_L2: RVX_LAUNCH(t, k_hnsw_search_short<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_hnsw_search_short<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_DOT: RVX_LAUNCH(t, k_hnsw_search_short<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, a); break;
+            default: RVX_LAUNCH(t, k_hnsw_search_short<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
+        }
+    } else
     switch (metric) {
         case RVX_METRIC_L2: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
         case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
