@@ -139,8 +139,11 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
     return rs;
 }
 
+#ifndef RVX_BUILD_WPE
+#define RVX_BUILD_WPE
+#endif
 template <int METRIC>
-__global__ __launch_bounds__(64) void k_build_insert(BuildArgs a) {
+__global__ __launch_bounds__(64) RVX_BUILD_WPE void k_build_insert(BuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int lane = threadIdx.x;
     const int ef = a.ef_c;
