@@ -76,6 +76,12 @@ void append_rows(rvx_index* ix, const float* dev_rows, const uint64_t* ids, int6
 void search_rows(const rvx_index* ix, const float* q, int64_t nq, int k, int ef, float* dd, int64_t* di, int32_t* dn,
                  bool exact) {
     const int d = ix->cfg.dim;
+    if (ix->n == 0) {  // an empty index answers every query with no result (flat.rs:36-76 over no entries)
+        RVX_HIP(hipMemsetD32Async((hipDeviceptr_t)dd, 0x7F800000u, (size_t)(nq * k), stream()));  // +inf
+        RVX_HIP(hipMemsetAsync(di, 0xFF, (size_t)(nq * k * 8), stream()));                         // row -1
+        if (dn) RVX_HIP(hipMemsetAsync(dn, 0, (size_t)(nq * 4), stream()));
+        return;
+    }
     float* qn = nullptr;
     if (ix->cfg.metric == RVX_METRIC_COSINE) {
         qn = scratch_f32("index_qnorm", nq);

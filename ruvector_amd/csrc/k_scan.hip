@@ -1018,6 +1018,11 @@ void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const
                 "scan needs dim % 4 == 0 and 16-B aligned rows");
     if (nq <= 0) return;
     last_scan_stats() = ScanStats{};
+    if (n <= 0) {  // no rows: every slot empty (distance +inf, row -1)
+        RVX_HIP(hipMemsetD32Async((hipDeviceptr_t)out_d, 0x7F800000u, (size_t)(nq * k), stream()));
+        RVX_HIP(hipMemsetAsync(out_i, 0xFF, (size_t)(nq * k * 8), stream()));
+        return;
+    }
     if (scan_topk_mfma(metric, q, qnorm, nq, x, xnorm, deleted, n, d, k, id_offset, out_d, out_i)) return;
     scan_topk_valu(metric, q, qnorm, nq, x, xnorm, deleted, n, d, k, id_offset, out_d, out_i, tag, curv);
 }
