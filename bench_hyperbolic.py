@@ -51,14 +51,17 @@ def main():
 
     log = lambda s: print(s, file=sys.stderr, flush=True)  # noqa: E731
     n, d, nq, k = a.n, a.dim, a.queries, 10
-    x = ball(n, d, 7)
-    q = ball(nq, d, 8)
-    xb = rv.Buffer.from_numpy(x)
+    import benchutil
+    with benchutil.heartbeat(f"generating {n} x {d}", log=log):
+        x = ball(n, d, 7)
+        q = ball(nq, d, 8)
+        xb = rv.Buffer.from_numpy(x)
     h = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=7))
     rv.synchronize()
     t0 = time.perf_counter()
-    h.insert_device(xb, n, d)
-    rv.synchronize()
+    with benchutil.heartbeat(f"building {n} x {d}", log=log):
+        h.insert_device(xb, n, d)
+        rv.synchronize()
     build_s = time.perf_counter() - t0
     log(f"build {n} x {d}: {build_s:.1f} s")
     del xb
