@@ -68,6 +68,11 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
                                                       const float* __restrict__ self_x, float* __restrict__ row_scale,
                                                       _Float16* __restrict__ planes, int64_t pstride) {
     const int lane = threadIdx.x & 63;
+#ifndef RVX_AGG_PRIO
+#define RVX_AGG_PRIO 0
+#endif
+    // overlapped launches: optionally issue ahead of the GEMM waves on the same SIMD
+    if constexpr (NT && RVX_AGG_PRIO > 0) __builtin_amdgcn_s_setprio(RVX_AGG_PRIO);
     // grid-stride over rows: the grid may be capped (persistent) so the gather
     // leaves CU slots to a concurrently running GEMM
     for (int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6); row < n;
