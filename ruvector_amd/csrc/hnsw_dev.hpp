@@ -117,9 +117,14 @@ __device__ __forceinline__ float row_dist(const float* __restrict__ qs, const fl
 // 16-B slot p ^ ((row >> 1) & 7) (conflict-free for the per-lane ds_read_b128).
 // Two stages: the next chunk's DMA is in flight while this one accumulates.
 // Requires no other vector-memory op of the wave between a fill and its wait.
+// NST stages per wave: 2 keeps the next chunk's DMA in flight; 1 halves the
+// wave's LDS so more waves fit a CU (the search takes it past ef 1024, where
+// the R list already costs most of the LDS: C3 10M x 768 ef 3200 5.9k -> 8.1k QPS,
+// equal at ef 800, -3.5% at ef 100; scripts/exp_wd_stages.sh).
 constexpr int WD_CH = 32;                     // dims per chunk
 constexpr int WD_STAGE = 64 * WD_CH * 4;      // bytes per stage
-constexpr int WD_LDS = 2 * WD_STAGE;          // bytes per wave
+constexpr int WD_LDS = 2 * WD_STAGE;          // bytes per wave, two stages
+__host__ __device__ constexpr int wd_lds(int nst) { return nst * WD_STAGE; }
 
 __host__ __device__ inline bool wave_dist_ok(int d) { return d % WD_CH == 0; }
 
@@ -153,11 +158,20 @@ __device__ __forceinline__ float wd_chunk(float acc, const float* qs, int c, int
 // in flight, everything older (this chunk) has landed — and before refilling a
 // stage it waits lgkmcnt(0) so the stage's reads have returned. The asm
 // statements clobber memory, which also keeps the DMA groups in issue order.
-template <int METRIC>
+template <int METRIC, int NST = 2>
 __device__ __forceinline__ float wd_run(const float* __restrict__ x, int d, const float* qs, const int (&rid)[8], int lane,
                                         unsigned char* s0, unsigned char* s1) {
     const int nch = d / WD_CH;
     float acc = 0.0f;
+    if constexpr (NST == 1) {
+        for (int c = 0; c < nch; ++c) {
+            wd_fill<METRIC>(x, d, rid, c, lane, s0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            acc = wd_chunk<METRIC>(acc, qs, c, lane, s0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        return acc;
+    }
     wd_fill<METRIC>(x, d, rid, 0, lane, s0);
     for (int c = 0; c < nch; c += 2) {
         if (c + 1 < nch) {
@@ -182,14 +196,14 @@ __device__ __forceinline__ float wd_run(const float* __restrict__ x, int d, cons
 }
 
 // All 64 lanes call together. row < 0: no row (the lane's result is garbage).
-template <int METRIC>
+template <int METRIC, int NST = 2>
 __device__ __forceinline__ float wave_dist(const float* qs, const float* __restrict__ x, int d, int row, float qn,
                                            float xn, unsigned char* stage, int lane) {
     int rid[8];
     const int mine = row < 0 ? 0 : row;
 #pragma unroll
     for (int i = 0; i < 8; ++i) rid[i] = __shfl(mine, 8 * i + (lane >> 3));
-    const float acc = wd_run<METRIC>(x, d, qs, rid, lane, stage, stage + WD_STAGE);
+    const float acc = wd_run<METRIC, NST>(x, d, qs, rid, lane, stage, stage + WD_STAGE);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stages are refilled by the next call
     return finish_dist<METRIC>(acc, qn, xn);
 }

@@ -53,16 +53,16 @@ struct SearchArgs {
 };
 
 // RB: float4s per streamed row batch of the per-lane distances (hnsw_dev.hpp
-// stream_acc).
-template <int METRIC, int RB>
+// stream_acc); NST: LDS stages of the wave-cooperative distances.
+template <int METRIC, int RB, int NST = 2>
 __device__ __forceinline__ void search_body(const SearchArgs& a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int lane = threadIdx.x;
     const int ef = a.ef;
     constexpr bool COOP_OK = METRIC != RVX_METRIC_POINCARE && METRIC != RVX_METRIC_HYP_L2;
     const bool coop = COOP_OK && a.coop;
-    unsigned char* wst = lds_raw;                                // [WD_LDS] distance stages (coop)
-    float* qs = reinterpret_cast<float*>(lds_raw + (coop ? WD_LDS : 0));  // [d rounded to 4]
+    unsigned char* wst = lds_raw;                                // [NST * WD_STAGE] distance stages (coop)
+    float* qs = reinterpret_cast<float*>(lds_raw + (coop ? wd_lds(NST) : 0));  // [d rounded to 4]
     const int dq = (a.d + 3) & ~3;
     float* rd = qs + dq;                                        // R dist [ef+1]
     int* ri = reinterpret_cast<int*>(rd + ef + 1);              // R id | expanded flag (bit 31)
@@ -88,7 +88,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             float dv;
             if constexpr (COOP_OK) {
                 if (coop) {
-                    dv = wave_dist<METRIC>(qs, a.x, a.d, node, qn,
+                    dv = wave_dist<METRIC, NST>(qs, a.x, a.d, node, qn,
                                            (METRIC == RVX_METRIC_COSINE && node >= 0) ? a.xnorm[node] : 0.0f, wst, lane);
                     return node >= 0 ? dv : INFINITY;
                 }
@@ -220,6 +220,11 @@ template <int METRIC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_hnsw_search_short(SearchArgs a) {
     search_body<METRIC, 4>(a);
 }
+// Wide searches over LDS-staged rows (coop, ef >= 1024): one distance stage.
+template <int METRIC>
+__global__ __launch_bounds__(64) void k_hnsw_search_wide(SearchArgs a) {
+    search_body<METRIC, ROW_BATCH, 1>(a);
+}
 
 }  // namespace
 
@@ -233,9 +238,11 @@ bool hnsw_coop(int metric, int d, int64_t rows) {
     return mode == 2 || rows * (int64_t)d * 4 >= min_bytes;
 }
 
+bool hnsw_wide_ef(bool coop, int ef) { return coop && ef >= 1024 && env_int("RVX_HNSW_WIDE", 1); }  // read per call
+
 size_t hnsw_search_lds(int d, int ef, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)WD_LDS : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 8;
+    return (coop ? (size_t)wd_lds(hnsw_wide_ef(coop, ef) ? 1 : 2) : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 8;
 }
 
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
@@ -269,6 +276,10 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         hipFuncSetAttribute((const void*)k_hnsw_search_short<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_hnsw_search_short<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         hipFuncSetAttribute((const void*)k_hnsw_search_short<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search_wide<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search_wide<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search_wide<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        hipFuncSetAttribute((const void*)k_hnsw_search_wide<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr = true;
     }
     const char* t = tag ? tag : "hnsw_search";
@@ -279,6 +290,13 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
             case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_hnsw_search_short<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
             case RVX_METRIC_DOT: RVX_LAUNCH(t, k_hnsw_search_short<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, a); break;
             default: RVX_LAUNCH(t, k_hnsw_search_short<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
+        }
+    } else if (hnsw_wide_ef(coop, ef)) {  // coop is never set for the Poincaré metrics
+        switch (metric) {
+            case RVX_METRIC_L2: RVX_LAUNCH(t, k_hnsw_search_wide<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_hnsw_search_wide<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_DOT: RVX_LAUNCH(t, k_hnsw_search_wide<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, a); break;
+            default: RVX_LAUNCH(t, k_hnsw_search_wide<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
         }
     } else
     switch (metric) {

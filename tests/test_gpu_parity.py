@@ -177,8 +177,13 @@ def test_hnsw_search_bit_exact_on_same_graph(monkeypatch, metric, short):
         assert np.array_equal(dist, rd)
 
 
-def test_hnsw_search_large_ef_bit_exact():
-    # ef far above the graph degree (R-only search: long merges, many expansions)
+@pytest.mark.parametrize("coop,wide", [("0", "1"), ("2", "1"), ("2", "0")])
+def test_hnsw_search_large_ef_bit_exact(monkeypatch, coop, wide):
+    # ef far above the graph degree (R-only search: long merges, many expansions);
+    # coop 2 forces the LDS-staged distances, whose ef >= 1024 kernel keeps one
+    # stage per wave (RVX_HNSW_WIDE=1) or two (0)
+    monkeypatch.setenv("RVX_HNSW_COOP", coop)
+    monkeypatch.setenv("RVX_HNSW_WIDE", wide)
     x, h, g, idx = _hnsw_pair(6000, 32, "l2", 8, 60, 11)
     q = O.fill_uniform(64 * 32, 12).reshape(64, 32)
     for k, ef in ((10, 1500), (100, 3000)):
