@@ -354,11 +354,11 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");
     static bool attr = false;
     if (!attr) {
-        hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_HYP_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_HYP_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
     switch (metric) {
