@@ -328,13 +328,13 @@ rvx_status rvx_edge_attention_forward_exchange(const rvx_edge_attention* a, cons
         // owned rows of T = x W_node^T into the whole table, every rank's rows to
         // every peer, then the per-edge scores/softmax/aggregate on owned rows
         // (queries T[o..o+n), keys = values = all of T by global column id)
+        // (the transform in row chunks, each chunk's rows exchanged while the
+        // next chunk transforms: produce_and_exchange)
         float* t = scratch_f32("efa_t", N * D);
-        transform(a, x_full->mem.as<float>() + o * nd, g->n, t + o * D, "efa_transform");
-        if (world > 1) {
-            ProfScope ps("efa_halo_exchange");
-            for (const ExchangeRound& r : exchange_plan(PLAN_WHOLE, offsets, world))
-                comm_exchange_rows(comm, t, D, r.r0.data(), r.rows.data(), stream());
-        }
+        const float* xf = x_full->mem.as<float>();
+        produce_and_exchange(comm, offsets, {{t, D}}, [&](int64_t r0, int64_t rows) {
+            transform(a, xf + r0 * nd, rows, t + r0 * D, "efa_transform");
+        });
         run_efa(a, g->n, g->row_ptr, g->col, g->e, t + o * D, N, t, t, ef ? ef->mem.as<float>() : nullptr,
                 y_full->mem.as<float>() + o * od);
     });

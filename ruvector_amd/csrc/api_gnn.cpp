@@ -626,20 +626,19 @@ rvx_status rvx_gnn_forward_exchange(const rvx_layer* l, const rvx_graph* g, cons
         RVX_REQUIRE(y_full->mem.bytes >= N * H * 4, RVX_ERR_DIMENSION_MISMATCH, "y_full smaller than N*hidden_dim");
         ComputeLock cl;
         // phase 1 on the owned rows, straight into the whole-table M (and,
-        // unfolded, K|V), then every rank's rows to every peer (one grouped p2p
-        // round per table on the library stream), then phase 2 on owned rows.
-        // Folded (RVX_GNN_FOLD=1/2) only M travels: H columns per row, not 3H.
+        // unfolded, K|V), every rank's rows to every peer, then phase 2 on owned
+        // rows. Folded (RVX_GNN_FOLD=1/2) only M travels: H columns per row, not 3H.
+        // Phase 1 runs in row chunks; each chunk's rows travel on the transfer
+        // stream while the next chunk's GEMMs run (produce_and_exchange).
         const bool fold = use_fold(l, world > 1);
         float* M = scratch_f32("rvl_m", N * H);
         float* KV = fold ? nullptr : scratch_f32("rvl_kv", N * 2 * H);
-        phase1_dev(l, g->n, x_full->mem.as<float>() + o * l->in, M + o * H, KV ? KV + o * 2 * H : nullptr);
-        if (world > 1) {
-            ProfScope ps("gnn_halo_exchange");
-            for (const ExchangeRound& r : exchange_plan(PLAN_WHOLE, offsets, world)) {
-                comm_exchange_rows(comm, M, H, r.r0.data(), r.rows.data(), stream());
-                if (KV) comm_exchange_rows(comm, KV, 2 * H, r.r0.data(), r.rows.data(), stream());
-            }
-        }
+        std::vector<TableRef> tables{{M, H}};
+        if (KV) tables.push_back({KV, 2 * H});
+        const float* x = x_full->mem.as<float>();
+        produce_and_exchange(comm, offsets, tables, [&](int64_t r0, int64_t rows) {
+            phase1_dev(l, rows, x + r0 * l->in, M + r0 * H, KV ? KV + r0 * 2 * H : nullptr);
+        });
         phase2_dev(l, g->n, g->row_ptr, g->col, g->max_deg, g->w, 1, M, KV, o, y_full->mem.as<float>() + o * H);
     });
 }

@@ -82,6 +82,31 @@ std::vector<ExchangeRound> exchange_plan(int kind, const int64_t* offsets, int w
     return plan;
 }
 
+void produce_and_exchange(rvx_comm* comm, const int64_t* offsets, const std::vector<TableRef>& tables,
+                          const std::function<void(int64_t r0, int64_t rows)>& produce) {
+    const int world = comm_size(comm), me = comm_rank(comm);
+    if (world <= 1) {
+        produce(offsets[me], offsets[me + 1] - offsets[me]);
+        return;
+    }
+    const std::vector<ExchangeRound> plan = exchange_plan(PLAN_SAGE, offsets, world);
+    const int rounds = (int)plan.size();
+    Device& d = device();
+    hipEvent_t* ev = pipeline_events(rounds + 1);
+    RVX_HIP(hipEventRecord(ev[rounds], d.stream));  // the transfer stream may not write rows still being read
+    RVX_HIP(hipStreamWaitEvent(d.xfer, ev[rounds], 0));
+    for (int c = 0; c < rounds; ++c) {
+        if (plan[c].rows[me] > 0) produce(plan[c].r0[me], plan[c].rows[me]);
+        RVX_HIP(hipEventRecord(ev[c], d.stream));
+        RVX_HIP(hipStreamWaitEvent(d.xfer, ev[c], 0));
+        StreamScope on_xfer(d.xfer);
+        ProfScope ps("halo_exchange");
+        for (const TableRef& t : tables) comm_exchange_rows(comm, t.first, t.second, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
+    }
+    RVX_HIP(hipEventRecord(ev[rounds], d.xfer));
+    RVX_HIP(hipStreamWaitEvent(d.stream, ev[rounds], 0));
+}
+
 namespace {
 
 // Finish a graph once row_ptr/col are on the device and a host row_ptr is known.

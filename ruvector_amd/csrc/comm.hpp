@@ -1,5 +1,7 @@
 // comm.hpp — internal RCCL helpers shared by the layer drivers.
 #pragma once
+#include <functional>
+#include <utility>
 #include <vector>
 
 #include "common.hpp"
@@ -28,5 +30,16 @@ std::vector<ExchangeRound> exchange_plan(int kind, const int64_t* offsets, int w
 // Row chunks of a GraphSAGE layer pipeline over n rows (same on every rank).
 int sage_chunks_for(int64_t n);
 int64_t chunk_step(int64_t n, int chunks);
+
+// Produce-then-exchange in row chunks (SURVEY.md §8e "chunked all-gather
+// pipelined with compute"): for each round c of exchange_plan(PLAN_SAGE),
+// produce(r0, rows) queues this rank's rows [r0, r0 + rows) (global ids, may be
+// empty) of every table on the library stream; the round's rows of every
+// (table, row_elems) then move to and from every peer on the transfer stream
+// while round c+1 computes. Returns with the library stream ordered after the
+// last round. World 1: one produce over the rank's rows, no exchange.
+using TableRef = std::pair<float*, int64_t>;
+void produce_and_exchange(rvx_comm* comm, const int64_t* offsets, const std::vector<TableRef>& tables,
+                          const std::function<void(int64_t r0, int64_t rows)>& produce);
 
 }  // namespace rvx
