@@ -229,22 +229,37 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
     if (chunks <= 0) chunks = sage_chunks_for(n);
     const int64_t step = chunk_step(n, chunks);
     Device& d = device();
-    hipEvent_t* ev = pipeline_events(chunks + 1);
+    hipEvent_t* ev = pipeline_events(chunks + 2);
+    // RVX_SAGE_CU_SPLIT (experiment, read per call): the GEMM and the gather on
+    // two streams owning disjoint CU halves instead of sharing every CU
+    const int split = chunks > 1 ? env_int("RVX_SAGE_CU_SPLIT", 0) : 0;
+    hipStream_t main_s = d.stream, gath_s = d.aux;
+    int main_cus = 0, gath_cus = 0;
+    if (split > 0) {
+        hipStream_t ss[2];
+        int cc[2];
+        cu_split_streams(split, ss, cc);
+        main_s = ss[0]; gath_s = ss[1]; main_cus = cc[0]; gath_cus = cc[1];
+    }
     if (chunks > 1) {
         RVX_HIP(hipEventRecord(ev[chunks], d.stream));  // aux may not overwrite agg before earlier work is done
-        RVX_HIP(hipStreamWaitEvent(d.aux, ev[chunks], 0));
+        RVX_HIP(hipStreamWaitEvent(gath_s, ev[chunks], 0));
+        if (main_s != d.stream) RVX_HIP(hipStreamWaitEvent(main_s, ev[chunks], 0));
     }
+    StreamScope on_main(main_s);
+    CuScope main_cu(main_cus);
     int c = 0;
     for (int64_t r0 = 0; r0 < n; r0 += step, ++c) {
         const int64_t rows = std::min(step, n - r0);
         if (chunks > 1) {
-            StreamScope on_aux(d.aux);
+            StreamScope on_aux(gath_s);
+            CuScope aux_cu(gath_cus);
             aggregate_rows(g->row_ptr + r0, g->col, nullptr, rows, x, l->in, a, /*empty_fill zeros*/ 0, 0,
                            h2p ? nullptr : agg + r0 * l->in, "sage_aggregate", /*overlapped*/ true,
                            x + (row_offset + r0) * l->in, h2 ? scale + r0 : nullptr,
                            h2p ? aplanes + r0 * 2 * l->in : nullptr, a_plane);
-            RVX_HIP(hipEventRecord(ev[c], d.aux));
-            RVX_HIP(hipStreamWaitEvent(d.stream, ev[c], 0));
+            RVX_HIP(hipEventRecord(ev[c], gath_s));
+            RVX_HIP(hipStreamWaitEvent(main_s, ev[c], 0));
         } else {
             aggregate_rows(g->row_ptr, g->col, nullptr, n, x, l->in, a, 0, 0, agg, "sage_aggregate", false,
                            x + row_offset * l->in, scale, aplanes, a_plane);
@@ -271,6 +286,10 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         if (hook) hook(c, r0, rows);
     }
     for (; hook && c < chunks; ++c) hook(c, n, 0);
+    if (main_s != d.stream) {
+        RVX_HIP(hipEventRecord(ev[chunks + 1], main_s));
+        RVX_HIP(hipStreamWaitEvent(d.stream, ev[chunks + 1], 0));
+    }
 }
 
 __global__ void k_gcn_isolated(const int32_t* iso, int64_t n_iso, const float* x, int dim, float* y) {
@@ -495,9 +514,9 @@ rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g
         const std::vector<ExchangeRound> plan = exchange_plan(PLAN_SAGE, offsets, world);
         const int chunks = (int)plan.size();
         Device& d = device();
-        hipEvent_t* ev = pipeline_events(2 * chunks + 2) + chunks + 1;
+        hipEvent_t* ev = pipeline_events(2 * chunks + 3) + chunks + 2;  // after sage_forward_dev's chunks + 2
         auto hook = [&](int c, int64_t, int64_t) {
-            RVX_HIP(hipEventRecord(ev[c], d.stream));
+            RVX_HIP(hipEventRecord(ev[c], stream()));  // chunk c's rows are complete on the pipeline's main stream
             RVX_HIP(hipStreamWaitEvent(d.xfer, ev[c], 0));
             StreamScope on_xfer(d.xfer);
             ProfScope ps("halo_exchange");

@@ -67,6 +67,9 @@ struct Device {
     hipStream_t aux = nullptr;     // ... except pipelined stages overlapped on this one
     hipStream_t xfer = nullptr;    // RCCL halo exchange overlapped with compute
     std::vector<hipEvent_t> pipe_events;  // timing-free events for stream hand-offs
+    // CU-partitioned stream pair (cu_split_streams): [0] the MFMA side, [1] the gather side
+    hipStream_t cu_split[2] = {nullptr, nullptr};
+    int cu_split_mode = 0, cu_split_count[2] = {0, 0};
     int num_cus = 0;
     int64_t hbm_bytes = 0;
     std::string arch;
@@ -83,6 +86,20 @@ inline int env_int(const char* name, int dflt) {
     const char* v = std::getenv(name);
     return (v && *v) ? std::atoi(v) : dflt;
 }
+
+// Two streams whose queues own complementary CU sets (hipExtStreamCreateWithCUMask),
+// for overlapping an MFMA-bound and an HBM-bound stage without sharing CUs.
+// mode 1: mask bit i to the MFMA side iff (i >> 3) & 1 == 0; mode 2: iff i & 1 == 0
+// (both give each side half the CUs; which half of an XCD depends on how the
+// queue maps mask bits to XCDs). Created once per mode; counts[] = CUs per side.
+void cu_split_streams(int mode, hipStream_t out[2], int counts[2]);
+// CUs the current launches may occupy: num_cus, or a CuScope's count.
+int active_cus();
+struct CuScope {
+    int prev;
+    explicit CuScope(int cus);
+    ~CuScope();
+};
 
 // Route this thread's launches to `s` for the scope's lifetime (pipelining).
 struct StreamScope {

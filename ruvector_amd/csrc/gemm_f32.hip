@@ -1353,7 +1353,7 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
     // with one block per tile (C4 layer GEMMs), so that stays the default.
     const int cap = persist >= 0 ? persist : env_int("RVX_GEMM_CAP", 0);
     int64_t grid = g.nblocks;
-    if (cap > 0) grid = std::min<int64_t>(grid, ((int64_t)cap * device().num_cus + 7) / 8 * 8);
+    if (cap > 0) grid = std::min<int64_t>(grid, ((int64_t)cap * active_cus() + 7) / 8 * 8);
     if (grid < g.nblocks && grid % 8 == 0 && env_int("RVX_GEMM_QUEUE", 1)) {
         g.queue = (unsigned*)scratch_bytes("gemm_h2_queue", 8 * 32 * 4);
         RVX_HIP(hipMemsetAsync(g.queue, 0, 8 * 32 * 4, stream()));

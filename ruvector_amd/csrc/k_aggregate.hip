@@ -215,7 +215,7 @@ void launch_agg(const char* t, const int64_t* rp, const int32_t* col, const floa
                 int empty_fill, int post_scale, float* out, int cap_per_cu, bool deep, bool nt, const float* self_x,
                 float* row_scale, _Float16* planes, int64_t pstride) {
     int64_t blocks = (n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
-    if (cap_per_cu > 0) blocks = std::min<int64_t>(blocks, (int64_t)cap_per_cu * device().num_cus);
+    if (cap_per_cu > 0) blocks = std::min<int64_t>(blocks, (int64_t)cap_per_cu * active_cus());
     const dim3 grid((unsigned)blocks), block(256);
     const bool vec = (dim % 4 == 0) && (((uintptr_t)x & 15) == 0) && (((uintptr_t)out & 15) == 0);
     RVX_REQUIRE(!planes || (vec && row_scale && self_x && empty_fill == 0), RVX_ERR_INVALID_SHAPE,

@@ -4,6 +4,8 @@
 #include <mutex>
 #include <unordered_map>
 
+#include <vector>
+
 #include "common.hpp"
 
 namespace rvx {
@@ -62,6 +64,34 @@ hipEvent_t* pipeline_events(int count) {
     }
     return d.pipe_events.data();
 }
+static thread_local int g_cu_override = 0;
+int active_cus() { return g_cu_override > 0 ? g_cu_override : device().num_cus; }
+CuScope::CuScope(int cus) : prev(g_cu_override) { g_cu_override = cus; }
+CuScope::~CuScope() { g_cu_override = prev; }
+
+void cu_split_streams(int mode, hipStream_t out[2], int counts[2]) {
+    Device& d = device();
+    if (d.cu_split_mode != mode) {
+        for (auto& st : d.cu_split)
+            if (st) { RVX_HIP(hipStreamSynchronize(st)); RVX_HIP(hipStreamDestroy(st)); st = nullptr; }
+        const int n = d.num_cus;
+        std::vector<uint32_t> m[2];
+        for (auto& v : m) v.assign((size_t)(n + 31) / 32, 0u);
+        int cnt[2] = {0, 0};
+        for (int i = 0; i < n; ++i) {
+            const int side = mode == 2 ? (i & 1) : ((i >> 3) & 1);
+            m[side][(size_t)i / 32] |= 1u << (i % 32);
+            ++cnt[side];
+        }
+        for (int k = 0; k < 2; ++k) {
+            RVX_HIP(hipExtStreamCreateWithCUMask(&d.cu_split[k], (uint32_t)m[k].size(), m[k].data()));
+            d.cu_split_count[k] = cnt[k];
+        }
+        d.cu_split_mode = mode;
+    }
+    for (int k = 0; k < 2; ++k) { out[k] = d.cu_split[k]; counts[k] = d.cu_split_count[k]; }
+}
+
 StreamScope::StreamScope(hipStream_t s) : prev(g_stream_override) { g_stream_override = s; }
 StreamScope::~StreamScope() { g_stream_override = prev; }
 
