@@ -163,10 +163,12 @@ def _hnsw_pair(n, d, metric, m, efc, seed):
     return x, h, g, idx
 
 
+@pytest.mark.parametrize("bitmap", ["1", "0"])  # visited set: per-query bitmap (small tables) or the tagged hash
 @pytest.mark.parametrize("short", ["1", "0"])  # d <= 256 kernel (4-float4 batches, 4 waves/SIMD) or the default
 @pytest.mark.parametrize("metric", ["l2", "cosine"])
-def test_hnsw_search_bit_exact_on_same_graph(monkeypatch, metric, short):
+def test_hnsw_search_bit_exact_on_same_graph(monkeypatch, metric, short, bitmap):
     monkeypatch.setenv("RVX_HNSW_SHORT", short)
+    monkeypatch.setenv("RVX_HNSW_BITMAP", bitmap)
     x, h, g, idx = _hnsw_pair(4000, 48, metric, 16, 100, 5)
     q = O.fill_uniform(200 * 48, 6).reshape(200, 48)
     for k, ef in ((10, 10), (10, 50), (1, 100), (32, 200)):
