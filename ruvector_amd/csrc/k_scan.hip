@@ -376,13 +376,27 @@ struct FilterArgs {
     float* part_v; int32_t* part_r;  // [nq][nsplit_total][FKP]
 };
 
+// The filter ranks by v = C_row + (acc * R_row) * Q_query, one multiply and one
+// FMA per (row, query) value (acc * R and the product with Q only move powers of
+// two for L2 / dot, so the only rounding is the FMA's):
+//   L2      R = 1/t_x, C = |x|^2, Q = -2/t_q      v = |x|^2 - 2 x.q (|q|^2 left out:
+//           a per-query shift, so lists, thresholds and the rerank's D = v_k + 2 eps
+//           stay consistent in the shifted units)
+//   dot     R = 1/t_x, C = 0,     Q = -1/t_q      v = -x.q
+//   cosine  R = 1/(t_x |x|), C = 1, Q = -1/(t_q |q|)   v = 1 - x.q/(|x||q|); a norm
+//           <= 1e-8 zeroes its factor (v = 1, distance.rs:58-62)
+// A deleted row (1/t_x = NaN) and a padding query (1/t_q = NaN) give v = NaN.
 template <int METRIC>
-__device__ __forceinline__ float approx_value(float acc, float xi, float qi, float xs, float qs, float xn, float qn) {
-    const float dot = (acc * xi) * qi;  // undo the power-of-two scales (exact)
-    if (METRIC == RVX_METRIC_L2) return (xs + qs) - 2.0f * dot;
-    if (METRIC == RVX_METRIC_DOT) return -dot;
-    // a degenerate norm gives 1; the 0 * dot keeps an invalid row's / padding query's NaN
-    return (qn > 1e-8f && xn > 1e-8f) ? 1.0f - dot / (qn * xn) : 1.0f + 0.0f * dot;
+__device__ __forceinline__ float2 row_factors(float2 pre) {  // {R, C} from {1/t_x, |x|^2 or |x|}
+    if (METRIC == RVX_METRIC_L2) return pre;
+    if (METRIC == RVX_METRIC_DOT) return make_float2(pre.x, 0.0f);
+    return make_float2(pre.y > 1e-8f ? pre.x / pre.y : 0.0f * pre.x, 1.0f);
+}
+template <int METRIC>
+__device__ __forceinline__ float query_factor(float qinv, float qn) {
+    if (METRIC == RVX_METRIC_L2) return -2.0f * qinv;
+    if (METRIC == RVX_METRIC_DOT) return -qinv;
+    return qn > 1e-8f ? -(qinv / qn) : 0.0f * qinv;
 }
 
 __device__ __forceinline__ bool lt_vr(float v, int r, float bv, int br) { return v < bv || (v == bv && r < br); }
@@ -417,7 +431,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     if (tid < FQ) { cand_n[tid] = 0; thr[tid] = INFINITY; fillc[tid] = 0; }
     if (tid < 2) ovf[tid] = 0;
 
-    float qi_[2], qs_[2], qn_[2];
+    float qf_[2];  // query factor Q
     bool qv_[2];
 #pragma unroll
     for (int fn = 0; fn < 2; ++fn) {
@@ -425,9 +439,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
         qv_[fn] = qg < a.nq;
         const int64_t qc = min(qg, a.nq - 1);
         const float2 c = a.qc[qc];
-        qi_[fn] = qv_[fn] ? c.x : __builtin_nanf("");  // padding query: every v is NaN
-        qs_[fn] = (METRIC == RVX_METRIC_L2) ? c.y : 0.0f;
-        qn_[fn] = (METRIC == RVX_METRIC_COSINE) ? c.y : 0.0f;
+        qf_[fn] = query_factor<METRIC>(qv_[fn] ? c.x : __builtin_nanf(""), c.y);  // padding query: NaN
     }
 
     // LDS-DMA fill: 1 KB pieces of 16 rows x 64 B; lane -> (row, 16-B chunk)
@@ -495,32 +507,38 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
     // Tile epilogue. The accumulators are overwritten in place by the
-    // approximate values (INF for rows past the split, deleted rows and padding
-    // queries); every value below its query's list threshold is offered, and an
-    // offered or rejected value becomes INF. Slots per query per round are
-    // bounded (FCB), so rounds repeat with the tightened thresholds until no
-    // offer overflowed (thresholds only fall, so a rejection is final).
-    // Invalid rows (past the split, deleted: 1/scale = NaN) and padding queries
-    // (qi_ = NaN) give v = NaN, which no threshold test admits. A value is
-    // tested with one compare whose lane mask is the uniform branch condition,
-    // so the common case (no lane below its threshold) costs the compare and a
-    // scalar branch; offered values are marked in a per-lane bit mask (rounds
-    // repeat while some query's candidate slots overflowed), rejected ones need
-    // no mark (thresholds only fall, so a rejection is final).
+    // approximate values v; invalid rows (past the split, deleted: 1/scale =
+    // NaN) and padding queries (Q = NaN) give v = NaN, which no threshold test
+    // admits. When no value of the tile is below its query's list threshold
+    // (the common case once the lists are full) the tile costs its values, a
+    // running min and one block-wide vote. Otherwise every value below the
+    // threshold is offered: one compare whose lane mask is the uniform branch
+    // condition; offered values are marked in a per-lane bit mask; slots per
+    // query per round are bounded (FCB), so rounds repeat with the tightened
+    // thresholds until no offer overflowed (thresholds only fall, so a
+    // rejection is final and needs no mark).
     auto epilogue = [&](int64_t rt, float2 pre) {
-        if (tid < FR) rowc[tid] = pre;
+        if (tid < FR) rowc[tid] = row_factors<METRIC>(pre);
         __syncthreads();
+        float vmin[2] = {INFINITY, INFINITY};
 #pragma unroll
         for (int fm = 0; fm < F_FM; ++fm)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const float2 c = rowc[wm * WROWS + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh];
-                const float xs = (METRIC == RVX_METRIC_L2) ? c.y : 0.0f;
-                const float xn = (METRIC == RVX_METRIC_COSINE) ? c.y : 0.0f;
 #pragma unroll
-                for (int fn = 0; fn < 2; ++fn)
-                    acc[fm][fn][e] = approx_value<METRIC>(acc[fm][fn][e], c.x, qi_[fn], xs, qs_[fn], xn, qn_[fn]);
+                for (int fn = 0; fn < 2; ++fn) {
+                    const float v = __builtin_fmaf(acc[fm][fn][e] * c.x, qf_[fn], c.y);
+                    acc[fm][fn][e] = v;
+                    vmin[fn] = fminf(vmin[fn], v);  // NaN-ignoring: an all-NaN lane stays NaN
+                }
             }
+        // Fast path: no value of the tile is below its query's threshold (every
+        // tile once the lists have warmed up) -> one compare per query, no offers.
+        bool any = false;
+#pragma unroll
+        for (int fn = 0; fn < 2; ++fn) any = any || vmin[fn] < thr[wn * 64 + fn * 32 + lr];
+        if (!__syncthreads_or(any)) return;
         static_assert(F_FM * 16 <= 64, "offered-value mask holds one bit per (fm, e)");
         uint64_t offered[2] = {0ull, 0ull};  // per fn: values already handed to the list
         for (int round = 0;; ++round) {
@@ -590,21 +608,46 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     for (int f = 0; f < F_NSTAGE - 1; ++f)
         if (f < iters) fill(f < nk ? cur_src : tile_src(r_beg + (f / nk) * FR), (f % nk) * FK, fsm + f * F_STAGE);
 
-    // one k-step: global step it, ring stage st (fill stage fst = st - 1 mod F_NSTAGE)
+    // One k-step: global step it, ring stage st. Every step issues one DMA group
+    // (k-step it + F_NSTAGE - 1 into the stage read in step it - 1; the last
+    // F_NSTAGE - 1 steps re-read the tile's first k-slice into a stage nobody
+    // reads again), so the groups in flight beyond the one a step waits for are
+    // a per-block constant. The group's four 1-KiB pieces are issued between
+    // the step's first MFMAs rather than ahead of them: both waves of a SIMD
+    // leave the barrier together, and a piece issued beside a running MFMA
+    // overlaps it instead of idling the matrix core.
+    const int64_t later_c = min((int64_t)F_NSTAGE - 2, iters - 1);
     auto kstep = [&](int64_t it, int64_t rt, int kt, int st) {
-        const int64_t later = min((int64_t)F_NSTAGE - 2, iters - it - 1);
-        if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        if (later_c >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (later_c == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (it + F_NSTAGE - 1 < iters) {  // the stage read in step it-1: every wave is past that read
-            const int fk = kt + F_NSTAGE - 1;
-            const int fst = st == 0 ? F_NSTAGE - 1 : st - 1;
-            if (fk < nk) fill(cur_src, fk * FK, fsm + fst * F_STAGE);
-            else if (fk < 2 * nk) fill(nxt_src, (fk - nk) * FK, fsm + fst * F_STAGE);
-            else fill(tile_src(rt + (fk / nk) * FR), (fk % nk) * FK, fsm + fst * F_STAGE);  // d < 64
+        const int fk = kt + F_NSTAGE - 1;
+        const int fst = st == 0 ? F_NSTAGE - 1 : st - 1;
+        TileSrc fs = cur_src;
+        int fk0 = 0;
+        if (it + F_NSTAGE - 1 < iters) {
+            if (fk < nk) fk0 = fk * FK;
+            else if (fk < 2 * nk) { fs = nxt_src; fk0 = (fk - nk) * FK; }
+            else { fs = tile_src(rt + (fk / nk) * FR); fk0 = (fk % nk) * FK; }  // d < 64
         }
+        unsigned char* fdst = fsm + fst * F_STAGE;
+        auto piece = [&](int j) {  // j: 0 rows/0, 1 queries/0, 2 rows/1, 3 queries/1
+            const int h = j >> 1;
+#ifdef RVX_ABLATE_DMA
+            return;
+#endif
+            if (j & 1)
+                __builtin_amdgcn_global_load_lds((const void*)(qbase + fk0 * 2 + qoff[h]),
+                                                 (__attribute__((address_space(3))) void*)(fdst + FR * 64 +
+                                                                                          (2 * wave + h) * 1024),
+                                                 16, 0, 0);
+            else
+                __builtin_amdgcn_global_load_lds((const void*)(fs.base + fk0 * 2 + fs.off[h]),
+                                                 (__attribute__((address_space(3))) void*)(fdst + (2 * wave + h) * 1024),
+                                                 16, 0, 0);
+        };
         const unsigned char* cur = fsm + st * F_STAGE;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -618,8 +661,15 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
 #pragma unroll
             for (int fm = 0; fm < F_FM; ++fm)
 #pragma unroll
-                for (int fn = 0; fn < 2; ++fn)
+                for (int fn = 0; fn < 2; ++fn) {
                     acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
+                    const int m = 2 * fm + fn;  // piece j follows MFMA j * F_FM / 2 of the step
+                    if (ks == 0 && m % (F_FM / 2) == 0 && m / (F_FM / 2) < 4) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        piece(m / (F_FM / 2));
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
         }
     };
 
