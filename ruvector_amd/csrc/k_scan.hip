@@ -374,7 +374,36 @@ struct FilterArgs {
     int64_t nq, row0, row_end; int d;
     int64_t rows_per_split; int split0, qtiles, nsplit_total;
     float* part_v; int32_t* part_r;  // [nq][nsplit_total][FKP]
+    // shared rejection bound per query (order-encoded float, see below), the
+    // result count k and max_x |x|^2 over ALL rows (for eps, as the rerank)
+    unsigned* gbound; int k; const unsigned* xsq_max_bits;
 };
+
+// Order-preserving float <-> uint (atomicMin over possibly negative values).
+__device__ __forceinline__ unsigned ord_enc(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord_dec(unsigned u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+// Smallest float above f (f itself for +INF / NaN): v < next_up(B) <=> v <= B.
+__device__ __forceinline__ float next_up(float f) {
+    if (!(f < INFINITY)) return f;
+    if (f == 0.0f) return __uint_as_float(1u);
+    const unsigned u = __float_as_uint(f);
+    return __uint_as_float((u & 0x80000000u) ? u - 1u : u + 1u);
+}
+
+// eps_q: bound on |v - reference value| for every row (f16 rounding 2^-11 per
+// operand, f32 accumulation, the reference's own f32 sum; 2x slack), shared by
+// the filter's rejection bound and the rerank so both compute the same bits.
+template <int METRIC>
+__device__ __forceinline__ float filter_eps(float qs, float xs_max) {
+    if (METRIC == RVX_METRIC_COSINE) return 0x1p-8f + 0x1p-12f;
+    const float qx = sqrtf(qs) * sqrtf(xs_max);
+    return (METRIC == RVX_METRIC_L2) ? 0x1p-8f * qx + 0x1p-12f * (qs + xs_max) : (0x1p-8f + 0x1p-12f) * qx;
+}
 
 // The filter ranks by v = C_row + (acc * R_row) * Q_query, one multiply and one
 // FMA per (row, query) value (acc * R and the product with Q only move powers of
@@ -440,6 +469,19 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
         const int64_t qc = min(qg, a.nq - 1);
         const float2 c = a.qc[qc];
         qf_[fn] = query_factor<METRIC>(qv_[fn] ? c.x : __builtin_nanf(""), c.y);  // padding query: NaN
+    }
+    // Shared rejection bound (lanes tid < FQ, one query each). A split's list
+    // holding k entries proves v_k <= its k-th value, so B_q = min over splits
+    // of (k-th value + 2 eps_q) is >= the rerank's D = v_k + 2 eps_q (same
+    // arithmetic, rounding is monotone): a value above B_q is never a
+    // candidate. Blocks publish with atomicMin and re-read B_q once per tile,
+    // so every split stops admitting what the others have already beaten.
+    const int64_t gq_idx = min<int64_t>(q0 + tid, a.nq - 1);
+    const bool gq_own = tid < FQ && q0 + tid < a.nq;
+    float geps = 0.0f, gb = INFINITY;
+    if (gq_own) {
+        geps = filter_eps<METRIC>(a.qc[gq_idx].y, __uint_as_float(*a.xsq_max_bits));
+        gb = ord_dec(__hip_atomic_load(a.gbound + gq_idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     }
 
     // LDS-DMA fill: 1 KB pieces of 16 rows x 64 B; lane -> (row, 16-B chunk)
@@ -518,6 +560,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     // thresholds until no offer overflowed (thresholds only fall, so a
     // rejection is final and needs no mark).
     auto epilogue = [&](int64_t rt, float2 pre) {
+        if (tid < FQ) thr[tid] = fminf(thr[tid], next_up(gb));  // admit v <= B_q
         if (tid < FR) rowc[tid] = row_factors<METRIC>(pre);
         __syncthreads();
         float vmin[2] = {INFINITY, INFINITY};
@@ -585,7 +628,14 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
                 }
                 fillc[ql] = fill_n;
                 cand_n[ql] = 0;
-                thr[ql] = fill_n == FKP ? bv[FKP - 1] : INFINITY;
+                if (gq_own && fill_n >= a.k) {
+                    const float ub = bv[a.k - 1] + 2.0f * geps;
+                    if (ub < gb) {
+                        gb = ub;
+                        atomicMin(a.gbound + gq_idx, ord_enc(ub));
+                    }
+                }
+                thr[ql] = fminf(fill_n == FKP ? bv[FKP - 1] : INFINITY, next_up(gb));
             }
             if (tid == 0) ovf[(round + 1) & 1] = 0;
             __syncthreads();
@@ -694,6 +744,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
         if (rt + FR >= r_end)
 #endif
         epilogue(rt, pre);
+        if (gq_own) gb = fminf(gb, ord_dec(__hip_atomic_load(a.gbound + gq_idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
 #pragma unroll
         for (int i = 0; i < F_FM; ++i)
 #pragma unroll
@@ -761,15 +812,7 @@ __global__ __launch_bounds__(256) void k_scan_rerank(RerankArgs a) {
         lrow = brr;
         vk = bv;
     }
-    float eps;
-    if (METRIC == RVX_METRIC_COSINE) {
-        eps = 0x1p-8f + 0x1p-12f;
-    } else {
-        const float xs_max = __uint_as_float(*a.xsq_max_bits);
-        const float qs = a.qc[qi].y;
-        const float qx = sqrtf(qs) * sqrtf(xs_max);
-        eps = (METRIC == RVX_METRIC_L2) ? 0x1p-8f * qx + 0x1p-12f * (qs + xs_max) : (0x1p-8f + 0x1p-12f) * qx;
-    }
+    const float eps = filter_eps<METRIC>(a.qc[qi].y, __uint_as_float(*a.xsq_max_bits));
     const float D = vk + 2.0f * eps;  // INF when fewer than k rows exist
     // a full list whose last entry is <= D may have dropped a needed row
     bool unsure = false;
@@ -878,6 +921,31 @@ __global__ __launch_bounds__(256) void k_rows_to_f16(const float* __restrict__ x
     }
 }
 
+// max over rows of sum x^2 (wave per row, any order), into max_sq_bits
+__global__ __launch_bounds__(256) void k_row_sq_max(const float* __restrict__ x, int64_t n, int d,
+                                                   unsigned* max_sq_bits) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    float run_max = 0.0f;
+    for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += nwaves) {
+        const float* xr = x + row * d;
+        float s = 0.0f;
+        for (int k = 4 * lane; k < d; k += 256) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + k);
+            s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        run_max = fmaxf(run_max, s);
+    }
+    if (lane == 0 && run_max > 0.0f) atomicMax(max_sq_bits, __float_as_uint(run_max));
+}
+
+void row_sq_max(const float* x, int64_t n, int d, unsigned* max_bits) {
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + 3) / 4, 4096));
+    RVX_LAUNCH("scan_f16", k_row_sq_max, dim3((unsigned)blocks), dim3(256), 0, x, n, d, max_bits);
+}
+
 void rows_to_f16(const float* x, int64_t n, int d, _Float16* xh, float2* rc, const float* cnorm,
                  const uint8_t* deleted, unsigned* max_bits, int32_t* bad) {
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + 3) / 4, 4096));
@@ -957,6 +1025,8 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     unsigned* max_bits = (unsigned*)(flags + 1);
     int32_t* unsure = flags + 4;
     RVX_HIP(hipMemsetAsync(flags, 0, (size_t)(16 + nq * 4), stream()));
+    unsigned* gbound = (unsigned*)scratch_bytes("mscan_gbound", nq * 4);
+    RVX_HIP(hipMemsetD32Async((hipDeviceptr_t)gbound, 0xFF800000u, (size_t)nq, stream()));  // ord_enc(+INF)
 
     static bool attr = false;
     if (!attr) {
@@ -969,12 +1039,15 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     }
     const bool cos = metric == RVX_METRIC_COSINE;
     rows_to_f16(q, nq, d, qh, qc, cos ? qnorm : nullptr, nullptr, nullptr, flags);
+    // the filter's shared bound needs eps from max |x|^2 over every row before
+    // the first chunk's filter (cosine: eps is a constant)
+    if (nchunks > 1 && !cos) row_sq_max(x, n, d, max_bits);
     for (int64_t c = 0; c < nchunks; ++c) {
         const int64_t c0 = c * chunk_rows, c1 = std::min(n, c0 + chunk_rows);
         rows_to_f16(x + c0 * d, c1 - c0, d, xh, xc, cos ? xnorm + c0 : nullptr, deleted ? deleted + c0 : nullptr,
                     max_bits, flags);
         FilterArgs fa{xh, xc, qh, qc, nq, c0, c1, d, rows_per_split, (int)(c * s_c), (int)qtiles, nsplit_total,
-                      part_v, part_r};
+                      part_v, part_r, gbound, k, max_bits};
         const dim3 grid((unsigned)(qtiles * s_c));
         const dim3 blk((unsigned)F_THREADS);
         if (wide) {
