@@ -442,7 +442,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     int32_t* cand_n = cand_r + FQ * FCB;                            // [FQ]
     float* thr = reinterpret_cast<float*>(cand_n + FQ);             // [FQ] list's FKP-th v (INF until full)
     int32_t* fillc = reinterpret_cast<int32_t*>(thr + FQ);          // [FQ]
-    int32_t* ovf = fillc + FQ;                                      // [2] candidate-slot overflow per round
+    int32_t* ovf = fillc + FQ;  // [0..1] candidate-slot overflow per round, [2..3] tile vote per tile parity
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
 
     for (int i = tid; i < FQ * FKP; i += F_THREADS) { best_v[i] = INFINITY; best_r[i] = -1; }
     if (tid < FQ) { cand_n[tid] = 0; thr[tid] = INFINITY; fillc[tid] = 0; }
-    if (tid < 2) ovf[tid] = 0;
+    if (tid < 4) ovf[tid] = 0;
 
     float qf_[2];  // query factor Q
     bool qv_[2];
@@ -526,18 +526,15 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
         }
     };
     constexpr int WROWS = 32 * F_FM;  // rows per wave
-    int a_rd[F_FM][2], b_rd[2][2];
+    // LDS read offsets of fragment 0 per k-half; the XOR swizzle depends on
+    // (row >> 2) & 3 = (lr >> 2) & 3 only (fragment rows differ by multiples of
+    // 32), so fragment f sits f * 2 KiB further: an immediate offset, not a VGPR
+    int a_rd[2], b_rd[2];
 #pragma unroll
-    for (int f = 0; f < F_FM; ++f) {
-        const int ra = wm * WROWS + f * 32 + lr;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) a_rd[f][ks] = ra * 64 + (((2 * ks + lh) ^ ((ra >> 2) & 3)) << 4);
-    }
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-        const int rb = wn * 64 + f * 32 + lr;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) b_rd[f][ks] = FR * 64 + rb * 64 + (((2 * ks + lh) ^ ((rb >> 2) & 3)) << 4);
+    for (int ks = 0; ks < 2; ++ks) {
+        const int sw = ((2 * ks + lh) ^ ((lr >> 2) & 3)) << 4;
+        a_rd[ks] = (wm * WROWS + lr) * 64 + sw;
+        b_rd[ks] = FR * 64 + (wn * 64 + lr) * 64 + sw;
     }
 
     f32x16 acc[F_FM][2];
@@ -581,7 +578,16 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
         bool any = false;
 #pragma unroll
         for (int fn = 0; fn < 2; ++fn) any = any || vmin[fn] < thr[wn * 64 + fn * 32 + lr];
-        if (!__syncthreads_or(any)) return;
+        // block vote: one flag per tile parity, one LDS barrier (no VMEM drain)
+        const int vp = 2 + (int)(((rt - r_beg) / FR) & 1);
+        if (__ballot(any) && lane == 0) ovf[vp] = 1;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const bool slow = ovf[vp] != 0;
+        if (tid == 0) ovf[vp ^ 1] = 0;  // every wave has read the other parity's flag (last tile)
+        if (!slow) return;
+#ifdef RVX_COUNT_SLOW
+        if (tid == 0) atomicAdd((unsigned*)a.xsq_max_bits + 2, 1u);
+#endif
         static_assert(F_FM * 16 <= 64, "offered-value mask holds one bit per (fm, e)");
         uint64_t offered[2] = {0ull, 0ull};  // per fn: values already handed to the list
         for (int round = 0;; ++round) {
@@ -589,6 +595,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
             for (int fn = 0; fn < 2; ++fn) {
                 const int ql = wn * 64 + fn * 32 + lr;
                 const float t = thr[ql];
+                if (!__ballot(vmin[fn] < t)) continue;  // none of the wave's 32 queries has a value below its threshold
 #pragma unroll
                 for (int fm = 0; fm < F_FM; ++fm)
 #pragma unroll
@@ -599,6 +606,9 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
                         if (!__ballot(pass)) continue;
                         if (!pass) continue;
                         const int slot = atomicAdd(&cand_n[ql], 1);
+#ifdef RVX_COUNT_SLOW
+                        atomicAdd((unsigned*)a.xsq_max_bits + 1, 1u);
+#endif
                         if (slot < FCB) {
                             cand_v[ql * FCB + slot] = v;
                             cand_r[ql * FCB + slot] =
@@ -704,10 +714,10 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
             h16x8 af[F_FM], bf[2];
 #pragma unroll
             for (int f = 0; f < F_FM; ++f)
-                af[f] = __builtin_bit_cast(h16x8, *reinterpret_cast<const u32x4*>(cur + a_rd[f][ks]));
+                af[f] = __builtin_bit_cast(h16x8, *reinterpret_cast<const u32x4*>(cur + a_rd[ks] + f * 2048));
 #pragma unroll
             for (int f = 0; f < 2; ++f)
-                bf[f] = __builtin_bit_cast(h16x8, *reinterpret_cast<const u32x4*>(cur + b_rd[f][ks]));
+                bf[f] = __builtin_bit_cast(h16x8, *reinterpret_cast<const u32x4*>(cur + b_rd[ks] + f * 2048));
 #pragma unroll
             for (int fm = 0; fm < F_FM; ++fm)
 #pragma unroll
@@ -1078,6 +1088,14 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     if (!hflags) RVX_HIP(hipHostMalloc((void**)&hflags, 16, hipHostMallocDefault));
     RVX_HIP(hipMemcpyAsync(hflags, flags, 16, hipMemcpyDeviceToHost, stream()));
     sync();
+#ifdef RVX_COUNT_SLOW
+    {
+        int32_t hf[4];
+        RVX_HIP(hipMemcpy(hf, flags, 16, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[scan] slow-path tiles %u offers %u (block-tiles %lld)\n", (unsigned)hf[3], (unsigned)hf[2],
+                (long long)(qtiles * ((n + FR - 1) / FR)));
+    }
+#endif
     if (hflags[0]) return false;  // unbounded inputs: the VALU scan owns the whole call
     std::vector<int32_t> redo;
     if (hflags[2] > 0) {
