@@ -145,3 +145,24 @@ def test_auto_mode_matches_valu_scan_at_768(monkeypatch, metric):
     vids, vdist = idx.brute_force_array(q, 10)
     assert rv.scan_last_stats()["valu"] == nq
     assert np.array_equal(ids, vids) and np.array_equal(dist, vdist)
+
+
+@pytest.mark.parametrize("metric,name", METRICS)
+def test_shared_bound_across_chunks_with_planted_ties(monkeypatch, metric, name):
+    """Splits share a per-query rejection bound (k-th listed value + 2 eps, min over
+    splits and chunks). Plant, in the LAST conversion chunk, exact copies of each
+    query's k-th nearest row from the first chunk: they tie with the k-th value and
+    must still reach the rerank after earlier chunks tightened the bound."""
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    monkeypatch.setenv("RVX_SCAN_MFMA_CHUNK_ROWS", "4096")
+    n, d, nq, k = 16384, 96, 260, 10
+    x = normal(n, d, 61)
+    q = normal(nq, d, 62)
+    first = x[:4096]
+    rids0, _ = O.flat_search(first, q[:64], k, name)
+    for i in range(64):  # one planted tie per query for the first 64 queries
+        x[n - 1 - i] = first[rids0[i, k - 1]]
+    ids, dist = flat(x, metric).brute_force_array(q, k)
+    assert rv.scan_last_stats()["mfma"] == nq
+    rids, rd = O.flat_search(x, q, k, name)
+    assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd)
