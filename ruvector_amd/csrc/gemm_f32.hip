@@ -53,6 +53,7 @@ struct GemmArgs {
     const _Float16* A0h; const _Float16* A1h; int64_t Ah_plane;
     // persistent split-f16 GEMM: per-XCD tile counters (stride 32 words), zeroed per launch
     unsigned* queue;
+    int xsplit;  // queue mode: XCD pair (2i, 2i+1) shares a row range, each XCD takes half the column tiles
 };
 
 __device__ __forceinline__ float epi_apply(int epi, float v) {
@@ -780,6 +781,11 @@ __device__ __forceinline__ int64_t xcd_first(int64_t nwg, int64_t xcd) {
     return xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
 }
 __device__ __forceinline__ int64_t xcd_count(int64_t nwg, int64_t xcd) { return nwg / 8 + (xcd < nwg % 8 ? 1 : 0); }
+__device__ __forceinline__ int64_t part_first(int64_t n, int64_t parts, int64_t i) {
+    const int64_t q = n / parts, r = n % parts;
+    return i < r ? i * (q + 1) : r * (q + 1) + (i - r) * q;
+}
+__device__ __forceinline__ int64_t part_count(int64_t n, int64_t parts, int64_t i) { return n / parts + (i < n % parts ? 1 : 0); }
 
 template <bool DUAL>
 __device__ __forceinline__ void h2g_tile(const GemmArgs& g, int epi, int64_t wgid) {
@@ -1152,13 +1158,19 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
     if (g.queue) {
         __shared__ int64_t s_t;
         const int64_t xcd = blockIdx.x % 8;
-        const int64_t first = xcd_first(g.nblocks, xcd), cnt = xcd_count(g.nblocks, xcd);
+        int64_t first = xcd_first(g.nblocks, xcd), cnt = xcd_count(g.nblocks, xcd);
+        const int half = g.xsplit ? g.tiles_n / 2 : 0;
+        if (half) {  // rows [first, first + cnt / half) of the pair's range, column tiles (xcd & 1) * half + [0, half)
+            const int64_t tm_tot = g.nblocks / g.tiles_n;
+            first = part_first(tm_tot, 4, xcd >> 1);
+            cnt = part_count(tm_tot, 4, xcd >> 1) * half;
+        }
         for (;;) {
             if (threadIdx.x == 0) s_t = (int64_t)atomicAdd(g.queue + 32 * xcd, 1u);
             __syncthreads();
             const int64_t t = s_t;
             if (t >= cnt) break;
-            h2g_tile<DUAL>(g, epi, first + t);
+            h2g_tile<DUAL>(g, epi, half ? (first + t / half) * g.tiles_n + (xcd & 1) * half + t % half : first + t);
             __syncthreads();  // LDS stages and s_t are reused by the next tile
         }
         return;
@@ -1357,6 +1369,10 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
     if (grid < g.nblocks && grid % 8 == 0 && env_int("RVX_GEMM_QUEUE", 1)) {
         g.queue = (unsigned*)scratch_bytes("gemm_h2_queue", 8 * 32 * 4);
         RVX_HIP(hipMemsetAsync(g.queue, 0, 8 * 32 * 4, stream()));
+        // XCD pairs split the column tiles: each L2 holds half of W's f16 planes
+        // (10M x 768 layer: GEMM fetch 10.5 -> 7.7 GB per launch, step time
+        // unchanged within noise, scripts/exp_xsplit.sh); RVX_GEMM_XSPLIT=0 restores
+        g.xsplit = (g.tiles_n % 2 == 0 && g.nblocks % g.tiles_n == 0) ? env_int("RVX_GEMM_XSPLIT", 1) : 0;
     }
     if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
     else RVX_LAUNCH(t, gemm_nt_h2g<false>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);

@@ -839,3 +839,29 @@ def test_poincare_distance_matrix():
     L.call("rvx_distance_matrix", L.METRIC_POINCARE, L.fptr(u), 20, L.fptr(v), 30, d, 1.0, L.fptr(out))
     ref = np.array([[O.poincare_distance(a, b) for b in v] for a in u], np.float32)
     assert_close(out, ref, 1e-5)
+
+
+@pytest.mark.parametrize("d", [256, 768])
+def test_graphsage_pipeline_xcd_split_tile_order(monkeypatch, d):
+    """The overlapped pipeline's persistent GEMM drains per-XCD tile queues; with
+    RVX_GEMM_XSPLIT (default) an XCD pair shares a row range and splits the column
+    tiles. Tile order must not change a bit of the output (2 and 6 column tiles)."""
+    n, deg = 400_000, 4
+    x = rv.Buffer(n * d * 4)
+    x.fill_uniform(n * d, 31, -1.0, 1.0)
+    g = rv.Graph.random(n, deg, 32)
+    layer = rv.GraphSAGELayer(d, d, num_samples=deg)
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("RVX_GEMM_XSPLIT", v)
+        y = rv.Buffer(n * d * 4)
+        layer.forward_device(x, g, y)
+        outs.append(y.download(np.float32, (n, d)))
+    assert np.array_equal(outs[0], outs[1])
+    xs = x.download(np.float32, (n, d))
+    rp, col = O.random_csr(n, deg, 32)
+    wn, ws = O.sage_init(d, d, 0), O.sage_init(d, d, 1000)
+    r0 = n - 700
+    ref = O.sage_forward(xs, rp, col, wn, ws, rows=(r0, 700))
+    dense = np.count_nonzero(ref, axis=1) >= d // 4
+    assert_close(outs[1][r0:][dense], ref[dense])
