@@ -319,10 +319,12 @@ size_t scan_lds_bytes(int k) {
 // few rows that can still be in the top-k:
 //   1. rows and queries are scaled by a power of two (exact) so the row max
 //      lands in [2^14, 2^15) and rounded to f16 (k_rows_to_f16);
-//   2. k_scan_filter: v_mfma_f32_32x32x16_f16 dot products over 128 rows x 128
-//      queries tiles, the approximate distance v (L2: |x|^2 + |q|^2 - 2 x.q
-//      in squared units; cosine / dot as the reference forms), and a running
-//      per-(query, row split) list of the FKP smallest v in LDS;
+//   2. k_scan_filter: v_mfma_f32_32x32x16_f16 dot products over 256 x 256 (or
+//      128 x 128) row x query tiles, the approximate value v (L2: |x|^2 - 2 x.q,
+//      squared units shifted by |q|^2; cosine / dot as the reference forms), a
+//      running per-(query, row split) list of the FKP smallest v in LDS, and a
+//      per-query bound shared by all splits (k-th listed value + 2 eps, min over
+//      splits) above which no value is admitted;
 //   3. k_scan_rerank (one wave per query): D = k-th smallest v + 2 eps_q, where
 //      eps_q bounds |v - reference value| for every row (f16 rounding 2^-11 per
 //      operand, f32 accumulation, the reference's own f32 sum; 2x slack). Every
