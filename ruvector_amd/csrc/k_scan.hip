@@ -481,6 +481,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     const int64_t gq_idx = min<int64_t>(q0 + tid, a.nq - 1);
     const bool gq_own = tid < FQ && q0 + tid < a.nq;
     float geps = 0.0f, gb = INFINITY;
+    unsigned graw = 0xFF800000u;  // last B_q read (ord_enc(+INF)); folded into gb at the next epilogue
     if (gq_own) {
         geps = filter_eps<METRIC>(a.qc[gq_idx].y, __uint_as_float(*a.xsq_max_bits));
         gb = ord_dec(__hip_atomic_load(a.gbound + gq_idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -559,6 +560,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     // thresholds until no offer overflowed (thresholds only fall, so a
     // rejection is final and needs no mark).
     auto epilogue = [&](int64_t rt, float2 pre) {
+        gb = fminf(gb, ord_dec(graw));  // read at the end of the last tile: its wait lands on the drain below
         if (tid < FQ) thr[tid] = fminf(thr[tid], next_up(gb));  // admit v <= B_q
         if (tid < FR) rowc[tid] = row_factors<METRIC>(pre);
         __syncthreads();
@@ -756,7 +758,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
         if (rt + FR >= r_end)
 #endif
         epilogue(rt, pre);
-        if (gq_own) gb = fminf(gb, ord_dec(__hip_atomic_load(a.gbound + gq_idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+        if (gq_own) graw = __hip_atomic_load(a.gbound + gq_idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int i = 0; i < F_FM; ++i)
 #pragma unroll
