@@ -211,7 +211,8 @@ def hnsw_leg(a, rank, world, comm):
     is a replica per GPU (search does not shard), built on the GPU; each rank
     answers its own 10k queries, so the job rate is the sum over ranks."""
     import bench_hnsw
-    res = bench_hnsw.run(100_000, 128, 10_000, 32, 200, [300, 400, 600, 800], 10, "l2",
+    # ef grid fine enough around the 0.95 crossing (C1: between ef 400 and 600)
+    res = bench_hnsw.run(100_000, 128, 10_000, 32, 200, [300, 400, 450, 500, 550, 600, 800], 10, "l2",
                          cpu=(rank == 0 and world == 1 and not a.no_cpu), log=lambda s: None)
     qps = res["qps_at_recall95"] or 0.0
     if comm is not None:
