@@ -577,8 +577,9 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
                     vmin[fn] = fminf(vmin[fn], v);  // NaN-ignoring: an all-NaN lane stays NaN
                 }
             }
-        // Fast path: no value of the tile is below its query's threshold (every
-        // tile once the lists have warmed up) -> one compare per query, no offers.
+        // Fast path: no value of the tile is below its query's threshold -> one
+        // compare per query, no offers (with 256 queries per tile most tiles still
+        // admit something).
         bool any = false;
 #pragma unroll
         for (int fn = 0; fn < 2; ++fn) any = any || vmin[fn] < thr[wn * 64 + fn * 32 + lr];
@@ -610,9 +611,6 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
                         if (!__ballot(pass)) continue;
                         if (!pass) continue;
                         const int slot = atomicAdd(&cand_n[ql], 1);
-#ifdef RVX_COUNT_SLOW
-                        atomicAdd((unsigned*)a.xsq_max_bits + 1, 1u);
-#endif
                         if (slot < FCB) {
                             cand_v[ql * FCB + slot] = v;
                             cand_r[ql * FCB + slot] =
@@ -1105,7 +1103,7 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     {
         int32_t hf[4];
         RVX_HIP(hipMemcpy(hf, flags, 16, hipMemcpyDeviceToHost));
-        fprintf(stderr, "[scan] slow-path tiles %u offers %u (block-tiles %lld)\n", (unsigned)hf[3], (unsigned)hf[2],
+        fprintf(stderr, "[scan] slow-path tiles %u (block-tiles %lld)\n", (unsigned)hf[3],
                 (long long)(qtiles * ((n + FR - 1) / FR)));
     }
 #endif
