@@ -622,7 +622,9 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
                     }
             }
             __syncthreads();
-            if (tid < FQ) {  // one lane per query: insertion into its sorted list
+            // one lane per query: insertion into its sorted list (a query with no
+            // offer this round keeps its list, threshold and published bound)
+            if (tid < FQ && cand_n[tid] != 0) {
                 const int ql = tid;
                 const int nc = min(cand_n[ql], FCB);
                 float* bv = best_v + ql * FKP;
