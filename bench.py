@@ -241,6 +241,21 @@ def scan_leg(a, x, n, d, rank, world, comm):
         qps = comm.allreduce([qps])[0]
     res["value"] = round(qps, 1)
     res["unit"] = "queries/s (recall@10 = 1.0, exact; replicas summed over GPUs)"
+    # HBM bytes per filter launch from the committed PMC passes of this workload
+    # (scripts/scan_traffic.sh -> profiles/pmc_traffic_scan.json), when they match
+    path = os.path.join(ROOT, "profiles", "pmc_traffic_scan.json")
+    rl = res.get("roofline")
+    if rl is not None and os.path.exists(path):
+        try:
+            pmc = json.load(open(path))
+        except ValueError:
+            pmc = {}
+        want = {"n": n, "d": d, "nq": 10_000, "k": 10, "metric": "l2",
+                "launches": res["mfma"]["kernel_ms"].get("launches", {}).get("scan_filter")}
+        ent = pmc.get("kernels", {}).get("scan_filter")
+        if ent and all((pmc.get("config") or {}).get(k) == v for k, v in want.items()):
+            rl["traffic"] = round(ent["hbm_bytes_per_launch"], 0)
+            rl["traffic_source"] = "rocprofv3 --pmc FETCH_SIZE(x2, gfx950) + WRITE_SIZE, profiles/pmc_traffic_scan.json"
     return res
 
 

@@ -22,6 +22,8 @@ TAGS = {  # kernel symbol substring -> bench tag
     "gemm_nt_h2g": "sage_gemm",
     "k_normalize_rows": "sage_normalize",
     "k_scan_topk": "scan_topk",
+    "k_scan_filter": "scan_filter",
+    "k_rows_to_f16": "scan_f16",
     "k_hnsw_search": "hnsw_search",
     "k_edge_attn": "gnn_edge_attention",
 }
