@@ -9,6 +9,18 @@ Ground truth: exact Poincaré scan (K8) on the GPU (bit-exact with the oracle's
 scan order). Reports build time, recall@10 / QPS over an ef sweep, QPS at
 recall >= 0.95, tangent-pruned search, and the oracle's CPU search on the same
 graph (bounded sample) with an id-equality check.
+
+--gpus N (one process per GPU, launched like bench.py by torch.distributed.run;
+RANK / WORLD_SIZE / LOCAL_RANK from the environment): the C5 configuration itself,
+node-range shards of --per-gpu points each (default 6.25M = 50M / 8; weak scaling,
+so N = 8 is the full 50M x 1024 corpus), every rank generating exactly its rows of
+the corpus on the GPU (rvx_fill_ball_rows). Each query batch runs
+ShardedHyperbolicHnsw::search across the GPUs (shard.rs:354-373;
+rvx_hyperbolic_sharded_search_device): rank 0's queries broadcast over RCCL, the
+local shard searched (exact Poincaré scan, tangent-pruned search, graph search),
+one all-gather of every rank's top-10 and the GPU merge. Ground truth = the exact
+mode (global exact top-10). Reports QPS per mode, recall@10 against the exact
+mode, the broadcast / all-gather / merge time, and the build time (max over ranks).
 """
 import argparse
 import json
@@ -38,6 +50,79 @@ def recall(gt, got):
     return float(np.mean([len(set(a.tolist()) & set(b.tolist())) / k for a, b in zip(gt, got)]))
 
 
+def main_sharded(a):
+    """C5 across GPUs: node-range shards + broadcast / all-gather / merge per query batch."""
+    import ruvector_amd as rv
+    from ruvector_amd.shard import REDUCE_MAX, RcclComm
+
+    import benchutil
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    rv.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    comm = RcclComm.from_env() if world > 1 else None
+    log = (lambda s: print(f"[rank {rank}] {s}", file=sys.stderr, flush=True))  # noqa: E731
+    n, d, nq, k = a.per_gpu, a.dim, a.queries, 10
+    r0 = rank * n
+
+    def barrier():
+        rv.synchronize()
+        if comm is not None:
+            comm.barrier()
+
+    def vmax(v):
+        return comm.allreduce([v], REDUCE_MAX)[0] if comm is not None else v
+
+    xb = rv.Buffer(n * d * 4)
+    xb.fill_ball(n, d, 7, r0)  # this rank's rows of the (world x n)-point corpus
+    qb = None
+    if rank == 0:
+        qb = rv.Buffer(nq * d * 4)
+        qb.fill_ball(nq, d, 8, 0)
+    h = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=7 + rank), dim=d)
+    barrier()
+    t0 = time.perf_counter()
+    with benchutil.heartbeat(f"building shard {rank}: {n} x {d}", log=log):
+        h.insert_device(xb, n, d)
+        rv.synchronize()
+    build_s = vmax(time.perf_counter() - t0)
+    del xb
+    t0 = time.perf_counter()
+    h.build_tangent_cache()
+    rv.synchronize()
+    cache_s = vmax(time.perf_counter() - t0)
+    grp = rv.ShardedHyperbolicSearch(h, comm, r0)
+    gid, dist = rv.Buffer(nq * k * 8), rv.Buffer(nq * k * 4)
+    modes = [("exact", 0), ("pruned", 0)] + [("search", int(e)) for e in a.ef.split(",")]
+    out_modes, gt = {}, None
+    prof = rv.Profiler()
+    for mode, ef in modes:
+        grp.search_device(qb, min(nq, 256), k, gid, dist, ef=ef, mode=mode)  # warm-up (scratch, code objects)
+        barrier()
+        with prof:
+            t0 = time.perf_counter()
+            with benchutil.heartbeat(f"{mode} ef={ef}", log=log):
+                grp.search_device(qb, nq, k, gid, dist, ef=ef, mode=mode)
+                barrier()
+            dt = vmax(time.perf_counter() - t0)
+        ids = gid.download(np.int64, (nq, k))
+        if mode == "exact":
+            gt = ids
+        phases = {t: round(prof.query(t)[0], 2) for t in ("shard_bcast", "shard_allgather", "shard_merge")}
+        key = mode if mode != "search" else f"search_ef{ef}"
+        out_modes[key] = {"qps": round(nq / dt, 1), "recall_at_10": round(recall(gt, ids), 4), "wall_ms": round(dt * 1e3, 1),
+                          "phase_ms_rank0": phases}
+        log(f"{key}: {out_modes[key]}")
+    if rank == 0:
+        total = world * n
+        print(json.dumps({
+            "metric": "C5 hyperbolic HNSW queries/s@recall, node-range sharded", "n_gpus": world,
+            "scaling": "weak", "config": {"workload": f"C5: {total} x {d} Poincaré ball (c=1), {world} node-range "
+                                                      f"shards of {n}, {nq} queries, k={k}, M=16 M0=32 ef_c=200"},
+            "build_s": round(build_s, 2), "tangent_cache_s": round(cache_s, 2), "modes": out_modes,
+            "ground_truth": "exact mode: global exact Poincaré top-10 over every shard",
+            "data": "synthetic (rvx_fill_ball_rows, seed 7 points / 8 queries)"}), flush=True)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--n", type=int, default=1_000_000)
@@ -46,7 +131,13 @@ def main():
     p.add_argument("--ef", default="50,100,200,400,800")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--gpus", type=int, default=0, help="node-range-sharded C5 across GPUs (see module doc)")
+    p.add_argument("--per-gpu", type=int, default=6_250_000, help="points per GPU shard with --gpus")
     a = p.parse_args()
+    if a.gpus or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        if a.ef == "50,100,200,400,800":
+            a.ef = "50,200"
+        return main_sharded(a)
     import ruvector_amd as rv
 
     log = lambda s: print(s, file=sys.stderr, flush=True)  # noqa: E731

@@ -98,6 +98,11 @@ rvx_status rvx_fill_uniform(rvx_buffer* buf, int64_t n_floats, uint64_t seed, fl
  * so a node-range shard generates exactly its slice of the global edge weights. */
 rvx_status rvx_fill_uniform_at(rvx_buffer* buf, int64_t n_floats, uint64_t seed, int64_t first, float lo, float hi);
 rvx_status rvx_fill_normal(rvx_buffer* buf, int64_t n_floats, uint64_t seed);
+/* C5 corpus rows [first_row, first_row + rows) (direction ~ N(0,1)
+ * normalised, radius rmax * U[0,1)), row-deterministic so node-range shards generate
+ * their rows of the single-GPU corpus: buf [rows][dim]. */
+rvx_status rvx_fill_ball_rows(rvx_buffer* buf, int64_t rows, int32_t dim, uint64_t seed, int64_t first_row,
+                              float rmax);
 rvx_status rvx_normalize_rows(rvx_buffer* buf, int64_t rows, int32_t dim); /* L2, as hnsw_integration_test.rs:21-28 */
 rvx_status rvx_random_csr(int64_t n, int32_t deg, uint64_t seed, rvx_buffer* row_ptr_i64, rvx_buffer* col_i32);
 /* Rows [row_begin, row_begin+n_rows) of the same n_total-node random CSR
@@ -359,10 +364,28 @@ rvx_status rvx_index_brute_force(const rvx_index* idx, const float* q, int64_t n
                                  uint64_t* out_ids, float* out_dist);
 rvx_status rvx_index_brute_force_device(const rvx_index* idx, const rvx_buffer* q, int64_t nq, int32_t k,
                                         rvx_buffer* out_ids_u64, rvx_buffer* out_dist_f32);
+/* Node-range-sharded search across processes (SURVEY.md §8e option 2; the merge of
+ * ShardedHyperbolicHnsw::search, crates/ruvector-hyperbolic-hnsw/src/shard.rs:354-373,
+ * applied to VectorIndex shards): one index shard per rank of `comm` (NULL = one
+ * process). Rank 0's queries q [nq][dim] are broadcast (q is ignored on other ranks;
+ * nq, k, ef, exact must agree on every rank), every rank searches its shard
+ * (exact != 0: the FlatIndex scan), one all-gather moves every rank's top-k and every
+ * rank merges them by distance, ties in rank order. Outputs as rvx_index_search (user
+ * ids are the caller's global keys), identical on every rank. */
+rvx_status rvx_index_sharded_search(const rvx_index* idx, rvx_comm* comm, const float* q, int64_t nq, int32_t k,
+                                    int32_t ef, int32_t exact, uint64_t* out_ids, float* out_dist,
+                                    int32_t* out_count);
+rvx_status rvx_index_sharded_search_device(const rvx_index* idx, rvx_comm* comm, const rvx_buffer* q, int64_t nq,
+                                           int32_t k, int32_t ef, int32_t exact, rvx_buffer* out_ids_u64,
+                                           rvx_buffer* out_dist_f32);
 /* Work of the most recent HNSW search launch in this process (any index): distance
  * evaluations, layer-0 expansions and queries — the algorithmic traffic of the search is
  * n_dist * dim * 4 + n_expand * deg_cap * 4 bytes. */
 rvx_status rvx_hnsw_last_search_stats(int64_t* n_dist, int64_t* n_expand, int64_t* nq);
+/* Visited-set form of that launch: bitmap 1 = per-slot bitmaps over all nodes (when
+ * min(nq, 1024) slots fit min(16 GiB, 1/4 of free HBM)), 0 = the tagged hash; slots =
+ * concurrent search slots. */
+rvx_status rvx_hnsw_last_search_visited(int32_t* bitmap, int32_t* slots);
 /* Path taken by the most recent exact scan in this process (rvx_index_brute_force*, FlatIndex
  * search): queries ranked by the MFMA filter + exact re-rank, queries scanned by the exact VALU
  * kernel, and queries the filter handed back to the VALU kernel (completeness not provable).
@@ -473,23 +496,23 @@ typedef struct {                 /* HyperbolicHnswConfig (hnsw.rs:36-72), metric
 } rvx_hyperbolic_config;
 /* HyperbolicHnswConfig::default() with dim = 0 (set it). */
 void rvx_hyperbolic_default_config(rvx_hyperbolic_config* cfg);
-/* HyperbolicHnsw::new (hnsw.rs:142-150). curvature <= 0 -> RVX_ERR_INVALID_PARAMETER (InvalidCurvature). */
+/* HyperbolicHnsw::new (hnsw.rs:143-151). curvature <= 0 -> RVX_ERR_INVALID_PARAMETER (InvalidCurvature). */
 rvx_status rvx_hyperbolic_create(const rvx_hyperbolic_config* cfg, rvx_hyperbolic** out);
 rvx_status rvx_hyperbolic_destroy(rvx_hyperbolic* h);
 /* The underlying graph index (borrowed; owned by h): rvx_index_graph_sizes /
  * export_graph / load_graph / len work on it. */
 rvx_status rvx_hyperbolic_index(rvx_hyperbolic* h, rvx_index** out);
-/* insert / insert_batch (hnsw.rs:192-261): each vector is projected into the
+/* insert / insert_batch (hnsw.rs:226-305): each vector is projected into the
  * ball; ids are insertion order (first_id returns the first new id). Invalidates
  * the tangent cache. */
 rvx_status rvx_hyperbolic_insert_batch(rvx_hyperbolic* h, const float* vecs, int64_t n, int64_t* first_id);
 rvx_status rvx_hyperbolic_insert_batch_device(rvx_hyperbolic* h, const rvx_buffer* vecs, int64_t n, int64_t* first_id);
 rvx_status rvx_hyperbolic_len(const rvx_hyperbolic* h, int64_t* len);
-/* search (hnsw.rs:400-423): ids [nq][k] (-1 past the end), distances ascending;
+/* search (hnsw.rs:427-447): ids [nq][k] (-1 past the end), distances ascending;
  * ef = max(ef or ef_search when 0, k). */
 rvx_status rvx_hyperbolic_search(const rvx_hyperbolic* h, const float* q, int64_t nq, int32_t k, int32_t ef,
                                  int64_t* ids, float* dist, int32_t* counts);
-/* search_with_pruning (hnsw.rs:425-483); without a tangent cache: search. */
+/* search_with_pruning (hnsw.rs:450-489); without a tangent cache: search. */
 rvx_status rvx_hyperbolic_search_with_pruning(const rvx_hyperbolic* h, const float* q, int64_t nq, int32_t k,
                                               int64_t* ids, float* dist, int32_t* counts);
 /* Exact scan by HyperbolicHnsw::distance (ground truth; k <= 128, dim % 4 == 0). */
@@ -498,12 +521,29 @@ rvx_status rvx_hyperbolic_brute_force(const rvx_hyperbolic* h, const float* q, i
 /* HBM-resident queries/outputs; mode 0 search, 1 exact, 2 with pruning. */
 rvx_status rvx_hyperbolic_search_device(const rvx_hyperbolic* h, const rvx_buffer* q, int64_t nq, int32_t k, int32_t ef,
                                         int32_t mode, rvx_buffer* ids_i64, rvx_buffer* dist);
-/* build_tangent_cache (hnsw.rs:485-497): Fréchet-mean centroid + log maps. */
+/* build_tangent_cache (hnsw.rs:492-503): Fréchet-mean centroid + log maps. */
 rvx_status rvx_hyperbolic_build_tangent_cache(rvx_hyperbolic* h);
 rvx_status rvx_hyperbolic_tangent_centroid(const rvx_hyperbolic* h, float* centroid);
 rvx_status rvx_hyperbolic_get_vector(const rvx_hyperbolic* h, int64_t id, float* out);
-/* set_curvature (hnsw.rs:505-528): reprojects all vectors, rebuilds an existing cache. */
+/* set_curvature (hnsw.rs:511-530): reprojects all vectors, rebuilds an existing cache. */
 rvx_status rvx_hyperbolic_set_curvature(rvx_hyperbolic* h, float curvature);
+/* ShardedHyperbolicHnsw::search (shard.rs:354-373) across processes: this rank's
+ * HyperbolicHnsw holds the node-range shard of global ids [id_base, id_base + len).
+ * Rank 0's queries q [nq][dim] are broadcast (ignored on other ranks; nq, k, ef and
+ * mode must agree on every rank), every rank runs mode 0 search (what shard.search
+ * calls, hnsw.rs:427), 1 exact scan or 2 search_with_pruning on its shard, one
+ * all-gather of every rank's top-k, and every rank merges by distance (ties in rank
+ * order, i.e. by global id) and keeps k. Results, identical on every rank, in the
+ * reference's shape Vec<(global_id, SearchResult{id: local_id, distance})>:
+ * out_gid / out_lid [nq][k] (-1 past the end), out_dist ascending, out_count [nq]
+ * (out_lid / out_count nullable). comm NULL: one process (a plain search with id_base). */
+rvx_status rvx_hyperbolic_sharded_search(const rvx_hyperbolic* h, rvx_comm* comm, int64_t id_base, const float* q,
+                                         int64_t nq, int32_t k, int32_t ef, int32_t mode, int64_t* out_gid,
+                                         int64_t* out_lid, float* out_dist, int32_t* out_count);
+rvx_status rvx_hyperbolic_sharded_search_device(const rvx_hyperbolic* h, rvx_comm* comm, int64_t id_base,
+                                                const rvx_buffer* q, int64_t nq, int32_t k, int32_t ef, int32_t mode,
+                                                rvx_buffer* out_gid_i64, rvx_buffer* out_lid_i64 /*nullable*/,
+                                                rvx_buffer* out_dist);
 
 /* ------------------------------------------------------------------ */
 /* Profiling: per-kernel device time measured with HIP events on the   */
@@ -541,7 +581,9 @@ rvx_status rvx_comm_allreduce_f64(rvx_comm* c, double* values, int32_t count, in
  * points use, each round stages this rank's rows in host memory and calls
  * `fn(user, send, send_bytes, recv, recv_bytes)` once: send this rank's block to
  * every peer and fill recv[p] (recv_bytes[p] bytes; recv[me] is NULL) from peer p.
- * Returns 0 on success. Collectives (all-gather, all-reduce) need RCCL. */
+ * Returns 0 on success. The sharded searches' broadcast (only the root sends) and
+ * all-gather of per-rank top-k run through the same call; the f32 all-gather and
+ * the all-reduces need RCCL. */
 typedef int32_t (*rvx_host_exchange_fn)(void* user, const void* send, int64_t send_bytes, void* const* recv,
                                         const int64_t* recv_bytes);
 rvx_status rvx_comm_init_host(int32_t nranks, int32_t rank, rvx_host_exchange_fn fn, void* user, rvx_comm** out);

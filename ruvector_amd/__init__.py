@@ -19,7 +19,7 @@ from .gnn import (GCNLayer, GnnError, GraphSAGELayer, RuvectorLayer, aggregate, 
                   hierarchical_forward_device)
 from .attention import DualSpaceAttention, DualSpaceConfig, EdgeFeaturedAttention, EdgeFeaturedConfig  # noqa: E402
 from .hyperbolic import (DualSpaceIndex, HyperbolicError, HyperbolicHnsw, HyperbolicHnswConfig,  # noqa: E402
-                         ShardedHyperbolicHnsw)
+                         ShardedHyperbolicHnsw, ShardedHyperbolicSearch)
 
 from .query import NeuralSearch, QueryMode, RuvectorQuery  # noqa: E402
 from .vector_db import DbOptions, SearchQuery, VectorDB, VectorEntry  # noqa: E402
@@ -30,7 +30,7 @@ __all__ = [
     "distance", "distance_matrix", "GCNLayer", "GnnError", "GraphSAGELayer", "RuvectorLayer", "aggregate",
     "differentiable_search", "differentiable_search_batch", "hierarchical_forward", "EdgeFeaturedAttention",
     "DualSpaceAttention", "DualSpaceConfig",
-    "EdgeFeaturedConfig", "HyperbolicError", "HyperbolicHnsw", "HyperbolicHnswConfig", "ShardedHyperbolicHnsw",
+    "EdgeFeaturedConfig", "HyperbolicError", "HyperbolicHnsw", "HyperbolicHnswConfig", "ShardedHyperbolicHnsw", "ShardedHyperbolicSearch",
     "DualSpaceIndex",
     "NeuralSearch", "QueryMode", "RuvectorQuery", "DbOptions", "SearchQuery", "VectorDB", "VectorEntry", "differentiable_search_device", "hnsw_last_search_stats", "scan_last_stats",
 ]

@@ -102,6 +102,7 @@ SIGNATURES = {
     "rvx_buffer_zero": (None, [P]),
     "rvx_fill_uniform": (None, [P, I64, U64, F32, F32]),
     "rvx_fill_uniform_at": (None, [P, I64, U64, I64, F32, F32]),
+    "rvx_fill_ball_rows": (None, [P, I64, I32, U64, I64, F32]),
     "rvx_fill_normal": (None, [P, I64, U64]),
     "rvx_normalize_rows": (None, [P, I64, I32]),
     "rvx_random_csr": (None, [I64, I32, U64, P, P]),
@@ -157,6 +158,9 @@ SIGNATURES = {
     "rvx_index_search_device": (None, [P, P, I64, I32, I32, P, P]),
     "rvx_index_brute_force": (None, [P, PF32, I64, I32, PU64, PF32]),
     "rvx_index_brute_force_device": (None, [P, P, I64, I32, P, P]),
+    "rvx_hnsw_last_search_visited": (None, [PI32, PI32]),
+    "rvx_index_sharded_search": (None, [P, P, PF32, I64, I32, I32, I32, PU64, PF32, PI32]),
+    "rvx_index_sharded_search_device": (None, [P, P, P, I64, I32, I32, I32, P, P]),
     "rvx_index_load_graph": (None, [P, C.POINTER(HnswGraph)]),
     "rvx_hyperbolic_default_config": (C.c_void_p, [C.POINTER(HyperbolicConfig)]),  # void
     "rvx_hyperbolic_create": (None, [C.POINTER(HyperbolicConfig), PP]),
@@ -169,6 +173,8 @@ SIGNATURES = {
     "rvx_hyperbolic_search_with_pruning": (None, [P, PF32, I64, I32, PI64, PF32, PI32]),
     "rvx_hyperbolic_brute_force": (None, [P, PF32, I64, I32, PI64, PF32]),
     "rvx_hyperbolic_search_device": (None, [P, P, I64, I32, I32, I32, P, P]),
+    "rvx_hyperbolic_sharded_search": (None, [P, P, I64, PF32, I64, I32, I32, I32, PI64, PI64, PF32, PI32]),
+    "rvx_hyperbolic_sharded_search_device": (None, [P, P, I64, P, I64, I32, I32, I32, P, P, P]),
     "rvx_hyperbolic_build_tangent_cache": (None, [P]),
     "rvx_hyperbolic_tangent_centroid": (None, [P, PF32]),
     "rvx_hyperbolic_get_vector": (None, [P, I64, PF32]),

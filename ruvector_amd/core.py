@@ -186,6 +186,24 @@ class _Index:
         """Exact scan (ties by id) into device buffers."""
         _check("rvx_index_brute_force_device", self._h, q.handle, int(nq), int(k), ids.handle, dist.handle)
 
+    def sharded_search_array(self, comm, queries, k: int, ef: int = 0, exact: bool = False):
+        """Node-range-sharded search across processes (rvx_index_sharded_search): this
+        index is one rank's shard of `comm` (None = one process); rank 0's queries are
+        broadcast (other ranks may pass nq), per-rank top-k all-gathered and merged by
+        distance on the GPU. Returns (ids u64, distances, counts), same on every rank."""
+        if isinstance(queries, (int, np.integer)):
+            nq, q = int(queries), None
+        else:
+            q = L.f32c(queries).reshape(-1, self.dimensions)
+            nq = q.shape[0]
+        ids = np.empty((nq, k), np.uint64)
+        d = np.empty((nq, k), np.float32)
+        cnt = np.empty(nq, np.int32)
+        _check("rvx_index_sharded_search", self._h, comm._h if comm is not None else None,
+               L.fptr(q) if q is not None else None, nq, int(k), int(ef), int(bool(exact)), L.u64ptr(ids),
+               L.fptr(d), L.i32ptr(cnt))
+        return ids, d, cnt
+
     def brute_force_array(self, queries: np.ndarray, k: int) -> Tuple[np.ndarray, np.ndarray]:
         q = L.f32c(queries)
         if q.ndim == 1:
@@ -220,7 +238,10 @@ def hnsw_last_search_stats() -> dict:
     """Work of the most recent HNSW search launch: distance evaluations, layer-0 expansions, queries."""
     a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
     _check("rvx_hnsw_last_search_stats", C.byref(a), C.byref(b), C.byref(c))
-    return {"n_dist": a.value, "n_expand": b.value, "nq": c.value}
+    v, sl = C.c_int32(), C.c_int32()
+    _check("rvx_hnsw_last_search_visited", C.byref(v), C.byref(sl))
+    return {"n_dist": a.value, "n_expand": b.value, "nq": c.value, "visited_bitmap": bool(v.value),
+            "slots": sl.value}
 
 
 def scan_last_stats() -> dict:

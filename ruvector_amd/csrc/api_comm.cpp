@@ -79,6 +79,61 @@ void comm_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int6
     RVX_NCCL(ncclGroupEnd());
 }
 
+void comm_broadcast_bytes(rvx_comm* c, void* buf, int64_t bytes, int root, hipStream_t s) {
+    if (!c || c->nranks <= 1 || bytes <= 0) return;
+    RVX_REQUIRE(root >= 0 && root < c->nranks, RVX_ERR_INVALID_PARAMETER, "bad broadcast root");
+    if (!c->host_fn) {
+        RVX_NCCL(ncclBroadcast(buf, buf, (size_t)bytes, ncclUint8, root, c->comm, s));
+        return;
+    }
+    // host transport: the root ships its block to every peer, the others receive from the root only
+    const int me = c->rank, w = c->nranks;
+    RVX_HIP(hipStreamSynchronize(s));
+    std::vector<uint8_t> host((size_t)bytes);
+    std::vector<void*> rptr(w, nullptr);
+    std::vector<int64_t> rbytes(w, 0);
+    if (me == root) {
+        RVX_HIP(hipMemcpy(host.data(), buf, (size_t)bytes, hipMemcpyDeviceToHost));
+    } else {
+        rptr[root] = host.data();
+        rbytes[root] = bytes;
+    }
+    const int32_t rc = c->host_fn(c->host_user, host.data(), me == root ? bytes : 0, rptr.data(), rbytes.data());
+    RVX_REQUIRE(rc == 0, RVX_ERR_COMM, "host transport failed with status " + std::to_string(rc));
+    if (me != root) RVX_HIP(hipMemcpy(buf, host.data(), (size_t)bytes, hipMemcpyHostToDevice));
+}
+
+void comm_allgather_bytes(rvx_comm* c, const void* send, void* recv, int64_t bytes, hipStream_t s) {
+    const int w = comm_size(c), me = comm_rank(c);
+    if (bytes <= 0) return;
+    if (w <= 1) {
+        if (recv != send) RVX_HIP(hipMemcpyAsync(recv, send, (size_t)bytes, hipMemcpyDeviceToDevice, s));
+        return;
+    }
+    if (!c->host_fn) {
+        RVX_NCCL(ncclAllGather(send, recv, (size_t)bytes, ncclUint8, c->comm, s));
+        return;
+    }
+    RVX_HIP(hipStreamSynchronize(s));
+    std::vector<uint8_t> mine((size_t)bytes);
+    RVX_HIP(hipMemcpy(mine.data(), send, (size_t)bytes, hipMemcpyDeviceToHost));
+    std::vector<std::vector<uint8_t>> blk(w);
+    std::vector<void*> rptr(w, nullptr);
+    std::vector<int64_t> rbytes(w, 0);
+    for (int p = 0; p < w; ++p) {
+        if (p == me) continue;
+        blk[p].resize((size_t)bytes);
+        rptr[p] = blk[p].data();
+        rbytes[p] = bytes;
+    }
+    const int32_t rc = c->host_fn(c->host_user, mine.data(), bytes, rptr.data(), rbytes.data());
+    RVX_REQUIRE(rc == 0, RVX_ERR_COMM, "host transport failed with status " + std::to_string(rc));
+    auto* out = static_cast<uint8_t*>(recv);
+    for (int p = 0; p < w; ++p)
+        RVX_HIP(hipMemcpy(out + (size_t)p * (size_t)bytes, p == me ? mine.data() : blk[p].data(), (size_t)bytes,
+                          hipMemcpyHostToDevice));
+}
+
 }  // namespace rvx
 
 extern "C" {

@@ -26,6 +26,12 @@ void* scratch_bytes(const std::string& slot, int64_t bytes) {
     return m->p;
 }
 float* scratch_f32(const std::string& slot, int64_t count) { return (float*)scratch_bytes(slot, count * 4); }
+int64_t scratch_held(const std::string& slot) {
+    const int dev = device().id;
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    auto it = g_scratch.find({dev, slot});
+    return it == g_scratch.end() || !it->second ? 0 : it->second->bytes;
+}
 
 ComputeLock::ComputeLock() {
     const int dev = device().id;

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <shared_mutex>
 
+#include "comm.hpp"
 #include "graph.hpp"
 #include "hnsw.hpp"
 #include "hyper.hpp"
@@ -63,6 +64,19 @@ void finish_ids(const int64_t* rows, const float* dist, int64_t nq, int k, int64
     if (total <= 0) return;
     hipLaunchKernelGGL(k_rows_to_ids, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream(), rows, dist, total,
                        ids, out_d);
+    RVX_HIP(hipGetLastError());
+}
+
+__global__ void k_offset_ids(const int64_t* in, int64_t total, int64_t base, int64_t* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < total) out[i] = in[i] >= 0 ? in[i] + base : -1;
+}
+
+// local ids of a node-range shard -> global ids (shard.rs:360-363: local + the shard's first id)
+void offset_ids(const int64_t* in, int64_t total, int64_t base, int64_t* out) {
+    if (total <= 0) return;
+    hipLaunchKernelGGL(k_offset_ids, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream(), in, total, base,
+                       out);
     RVX_HIP(hipGetLastError());
 }
 
@@ -303,6 +317,79 @@ rvx_status rvx_hyperbolic_search_device(const rvx_hyperbolic* h, const rvx_buffe
         const int m = (mode == 2 && !h->ix.tan_valid) ? 0 : mode;
         float* dq = projected_queries(h, q->mem.as<float>(), nq, true);
         search_dev(h, dq, nq, k, ef, ids->mem.as<int64_t>(), dist->mem.as<float>(), nullptr, m);
+    });
+}
+
+// ShardedHyperbolicHnsw::search across processes (shard.rs:354-373): rank 0's
+// queries are broadcast, every rank searches its node-range shard (local ids +
+// id_base = global ids), one all-gather moves every rank's top-k, and each rank
+// merges them on the GPU. q_dev: the queries on rank 0 (device), ignored elsewhere.
+static void sharded_search_dev(const rvx_hyperbolic* h, rvx_comm* comm, int64_t id_base, const float* q_dev,
+                               int64_t nq, int k, int ef, int mode, int64_t* gid, int64_t* lid, float* dist,
+                               int32_t* counts) {
+    const int d = h->ix.cfg.dim;
+    float* dq = scratch_f32("shard_q", nq * d);
+    if (comm_rank(comm) == 0)
+        RVX_HIP(hipMemcpyAsync(dq, q_dev, (size_t)(nq * d * 4), hipMemcpyDeviceToDevice, stream()));
+    {
+        ProfScope ps("shard_bcast");
+        comm_broadcast_bytes(comm, dq, nq * d * 4, 0, stream());
+    }
+    project_rows(dq, nq, d, h->ix.curv);
+    const int m = (mode == 2 && !h->ix.tan_valid) ? 0 : mode;  // no cache -> regular search (hnsw.rs:450-454)
+    auto* li = (int64_t*)scratch_bytes("shard_local_i", nq * k * 8);
+    float* ld = scratch_f32("shard_local_d", nq * k);
+    search_dev(h, dq, nq, k, ef, li, ld, nullptr, m);
+    auto* gi = (int64_t*)scratch_bytes("shard_local_g", nq * k * 8);
+    offset_ids(li, nq * k, id_base, gi);
+    sharded_merge(comm, gi, li, ld, nq, k, gid, lid, dist, counts);
+}
+
+rvx_status rvx_hyperbolic_sharded_search(const rvx_hyperbolic* h, rvx_comm* comm, int64_t id_base, const float* q,
+                                         int64_t nq, int32_t k, int32_t ef, int32_t mode, int64_t* out_gid,
+                                         int64_t* out_lid, float* out_dist, int32_t* out_count) {
+    return guard([&] {
+        RVX_REQUIRE(h && nq >= 0 && k >= 1 && mode >= 0 && mode <= 2 && id_base >= 0, RVX_ERR_INVALID_PARAMETER,
+                    "bad sharded search arguments");
+        RVX_REQUIRE(nq == 0 || (out_gid && out_dist && (comm_rank(comm) != 0 || q)), RVX_ERR_INVALID_PARAMETER,
+                    "null argument");
+        if (nq == 0) return;
+        std::shared_lock<std::shared_mutex> lk(h->ix.mu);
+        ComputeLock cl;
+        const int d = h->ix.cfg.dim;
+        float* hq = scratch_f32("shard_hq", nq * d);
+        if (comm_rank(comm) == 0)
+            RVX_HIP(hipMemcpyAsync(hq, q, (size_t)(nq * d * 4), hipMemcpyHostToDevice, stream()));
+        auto* gi = (int64_t*)scratch_bytes("shard_out_g", nq * k * 8);
+        auto* li = (int64_t*)scratch_bytes("shard_out_l", nq * k * 8);
+        float* dd = scratch_f32("shard_out_d", nq * k);
+        auto* dn = (int32_t*)scratch_bytes("shard_out_n", nq * 4);
+        sharded_search_dev(h, comm, id_base, hq, nq, k, ef, mode, gi, li, dd, dn);
+        RVX_HIP(hipMemcpyAsync(out_gid, gi, (size_t)(nq * k * 8), hipMemcpyDeviceToHost, stream()));
+        if (out_lid) RVX_HIP(hipMemcpyAsync(out_lid, li, (size_t)(nq * k * 8), hipMemcpyDeviceToHost, stream()));
+        RVX_HIP(hipMemcpyAsync(out_dist, dd, (size_t)(nq * k * 4), hipMemcpyDeviceToHost, stream()));
+        if (out_count) RVX_HIP(hipMemcpyAsync(out_count, dn, (size_t)(nq * 4), hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
+rvx_status rvx_hyperbolic_sharded_search_device(const rvx_hyperbolic* h, rvx_comm* comm, int64_t id_base,
+                                                const rvx_buffer* q, int64_t nq, int32_t k, int32_t ef, int32_t mode,
+                                                rvx_buffer* out_gid, rvx_buffer* out_lid, rvx_buffer* out_dist) {
+    return guard([&] {
+        RVX_REQUIRE(h && nq >= 0 && k >= 1 && mode >= 0 && mode <= 2 && id_base >= 0 && out_gid && out_dist,
+                    RVX_ERR_INVALID_PARAMETER, "bad sharded search arguments");
+        RVX_REQUIRE(comm_rank(comm) != 0 || (q && q->mem.bytes >= nq * h->cfg.dim * 4), RVX_ERR_DIMENSION_MISMATCH,
+                    "query buffer too small");
+        RVX_REQUIRE(out_gid->mem.bytes >= nq * k * 8 && out_dist->mem.bytes >= nq * k * 4 &&
+                        (!out_lid || out_lid->mem.bytes >= nq * k * 8),
+                    RVX_ERR_DIMENSION_MISMATCH, "output buffer too small");
+        if (nq == 0) return;
+        std::shared_lock<std::shared_mutex> lk(h->ix.mu);
+        ComputeLock cl;
+        sharded_search_dev(h, comm, id_base, comm_rank(comm) == 0 ? q->mem.as<float>() : nullptr, nq, k, ef, mode,
+                           out_gid->mem.as<int64_t>(), out_lid ? out_lid->mem.as<int64_t>() : nullptr,
+                           out_dist->mem.as<float>(), nullptr);
     });
 }
 

@@ -5,6 +5,7 @@
 #include <shared_mutex>
 #include <unordered_map>
 
+#include "comm.hpp"
 #include "graph.hpp"
 #include "hnsw.hpp"
 #include "hyper.hpp"
@@ -337,6 +338,73 @@ rvx_status rvx_index_brute_force(const rvx_index* ix, const float* q, int64_t nq
     });
 }
 
+// Node-range-sharded VectorIndex search across processes (SURVEY.md §8e option 2, the
+// merge of shard.rs:354-373 applied to ruvector-core indices): rank 0's queries are
+// broadcast, every rank searches its shard (exact = 1: FlatIndex scan), the per-rank
+// (user id, distance) lists are all-gathered and merged on every rank by distance,
+// ties in rank order. User ids are global by construction (the caller's keys).
+static void index_sharded_dev(const rvx_index* ix, rvx_comm* comm, const float* q_dev, int64_t nq, int k, int ef,
+                              bool exact, uint64_t* oi, float* od, int32_t* on) {
+    const int d = ix->cfg.dim;
+    float* dq = scratch_f32("shard_q", nq * d);
+    if (comm_rank(comm) == 0)
+        RVX_HIP(hipMemcpyAsync(dq, q_dev, (size_t)(nq * d * 4), hipMemcpyDeviceToDevice, stream()));
+    {
+        ProfScope ps("shard_bcast");
+        comm_broadcast_bytes(comm, dq, nq * d * 4, 0, stream());
+    }
+    float* dd = scratch_f32("index_dd", nq * k);
+    int64_t* di = (int64_t*)scratch_bytes("index_di", nq * k * 8);
+    search_rows(ix, dq, nq, k, ef, dd, di, nullptr, exact);
+    auto* li = (uint64_t*)scratch_bytes("shard_local_u", nq * k * 8);
+    float* ld = scratch_f32("shard_local_d", nq * k);
+    map_out(ix, di, dd, nq, k, li, ld, nullptr, !exact && ix->cfg.kind == RVX_INDEX_HNSW);
+    sharded_merge(comm, (const int64_t*)li, nullptr, ld, nq, k, (int64_t*)oi, nullptr, od, on);
+}
+
+rvx_status rvx_index_sharded_search(const rvx_index* ix, rvx_comm* comm, const float* q, int64_t nq, int32_t k,
+                                    int32_t ef, int32_t exact, uint64_t* out_ids, float* out_dist,
+                                    int32_t* out_count) {
+    return guard([&] {
+        check_query_args(ix, nq, k);
+        RVX_REQUIRE(nq == 0 || (out_ids && out_dist && (comm_rank(comm) != 0 || q)), RVX_ERR_INVALID_PARAMETER,
+                    "null argument");
+        if (nq == 0) return;
+        std::shared_lock<std::shared_mutex> lk(ix->mu);
+        ComputeLock cl;
+        const int d = ix->cfg.dim;
+        float* hq = scratch_f32("shard_hq", nq * d);
+        if (comm_rank(comm) == 0)
+            RVX_HIP(hipMemcpyAsync(hq, q, (size_t)(nq * d * 4), hipMemcpyHostToDevice, stream()));
+        uint64_t* oi = (uint64_t*)scratch_bytes("shard_out_u", nq * k * 8);
+        float* od = scratch_f32("shard_out_d", nq * k);
+        int32_t* on = (int32_t*)scratch_bytes("shard_out_n", nq * 4);
+        index_sharded_dev(ix, comm, hq, nq, k, ef, exact != 0, oi, od, on);
+        RVX_HIP(hipMemcpyAsync(out_ids, oi, (size_t)(nq * k * 8), hipMemcpyDeviceToHost, stream()));
+        RVX_HIP(hipMemcpyAsync(out_dist, od, (size_t)(nq * k * 4), hipMemcpyDeviceToHost, stream()));
+        if (out_count) RVX_HIP(hipMemcpyAsync(out_count, on, (size_t)(nq * 4), hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
+rvx_status rvx_index_sharded_search_device(const rvx_index* ix, rvx_comm* comm, const rvx_buffer* q, int64_t nq,
+                                           int32_t k, int32_t ef, int32_t exact, rvx_buffer* out_ids,
+                                           rvx_buffer* out_dist) {
+    return guard([&] {
+        check_query_args(ix, nq, k);
+        RVX_REQUIRE(out_ids && out_dist, RVX_ERR_INVALID_PARAMETER, "null buffer");
+        RVX_REQUIRE(comm_rank(comm) != 0 || (q && q->mem.bytes >= nq * ix->cfg.dim * 4), RVX_ERR_DIMENSION_MISMATCH,
+                    "query buffer too small");
+        RVX_REQUIRE(out_ids->mem.bytes >= nq * k * 8 && out_dist->mem.bytes >= nq * k * 4, RVX_ERR_DIMENSION_MISMATCH,
+                    "output buffers too small");
+        if (nq == 0) return;
+        std::shared_lock<std::shared_mutex> lk(ix->mu);
+        ComputeLock cl;
+        index_sharded_dev(ix, comm, comm_rank(comm) == 0 ? q->mem.as<float>() : nullptr, nq, k, ef, exact != 0,
+                          out_ids->mem.as<uint64_t>(), out_dist->mem.as<float>(), nullptr);
+    });
+}
+
 rvx_status rvx_index_load_graph(rvx_index* ix, const rvx_hnsw_graph* hg) {
     return guard([&] {
         RVX_REQUIRE(ix && hg, RVX_ERR_INVALID_PARAMETER, "null argument");
@@ -455,6 +523,13 @@ rvx_status rvx_hnsw_last_search_stats(int64_t* n_dist, int64_t* n_expand, int64_
         if (n_dist) *n_dist = g_search_stats.n_dist;
         if (n_expand) *n_expand = g_search_stats.n_expand;
         if (nq) *nq = g_search_stats.nq;
+    });
+}
+
+rvx_status rvx_hnsw_last_search_visited(int32_t* bitmap, int32_t* slots) {
+    return guard([&] {
+        if (bitmap) *bitmap = g_search_stats.visited_bitmap;
+        if (slots) *slots = g_search_stats.slots;
     });
 }
 

@@ -21,6 +21,22 @@ int comm_size(const rvx_comm* c);
 void comm_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int64_t* r0, const int64_t* rows,
                         hipStream_t s);
 
+// Sharded search collectives (SURVEY.md §8e option 2, shard.rs:354-373), on stream `s`,
+// over RCCL or the host-staged transport:
+// broadcast `bytes` of device memory `buf` from rank `root` to every rank (in place);
+void comm_broadcast_bytes(rvx_comm* c, void* buf, int64_t bytes, int root, hipStream_t s);
+// all-gather: every rank's `bytes` at `send` into recv [nranks][bytes] (rank-major).
+void comm_allgather_bytes(rvx_comm* c, const void* send, void* recv, int64_t bytes, hipStream_t s);
+
+// ShardedHyperbolicHnsw::search merge (shard.rs:354-373) across ranks: this rank's
+// per-query hits gid/lid/dist [nq][k] (ascending; an empty slot has gid -1 and
+// +inf) are all-gathered and every rank merges all ranks' lists by distance,
+// ties in rank order then list order (for node-range shards: by global id), and
+// keeps the first k: out_gid/out_lid/out_dist [nq][k], out_count [nq] (nullable:
+// out_lid, out_count). Device pointers, library stream; lid may be null (zeros).
+void sharded_merge(rvx_comm* c, const int64_t* gid, const int64_t* lid, const float* dist, int64_t nq, int k,
+                   int64_t* out_gid, int64_t* out_lid, float* out_dist, int32_t* out_count);
+
 // Exchange round plan (rvx_exchange_plan): plan[c] = {r0[p], rows[p]} of round c.
 enum { PLAN_SAGE = 0, PLAN_WHOLE = 1 };
 struct ExchangeRound {

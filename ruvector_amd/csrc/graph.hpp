@@ -32,6 +32,8 @@ namespace rvx {
 // lock (ComputeLock) for the duration of the op that uses them.
 float* scratch_f32(const std::string& slot, int64_t count);
 void* scratch_bytes(const std::string& slot, int64_t bytes);
+// Bytes the slot holds now (0 if never used).
+int64_t scratch_held(const std::string& slot);
 
 // Serialises compute entry points per device (they share scratch and stream).
 struct ComputeLock {

@@ -39,6 +39,7 @@ bool hnsw_coop(int metric, int d, int64_t rows);
 // bytes = n_dist * d * 4 + n_expand * deg_cap * 4 per launch).
 struct SearchStats {
     int64_t n_dist = 0, n_expand = 0, nq = 0;
+    int32_t visited_bitmap = 0, slots = 0;  // visited-set form and search slots of the launch
 };
 extern SearchStats g_search_stats;
 

@@ -36,6 +36,36 @@ __global__ void k_fill_normal(float* p, int64_t n, uint64_t s0) {
     }
 }
 
+// C5 points: row r of the global corpus = direction ~ N(0,1)^dim
+// normalised, times radius rmax * U[0,1): the normals are elements [r*dim, (r+1)*dim)
+// of the fill_normal(seed) stream and the radius element r of the
+// fill_uniform(seed + 1) stream, so a node-range shard generates exactly its rows of
+// the single-GPU corpus. One wave per row; the norm is a wave reduction.
+__global__ __launch_bounds__(256) void k_fill_ball_rows(float* p, int64_t rows, int dim, uint64_t s_dir,
+                                                        uint64_t s_rad, int64_t first_row, float rmax) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int64_t g = first_row + r;
+    float* row = p + r * dim;
+    float ss = 0.0f;
+    for (int j = lane; j < dim; j += 64) {
+        const uint64_t i = (uint64_t)(g * dim + j);
+        const uint64_t h1 = splitmix64(s_dir + 2 * i);
+        const uint64_t h2 = splitmix64(s_dir + 2 * i + 1);
+        const float u1 = (float)((uint32_t)(h1 >> 40) + 1u) * 5.9604644775390625e-08f;
+        const float u2 = (float)(uint32_t)(h2 >> 40) * 5.9604644775390625e-08f;
+        const float v = sqrtf(-2.0f * logf(u1)) * cosf(6.283185307179586f * u2);
+        row[j] = v;
+        ss += v * v;
+    }
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    const uint64_t hr = splitmix64(s_rad + (uint64_t)g);
+    const float rad = rmax * ((float)(uint32_t)(hr >> 40) * 5.9604644775390625e-08f);
+    const float scale = ss > 0.0f ? rad / sqrtf(ss) : 0.0f;
+    for (int j = lane; j < dim; j += 64) row[j] *= scale;
+}
+
 // One wave per row: norm = sqrt(sum x^2); x /= norm (true division, as
 // normalize_vector in crates/ruvector-core/tests/hnsw_integration_test.rs:21-28
 // and the GraphSAGE output normalisation, graphsage.rs:177-182).
@@ -133,6 +163,14 @@ void fill_uniform_at(float* p, int64_t n, uint64_t seed, int64_t first, float lo
                        splitmix64(seed) + (uint64_t)first, lo, hi - lo);
     RVX_HIP(hipGetLastError());
 }
+void fill_ball_rows(float* p, int64_t rows, int dim, uint64_t seed, int64_t first_row, float rmax) {
+    if (rows <= 0) return;
+    ProfScope ps("fill_ball");
+    hipLaunchKernelGGL(k_fill_ball_rows, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream(), p, rows, dim,
+                       splitmix64(seed), splitmix64(seed + 1), first_row, rmax);
+    RVX_HIP(hipGetLastError());
+}
+
 void fill_normal(float* p, int64_t n, uint64_t seed) {
     ProfScope ps("fill_normal");
     hipLaunchKernelGGL(k_fill_normal, dim3(grid_for(n, 256)), dim3(256), 0, stream(), p, n, splitmix64(seed));
@@ -189,6 +227,14 @@ rvx_status rvx_fill_normal(rvx_buffer* buf, int64_t n, uint64_t seed) {
     return guard([&] {
         RVX_REQUIRE(buf && n >= 0 && n * 4 <= buf->mem.bytes, RVX_ERR_INVALID_PARAMETER, "buffer too small");
         fill_normal(buf->mem.as<float>(), n, seed);
+    });
+}
+rvx_status rvx_fill_ball_rows(rvx_buffer* buf, int64_t rows, int32_t dim, uint64_t seed, int64_t first_row,
+                              float rmax) {
+    return guard([&] {
+        RVX_REQUIRE(buf && rows >= 0 && dim > 0 && first_row >= 0 && rows * dim * 4 <= buf->mem.bytes,
+                    RVX_ERR_INVALID_PARAMETER, "buffer too small");
+        fill_ball_rows(buf->mem.as<float>(), rows, dim, seed, first_row, rmax);
     });
 }
 rvx_status rvx_normalize_rows(rvx_buffer* buf, int64_t rows, int32_t dim) {

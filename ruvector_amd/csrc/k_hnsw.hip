@@ -209,7 +209,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             a.out_d[qi * a.k + s] = s < take ? rd[s] : INFINITY;
             a.out_i[qi * a.k + s] = s < take ? (int64_t)(ri[s] & ID_MASK) : (int64_t)-1;
         }
-        if (lane == 0) a.out_n[qi] = take;
+        if (lane == 0 && a.out_n) a.out_n[qi] = take;  // counts are optional (device entry points)
         __builtin_amdgcn_wave_barrier();
     }
     if (lane == 0 && a.stats) {
@@ -266,17 +266,29 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
                 "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
     const unsigned vcap = visited_capacity(ef);
     // visited set: a per-slot bitmap over all n nodes (cleared per query by its
-    // wave: no launch-wide memset, no probing, n/8 bytes touched) when every
-    // slot's bitmap fits 16 GB together (10M nodes x 8192 slots = 10 GB), else
-    // the tagged hash (zeroed per launch). C1 ef 600: 336k -> 438k QPS; 4M x 768
+    // wave: no launch-wide memset, no probing, n/8 bytes touched) when at least
+    // min(nq, 1024) slots' bitmaps fit the budget — what the scratch slot already
+    // holds, else min(16 GiB, 1/4 of the free HBM), as the exact scan sizes its f16
+    // image (10M nodes x 8192 slots = 10 GB) — else the tagged hash (zeroed per
+    // launch; it stays for 100M-node tables). C1 ef 600: 336k -> 438k QPS; 4M x 768
     // ef 1600: 16.6k -> 22.2k
-    // (the hash stays for 100M-node tables)
     const int64_t vwords = (g.n + 127) / 128 * 4;
     const int bm_mode = env_int("RVX_HNSW_BITMAP", 1);  // 0 off, 1 auto, 2 force (tests); read per call
     const int64_t bm_slots = std::min<int64_t>(nq, 8192);
-    const bool bitmap = bm_mode == 2 || (bm_mode == 1 && bm_slots * vwords * 4 <= ((int64_t)16 << 30));
+    const int64_t held = scratch_held("hnsw_vbits");
+    int64_t budget = held;
+    {
+        size_t fr = 0, tot = 0;
+        RVX_HIP(hipMemGetInfo(&fr, &tot));
+        budget = std::max<int64_t>(held, std::min<int64_t>((int64_t)16 << 30, ((int64_t)fr + held) / 4));
+        const int64_t cap_mb = env_int("RVX_HNSW_BITMAP_BUDGET_MB", 0);  // tests force a small budget
+        if (cap_mb > 0) budget = std::min<int64_t>(budget, cap_mb << 20);
+    }
+    const int64_t fit_slots = budget / (vwords * 4);
+    const bool bitmap = bm_mode == 2 || (bm_mode == 1 && fit_slots >= std::min<int64_t>(bm_slots, 1024));
     const int64_t mem_slots = std::max<int64_t>(256, ((int64_t)8 << 30) / ((int64_t)vcap * 8));
-    const int nslots = (int)(bitmap ? bm_slots : std::min<int64_t>(bm_slots, mem_slots));
+    const int nslots = (int)(bitmap ? (bm_mode == 2 ? bm_slots : std::min(bm_slots, fit_slots))
+                                    : std::min<int64_t>(bm_slots, mem_slots));
     unsigned long long* vis = nullptr;
     unsigned* vbits = nullptr;
     if (bitmap) {
@@ -345,6 +357,8 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     g_search_stats.n_dist = (int64_t)tally[0];
     g_search_stats.n_expand = (int64_t)tally[1];
     g_search_stats.nq = nq;
+    g_search_stats.visited_bitmap = bitmap ? 1 : 0;
+    g_search_stats.slots = nslots;
 }
 
 }  // namespace rvx

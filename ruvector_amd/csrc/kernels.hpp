@@ -68,6 +68,7 @@ void split_h2_rows(const float* B0, const float* B1, int N, int K, _Float16* P0,
 void fill_uniform(float* p, int64_t n, uint64_t seed, float lo, float hi);
 void fill_uniform_at(float* p, int64_t n, uint64_t seed, int64_t first, float lo, float hi);
 void fill_normal(float* p, int64_t n, uint64_t seed);
+void fill_ball_rows(float* p, int64_t rows, int dim, uint64_t seed, int64_t first_row, float rmax);
 void normalize_rows(float* p, int64_t rows, int dim, bool divide_only_if_positive, const char* tag);
 void random_csr(int64_t n, int deg, uint64_t seed, int64_t* row_ptr, int32_t* col);
 void random_csr_shard(int64_t n_total, int64_t row_begin, int64_t n_rows, int deg, uint64_t seed, int64_t* row_ptr,

@@ -82,6 +82,10 @@ class Buffer:
     def fill_normal(self, n: int, seed: int) -> None:
         L.call("rvx_fill_normal", self._h, int(n), int(seed))
 
+    def fill_ball(self, rows: int, dim: int, seed: int, first_row: int = 0, rmax: float = 0.9) -> None:
+        """Rows [first_row, first_row+rows) of the C5 corpus (rvx_fill_ball_rows)."""
+        L.call("rvx_fill_ball_rows", self._h, int(rows), int(dim), int(seed), int(first_row), float(rmax))
+
     def normalize_rows(self, rows: int, dim: int) -> None:
         L.call("rvx_normalize_rows", self._h, int(rows), int(dim))
 

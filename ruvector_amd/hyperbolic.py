@@ -249,6 +249,7 @@ class ShardedHyperbolicHnsw:
         return len(self.shards)
 
     def search_batch(self, queries, k: int) -> Tuple[np.ndarray, np.ndarray]:
+        """(global ids, distances) [nq][k] of the merged search (-1 / inf past the end)."""
         parts = []
         for s, base in zip(self.shards, self.offsets):
             ids, d, _ = s.search_batch(queries, k)
@@ -256,8 +257,71 @@ class ShardedHyperbolicHnsw:
         return merge_shard_results(parts, k)
 
     def search(self, query, k: int) -> List[Tuple[int, SearchResult]]:
+        """Vec<(global_id, SearchResult{id: local_id, distance})> (shard.rs:354-373)."""
         ids, d = self.search_batch(np.asarray(query, np.float32).reshape(1, -1), k)
-        return [(int(i), SearchResult(int(i), float(x))) for i, x in zip(ids[0], d[0]) if i >= 0]
+        out = []
+        for g, x in zip(ids[0], d[0]):
+            if g < 0:
+                continue
+            s = int(np.searchsorted(self.offsets, g, side="right")) - 1
+            out.append((int(g), SearchResult(int(g) - self.offsets[s], float(x))))
+        return out
+
+
+SEARCH_MODES = {"search": 0, "exact": 1, "pruned": 2}
+
+
+class ShardedHyperbolicSearch:
+    """ShardedHyperbolicHnsw::search (shard.rs:354-373) with one node-range shard per
+    process / GPU (SURVEY.md §8e option 2): this process's HyperbolicHnsw holds global
+    ids [id_base, id_base + len). search_batch broadcasts rank 0's queries, searches
+    every shard, all-gathers each rank's top-k over `comm` (RcclComm over xGMI, or any
+    communicator handle of librvx; None = one process) and merges on the GPU
+    (rvx_hyperbolic_sharded_search). mode: "search" (what shard.search runs,
+    hnsw.rs:427), "exact" or "pruned" (search_with_pruning, hnsw.rs:450)."""
+
+    def __init__(self, shard: HyperbolicHnsw, comm=None, id_base: int = 0):
+        if shard._h is None:
+            raise HyperbolicError(2, "the shard needs a dimension (create it with dim= or insert first)")
+        self.shard, self.comm, self.id_base = shard, comm, int(id_base)
+
+    @property
+    def rank(self) -> int:
+        return 0 if self.comm is None else int(self.comm.rank)
+
+    def search_batch(self, queries, k: int, ef: int = 0, mode: str = "search"):
+        """queries [nq][dim] (read on rank 0; other ranks pass nq or an array of that
+        shape). Returns (global ids, local ids, distances, counts), same on every rank."""
+        d = self.shard._dim
+        if isinstance(queries, (int, np.integer)):
+            nq, q = int(queries), None
+        else:
+            q = L.f32c(queries).reshape(-1, d)
+            nq = q.shape[0]
+        if self.rank == 0 and q is None:
+            raise HyperbolicError(2, "rank 0 must pass the queries")
+        gid = np.empty((nq, k), np.int64)
+        lid = np.empty((nq, k), np.int64)
+        dist = np.empty((nq, k), np.float32)
+        cnt = np.empty(nq, np.int32)
+        _check("rvx_hyperbolic_sharded_search", self.shard._h, self.comm._h if self.comm is not None else None,
+               self.id_base, L.fptr(q) if q is not None else None, nq, int(k), int(ef), SEARCH_MODES[mode],
+               L.i64ptr(gid), L.i64ptr(lid), L.fptr(dist), L.i32ptr(cnt))
+        return gid, lid, dist, cnt
+
+    def search(self, query, k: int) -> List[Tuple[int, SearchResult]]:
+        """Vec<(global_id, SearchResult{id: local_id, distance})>, as shard.rs:354-373."""
+        q = None if query is None else np.asarray(query, np.float32).reshape(1, -1)
+        gid, lid, dist, cnt = self.search_batch(q if q is not None else 1, k)
+        return [(int(gid[0, s]), SearchResult(int(lid[0, s]), float(dist[0, s]))) for s in range(int(cnt[0]))]
+
+    def search_device(self, queries: Optional[Buffer], nq: int, k: int, gid: Buffer, dist: Buffer,
+                      lid: Optional[Buffer] = None, ef: int = 0, mode: str = "search") -> None:
+        """HBM-resident form: queries on rank 0, outputs (int64 ids) on every rank."""
+        _check("rvx_hyperbolic_sharded_search_device", self.shard._h,
+               self.comm._h if self.comm is not None else None, self.id_base,
+               queries.handle if queries is not None else None, int(nq), int(k), int(ef), SEARCH_MODES[mode],
+               gid.handle, lid.handle if lid is not None else None, dist.handle)
 
 
 class DualSpaceIndex:

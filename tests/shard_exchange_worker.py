@@ -36,7 +36,8 @@ def main():
     import oracle as O
     import ruvector_amd as rv
     from ruvector_amd.attention import EdgeFeaturedAttention, EdgeFeaturedConfig
-    from ruvector_amd.shard import PLAN_SAGE, HostComm, exchange_plan
+    from host_comm import HostComm
+    from ruvector_amd.shard import PLAN_SAGE, exchange_plan
 
     from datetime import timedelta
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=90))

@@ -7,8 +7,9 @@ keys = values = the layer-3 rows of the neighbours and the edge weight as the
 1-d edge feature). Isolated rows take the reference's deg-0 paths
 (LayerNorm(w_msg x), layer.rs:385-389; zero attention output).
 
-Tolerance: 1e-5 of max|ref| over the compared rows (north star), per layer and
-for the head.
+Tolerance (north star 1e-5 relative), per layer and for the head: normwise
+(1e-5 of max|ref| over the compared rows) and per row (||gpu_r - ref_r||_2 /
+||ref_r||_2, tests/parity.py).
 """
 import json
 
@@ -16,6 +17,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+from parity import row_rel_err
 
 rv = pytest.importorskip("ruvector_amd")
 from ruvector_amd.attention import EdgeFeaturedAttention, EdgeFeaturedConfig  # noqa: E402
@@ -75,10 +77,14 @@ def test_c4_stack_matches_oracle(entry):
         h = O.rvl_forward_graph(W, h, rp, col, ew, threads=16)
         e = rel_err(got[i], h)
         assert e <= TOL, f"layer {i + 1}: relative error {e:.3e}"
+        e = row_rel_err(got[i], h)
+        assert e <= TOL, f"layer {i + 1}: per-row relative error {e:.3e}"
     rows = sorted(set(range(0, n, 2)) | set(isolated))
     ref = np.stack([O.efa_compute(d, 1, heads, h[i], h[col[rp[i]:rp[i + 1]]], h[col[rp[i]:rp[i + 1]]],
                                   ew[rp[i]:rp[i + 1]].reshape(-1, 1)) for i in rows])
     e = rel_err(y[rows], ref)
     assert e <= TOL, f"attention head: relative error {e:.3e}"
+    e = row_rel_err(y[rows], ref)
+    assert e <= TOL, f"attention head: per-row relative error {e:.3e}"
     assert len(rows) >= 256
     assert np.all(y[isolated] == 0.0) and np.all(ref[[rows.index(i) for i in isolated]] == 0.0)

@@ -79,3 +79,22 @@ def test_exact_scan_k_equals_n_and_duplicate_rows():
     rids, rd = O.flat_search(x, q, 16, "l2")
     assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd)
     assert np.array_equal(rids[0], np.arange(16))
+
+
+def test_hnsw_visited_bitmap_respects_the_hbm_budget(monkeypatch):
+    """The per-slot visited bitmaps are only taken when min(nq, 1024) slots fit the
+    budget (min(16 GiB, 1/4 of free HBM)); a small budget (forced here) selects the
+    tagged hash, with the same results (the bitmap ignored free HBM)."""
+    n, d = 200_000, 32
+    x = O.fill_uniform(n * d, 91).reshape(n, d)
+    idx = rv.HnswIndex(d, rv.DistanceMetric.Euclidean, rv.HnswConfig(m=8, ef_construction=40, ef_search=40))
+    idx.add_array(x, np.arange(n, dtype=np.uint64))
+    q = O.fill_uniform(2000 * d, 92).reshape(2000, d)
+    ids_a, dist_a, cnt_a = idx.search_array(q, 10, 64)
+    st = rv.core.hnsw_last_search_stats()
+    assert st["visited_bitmap"] and st["slots"] == 2000
+    monkeypatch.setenv("RVX_HNSW_BITMAP_BUDGET_MB", "1")  # 25 KB per slot at 200k nodes -> 41 slots < 1024
+    ids_b, dist_b, cnt_b = idx.search_array(q, 10, 64)
+    st = rv.core.hnsw_last_search_stats()
+    assert not st["visited_bitmap"]
+    assert np.array_equal(ids_a, ids_b) and np.array_equal(dist_a, dist_b) and np.array_equal(cnt_a, cnt_b)

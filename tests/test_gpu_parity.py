@@ -1,11 +1,13 @@
 """GPU parity: the HIP path (through the C ABI) against the CPU oracle.
 
 Bar (north star): bit-exact for integer/index work and top-k ids; within
-1e-5 relative on f32 embeddings. "Relative" here is max|gpu - ref| divided by
-max|ref| over the compared row block (TOL below), i.e. error measured against
-the embedding's scale, plus an element-wise check with an absolute floor.
-Kernels that restate the reference's scalar arithmetic (distances,
-aggregation, generators, differentiable_search) are required to be bit-exact.
+1e-5 relative on f32 embeddings, checked two ways by assert_close
+(tests/parity.py): normwise, max|gpu - ref| / max|ref| over the compared row
+block, and per row, ||gpu_r - ref_r||_2 / ||ref_r||_2 for every row (zero
+reference rows against the largest row norm), which bounds every element by
+1e-5 of its row's norm. Kernels that restate the reference's scalar arithmetic
+(distances, aggregation, generators, differentiable_search) are required to be
+bit-exact.
 """
 import json
 import math
@@ -14,23 +16,12 @@ import numpy as np
 import pytest
 
 import oracle as O
+from parity import assert_close, rel_err, row_rel_err, row_rel_vs  # noqa: F401
 
 rv = pytest.importorskip("ruvector_amd")
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-5
-
-
-def rel_err(a, b):
-    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
-    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-30))
-
-
-def assert_close(a, b, tol=TOL):
-    assert a.shape == b.shape
-    assert np.all(np.isfinite(a)) == np.all(np.isfinite(b))
-    e = rel_err(a, b)
-    assert e <= tol, f"relative error {e:.3e} > {tol}"
 
 
 # ------------------------------------------------------------------ generators
@@ -278,9 +269,8 @@ def test_graphsage_sampling_matches_oracle(k, in_f, out_f, n):
 
 
 @pytest.mark.parametrize("wm,dma,m16", [(4, 1, 0), (8, 1, 0), (8, 0, 0), (4, 1, 1)])
-# out_f = 200 is avoided: with the deterministic init a few rows cancel to a
-# pre-normalisation norm of ~1e-4 (ill-conditioned for any f32 evaluation,
-# the oracle included); 232 gives a ragged 104-column second N-tile.
+# out_f = 200 (ill-conditioned rows) runs in test_graphsage_ill_conditioned_rows_f64_anchor;
+# 232 gives a ragged 104-column second N-tile.
 @pytest.mark.parametrize("in_f,out_f,n", [(768, 768, 600), (96, 232, 1000), (64, 130, 257), (96, 256, 1000),
                                          (128, 232, 1000)])
 def test_graphsage_gemm_tilings(monkeypatch, wm, dma, m16, in_f, out_f, n):
@@ -374,6 +364,35 @@ def sage_forward_f64(x, rp, col, wn, ws, r0, rows):
     return out
 
 
+@pytest.mark.parametrize("gemm", ["h2", "x3"])
+@pytest.mark.parametrize("in_f,out_f,n", [(96, 200, 1000), (768, 200, 600)])
+def test_graphsage_ill_conditioned_rows_f64_anchor(monkeypatch, gemm, in_f, out_f, n):
+    """out_f = 200 with the deterministic init (graphsage.rs:56-78): a few rows cancel to
+    a pre-normalisation norm ~1e-4 times the others, so their L2-normalised output
+    amplifies f32 rounding (the f32 reference-order oracle itself is ~1e-3 off the
+    exact value there). Bar anchored on f64, per row: the GPU's error vs the f64
+    layer is within the oracle's own error + 1e-5, and on rows the oracle evaluates
+    to 1e-6 of the exact value the GPU meets 1e-5 against the oracle."""
+    if gemm == "x3":
+        monkeypatch.setenv("RVX_GEMM_H2", "0")
+    deg = 7
+    x = O.fill_uniform(n * in_f, 5 + n).reshape(n, in_f)
+    rp, col = O.random_csr(n, deg, 31)
+    g = rv.Graph.from_csr(rp, col)
+    layer = rv.GraphSAGELayer(in_f, out_f, num_samples=deg)
+    y = layer.forward_graph(x, g)
+    wn, ws = O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000)
+    ref = O.sage_forward(x, rp, col, wn, ws, 0)
+    ref64 = sage_forward_f64(x, rp, col, wn, ws, 0, n)
+    e_gpu, e_orc = row_rel_vs(y, ref64), row_rel_vs(ref, ref64)
+    assert np.all(e_gpu <= e_orc + 1e-5), float(np.max(e_gpu - e_orc))
+    good = e_orc <= 1e-6
+    assert good.sum() >= 0.9 * n
+    assert_close(y[good], ref[good])
+    print(f"worst row: GPU vs f64 {e_gpu.max():.2e}, oracle vs f64 {e_orc.max():.2e}; "
+          f"{n - good.sum()} ill-conditioned rows")
+
+
 def test_graphsage_chunked_pipeline_and_exchange_entry():
     """n >= 24*16384 rows runs the two-stream row-chunk pipeline (api_graph.cpp
     sage_forward_dev); rvx_sage_forward_exchange at world 1 writes the same rows."""
@@ -406,6 +425,7 @@ def test_graphsage_chunked_pipeline_and_exchange_entry():
         g32 = got[r0:r0 + 3000]
         e_gpu, e_orc = rel_err(g32, ref64), rel_err(ref, ref64)
         assert e_gpu <= e_orc + 1e-5, (r0, e_gpu, e_orc)
+        assert np.all(row_rel_vs(g32, ref64) <= row_rel_vs(ref, ref64) + 1e-5), r0  # the same rule per row
         dense = np.count_nonzero(ref, axis=1) >= d // 4
         assert_close(g32[dense], ref[dense])
         print(f"rows {r0}+3000: GPU vs f64 {e_gpu:.2e}, f32 oracle vs f64 {e_orc:.2e}, GPU vs oracle {rel_err(g32, ref):.2e}")

@@ -196,7 +196,8 @@ def _host_comm_worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     import ctypes as C
     import torch.distributed as dist
-    from ruvector_amd.shard import HostComm
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from host_comm import HostComm
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -208,6 +209,15 @@ def _host_comm_worker(rank, world, port, q):
         nbytes = (C.c_int64 * world)(*[0 if p == rank else sizes[p] * 4 for p in range(world)])
         rc = comm._fn(None, send.ctypes.data, sizes[rank] * 4, ptrs, nbytes)
         ok = rc == 0 and all(np.all(recv[p][:sizes[p]] == 10.0 * p + 1) for p in range(world) if p != rank)
+        # broadcast shape (comm_broadcast_bytes): only the root (rank world-1) sends,
+        # every other rank receives from the root alone
+        root = world - 1
+        blk = np.arange(7, dtype=np.float32) + 100.0
+        got = np.zeros(7, np.float32)
+        ptrs = (C.c_void_p * world)(*[got.ctypes.data if (p == root and rank != root) else None for p in range(world)])
+        nbytes = (C.c_int64 * world)(*[28 if (p == root and rank != root) else 0 for p in range(world)])
+        rc = comm._fn(None, blk.ctypes.data, 28 if rank == root else 0, ptrs, nbytes)
+        ok = ok and rc == 0 and (rank == root or np.array_equal(got, blk))
         q.put((rank, bool(ok)))
     finally:
         dist.destroy_process_group()
