@@ -95,7 +95,10 @@ def run(n=10_000_000, d=768, nq=10_000, k=10, metric_name="l2", cpu_queries=16, 
         fi = np.empty((16, k), np.int64)
         fd = np.empty((16, k), np.float32)
         nfast, fdt = 0, 0.0
-        while nfast + 16 <= nq and (nfast == 0 or fdt < cpu_seconds):
+        if nq < 16:  # the fast leg times 16-query batches; tile the queries up to one batch
+            qb = rv.Buffer.from_numpy(np.resize(qb.download(np.float32, (nq, d)), (16, d)).astype(np.float32))
+            ids = np.resize(ids, (16, k))
+        while nfast + 16 <= max(nq, 16) and (nfast == 0 or fdt < cpu_seconds):
             qq = qb.download(np.float32, (16, d), offset=nfast * d * 4)
             t0 = time.perf_counter()
             O.lib().orc_flat_search_fast(O.fp(x), n, d, mcode, O.fp(qq), 16, k, O.ip64(fi), O.fp(fd), threads)

@@ -339,6 +339,9 @@ struct OHnsw {
     OHnsw() : count_at_level(17) {}
     const float* v(int64_t i) const { return data.data() + i * d; }
     bool fast = false;  // CPU-baseline SIMD distances (not the reference order)
+    // query-path stop rule: (d, id) as the GPU's R-only search (default), or the
+    // reference's distance-only test (hnsw.rs:913-1055, ties in heap order)
+    bool lex_stop = true;
     float dist(const float* a, int64_t j) const {
         return fast ? fast_distance(a, v(j), d, metric) : orc_distance(a, v(j), d, metric);
     }
@@ -496,6 +499,7 @@ void orc_hnsw_free(void* hp) { delete static_cast<OHnsw*>(hp); }
 
 // CPU-baseline fast mode: SIMD distances for build and search (bench only).
 void orc_hnsw_set_fast(void* hp, int32_t on) { static_cast<OHnsw*>(hp)->fast = on != 0; }
+void orc_hnsw_set_lex_stop(void* hp, int32_t on) { static_cast<OHnsw*>(hp)->lex_stop = on != 0; }
 int32_t orc_simd_width() { return g_avx512 ? 512 : 256; }
 
 // Sequential add_batch (index/hnsw.rs:314-319) for nthreads <= 1, otherwise
@@ -546,7 +550,7 @@ void orc_hnsw_search(void* hp, const float* q, int64_t nq, int32_t k, int32_t ef
         const int ef = std::max(ef_arg, k);
         int layer_to_search = 0;
         while (layer_to_search < 16 && h.count_at_level[layer_to_search].load() == 0) ++layer_to_search;
-        const std::vector<Cand> r = search_layer(h, qv, pivot, ef, layer_to_search, /*lex_stop=*/true);
+        const std::vector<Cand> r = search_layer(h, qv, pivot, ef, layer_to_search, h.lex_stop);
         const int last = std::min<int64_t>(std::min(k, ef), (int64_t)r.size());
         for (int s = 0; s < last; ++s) { oi[s] = r[s].id; od[s] = r[s].d; }
         if (out_n) out_n[qi] = last;

@@ -226,6 +226,12 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
                             gemm_h2_ok(std::max<int64_t>(n, 1), l->out, GemmOperand{x, l->in, nullptr, l->in, l->in},
                                        nullptr));
     float* scale = h2 ? scratch_f32("sage_scale", std::max<int64_t>(n, 1)) : nullptr;
+    // the dual GEMM with ReLU + normalisation fused, one block per 64 rows x all columns:
+    // A read once, no normalise pass (k_sage_gemm.hip); same bits as gemm_nt_h2 + normalize_rows
+    const int64_t wplane = (int64_t)l->in * l->out;
+    const bool fused = h2 && !h2p &&
+                       sage_gemm_fused_ok(std::max<int64_t>(n, 1), l->out, l->in, l->in, l->in, l->in, l->in, l->in,
+                                          wplane, wplane, l->out, agg, x + row_offset * l->in, y);
     GemmEpilogue ep;
     ep.epi = GEMM_EPI_RELU;
     // Rows are independent, so the layer runs as a two-stage pipeline over
@@ -276,6 +282,13 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
                         l->ws_h2.as<_Float16>(), scale + r0, l->w_inv.as<float>(), ep, y + r0 * l->out, l->out,
                         "sage_gemm");
             if (l->normalize) normalize_rows(y + r0 * l->out, rows, l->out, true, "sage_normalize");
+            if (hook) hook(c, r0, rows);
+            continue;
+        }
+        if (fused) {
+            sage_gemm_fused(rows, l->out, agg + r0 * l->in, l->in, l->in, x + (row_offset + r0) * l->in, l->in, l->in,
+                            l->wn_h2.as<_Float16>(), l->in, wplane, l->ws_h2.as<_Float16>(), l->in, wplane, scale + r0,
+                            l->w_inv.as<float>(), y + r0 * l->out, l->out, l->normalize != 0, "sage_gemm");
             if (hook) hook(c, r0, rows);
             continue;
         }

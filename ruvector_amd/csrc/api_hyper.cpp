@@ -40,7 +40,7 @@ void insert_rows(rvx_hyperbolic* h, const float* rows, int64_t n, bool on_device
     invalidate_tangent(h);
 }
 
-// queries projected into the ball (search / search_with_pruning, hnsw.rs:409, :449)
+// queries projected into the ball (search / search_with_pruning, hnsw.rs:431, :458)
 float* projected_queries(const rvx_hyperbolic* h, const float* q, int64_t nq, bool on_device) {
     const int d = h->ix.cfg.dim;
     float* dq = scratch_f32("hyp_q", nq * d);
@@ -105,7 +105,7 @@ void search_dev(const rvx_hyperbolic* h, const float* dq, int64_t nq, int k, int
             sync();
         }
     } else if (mode == 2) {
-        // search_with_pruning (hnsw.rs:440-483): tangent-space L2 scan of every
+        // search_with_pruning (hnsw.rs:450-489): tangent-space L2 scan of every
         // point, keep k * prune_factor, exact Poincaré re-rank
         RVX_REQUIRE(ix->cfg.metric == RVX_METRIC_POINCARE, RVX_ERR_UNSUPPORTED,
                     "search_with_pruning is implemented for the Poincaré metric");
@@ -117,7 +117,9 @@ void search_dev(const rvx_hyperbolic* h, const float* dq, int64_t nq, int k, int
         log_map_rows(dq, nq, d, ix->tan_norms.as<float>(), pdev::norm_sq(cen.data(), d), ix->curv, qt);
         float* cdist = scratch_f32("hyp_cand_d", nq * nc);
         auto* cand = (int64_t*)scratch_bytes("hyp_cand_i", nq * nc * 8);
-        scan_topk(RVX_METRIC_L2, qt, nullptr, nq, ix->tan_coords.as<float>(), nullptr, nullptr, ix->n, d, nc, 0, cdist,
+        // tangent_distance_squared (tangent.rs:105-117): the sequential sum without a
+        // square root, ranked (distance, id) as the reference's stable sort
+        scan_topk(METRIC_L2SQ, qt, nullptr, nq, ix->tan_coords.as<float>(), nullptr, nullptr, ix->n, d, nc, 0, cdist,
                   cand, "hyp_tangent_scan");
         rerank(dq, nq, ix->vecs.as<float>(), d, ix->curv, cand, nc, k, rd, rows, counts);
     } else {
@@ -276,7 +278,7 @@ static rvx_status hyp_search_host(const rvx_hyperbolic* h, const float* q, int64
         if (nq == 0) return;
         std::shared_lock<std::shared_mutex> lk(h->ix.mu);
         ComputeLock cl;
-        const int m = (mode == 2 && !h->ix.tan_valid) ? 0 : mode;  // no cache -> regular search (hnsw.rs:441-444)
+        const int m = (mode == 2 && !h->ix.tan_valid) ? 0 : mode;  // no cache -> regular search (hnsw.rs:452-454)
         float* dq = projected_queries(h, q, nq, false);
         auto* di = (int64_t*)scratch_bytes("hyp_out_i", nq * k * 8);
         float* dd = scratch_f32("hyp_out_d", nq * k);
@@ -397,7 +399,7 @@ rvx_status rvx_hyperbolic_build_tangent_cache(rvx_hyperbolic* h) {
     return guard([&] {
         RVX_REQUIRE(h, RVX_ERR_INVALID_PARAMETER, "null argument");
         std::unique_lock<std::shared_mutex> lk(h->ix.mu);
-        if (h->ix.n == 0) return;  // build_tangent_cache: Ok(()) on an empty index (hnsw.rs:487-489)
+        if (h->ix.n == 0) return;  // build_tangent_cache: Ok(()) on an empty index (hnsw.rs:493-495)
         ComputeLock cl;
         build_tangent(h);
     });

@@ -109,13 +109,11 @@ void project_rows(float* x, int64_t n, int d, float c) {
 void poincare_topk(const float* q, int64_t nq, const float* x, int64_t n, int d, float c, int k, float* out_d,
                    int64_t* out_i) {
     if (nq <= 0) return;
-    // the tiled exact scan (k_scan.hip) with the Poincaré metric: |q-x|^2 per
-    // pair in fused_norms' chunked order, squared norms precomputed per row
-    float* qn = scratch_f32("hyp_bf_qn", nq);
-    float* xn = scratch_f32("hyp_bf_xn", n);
-    row_norm_sq(q, nq, d, qn);
-    row_norm_sq(x, n, d, xn);
-    scan_topk(RVX_METRIC_POINCARE, q, qn, nq, x, xn, nullptr, n, d, k, 0, out_d, out_i, "hyp_brute_force", c);
+    // the exact scan (k_scan.hip) with the Poincaré metric: the MFMA filter with
+    // per-row bounds and a reference-order rerank for query batches (K10), else the
+    // tiled VALU scan with |q-x|^2 per pair in fused_norms' chunked order and the
+    // squared norms computed there (K8); identical results either way
+    scan_topk(RVX_METRIC_POINCARE, q, nullptr, nq, x, nullptr, nullptr, n, d, k, 0, out_d, out_i, "hyp_brute_force", c);
 }
 
 void log_map_rows(const float* x, int64_t n, int d, const float* negp_dev, float np_sq, float c, float* out) {

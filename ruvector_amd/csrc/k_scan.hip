@@ -34,7 +34,7 @@ constexpr int TQ = 32, TR = 128, BKD = 32, ROWF = BKD + 4;
 
 template <int METRIC>
 __device__ __forceinline__ float pair_step(float acc, float q, float x) {
-    if (METRIC == RVX_METRIC_L2) { const float d = q - x; return acc + d * d; }
+    if (METRIC == RVX_METRIC_L2 || METRIC == METRIC_L2SQ) { const float d = q - x; return acc + d * d; }
     if (METRIC == RVX_METRIC_L1) return acc + fabsf(q - x);
     return acc + q * x;  // cosine / dot
 }
@@ -362,7 +362,8 @@ struct FCfg {
     static constexpr int THREADS = 64 * 2 * WQ;
     static constexpr int FQ = 64 * WQ, FR = 64 * FM;
     static constexpr int STAGE = (FR + FQ) * FK * 2;  // f16 rows then f16 queries, 64 B per row
-    static constexpr int LDS = F_NSTAGE * STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 8;
+    // + row constants (float4) and per-query {Qs, P} of the per-row-bound metrics
+    static constexpr int LDS = F_NSTAGE * STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 16 + FQ * 8;
     static constexpr int BLOCKS = WIDE ? 1 : 2;
     static_assert(FQ == FR && FR == 32 * THREADS / 64, "DMA pieces assume FR = FQ = 32 x waves");
 };
@@ -379,6 +380,8 @@ struct FilterArgs {
     // shared rejection bound per query (order-encoded float, see below), the
     // result count k and max_x |x|^2 over ALL rows (for eps, as the rerank)
     unsigned* gbound; int k; const unsigned* xsq_max_bits;
+    // per-row-bound metrics (Poincaré, squared L2): row factors {R, C, S, N} and beta
+    const float4* xc4; float beta;
 };
 
 // Order-preserving float <-> uint (atomicMin over possibly negative values).
@@ -436,6 +439,8 @@ template <int METRIC, bool WIDE>
 __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_scan_filter(FilterArgs a) {
     using Cf = FCfg<WIDE>;
     constexpr int FQ = Cf::FQ, FR = Cf::FR, F_STAGE = Cf::STAGE, F_FM = Cf::FM, F_THREADS = Cf::THREADS;
+    // per-row bounds (Poincaré, squared L2; see rows_to_f16_pr): the lists rank lower bounds
+    constexpr bool PRB = METRIC == RVX_METRIC_POINCARE || METRIC == METRIC_L2SQ;
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
     float* best_v = reinterpret_cast<float*>(fsm + F_NSTAGE * F_STAGE);  // [FQ][FKP] ascending (v, row)
     int32_t* best_r = reinterpret_cast<int32_t*>(best_v + FQ * FKP);
@@ -457,6 +462,8 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     const int64_t r_end = min(a.row_end, r_beg + a.rows_per_split);
 
     float2* rowc = reinterpret_cast<float2*>(ovf + 4);              // [FR] current tile's row constants
+    float4* rowc4 = reinterpret_cast<float4*>(ovf + 4);             // [FR] (per-row-bound metrics)
+    float2* qfac = reinterpret_cast<float2*>(rowc4 + FR);           // [FQ] {Qs, P} (per-row-bound metrics)
 
     for (int i = tid; i < FQ * FKP; i += F_THREADS) { best_v[i] = INFINITY; best_r[i] = -1; }
     if (tid < FQ) { cand_n[tid] = 0; thr[tid] = INFINITY; fillc[tid] = 0; }
@@ -470,7 +477,15 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
         qv_[fn] = qg < a.nq;
         const int64_t qc = min(qg, a.nq - 1);
         const float2 c = a.qc[qc];
-        qf_[fn] = query_factor<METRIC>(qv_[fn] ? c.x : __builtin_nanf(""), c.y);  // padding query: NaN
+        if constexpr (PRB) qf_[fn] = -2.0f * (qv_[fn] ? c.x : __builtin_nanf(""));
+        else qf_[fn] = query_factor<METRIC>(qv_[fn] ? c.x : __builtin_nanf(""), c.y);  // padding query: NaN
+    }
+    if constexpr (PRB) {
+        // L = S*|q|^2*(1-beta) + (acc*R)*Q + C + N*P, P = -1.5 2^-9 |q| (the f16 term of the bound)
+        if (tid < FQ) {
+            const float2 c = a.qc[min<int64_t>(q0 + tid, a.nq - 1)];
+            qfac[tid] = make_float2(c.y * (1.0f - a.beta), -0x1.8p-9f * sqrtf(c.y));
+        }
     }
     // Shared rejection bound (lanes tid < FQ, one query each). A split's list
     // holding k entries proves v_k <= its k-th value, so B_q = min over splits
@@ -559,12 +574,33 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     // query per round are bounded (FCB), so rounds repeat with the tightened
     // thresholds until no offer overflowed (thresholds only fall, so a
     // rejection is final and needs no mark).
-    auto epilogue = [&](int64_t rt, float2 pre) {
+    auto epilogue = [&](int64_t rt, float4 pre) {
         gb = fminf(gb, ord_dec(graw));  // read at the end of the last tile: its wait lands on the drain below
         if (tid < FQ) thr[tid] = fminf(thr[tid], next_up(gb));  // admit v <= B_q
-        if (tid < FR) rowc[tid] = row_factors<METRIC>(pre);
+        if (tid < FR) {
+            if constexpr (PRB) rowc4[tid] = pre;
+            else rowc[tid] = row_factors<METRIC>(make_float2(pre.x, pre.y));
+        }
         __syncthreads();
         float vmin[2] = {INFINITY, INFINITY};
+        if constexpr (PRB) {
+            float2 qsp[2];
+#pragma unroll
+            for (int fn = 0; fn < 2; ++fn) qsp[fn] = qfac[wn * 64 + fn * 32 + lr];
+#pragma unroll
+            for (int fm = 0; fm < F_FM; ++fm)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const float4 c = rowc4[wm * WROWS + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh];
+#pragma unroll
+                    for (int fn = 0; fn < 2; ++fn) {
+                        const float v = __builtin_fmaf(
+                            c.w, qsp[fn].y, __builtin_fmaf(c.z, qsp[fn].x, __builtin_fmaf(acc[fm][fn][e] * c.x, qf_[fn], c.y)));
+                        acc[fm][fn][e] = v;
+                        vmin[fn] = fminf(vmin[fn], v);
+                    }
+                }
+        } else {
 #pragma unroll
         for (int fm = 0; fm < F_FM; ++fm)
 #pragma unroll
@@ -577,6 +613,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
                     vmin[fn] = fminf(vmin[fn], v);  // NaN-ignoring: an all-NaN lane stays NaN
                 }
             }
+        }
         // Fast path: no value of the tile is below its query's threshold -> one
         // compare per query, no offers (with 256 queries per tile most tiles still
         // admit something).
@@ -642,7 +679,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
                 }
                 fillc[ql] = fill_n;
                 cand_n[ql] = 0;
-                if (gq_own && fill_n >= a.k) {
+                if (!PRB && gq_own && fill_n >= a.k) {
                     const float ub = bv[a.k - 1] + 2.0f * geps;
                     if (ub < gb) {
                         gb = ub;
@@ -742,7 +779,13 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     int64_t it = 0;
     for (int64_t rt = r_beg; rt < r_end; rt += FR) {
         // the tile's row constants, consumed by its epilogue
-        const float2 pre = (tid < FR && rt + tid < r_end) ? a.xc[rt + tid - a.row0] : make_float2(NAN, 0.0f);
+        float4 pre;
+        if constexpr (PRB) {
+            pre = (tid < FR && rt + tid < r_end) ? a.xc4[rt + tid - a.row0] : make_float4(NAN, 0.0f, 0.0f, 0.0f);
+        } else {
+            const float2 p2 = (tid < FR && rt + tid < r_end) ? a.xc[rt + tid - a.row0] : make_float2(NAN, 0.0f);
+            pre = make_float4(p2.x, p2.y, 0.0f, 0.0f);
+        }
         if (rt + FR < r_end) nxt_src = tile_src(rt + FR);
         if (unrolled) {
             for (int kt = 0; kt < nk; kt += F_NSTAGE, it += F_NSTAGE)
@@ -885,6 +928,221 @@ __global__ __launch_bounds__(256) void k_scan_rerank(RerankArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Per-row bounds (Poincaré distance and the tangent scan's squared L2).
+//
+// The global eps above bounds |v - reference| with max_x |x| for every row. That
+// is tight for rows of similar norm (10M x 768 N(0,1)) but not for the C5 data,
+// where the nearest rows (small radius, or the tangent coordinates of such
+// points) are far shorter than the longest row, and for the Poincaré distance
+// the ranking quantity carries a per-row factor. Here every (row, query) value
+// is a LOWER bound L of the reference's own ranking quantity T, with the row's
+// own norm in the bound:
+//   |x.q - x^.q^/(t_x t_q)| <= 2^-10 |x||q| (f16 rounding) + f32 accumulation
+//   |T_sum - |q-x|^2| <= (d+2) 2^-24 (|q|^2+|x|^2)  (the reference's f32 sum, and
+//                                                    the |x|^2 / |q|^2 estimates)
+//   E = 1.5 2^-9 |q||x| + beta (|q|^2+|x|^2),  beta = 2^-12 max(1, d/1024)
+//   (v = |x|^2 - 2 x.q carries twice the dot's 1.06 2^-10 |x||q|: 1.4x slack; beta 1.3x)
+//   squared L2 (tangent_distance_squared): T = sum (q-x)^2 in [|q|^2+v-E, |q|^2+v+E],
+//     v = |x|^2 - 2 x.q from the MFMA dot
+//   Poincaré: arg - 1 = 2c |q-x|^2 / (lambda_q lambda_x) with lambda_q fixed per query,
+//     so the ranking is T = s_x |q-x|^2, s_x = 1/max(1 - c|x|^2, 1e-5), known to
+//     relative delta_s = (c 2^-13 |x|^2 + 2^-22) / lambda_x (the reference's |x|^2
+//     sum and the subtraction), widened by rho = 2^-13 for the reference's own
+//     rounding of arg and fast_acosh (at most a few ulp, and the 8e-6 relative jump
+//     at its delta = 1e-4 branch): T in [s_lo (|q|^2+v-E), s_hi (|q|^2+v+E)].
+// Rows whose delta_s exceeds 2^-6 (points on the ball's edge) send the call to
+// the VALU scan. Next to distance 0 the Poincaré distance is quantised by the f32
+// rounding of arg = 1 + (2c/lambda_q) T (ties broken by id), so the rerank widens Uk by
+// 2^-22 (1/2c + Uk) there. L = s_lo (|q|^2 (1-beta) + |x|^2 (1-beta) - 2 x.q - 1.5 2^-9|q||x|)
+// is one multiply and three FMAs per value from row factors {R = s_lo/t_x,
+// C = s_lo |x|^2 (1-beta), S = s_lo, N = s_lo |x|} and query factors {Q = -2/t_q,
+// Qs = |q|^2 (1-beta), P = -1.5 2^-9 |q|}. The rerank rebuilds each listed row's
+// upper bound U = s_hi (L/s_lo + 2.0625 E) (the 1/32 covers the f32 rounding of L),
+// takes Uk = k-th smallest U, and computes the reference distance of every listed
+// row with L <= Uk; a split whose full list ends at or below Uk may have dropped a
+// needed row and the query goes to the VALU scan.
+__global__ __launch_bounds__(256) void k_rows_to_f16_pr(const float* __restrict__ x, int64_t n, int d,
+                                                       _Float16* __restrict__ xh, float4* __restrict__ rc4,
+                                                       float4* __restrict__ rb, const uint8_t* __restrict__ deleted,
+                                                       float c, float beta, int32_t* bad) {
+    typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    bool run_ok = true;
+    for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < n; row += nwaves) {
+        const float* xr = x + row * d;
+        float m = 0.0f, s = 0.0f;
+        bool fin = true;
+        for (int k = 4 * lane; k < d; k += 256) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + k);
+            fin = fin && __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z) &&
+                  __builtin_isfinite(v.w);
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+            s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            m = fmaxf(m, __shfl_xor(m, o));
+            s += __shfl_xor(s, o);
+        }
+        fin = !__any(!fin);
+        const float t = h2_scale_dev(m);
+        for (int k = 4 * lane; k < d; k += 256) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + k);
+            h16x4 h = {(_Float16)(v.x * t), (_Float16)(v.y * t), (_Float16)(v.z * t), (_Float16)(v.w * t)};
+            *reinterpret_cast<h16x4*>(xh + row * d + k) = h;
+        }
+        float s_lo = 1.0f, s_hi = 1.0f;
+        bool ok = true;
+        if (c > 0.0f) {  // Poincaré: s_x = 1 / max(1 - c|x|^2, EPS)
+            const float lam = fmaxf(1.0f - c * s, pdev::EPS);
+            const float ds = (c * s * 0x1p-13f + 0x1p-22f) / lam;
+            ok = ds <= 0x1p-6f;
+            const float sx = 1.0f / lam;
+            s_lo = sx * (1.0f - ds) * (1.0f - 0x1p-13f);
+            s_hi = sx * (1.0f + ds) * (1.0f + 0x1p-13f);
+        }
+        const float nrm = sqrtf(s);
+        if (lane == 0) {
+            const bool del = deleted && deleted[row];
+            rc4[row] = make_float4(del ? NAN : s_lo / t, s_lo * s * (1.0f - beta), s_lo, s_lo * nrm);
+            rb[row] = make_float4(s_lo, s_hi, s, nrm);
+        }
+        run_ok = run_ok && ok && fin && __builtin_isfinite(s) && (m == 0.0f || (ilogbf(m) >= -60 && ilogbf(m) <= 60));
+    }
+    if (lane == 0 && !run_ok) atomicOr(bad, 1);
+}
+
+struct RerankPrArgs {
+    const float* q; const float2* qc;  // queries and {1/t_q, |q|^2}
+    const float* x; const float4* rb;  // rows and {s_lo, s_hi, |x|^2, |x|} of every row
+    int64_t nq; int d, k, nsplit_total;
+    const float* part_v; const int32_t* part_r;
+    float beta, curv;
+    int64_t id_offset;
+    float* out_d; int64_t* out_i; int32_t* unsure;
+};
+
+// one wave per query: Uk, candidates, reference distances, top-k by (distance, id)
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_scan_rerank_pr(RerankPrArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (qi >= a.nq) return;
+    const int total = a.nsplit_total * FKP;
+    const float* pv = a.part_v + qi * total;
+    const int32_t* pr = a.part_r + qi * total;
+    const float q2 = a.qc[qi].y, qn = sqrtf(q2);
+    float l[F_MAXE], u[F_MAXE];
+    int32_t r[F_MAXE];
+#pragma unroll
+    for (int j = 0; j < F_MAXE; ++j) {
+        const int c = lane + 64 * j;
+        const bool ok = c < total && pr[c] >= 0;
+        l[j] = ok ? pv[c] : INFINITY;
+        r[j] = ok ? pr[c] : INT32_MAX;
+        u[j] = INFINITY;
+        if (ok) {
+            const float4 b = a.rb[r[j]];
+            const float e = 0x1.8p-9f * qn * b.w + a.beta * (q2 + b.z);
+            u[j] = b.y * (l[j] / b.x + 2.0625f * e);
+        }
+    }
+    // k-th smallest upper bound (rows are distinct across lists)
+    float lu = -INFINITY, uk = INFINITY;
+    int32_t lrow = INT32_MIN;
+    for (int s = 0; s < a.k; ++s) {
+        float bu = INFINITY;
+        int32_t brr = INT32_MAX;
+#pragma unroll
+        for (int j = 0; j < F_MAXE; ++j) {
+            const bool after = u[j] > lu || (u[j] == lu && r[j] > lrow);
+            if (after && lt_vr(u[j], r[j], bu, brr)) { bu = u[j]; brr = r[j]; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ou = __shfl_xor(bu, o);
+            const int32_t orr = __shfl_xor(brr, o);
+            if (lt_vr(ou, orr, bu, brr)) { bu = ou; brr = orr; }
+        }
+        lu = bu;
+        lrow = brr;
+        uk = bu;
+    }
+    // Poincaré: arg = 1 + (2c/lambda_q) T is rounded to f32 next to 1, so rows whose T
+    // differ by less than ~ulp(arg) lambda_q / 2c share one distance (all T below
+    // 2^-24 lambda_q / 2c give distance 0) and are ordered by id: a row ties with the
+    // k-th while its T exceeds Uk by up to 2^-23 (lambda_q / 2c + T) (both roundings
+    // and the division's); 2x slack.
+    const float thr = (METRIC == RVX_METRIC_POINCARE) ? uk + 0x1p-22f * (0.5f / a.curv + fabsf(uk)) : uk;
+    bool unsure = false;
+    for (int s = lane; s < a.nsplit_total; s += 64) {
+        const int c = s * FKP + FKP - 1;
+        if (pr[c] >= 0 && pv[c] <= thr) unsure = true;
+    }
+    if (__any(unsure)) {
+        if (lane == 0) {
+            a.unsure[qi] = 1;
+            atomicAdd(a.unsure - 2, 1);
+        }
+        return;
+    }
+    const float* qrow = a.q + qi * a.d;
+    float ex[F_MAXE];
+#pragma unroll
+    for (int j = 0; j < F_MAXE; ++j) {
+        ex[j] = INFINITY;
+        if (r[j] == INT32_MAX || !(l[j] <= thr)) continue;
+        const float* xr = a.x + (int64_t)r[j] * a.d;
+        if constexpr (METRIC == RVX_METRIC_POINCARE) {  // fused_norms chunk order, then from_norms (as K8)
+            float ds = 0.0f, nu = 0.0f, nv = 0.0f;
+            for (int kk = 0; kk < a.d; kk += 4) {
+                const float4 qv = *reinterpret_cast<const float4*>(qrow + kk);
+                const float4 xv = *reinterpret_cast<const float4*>(xr + kk);
+                const float d0 = qv.x - xv.x, d1 = qv.y - xv.y, d2 = qv.z - xv.z, d3 = qv.w - xv.w;
+                ds = ds + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
+                nu = nu + (((qv.x * qv.x + qv.y * qv.y) + qv.z * qv.z) + qv.w * qv.w);
+                nv = nv + (((xv.x * xv.x + xv.y * xv.y) + xv.z * xv.z) + xv.w * xv.w);
+            }
+            ex[j] = pdev::from_norms(ds, nu, nv, a.curv);
+        } else {  // tangent_distance_squared: sequential sum of (q - x)^2
+            float acc = 0.0f;
+            for (int kk = 0; kk < a.d; kk += 4) {
+                const float4 qv = *reinterpret_cast<const float4*>(qrow + kk);
+                const float4 xv = *reinterpret_cast<const float4*>(xr + kk);
+                acc = pair_step<METRIC_L2SQ>(acc, qv.x, xv.x);
+                acc = pair_step<METRIC_L2SQ>(acc, qv.y, xv.y);
+                acc = pair_step<METRIC_L2SQ>(acc, qv.z, xv.z);
+                acc = pair_step<METRIC_L2SQ>(acc, qv.w, xv.w);
+            }
+            ex[j] = acc;
+        }
+    }
+    float ld = -INFINITY;
+    int64_t li = INT64_MIN;
+    for (int s = 0; s < a.k; ++s) {
+        float bd = INFINITY;
+        int64_t bi = INT64_MAX;
+#pragma unroll
+        for (int j = 0; j < F_MAXE; ++j) {
+            const int64_t id = r[j] == INT32_MAX ? INT64_MAX : (int64_t)r[j] + a.id_offset;
+            if (ex[j] == INFINITY && id == INT64_MAX) continue;
+            const bool after = ex[j] > ld || (ex[j] == ld && id > li);
+            if (after && better(ex[j], id, bd, bi)) { bd = ex[j]; bi = id; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float od = __shfl_xor(bd, o);
+            const int64_t oi = __shfl_xor(bi, o);
+            if (better(od, oi, bd, bi)) { bd = od; bi = oi; }
+        }
+        if (lane == 0) { a.out_d[qi * a.k + s] = bd; a.out_i[qi * a.k + s] = bi; }
+        ld = bd;
+        li = bi;
+    }
+}
+
 // Waves stride over rows: power-of-two scale t (row max in [2^14, 2^15)),
 // f16(x*t), and the row constants {1/t, or NaN for a deleted row; cnorm[row]
 // when given (cosine) else sum x^2 (any order; only the filter uses it)}, the
@@ -988,17 +1246,22 @@ void scan_topk_valu(int metric, const float* q, const float* qnorm, int64_t nq, 
 
 // Returns false (nothing written) when the call should take the VALU scan.
 bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
-                    const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i) {
+                    const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
+                    float curv) {
     const int mode = env_int("RVX_SCAN_MFMA", 1);  // 0 off, 1 auto, 2 force (tests); read per call
     if (mode == 0) return false;
-    if (metric != RVX_METRIC_L2 && metric != RVX_METRIC_COSINE && metric != RVX_METRIC_DOT) return false;
+    const bool prb = metric == RVX_METRIC_POINCARE || metric == METRIC_L2SQ;  // per-row bounds
+    if (metric != RVX_METRIC_L2 && metric != RVX_METRIC_COSINE && metric != RVX_METRIC_DOT && !prb) return false;
+    if (metric == RVX_METRIC_POINCARE && !(curv > 0.0f)) return false;
     // tile shape: RVX_SCAN_WIDE 0/1 forces it (tests), else 256^2 for d >= 512
     const int wide_env = env_int("RVX_SCAN_WIDE", -1);
     const bool wide = wide_env >= 0 ? wide_env != 0 : d >= 512;
     const int FR = wide ? FCfg<true>::FR : FCfg<false>::FR, FQ = wide ? FCfg<true>::FQ : FCfg<false>::FQ;
     const int F_LDS = wide ? FCfg<true>::LDS : FCfg<false>::LDS;
     const int F_THREADS = wide ? FCfg<true>::THREADS : FCfg<false>::THREADS;
-    if (d % FK != 0 || k > FKP || n >= ((int64_t)1 << 31) - FR || nq <= 0 || n <= 0) return false;
+    // k > FKP: the lists stay FKP long (no single split proves a k-th value, so the
+    // shared bound is off) and the rerank's completeness test decides per query
+    if (d % FK != 0 || k > SCAN_MAX_K || n >= ((int64_t)1 << 31) - FR || nq <= 0 || n <= 0) return false;
     if (metric == RVX_METRIC_COSINE && (!qnorm || !xnorm)) return false;
     if (mode == 1 && (nq < 256 || n < 65536)) return false;
     // rows converted per chunk: the f16 image of the whole table when it fits
@@ -1034,6 +1297,10 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
         const double t = (double)waves * ((double)tiles / (double)s + 8.0);
         if (t < best_t * (1.0 - 1e-9)) { best_t = t; s_c = s; }
     }
+    // k beyond one list: as many splits as the rerank holds (down to 2 tiles per
+    // split), so the candidates spread over many FKP-long lists and few queries
+    // find a list full inside their window (C5 tangent scan: k * prune_factor = 100)
+    if (k > FKP) s_c = std::max<int64_t>(s_c, std::min<int64_t>(max_splits / nchunks, std::max<int64_t>(1, tiles / 2)));
     int64_t rows_per_split = ((chunk_rows + s_c - 1) / s_c + FR - 1) / FR * FR;
     s_c = (chunk_rows + rows_per_split - 1) / rows_per_split;
     const int nsplit_total = (int)(nchunks * s_c);
@@ -1050,6 +1317,9 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     RVX_HIP(hipMemsetAsync(flags, 0, (size_t)(16 + nq * 4), stream()));
     unsigned* gbound = (unsigned*)scratch_bytes("mscan_gbound", nq * 4);
     RVX_HIP(hipMemsetD32Async((hipDeviceptr_t)gbound, 0xFF800000u, (size_t)nq, stream()));  // ord_enc(+INF)
+    float4* xc4 = prb ? (float4*)scratch_bytes("mscan_xc4", chunk_rows * 16) : nullptr;
+    float4* rb = prb ? (float4*)scratch_bytes("mscan_rb", n * 16) : nullptr;
+    const float beta = 0x1p-12f * std::max(1.0f, (float)d / 1024.0f);
 
     static bool attr = false;
     if (!attr) {
@@ -1057,6 +1327,8 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
         RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<M, W>, hipFuncAttributeMaxDynamicSharedMemorySize, FCfg<W>::LDS))
         RVX_FILTER_ATTR(RVX_METRIC_L2, true); RVX_FILTER_ATTR(RVX_METRIC_COSINE, true); RVX_FILTER_ATTR(RVX_METRIC_DOT, true);
         RVX_FILTER_ATTR(RVX_METRIC_L2, false); RVX_FILTER_ATTR(RVX_METRIC_COSINE, false); RVX_FILTER_ATTR(RVX_METRIC_DOT, false);
+        RVX_FILTER_ATTR(RVX_METRIC_POINCARE, true); RVX_FILTER_ATTR(METRIC_L2SQ, true);
+        RVX_FILTER_ATTR(RVX_METRIC_POINCARE, false); RVX_FILTER_ATTR(METRIC_L2SQ, false);
 #undef RVX_FILTER_ATTR
         attr = true;
     }
@@ -1064,25 +1336,36 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     rows_to_f16(q, nq, d, qh, qc, cos ? qnorm : nullptr, nullptr, nullptr, flags);
     // the filter's shared bound needs eps from max |x|^2 over every row before
     // the first chunk's filter (cosine: eps is a constant)
-    if (nchunks > 1 && !cos) row_sq_max(x, n, d, max_bits);
+    if (nchunks > 1 && !cos && !prb) row_sq_max(x, n, d, max_bits);
     for (int64_t c = 0; c < nchunks; ++c) {
         const int64_t c0 = c * chunk_rows, c1 = std::min(n, c0 + chunk_rows);
-        rows_to_f16(x + c0 * d, c1 - c0, d, xh, xc, cos ? xnorm + c0 : nullptr, deleted ? deleted + c0 : nullptr,
-                    max_bits, flags);
+        if (prb) {
+            const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((c1 - c0 + 3) / 4, 4096));
+            RVX_LAUNCH("scan_f16", k_rows_to_f16_pr, dim3((unsigned)blocks), dim3(256), 0, x + c0 * d, c1 - c0, d, xh, xc4,
+                       rb + c0, deleted ? deleted + c0 : nullptr, metric == RVX_METRIC_POINCARE ? curv : 0.0f, beta,
+                       flags);
+        } else {
+            rows_to_f16(x + c0 * d, c1 - c0, d, xh, xc, cos ? xnorm + c0 : nullptr, deleted ? deleted + c0 : nullptr,
+                        max_bits, flags);
+        }
         FilterArgs fa{xh, xc, qh, qc, nq, c0, c1, d, rows_per_split, (int)(c * s_c), (int)qtiles, nsplit_total,
-                      part_v, part_r, gbound, k, max_bits};
+                      part_v, part_r, gbound, k, max_bits, xc4, beta};
         const dim3 grid((unsigned)(qtiles * s_c));
         const dim3 blk((unsigned)F_THREADS);
         if (wide) {
             switch (metric) {
                 case RVX_METRIC_L2: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, true>), grid, blk, F_LDS, fa); break;
                 case RVX_METRIC_COSINE: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, true>), grid, blk, F_LDS, fa); break;
+                case RVX_METRIC_POINCARE: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, true>), grid, blk, F_LDS, fa); break;
+                case METRIC_L2SQ: RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, true>), grid, blk, F_LDS, fa); break;
                 default: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, true>), grid, blk, F_LDS, fa); break;
             }
         } else {
             switch (metric) {
                 case RVX_METRIC_L2: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, false>), grid, blk, F_LDS, fa); break;
                 case RVX_METRIC_COSINE: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, false>), grid, blk, F_LDS, fa); break;
+                case RVX_METRIC_POINCARE: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, false>), grid, blk, F_LDS, fa); break;
+                case METRIC_L2SQ: RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, false>), grid, blk, F_LDS, fa); break;
                 default: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, false>), grid, blk, F_LDS, fa); break;
             }
         }
@@ -1090,6 +1373,11 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     RerankArgs ra{q, qnorm, qc, x, xnorm, nq, d, k, nsplit_total, part_v, part_r, max_bits, id_offset, out_d, out_i,
                   unsure};
     const dim3 rg((unsigned)((nq + 3) / 4));
+    if (prb) {
+        RerankPrArgs rp{q, qc, x, rb, nq, d, k, nsplit_total, part_v, part_r, beta, curv, id_offset, out_d, out_i, unsure};
+        if (metric == RVX_METRIC_POINCARE) RVX_LAUNCH("scan_rerank", k_scan_rerank_pr<RVX_METRIC_POINCARE>, rg, dim3(256), 0, rp);
+        else RVX_LAUNCH("scan_rerank", k_scan_rerank_pr<METRIC_L2SQ>, rg, dim3(256), 0, rp);
+    } else
     switch (metric) {
         case RVX_METRIC_L2: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_L2>, rg, dim3(256), 0, ra); break;
         case RVX_METRIC_COSINE: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_COSINE>, rg, dim3(256), 0, ra); break;
@@ -1126,14 +1414,24 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     int32_t* didx = (int32_t*)scratch_bytes("mscan_redo_idx", cnt * 4);
     RVX_HIP(hipMemcpyAsync(didx, redo.data(), (size_t)cnt * 4, hipMemcpyHostToDevice, stream()));
     float* rq = scratch_f32("mscan_redo_q", cnt * d);
-    float* rqn = metric == RVX_METRIC_COSINE ? scratch_f32("mscan_redo_qn", cnt) : nullptr;
+    const bool pc = metric == RVX_METRIC_POINCARE;
+    float* rqn = (metric == RVX_METRIC_COSINE || pc) ? scratch_f32("mscan_redo_qn", cnt) : nullptr;
     float* rd = scratch_f32("mscan_redo_d", cnt * k);
     int64_t* ri = (int64_t*)scratch_bytes("mscan_redo_i", cnt * k * 8);
     RVX_LAUNCH("scan_gather", k_gather_rows, dim3((unsigned)((cnt * d + 255) / 256)), dim3(256), 0, q, didx, cnt, d, rq);
-    if (rqn)
+    if (rqn && !pc)
         RVX_LAUNCH("scan_gather", k_gather_rows, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, qnorm, didx, cnt, 1,
                    rqn);
-    scan_topk_valu(metric, rq, rqn, cnt, x, xnorm, deleted, n, d, k, id_offset, rd, ri, "scan_fallback", 1.0f);
+    const float* xn = xnorm;
+    if (pc) {  // the VALU Poincaré scan takes squared norms in norm_squared's chunk order
+        row_norm_sq(rq, cnt, d, rqn);
+        if (!xn) {
+            float* t = scratch_f32("mscan_redo_xn", n);
+            row_norm_sq(x, n, d, t);
+            xn = t;
+        }
+    }
+    scan_topk_valu(metric, rq, rqn, cnt, x, xn, deleted, n, d, k, id_offset, rd, ri, "scan_fallback", curv);
     RVX_LAUNCH("scan_gather", k_scatter_topk, dim3((unsigned)((cnt * k + 255) / 256)), dim3(256), 0, rd, ri, didx, cnt,
                k, out_d, out_i);
     return true;
@@ -1177,7 +1475,15 @@ void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const
         RVX_HIP(hipMemsetAsync(out_i, 0xFF, (size_t)(nq * k * 8), stream()));
         return;
     }
-    if (scan_topk_mfma(metric, q, qnorm, nq, x, xnorm, deleted, n, d, k, id_offset, out_d, out_i)) return;
+    if (scan_topk_mfma(metric, q, qnorm, nq, x, xnorm, deleted, n, d, k, id_offset, out_d, out_i, curv)) return;
+    if (metric == RVX_METRIC_POINCARE && (!qnorm || !xnorm)) {  // squared norms for the VALU scan (K8)
+        float* qn = scratch_f32("scan_pc_qn", nq);
+        float* xn = scratch_f32("scan_pc_xn", n);
+        row_norm_sq(q, nq, d, qn);
+        row_norm_sq(x, n, d, xn);
+        qnorm = qn;
+        xnorm = xn;
+    }
     scan_topk_valu(metric, q, qnorm, nq, x, xnorm, deleted, n, d, k, id_offset, out_d, out_i, tag, curv);
 }
 
@@ -1207,6 +1513,7 @@ void scan_topk_valu(int metric, const float* q, const float* qnorm, int64_t nq, 
         RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<RVX_METRIC_HYP_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_topk<METRIC_L2SQ>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr_done = true;
     }
     const dim3 grid((unsigned)qtiles, (unsigned)nchunks);
@@ -1218,6 +1525,7 @@ void scan_topk_valu(int metric, const float* q, const float* qnorm, int64_t nq, 
         case RVX_METRIC_L1: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_L1>, grid, dim3(256), lds, a); break;
         case RVX_METRIC_POINCARE: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_POINCARE>, grid, dim3(256), lds, a); break;
         case RVX_METRIC_HYP_L2: RVX_LAUNCH(t, k_scan_topk<RVX_METRIC_HYP_L2>, grid, dim3(256), lds, a); break;
+        case METRIC_L2SQ: RVX_LAUNCH(t, k_scan_topk<METRIC_L2SQ>, grid, dim3(256), lds, a); break;
         default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by the flat scan");
     }
     RVX_LAUNCH("scan_merge", k_merge_topk, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, part_d, part_i, nq,

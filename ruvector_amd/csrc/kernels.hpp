@@ -67,6 +67,15 @@ void split_h2_rows(const float* B0, const float* B1, int N, int K, _Float16* P0,
 // ---- data generators (k_data.hip) ---------------------------------------
 void fill_uniform(float* p, int64_t n, uint64_t seed, float lo, float hi);
 void fill_uniform_at(float* p, int64_t n, uint64_t seed, int64_t first, float lo, float hi);
+// GraphSAGE dual GEMM with ReLU + row L2 normalisation fused, one block per 64 rows x
+// all N columns (k_sage_gemm.hip; N in {256, 512, 768, 1024}); bit-identical to
+// gemm_nt_h2 + normalize_rows. RVX_SAGE_FUSED=0 turns it off (read per call).
+bool sage_gemm_fused_ok(int64_t M, int N, int K0, int K1, int64_t lda0, int64_t lda1, int64_t ldb0, int64_t ldb1,
+                        int64_t plane0, int64_t plane1, int64_t ldc, const void* A0, const void* A1, const void* C);
+void sage_gemm_fused(int64_t M, int N, const float* A0, int64_t lda0, int K0, const float* A1, int64_t lda1, int K1,
+                     const _Float16* B0h, int64_t ldb0, int64_t plane0, const _Float16* B1h, int64_t ldb1,
+                     int64_t plane1, const float* a_scale, const float* b_inv, float* C, int64_t ldc, bool normalize,
+                     const char* tag);
 void fill_normal(float* p, int64_t n, uint64_t seed);
 void fill_ball_rows(float* p, int64_t rows, int dim, uint64_t seed, int64_t first_row, float rmax);
 void normalize_rows(float* p, int64_t rows, int dim, bool divide_only_if_positive, const char* tag);

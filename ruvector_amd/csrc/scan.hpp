@@ -5,6 +5,10 @@
 namespace rvx {
 
 constexpr int SCAN_MAX_K = 128;
+// Internal metric id (not in rvx.h): squared L2 as a sequential f32 sum without the
+// square root, TangentCache::tangent_distance_squared (crates/ruvector-hyperbolic-
+// hnsw/src/tangent.rs:105-117), the ranking of search_with_pruning's tangent scan.
+constexpr int METRIC_L2SQ = 16;
 
 // Path of the most recent scan_topk call (rvx_scan_last_stats).
 struct ScanStats {

@@ -95,11 +95,14 @@ class VectorDB:
             raise RuvectorError(1, f"DimensionMismatch expected {self.options.dimensions} actual {v.size}")
 
     def _store(self, entries: Sequence[VectorEntry]) -> List[str]:
-        vecs = [L.f32c(e.vector).reshape(-1) for e in entries]
-        for v in vecs:  # storage validates every entry before storing any (storage_memory.rs:67-75)
-            self._check_dim(v)
+        """MemoryStorage::insert_batch (storage_memory.rs:68-99): entries are stored one
+        at a time and the first one of the wrong dimension returns DimensionMismatch;
+        the entries before it stay stored (and, as VectorDB::insert_batch returns
+        before index.add_batch, vector_db.rs:154-165, are never indexed)."""
         ids = []
-        for e, v in zip(entries, vecs):
+        for e in entries:
+            v = L.f32c(e.vector).reshape(-1)
+            self._check_dim(v)
             if e.id is not None:
                 vid = e.id
             else:
@@ -131,7 +134,7 @@ class VectorDB:
         return self.insert_batch([entry])[0]
 
     def insert_batch(self, entries: Sequence[VectorEntry]) -> List[str]:
-        """VectorDB::insert_batch (vector_db.rs:149-163)."""
+        """VectorDB::insert_batch (vector_db.rs:154-168)."""
         with self._lock:
             if not entries:
                 return []

@@ -38,6 +38,7 @@ _SIG = {
     "orc_hnsw_new": (P, [I64, I32, I32, I32, I32, U64]),
     "orc_hnsw_free": (None, [P]),
     "orc_hnsw_set_fast": (None, [P, I32]),
+    "orc_hnsw_set_lex_stop": (None, [P, I32]),
     "orc_simd_width": (I32, []),
     "orc_flat_search_fast": (None, [PF, I64, I64, I32, PF, I64, I32, PI64, PF, I32]),
     "orc_hnsw_insert": (None, [P, PF, I64, I32]),
@@ -165,13 +166,17 @@ class Hnsw:
         v = f32(vecs)
         lib().orc_hnsw_insert(self._h, fp(v), v.shape[0], threads)
 
-    def search(self, q, k, ef, threads=8):
+    def search(self, q, k, ef, threads=8, lex_stop=True):
+        """lex_stop False: the reference's distance-only stop test (hnsw.rs:913-1055)
+        instead of the (d, id) rule the GPU search shares."""
         q = f32(q)
         nq = q.shape[0]
         ids = np.empty((nq, k), np.int64)
         d = np.empty((nq, k), np.float32)
         cnt = np.empty(nq, np.int32)
+        lib().orc_hnsw_set_lex_stop(self._h, int(bool(lex_stop)))
         lib().orc_hnsw_search(self._h, fp(q), nq, k, ef, ip64(ids), fp(d), ip32(cnt), threads)
+        lib().orc_hnsw_set_lex_stop(self._h, 1)
         return ids, d, cnt
 
     def export(self):

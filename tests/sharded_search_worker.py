@@ -82,6 +82,7 @@ def main():
         h.load_graph(orc[rank].export())
         grp = rv.ShardedHyperbolicSearch(h, comm, o0)
         checks = {}
+        expect = {}
         for k, ef in ((10, 0), (5, 100), (1, 0)):
             gid, lid, gd, cnt = grp.search_batch(qa, k, ef)
             parts = []
@@ -91,6 +92,7 @@ def main():
             ei, ed = merge(parts, k)
             owner = np.searchsorted(offsets, np.maximum(ei, 0), side="right") - 1
             el = np.where(ei >= 0, ei - np.asarray(offsets)[owner], -1)
+            expect[(k, ef)] = ei
             checks[f"search_k{k}_ef{ef}"] = bool(
                 np.array_equal(gid, ei) and np.array_equal(lid, el) and close(gd, ed) and
                 np.array_equal(cnt, (ei >= 0).sum(1)))
@@ -100,9 +102,10 @@ def main():
                  for s, o in enumerate(orc) for oi, od in [o.brute_force(q, 10)]]
         ei, ed = merge(parts, 10)
         checks["exact_k10"] = bool(np.array_equal(gid, ei) and close(gd, ed))
-        one = grp.search(q[3] if rank == 0 else None, 10)
-        checks["shape"] = all(g == int(ei[3, j]) and r.id == g - offsets[int(np.searchsorted(offsets, g, "right")) - 1]
-                              for j, (g, r) in enumerate(one)) and len(one) == int((ei[3] >= 0).sum())
+        one = grp.search(q[3] if rank == 0 else None, 10)  # shard.search = graph search (hnsw.rs:427)
+        e10 = expect[(10, 0)]
+        checks["shape"] = all(g == int(e10[3, j]) and r.id == g - offsets[int(np.searchsorted(offsets, g, "right")) - 1]
+                              for j, (g, r) in enumerate(one)) and len(one) == int((e10[3] >= 0).sum())
         # search_with_pruning (mode 2) after building every shard's tangent cache
         h.build_tangent_cache()
         for o in orc:

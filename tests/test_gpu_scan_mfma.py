@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+from parity import same_topk_poincare
 
 rv = pytest.importorskip("ruvector_amd")
 pytestmark = pytest.mark.gpu
@@ -166,3 +167,103 @@ def test_shared_bound_across_chunks_with_planted_ties(monkeypatch, metric, name)
     assert rv.scan_last_stats()["mfma"] == nq
     rids, rd = O.flat_search(x, q, k, name)
     assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd)
+
+
+# ---- k > 16 (FKP-long lists, no shared bound) and the per-row-bound metrics ----
+@pytest.mark.parametrize("metric,name", METRICS)
+@pytest.mark.parametrize("k", [17, 64, 128])
+def test_large_k_bit_exact(monkeypatch, metric, name, k):
+    """k beyond one split's list: the rerank proves completeness from the union of the
+    splits' lists (or re-runs the query on the VALU scan); results as the oracle."""
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    n, d, nq = 30011, 64, 260
+    x = normal(n, d, 71)
+    q = normal(nq, d, 72)
+    ids, dist = flat(x, metric).brute_force_array(q, k)
+    st = rv.scan_last_stats()
+    assert st["mfma"] == nq, st
+    rids, rd = O.flat_search(x, q, k, name)
+    assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd)
+
+
+def ball_points(n, d, seed, rmax=0.9):
+    r = np.random.default_rng(seed)
+    v = r.standard_normal((n, d)).astype(np.float32)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    return (v * (rmax * r.random((n, 1)))).astype(np.float32)
+
+
+@pytest.mark.parametrize("d,wide", [(1024, "1"), (768, "1"), (128, "0"), (64, "1")])
+@pytest.mark.parametrize("k", [10, 100])
+def test_poincare_filter_matches_valu_and_oracle(monkeypatch, d, wide, k):
+    """HyperbolicHnsw exact scan through the MFMA filter with per-row bounds
+    (k_rows_to_f16_pr / k_scan_rerank_pr): ids and distances identical to the VALU
+    Poincaré scan (K8) and to the oracle's exact scan on the C5 generator."""
+    n, nq = 70_000 if d >= 768 else 30_000, 300
+    x = ball_points(n, d, 80 + d)
+    q = ball_points(nq, d, 81 + d)
+    h = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=1, ef_construction=16, max_connections=4,
+                                                  max_connections_0=8), dim=d)
+    h.insert_batch(x)
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    monkeypatch.setenv("RVX_SCAN_WIDE", wide)
+    ids, dist, _ = h.brute_force(q, k)
+    st = rv.scan_last_stats()
+    assert st["mfma"] == nq and st["fallback"] <= nq // 50, st
+    monkeypatch.setenv("RVX_SCAN_MFMA", "0")
+    vids, vdist, _ = h.brute_force(q, k)
+    assert rv.scan_last_stats()["valu"] == nq
+    assert np.array_equal(ids, vids) and np.array_equal(dist, vdist)
+    o = O.Hyp.from_graph(x, h.export_graph())  # every point lies inside the ball: stored == x
+    rids, rd = o.brute_force(q[:40], k)
+    assert same_topk_poincare(ids[:40], dist[:40], rids, rd, q[:40], x)
+
+
+def test_poincare_filter_chunks_deletions_free_and_edge_rows(monkeypatch):
+    """Several conversion chunks; rows on the ball's edge (lambda ~ 1e-5, the bound's
+    relative width > 2^-6) send the whole call to the VALU scan."""
+    d, n, nq = 128, 20_000, 260
+    x = ball_points(n, d, 90)
+    q = ball_points(nq, d, 91)
+    h = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=2, ef_construction=16, max_connections=4,
+                                                  max_connections_0=8), dim=d)
+    h.insert_batch(x)
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    monkeypatch.setenv("RVX_SCAN_MFMA_CHUNK_ROWS", "4096")
+    ids, dist, _ = h.brute_force(q, 10)
+    assert rv.scan_last_stats()["mfma"] == nq
+    monkeypatch.setenv("RVX_SCAN_MFMA", "0")
+    vids, vdist, _ = h.brute_force(q, 10)
+    assert np.array_equal(ids, vids) and np.array_equal(dist, vdist)
+    edge = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=2, ef_construction=16, max_connections=4,
+                                                     max_connections_0=8), dim=d)
+    y = x.copy()
+    y[5] *= 50.0  # projected onto the ball's edge
+    edge.insert_batch(y)
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    ids, dist, _ = edge.brute_force(q, 10)
+    assert rv.scan_last_stats()["valu"] == nq
+    monkeypatch.setenv("RVX_SCAN_MFMA", "0")
+    vids, vdist, _ = edge.brute_force(q, 10)
+    assert np.array_equal(ids, vids) and np.array_equal(dist, vdist)
+
+
+@pytest.mark.parametrize("d", [1024, 256])
+def test_tangent_pruned_scan_through_the_filter(monkeypatch, d):
+    """search_with_pruning's tangent scan (k * prune_factor = 100 candidates by
+    tangent_distance_squared) through the MFMA filter gives the same candidates, hence
+    the same results, as the VALU scan."""
+    n, nq = 70_000, 300
+    x = ball_points(n, d, 95)
+    q = ball_points(nq, d, 96)
+    h = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=3, ef_construction=16, max_connections=4,
+                                                  max_connections_0=8), dim=d)
+    h.insert_batch(x)
+    h.build_tangent_cache()
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    ids, dist, _ = h.search_with_pruning_batch(q, 10)
+    st = rv.scan_last_stats()
+    assert st["mfma"] == nq and st["fallback"] <= nq // 50, st
+    monkeypatch.setenv("RVX_SCAN_MFMA", "0")
+    vids, vdist, _ = h.search_with_pruning_batch(q, 10)
+    assert np.array_equal(ids, vids) and np.array_equal(dist, vdist)
