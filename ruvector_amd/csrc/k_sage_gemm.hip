@@ -260,7 +260,11 @@ __global__ __launch_bounds__(512) void k_sage_gemm_fused(SageGemmArgs g) {
 
 bool sage_gemm_fused_ok(int64_t M, int N, int K0, int K1, int64_t lda0, int64_t lda1, int64_t ldb0, int64_t ldb1,
                         int64_t plane0, int64_t plane1, int64_t ldc, const void* A0, const void* A1, const void* C) {
-    if (!env_int("RVX_SAGE_FUSED", 1) || M <= 0) return false;  // read per call: tests cover both
+    // opt-in (read per call, tests cover both): in the overlapped 10M x 768 pipeline it
+    // measured 1.16G vs 1.39G edges/s for gemm_nt_h2 + normalize_rows (every block streams
+    // all 4.7 MB of W from L2 / Infinity Cache beside the gather, one 8-wave block per CU
+    // waits at every 16-deep k step; profiles/r03_sage_fused_ab.txt)
+    if (!env_int("RVX_SAGE_FUSED", 0) || M <= 0) return false;
     if (N != 256 && N != 512 && N != 768 && N != 1024) return false;
     if (K0 % 16 || K1 % 16 || lda0 % 4 || lda1 % 4 || ldb0 % 8 || ldb1 % 8 || ldc % 4) return false;
     if ((((uintptr_t)A0 | (uintptr_t)A1 | (uintptr_t)C) & 15) != 0) return false;

@@ -69,7 +69,7 @@ void fill_uniform(float* p, int64_t n, uint64_t seed, float lo, float hi);
 void fill_uniform_at(float* p, int64_t n, uint64_t seed, int64_t first, float lo, float hi);
 // GraphSAGE dual GEMM with ReLU + row L2 normalisation fused, one block per 64 rows x
 // all N columns (k_sage_gemm.hip; N in {256, 512, 768, 1024}); bit-identical to
-// gemm_nt_h2 + normalize_rows. RVX_SAGE_FUSED=0 turns it off (read per call).
+// gemm_nt_h2 + normalize_rows. Opt-in: RVX_SAGE_FUSED=1 (read per call).
 bool sage_gemm_fused_ok(int64_t M, int N, int K0, int K1, int64_t lda0, int64_t lda1, int64_t ldb0, int64_t ldb1,
                         int64_t plane0, int64_t plane1, int64_t ldc, const void* A0, const void* A1, const void* C);
 void sage_gemm_fused(int64_t M, int N, const float* A0, int64_t lda0, int K0, const float* A1, int64_t lda1, int K1,

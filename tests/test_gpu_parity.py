@@ -895,3 +895,21 @@ def test_graphsage_pipeline_xcd_split_tile_order(monkeypatch, d):
     ref = O.sage_forward(xs, rp, col, wn, ws, rows=(r0, 700))
     dense = np.count_nonzero(ref, axis=1) >= d // 4
     assert_close(outs[1][r0:][dense], ref[dense])
+
+
+@pytest.mark.parametrize("in_f,out_f,n,deg", [(768, 768, 600, 9), (96, 256, 1000, 5), (64, 512, 257, 0),
+                                               (128, 1024, 300, 3)])
+def test_graphsage_fused_full_width_gemm_bits(monkeypatch, in_f, out_f, n, deg):
+    """The opt-in fused GEMM (RVX_SAGE_FUSED=1, k_sage_gemm.hip: 64 rows x all columns per
+    block, ReLU + L2 normalisation in the epilogue) writes the same bits as gemm_nt_h2 +
+    normalize_rows, and the oracle's values (deg 0: all-empty neighbourhoods)."""
+    x = O.fill_uniform(n * in_f, 90 + n).reshape(n, in_f)
+    rp, col = O.random_csr(n, deg, 91)
+    g = rv.Graph.from_csr(rp, col)
+    layer = rv.GraphSAGELayer(in_f, out_f, num_samples=max(deg, 1))
+    monkeypatch.setenv("RVX_SAGE_FUSED", "0")
+    y0 = layer.forward_graph(x, g)
+    monkeypatch.setenv("RVX_SAGE_FUSED", "1")
+    y1 = layer.forward_graph(x, g)
+    assert np.array_equal(y0, y1)
+    assert_close(y1, O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0))
