@@ -189,6 +189,8 @@ def main():
         "kernel_ms": {k: round(v["total_ms"] / max(v["launches"], 1), 4) for k, v in kern.items()},
     }
 
+    if comm is not None:
+        line["multi_gpu"] = exchange_report(a, kern, comm, world, rank, offsets, d, layers)
     if rank == 0 and world == 1 and not a.no_cpu:
         line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, tables, n_tot, d, deg, layers)
     if world == 1:
@@ -203,6 +205,35 @@ def main():
         print(json.dumps(line), flush=True)
     if comm is not None:
         comm.barrier()
+
+
+def exchange_report(a, kern, comm, world, rank, offsets, d, layers):
+    """Per-rank view of the halo exchange (the 8-GPU bottleneck candidate): bytes this rank
+    sends / receives per exchanged layer, the transfer stream's exchange time and the
+    exposed tail the compute stream waits for (rvx profiler tag exchange_wait: from the
+    last chunk's compute to the last round's arrival), per layer, for every rank."""
+    exchanged = max(layers - 1, 0)
+    n_loc = int(offsets[rank + 1] - offsets[rank])
+    n_tot = int(offsets[-1])
+
+    def per_rank(v):  # every rank's value, via one RCCL sum of a one-hot vector
+        vec = [0.0] * world
+        vec[rank] = float(v)
+        return comm.allreduce(vec)
+
+    def ms_per_layer(tag):
+        k = kern.get(tag)
+        return (k["total_ms"] / a.steps / max(exchanged, 1)) if k else 0.0
+
+    wait = per_rank(ms_per_layer("exchange_wait"))
+    xfer = per_rank(ms_per_layer("halo_exchange"))
+    return {"exchanged_layers_per_step": exchanged,
+            "bytes_sent_per_layer": [int(offsets[p + 1] - offsets[p]) * d * 4 * (world - 1) for p in range(world)],
+            "bytes_recv_per_layer": [(n_tot - int(offsets[p + 1] - offsets[p])) * d * 4 for p in range(world)],
+            "exchange_ms_per_layer": [round(v, 3) for v in xfer],
+            "exchange_wait_ms_per_layer": [round(v, 3) for v in wait],
+            "note": "exchange_ms: transfer-stream time of the chunked RCCL p2p rounds (overlapped with compute); "
+                    "exchange_wait: the part the compute stream waited for after its last chunk"}
 
 
 def hnsw_leg(a, rank, world, comm):

@@ -110,6 +110,7 @@ void produce_and_exchange(rvx_comm* comm, const int64_t* offsets, const std::vec
         for (const TableRef& t : tables) comm_exchange_rows(comm, t.first, t.second, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
     }
     RVX_HIP(hipEventRecord(ev[rounds], d.xfer));
+    ProfScope ps("exchange_wait");  // the exchange tail the compute stream waits for
     RVX_HIP(hipStreamWaitEvent(d.stream, ev[rounds], 0));
 }
 
@@ -543,7 +544,12 @@ rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g
         };
         sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], chunks, hook);
         RVX_HIP(hipEventRecord(ev[chunks], d.xfer));
-        RVX_HIP(hipStreamWaitEvent(d.stream, ev[chunks], 0));
+        {
+            // the exchange's tail the compute stream waits for: from the last chunk's
+            // compute to the last round's arrival (what the overlap did not hide)
+            ProfScope ps("exchange_wait");
+            RVX_HIP(hipStreamWaitEvent(d.stream, ev[chunks], 0));
+        }
     });
 }
 

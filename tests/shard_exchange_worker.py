@@ -64,7 +64,11 @@ def main():
         for b in (y1, y2):
             b.upload(np.full((N, d), np.nan, np.float32))  # unreceived rows would stay NaN
         call = rv._lib.call
-        call("rvx_sage_forward_exchange", layer._h, g_loc.handle, xb.handle, y1.handle, off_p, comm._h, 1)
+        prof = rv.Profiler()
+        with prof:
+            call("rvx_sage_forward_exchange", layer._h, g_loc.handle, xb.handle, y1.handle, off_p, comm._h, 1)
+            rv.synchronize()
+        res["prof_tags"] = {t: prof.query(t)[1] for t in ("halo_exchange", "exchange_wait")}
         call("rvx_sage_forward_exchange", layer._h, g_loc.handle, y1.handle, y2.handle, off_p, comm._h, 0)
         call("rvx_sage_forward_exchange", layer._h, g_full.handle, xb.handle, r1.handle, one_p, None, 0)
         call("rvx_sage_forward_exchange", layer._h, g_full.handle, r1.handle, r2.handle, one_p, None, 0)

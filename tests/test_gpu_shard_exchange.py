@@ -51,6 +51,8 @@ def test_exchange_entry_points_multi_rank(offsets, tmp_path):
     for r in res:
         assert "error" not in r, r.get("error")
         assert r["rounds"] == 3
+        # bench.py's multi-GPU report reads these tags: one transfer per round, one exposed wait per layer
+        assert r["prof_tags"] == {"halo_exchange": 3, "exchange_wait": 1}, r["prof_tags"]
         assert r["sage_layer1_all_rows_equal"] and r["sage_layer1_halo_rows"] > 0, r
         assert r["sage_layer2_owned_equal"], r
         assert r["sage_layer1_vs_oracle"] <= 1e-5, r
