@@ -363,7 +363,8 @@ struct FCfg {
     static constexpr int FQ = 64 * WQ, FR = 64 * FM;
     static constexpr int STAGE = (FR + FQ) * FK * 2;  // f16 rows then f16 queries, 64 B per row
     // + row constants (float4) and per-query {Qs, P} of the per-row-bound metrics
-    static constexpr int LDS = F_NSTAGE * STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 16 + FQ * 8;
+    // + per-query shared bound B_q and eps_q (group insertion, RVX_SCAN_GROUP_INSERT)
+    static constexpr int LDS = F_NSTAGE * STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 16 + FQ * 8 + FQ * 8;
     static constexpr int BLOCKS = WIDE ? 1 : 2;
     static_assert(FQ == FR && FR == 32 * THREADS / 64, "DMA pieces assume FR = FQ = 32 x waves");
 };
@@ -435,7 +436,7 @@ __device__ __forceinline__ float query_factor(float qinv, float qn) {
 
 __device__ __forceinline__ bool lt_vr(float v, int r, float bv, int br) { return v < bv || (v == bv && r < br); }
 
-template <int METRIC, bool WIDE>
+template <int METRIC, bool WIDE, bool GROUP>
 __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_scan_filter(FilterArgs a) {
     using Cf = FCfg<WIDE>;
     constexpr int FQ = Cf::FQ, FR = Cf::FR, F_STAGE = Cf::STAGE, F_FM = Cf::FM, F_THREADS = Cf::THREADS;
@@ -464,6 +465,8 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     float2* rowc = reinterpret_cast<float2*>(ovf + 4);              // [FR] current tile's row constants
     float4* rowc4 = reinterpret_cast<float4*>(ovf + 4);             // [FR] (per-row-bound metrics)
     float2* qfac = reinterpret_cast<float2*>(rowc4 + FR);           // [FQ] {Qs, P} (per-row-bound metrics)
+    float* gbl = reinterpret_cast<float*>(qfac + FQ);               // [FQ] B_q as this block knows it
+    float* gepsl = gbl + FQ;                                        // [FQ] eps_q
 
     for (int i = tid; i < FQ * FKP; i += F_THREADS) { best_v[i] = INFINITY; best_r[i] = -1; }
     if (tid < FQ) { cand_n[tid] = 0; thr[tid] = INFINITY; fillc[tid] = 0; }
@@ -500,6 +503,10 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     if (gq_own) {
         geps = filter_eps<METRIC>(a.qc[gq_idx].y, __uint_as_float(*a.xsq_max_bits));
         gb = ord_dec(__hip_atomic_load(a.gbound + gq_idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    if (tid < FQ) {  // LDS copies for the group insertion (whichever lanes insert a query's offers)
+        gbl[tid] = gb;
+        gepsl[tid] = geps;
     }
 
     // LDS-DMA fill: 1 KB pieces of 16 rows x 64 B; lane -> (row, 16-B chunk)
@@ -575,8 +582,11 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     // thresholds until no offer overflowed (thresholds only fall, so a
     // rejection is final and needs no mark).
     auto epilogue = [&](int64_t rt, float4 pre) {
-        gb = fminf(gb, ord_dec(graw));  // read at the end of the last tile: its wait lands on the drain below
-        if (tid < FQ) thr[tid] = fminf(thr[tid], next_up(gb));  // admit v <= B_q
+        if (tid < FQ) {  // B_q read at the end of the last tile: its wait lands on the drain below
+            gb = fminf(gbl[tid], ord_dec(graw));
+            gbl[tid] = gb;
+            thr[tid] = fminf(thr[tid], next_up(gb));  // admit v <= B_q
+        }
         if (tid < FR) {
             if constexpr (PRB) rowc4[tid] = pre;
             else rowc[tid] = row_factors<METRIC>(make_float2(pre.x, pre.y));
@@ -659,9 +669,13 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
                     }
             }
             __syncthreads();
-            // one lane per query: insertion into its sorted list (a query with no
-            // offer this round keeps its list, threshold and published bound)
-            if (tid < FQ && cand_n[tid] != 0) {
+            // Insertion of this round's offers into the sorted lists (a query with no
+            // offer keeps its list, threshold and published bound). A 16-lane group
+            // holds one query's list in registers, lane j = slot j: per offer one
+            // ballot gives its rank, one shuffle shifts the tail — no dependent LDS
+            // round trips; the groups of all waves take the queries in turn.
+            if constexpr (!GROUP) {
+            if (tid < FQ && cand_n[tid] != 0) {  // one lane per query, serial insertion (round 2 form)
                 const int ql = tid;
                 const int nc = min(cand_n[ql], FCB);
                 float* bv = best_v + ql * FKP;
@@ -679,14 +693,62 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
                 }
                 fillc[ql] = fill_n;
                 cand_n[ql] = 0;
+                float gbq = gbl[ql];
                 if (!PRB && gq_own && fill_n >= a.k) {
-                    const float ub = bv[a.k - 1] + 2.0f * geps;
-                    if (ub < gb) {
-                        gb = ub;
+                    const float ub = bv[a.k - 1] + 2.0f * gepsl[ql];
+                    if (ub < gbq) {
+                        gbq = ub;
+                        gbl[ql] = ub;
                         atomicMin(a.gbound + gq_idx, ord_enc(ub));
                     }
                 }
-                thr[ql] = fminf(fill_n == FKP ? bv[FKP - 1] : INFINITY, next_up(gb));
+                thr[ql] = fminf(fill_n == FKP ? bv[FKP - 1] : INFINITY, next_up(gbq));
+            }
+            } else {
+            static_assert(FKP == 16, "group insertion: one lane per list slot");
+            const int grp = lane >> 4, gl = lane & 15;
+#pragma unroll 1
+            for (int ql = wave * 4 + grp; ql < FQ; ql += F_THREADS / 16) {
+                const int nc = min(cand_n[ql], FCB);
+                if (nc == 0) continue;
+                float bvj = best_v[ql * FKP + gl];
+                int32_t brj = best_r[ql * FKP + gl];
+                int fill_n = fillc[ql];
+#pragma unroll 1
+                for (int c = 0; c < nc; ++c) {
+                    const float v = cand_v[ql * FCB + c];
+                    const int32_t r = cand_r[ql * FCB + c];
+                    const bool less = gl < fill_n && lt_vr(bvj, brj, v, r);
+                    const int pos = __popcll((__ballot(less) >> (16 * grp)) & 0xFFFFull);
+                    // slot j-1 -> j inside each 16-lane row (DPP row_shr:1)
+                    const float upv = __int_as_float(
+                        __builtin_amdgcn_update_dpp(__float_as_int(bvj), __float_as_int(bvj), 0x111, 0xF, 0xF, false));
+                    const int32_t upr = __builtin_amdgcn_update_dpp(brj, brj, 0x111, 0xF, 0xF, false);
+                    if (pos < FKP) {  // group-uniform
+                        if (gl == pos) { bvj = v; brj = r; }
+                        else if (gl > pos) { bvj = upv; brj = upr; }
+                        fill_n = min(fill_n + 1, FKP);
+                    }
+                }
+                best_v[ql * FKP + gl] = bvj;
+                best_r[ql * FKP + gl] = brj;
+                if (gl == 0) {  // the group's own writes are ordered before these reads (one wave)
+                    const float vk = best_v[ql * FKP + (a.k < FKP ? a.k : FKP) - 1];
+                    const float vlast = best_v[ql * FKP + FKP - 1];
+                    fillc[ql] = fill_n;
+                    cand_n[ql] = 0;
+                    float gbq = gbl[ql];
+                    if (!PRB && q0 + ql < a.nq && fill_n >= a.k) {
+                        const float ub = vk + 2.0f * gepsl[ql];
+                        if (ub < gbq) {
+                            gbq = ub;
+                            gbl[ql] = ub;
+                            atomicMin(a.gbound + q0 + ql, ord_enc(ub));
+                        }
+                    }
+                    thr[ql] = fminf(fill_n == FKP ? vlast : INFINITY, next_up(gbq));
+                }
+            }
             }
             if (tid == 0) ovf[(round + 1) & 1] = 0;
             __syncthreads();
@@ -1324,7 +1386,8 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     static bool attr = false;
     if (!attr) {
 #define RVX_FILTER_ATTR(M, W) \
-        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<M, W>, hipFuncAttributeMaxDynamicSharedMemorySize, FCfg<W>::LDS))
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<M, W, false>, hipFuncAttributeMaxDynamicSharedMemorySize, FCfg<W>::LDS)); \
+        RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<M, W, true>, hipFuncAttributeMaxDynamicSharedMemorySize, FCfg<W>::LDS))
         RVX_FILTER_ATTR(RVX_METRIC_L2, true); RVX_FILTER_ATTR(RVX_METRIC_COSINE, true); RVX_FILTER_ATTR(RVX_METRIC_DOT, true);
         RVX_FILTER_ATTR(RVX_METRIC_L2, false); RVX_FILTER_ATTR(RVX_METRIC_COSINE, false); RVX_FILTER_ATTR(RVX_METRIC_DOT, false);
         RVX_FILTER_ATTR(RVX_METRIC_POINCARE, true); RVX_FILTER_ATTR(METRIC_L2SQ, true);
@@ -1352,21 +1415,25 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
                       part_v, part_r, gbound, k, max_bits, xc4, beta};
         const dim3 grid((unsigned)(qtiles * s_c));
         const dim3 blk((unsigned)F_THREADS);
+        // list insertion: one lane per query (0, default) or 16-lane groups with one list
+        // slot per lane (1, opt-in: spills ~100 B/lane in the 256-register wide tile and ran
+        // 225 vs 173 ms at 10M x 768 / 10k, scripts/exp_scan_group.sh); read per call
+        const bool group = env_int("RVX_SCAN_GROUP", 0) != 0;
         if (wide) {
             switch (metric) {
-                case RVX_METRIC_L2: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, true>), grid, blk, F_LDS, fa); break;
-                case RVX_METRIC_COSINE: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, true>), grid, blk, F_LDS, fa); break;
-                case RVX_METRIC_POINCARE: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, true>), grid, blk, F_LDS, fa); break;
-                case METRIC_L2SQ: RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, true>), grid, blk, F_LDS, fa); break;
-                default: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, true>), grid, blk, F_LDS, fa); break;
+                case RVX_METRIC_L2: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, true, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, true, false>), grid, blk, F_LDS, fa); break;
+                case RVX_METRIC_COSINE: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, true, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, true, false>), grid, blk, F_LDS, fa); break;
+                case RVX_METRIC_POINCARE: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, true, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, true, false>), grid, blk, F_LDS, fa); break;
+                case METRIC_L2SQ: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, true, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, true, false>), grid, blk, F_LDS, fa); break;
+                default: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, true, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, true, false>), grid, blk, F_LDS, fa); break;
             }
         } else {
             switch (metric) {
-                case RVX_METRIC_L2: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, false>), grid, blk, F_LDS, fa); break;
-                case RVX_METRIC_COSINE: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, false>), grid, blk, F_LDS, fa); break;
-                case RVX_METRIC_POINCARE: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, false>), grid, blk, F_LDS, fa); break;
-                case METRIC_L2SQ: RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, false>), grid, blk, F_LDS, fa); break;
-                default: RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, false>), grid, blk, F_LDS, fa); break;
+                case RVX_METRIC_L2: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, false, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, false, false>), grid, blk, F_LDS, fa); break;
+                case RVX_METRIC_COSINE: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, false, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, false, false>), grid, blk, F_LDS, fa); break;
+                case RVX_METRIC_POINCARE: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, false, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, false, false>), grid, blk, F_LDS, fa); break;
+                case METRIC_L2SQ: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, false, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, false, false>), grid, blk, F_LDS, fa); break;
+                default: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, false, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, false, false>), grid, blk, F_LDS, fa); break;
             }
         }
     }
