@@ -337,7 +337,7 @@ typedef struct {
     int32_t kind;            /* RVX_INDEX_FLAT / RVX_INDEX_HNSW (VectorDB picks HNSW iff hnsw_config, vector_db.rs:81-98) */
     int32_t dim;
     int32_t metric;          /* RVX_METRIC_* */
-    int32_t m;               /* HnswConfig::m (types.rs:87-96: 32) */
+    int32_t m;               /* HnswConfig::m (types.rs:87-96: 32); the GPU build takes m <= 128 (layer 0: 2m) */
     int32_t ef_construction; /* 200 */
     int32_t ef_search;       /* 100 */
     int64_t max_elements;    /* 10_000_000 */
@@ -484,8 +484,8 @@ rvx_status rvx_distance_matrix(int32_t metric, const float* q, int64_t nq, const
 typedef struct rvx_hyperbolic rvx_hyperbolic;
 typedef struct {                 /* HyperbolicHnswConfig (hnsw.rs:36-72), metric Poincaré or Euclidean */
     int32_t dim;
-    int32_t max_connections;     /* M, 16 */
-    int32_t max_connections_0;   /* M0 at layer 0, 32 (<= 64) */
+    int32_t max_connections;     /* M, 16 (<= 128 for the GPU build) */
+    int32_t max_connections_0;   /* M0 at layer 0, 32 (<= 256 for the GPU build) */
     int32_t ef_construction;     /* 200 */
     int32_t ef_search;           /* 50 */
     float   level_mult;          /* 1 / ln(16) */

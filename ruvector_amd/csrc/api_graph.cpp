@@ -296,13 +296,19 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         GemmOperand s0{agg + r0 * l->in, l->in, l->wn_t.as<float>(), l->in, l->in, l->wn_x3.as<uint16_t>(), plane};
         GemmOperand s1{x + (row_offset + r0) * l->in, l->in, l->ws_t.as<float>(), l->in, l->in,
                        l->ws_x3.as<uint16_t>(), plane};
+        // opt-in: the h2g GEMM normalises its own rows (last column tile of each 128-row
+        // block, same bits as normalize_rows) instead of a separate pass over y
+        GemmEpilogue epn = ep;
+        epn.normalize_rows = h2 && l->normalize && gemm_h2_rownorm_ok(l->out, y, l->out);
         if (h2)
             gemm_nt_h2(rows, l->out, s0, l->wn_h2.as<_Float16>(), &s1, l->ws_h2.as<_Float16>(), scale + r0,
-                       l->w_inv.as<float>(), ep, y + r0 * l->out, l->out, "sage_gemm",
+                       l->w_inv.as<float>(), epn, y + r0 * l->out, l->out, "sage_gemm",
                        chunks > 1 ? env_int("RVX_SAGE_GEMM_CAP", 2) : -1);
         else
             gemm_nt(rows, l->out, s0, &s1, ep, y + r0 * l->out, l->out, "sage_gemm");
-        if (l->normalize) normalize_rows(y + r0 * l->out, rows, l->out, true, "sage_normalize");
+#ifndef RVX_AB_NO_NORMALIZE  // timing-only ablation build (scripts/exp_sage_ablate.sh): results wrong
+        if (l->normalize && !epn.normalize_rows) normalize_rows(y + r0 * l->out, rows, l->out, true, "sage_normalize");
+#endif
         if (hook) hook(c, r0, rows);
     }
     for (; hook && c < chunks; ++c) hook(c, n, 0);

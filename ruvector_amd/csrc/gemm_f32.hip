@@ -54,6 +54,8 @@ struct GemmArgs {
     // persistent split-f16 GEMM: per-XCD tile counters (stride 32 words), zeroed per launch
     unsigned* queue;
     int xsplit;  // queue mode: XCD pair (2i, 2i+1) shares a row range, each XCD takes half the column tiles
+    // in-launch row normalisation (h2g): one arrival ticket per 128-row tile, zeroed per launch
+    unsigned* row_tickets;
 };
 
 __device__ __forceinline__ float epi_apply(int epi, float v) {
@@ -787,6 +789,61 @@ __device__ __forceinline__ int64_t part_first(int64_t n, int64_t parts, int64_t 
 }
 __device__ __forceinline__ int64_t part_count(int64_t n, int64_t parts, int64_t i) { return n / parts + (i < n % parts ? 1 : 0); }
 
+// End of a tile episode with in-launch row normalisation: every column tile of a
+// 128-row block publishes its stores (each wave's vmcnt drain, the block barrier,
+// one agent-scope release) and takes an arrival ticket; the block that draws the
+// last ticket acquires and normalises the 128 rows over all N columns
+// (cdna_hip_programming.md §6 Guideline 16, counter form: correct for any
+// placement of the column tiles over XCDs/CUs; no block waits on another). The
+// row pass is k_normalize_rows_vec's arithmetic (k_data.hip: per-lane float4
+// slots 4 lane + 256 j, sequential squares, xor-tree sum, sqrtf, true division),
+// so C is bit-identical to the GEMM followed by normalize_rows(only_positive).
+__device__ __forceinline__ void h2g_rownorm(const GemmArgs& g, int64_t tm, int64_t m0, unsigned char* lds) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    volatile int* flag = reinterpret_cast<volatile int*>(lds);  // k-loop stages are free here
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(g.row_tickets + tm, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t == (unsigned)(g.tiles_n - 1);
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
+    }
+    __syncthreads();
+    const int last = *flag;
+    if (!last) return;  // the caller's next barrier precedes any reuse of the stages
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int r = wave; r < 128; r += 4) {
+        const int64_t row = m0 + r;
+        if (row >= g.M) break;
+        float* x = g.C + row * g.ldc + 4 * lane;
+        float4 v[4];
+        float s = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // slots past N add +0: the same sum as NV = ceil(N / 256) slots
+            const bool on = 4 * lane + 256 * j < g.N;
+            v[j] = on ? *reinterpret_cast<const float4*>(x + 256 * j) : make_float4(0.f, 0.f, 0.f, 0.f);
+            s = __fadd_rn(s, __fmul_rn(v[j].x, v[j].x));
+            s = __fadd_rn(s, __fmul_rn(v[j].y, v[j].y));
+            s = __fadd_rn(s, __fmul_rn(v[j].z, v[j].z));
+            s = __fadd_rn(s, __fmul_rn(v[j].w, v[j].w));
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        const float norm = sqrtf(s);
+        if (!(norm > 0.0f)) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (4 * lane + 256 * j < g.N)
+                *reinterpret_cast<float4*>(x + 256 * j) =
+                    make_float4(v[j].x / norm, v[j].y / norm, v[j].z / norm, v[j].w / norm);
+    }
+}
+
 template <bool DUAL>
 __device__ __forceinline__ void h2g_tile(const GemmArgs& g, int epi, int64_t wgid) {
     constexpr int XA = 128 * 128;             // f32 A tile bytes per stage
@@ -959,6 +1016,7 @@ __device__ __forceinline__ void h2g_tile(const GemmArgs& g, int epi, int64_t wgi
             }
         }
     }
+    if (g.row_tickets) h2g_rownorm(g, tm, m0, xsm);
 }
 
 // Pre-split variant ("h2p") of the split-f16 GEMM: the producer (the SAGE
@@ -1331,6 +1389,14 @@ bool gemm_h2_ok(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1) 
     return ok(s0) && (!s1 || ok(*s1));
 }
 
+// Opt-in (RVX_GEMM_ROWNORM=1, read per call; tests force both): bit-identical, but in the
+// overlapped 10M x 768 layer the per-tile agent-scope release (an L2 write-back beside the
+// gather's stores) costs more than the pass it removes: 491-526 vs 457-465 ms/step
+// (scripts/exp_rownorm_ab.sh, profiles/r03_sage_rownorm_ab.txt).
+bool gemm_h2_rownorm_ok(int N, const float* C, int64_t ldc) {
+    return env_int("RVX_GEMM_ROWNORM", 0) && N % 4 == 0 && N <= 1024 && ldc % 4 == 0 && aligned16(C);
+}
+
 void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
                 const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
                 int64_t ldc, const char* tag, int persist) {
@@ -1373,6 +1439,12 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
         // (10M x 768 layer: GEMM fetch 10.5 -> 7.7 GB per launch, step time
         // unchanged within noise, scripts/exp_xsplit.sh); RVX_GEMM_XSPLIT=0 restores
         g.xsplit = (g.tiles_n % 2 == 0 && g.nblocks % g.tiles_n == 0) ? env_int("RVX_GEMM_XSPLIT", 1) : 0;
+    }
+    if (ep.normalize_rows) {
+        RVX_REQUIRE(gemm_h2_rownorm_ok(N, C, ldc), RVX_ERR_INVALID_SHAPE, "row normalisation needs N % 4 == 0, N <= 1024");
+        const int64_t tiles_m = (M + 127) / 128;
+        g.row_tickets = (unsigned*)scratch_bytes("gemm_h2_row_tickets", tiles_m * 4);
+        RVX_HIP(hipMemsetAsync(g.row_tickets, 0, (size_t)tiles_m * 4, stream()));
     }
     if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
     else RVX_LAUNCH(t, gemm_nt_h2g<false>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);

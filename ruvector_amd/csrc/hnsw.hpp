@@ -13,6 +13,7 @@ struct HnswDev {
     int64_t n = 0;
     int max_level = 0;
     int64_t entry = 0;
+    int max_deg = 0;  // longest layer-0 list (sizes the hashed visited set)
     const int64_t* rp0 = nullptr;
     const int* col0 = nullptr;
     const int* up_ids = nullptr;

@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 
 #include "poincare_dev.hpp"
@@ -228,11 +229,13 @@ __device__ __forceinline__ bool visit_claim(unsigned long long* vis, unsigned vm
     return false;  // table full: cannot happen below vmask+1 visited nodes
 }
 
-// visited-table size for a search of width ef (load factor well below 1/2)
-inline unsigned visited_capacity(int ef) {
+// visited-table size for a search of width ef over lists of <= max_deg neighbours
+// (load factor well below 1/2)
+inline unsigned visited_capacity(int ef, int max_deg = 64) {
     unsigned v = VCAP_MIN;
-    // a search of width ef expands ~ef..2ef nodes of <= 64 neighbours each
-    while (v < (unsigned)ef * 256u && v < (1u << 23)) v <<= 1;
+    // a search of width ef expands ~ef..2ef nodes of <= max_deg neighbours each
+    const uint64_t want = (uint64_t)ef * 4u * (uint64_t)std::max(max_deg, 64);
+    while (v < want && v < (1u << 24)) v <<= 1;
     return v;
 }
 

@@ -120,6 +120,7 @@ void hnsw_install(rvx_index* ix, HostGraph&& hg) {
     g.n = n;
     g.max_level = hg.max_level;
     g.entry = hg.entry;
+    for (int64_t i = 0; i < n; ++i) g.max_deg = std::max<int>(g.max_deg, (int)(hg.rp0[i + 1] - hg.rp0[i]));
     ix->rp0.reset((n + 1) * 8);
     ix->rp0.upload(hg.rp0.data(), (n + 1) * 8);
     ix->col0.reset(std::max<int64_t>((int64_t)hg.col0.size(), 1) * 4);
@@ -155,8 +156,8 @@ void hnsw_install(rvx_index* ix, HostGraph&& hg) {
 void hnsw_insert_range(rvx_index* ix, int64_t first, int64_t count) {
     RVX_REQUIRE(ix->build_valid, RVX_ERR_UNSUPPORTED,
                 "adding vectors to an HNSW index whose graph was loaded with rvx_index_load_graph is not supported");
-    RVX_REQUIRE(ix->hyper ? (ix->cfg.m <= 64 && ix->m0 <= 128) : ix->cfg.m <= 64, RVX_ERR_UNSUPPORTED,
-                "GPU HNSW construction supports layer-0 lists of <= 128 and upper lists of <= 64 neighbours");
+    RVX_REQUIRE(ix->hyper ? (ix->cfg.m <= 128 && ix->m0 <= 256) : ix->cfg.m <= 128, RVX_ERR_UNSUPPORTED,
+                "GPU HNSW construction supports layer-0 lists of <= 256 and upper lists of <= 128 neighbours");
     RVX_REQUIRE(ix->cfg.metric != RVX_METRIC_DOT, RVX_ERR_INVALID_PARAMETER, "DotProduct cannot be used with HNSW");
     if (count <= 0) return;
     const int M = ix->cfg.m, C0 = ix->hyper ? ix->m0 : 2 * M, max_layer = std::min(16, ix->cfg.dim);

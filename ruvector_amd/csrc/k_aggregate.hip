@@ -178,6 +178,9 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
                     empty_fill == 1 ? *reinterpret_cast<const float4*>(self + 256 * j) : make_float4(0, 0, 0, 0);
         continue;
     }
+#ifdef RVX_AB_NO_AGG_WRITE  // timing-only ablation build (scripts/exp_sage_ablate.sh): results wrong
+    if (NT && acc[0].x == 12345.0f)
+#endif
 #pragma unroll
     for (int j = 0; j < NV; ++j)
         if (active[j]) *reinterpret_cast<float4*>(dst + 256 * j) = acc[j];

@@ -264,7 +264,7 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     if (nq <= 0) return;
     RVX_REQUIRE(ef >= 1 && ef <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER,
                 "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
-    const unsigned vcap = visited_capacity(ef);
+    const unsigned vcap = visited_capacity(ef, g.max_deg);
     // visited set: a per-slot bitmap over all n nodes (cleared per query by its
     // wave: no launch-wide memset, no probing, n/8 bytes touched) when at least
     // min(nq, 1024) slots' bitmaps fit the budget — what the scratch slot already

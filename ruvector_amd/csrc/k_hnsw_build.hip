@@ -34,7 +34,7 @@ namespace rvx {
 namespace {
 using namespace hnswdev;
 
-constexpr int MAX_C0 = 128;  // layer-0 list capacity (2M for hnsw_rs: M <= 64)
+constexpr int MAX_C0 = 256;  // layer-0 list capacity (2M for hnsw_rs: M <= 128)
 
 struct BuildArgs {
     BuildGraph G;
@@ -253,6 +253,8 @@ __global__ __launch_bounds__(64) RVX_BUILD_WPE void k_build_insert(BuildArgs a) 
 
 // One wave per list that received reverse edges (the record that found the
 // chain head empty owns it): merge old list ∪ new entries, keep the best cap.
+// Lane j holds elements j, 64 + j, ... of the sorted list (NE per lane, cap <= 64 NE).
+template <int NE>
 __global__ __launch_bounds__(256) void k_build_merge(BuildArgs a, int nrec) {
     const int lane = threadIdx.x & 63;
     const int wave = (blockIdx.x * 4) + (threadIdx.x >> 6);
@@ -284,33 +286,62 @@ __global__ __launch_bounds__(256) void k_build_merge(BuildArgs a, int nrec) {
             cap = a.G.M;
         }
         int cnt = *cntp;
-        // lane j holds elements j and 64 + j of the sorted list (cap <= 128)
-        float md = lane < cnt ? ds[lane] : INFINITY, md1 = 64 + lane < cnt ? ds[64 + lane] : INFINITY;
-        int mi = lane < cnt ? ids[lane] : INT_MAX, mi1 = 64 + lane < cnt ? ids[64 + lane] : INT_MAX;
+        float md[NE];
+        int mi[NE];
+#pragma unroll
+        for (int j = 0; j < NE; ++j) {
+            const int e = 64 * j + lane;
+            md[j] = e < cnt ? ds[e] : INFINITY;
+            mi[j] = e < cnt ? ids[e] : INT_MAX;
+        }
         int steps = 0;
         for (int h = a.rev_head[key]; h >= 0 && h < nrec && steps < nrec; h = a.rev_next[h], ++steps) {
             const float d = a.rev_d[h];
             const int id = a.rev_src[h];
-            if (__ballot(mi == id || mi1 == id) != 0ull) continue;  // already present
+            bool dup = false;
+#pragma unroll
+            for (int j = 0; j < NE; ++j) dup = dup || mi[j] == id;
+            if (__ballot(dup) != 0ull) continue;  // already present
             if (cnt == cap) {
-                const float ld = cap <= 64 ? __shfl(md, cap - 1) : __shfl(md1, cap - 65);
-                const int li2 = cap <= 64 ? __shfl(mi, cap - 1) : __shfl(mi1, cap - 65);
+                const int jl = (cap - 1) >> 6, ll = (cap - 1) & 63;
+                float ld = INFINITY;
+                int li2 = INT_MAX;
+#pragma unroll
+                for (int j = 0; j < NE; ++j) {
+                    const float tv = __shfl(md[j], ll);
+                    const int ti = __shfl(mi[j], ll);
+                    if (j == jl) { ld = tv; li2 = ti; }
+                }
                 if (!lt(d, id, ld, li2)) continue;
             }
-            const int pos = __popcll(__ballot(lane < cnt && lt(md, mi, d, id))) +
-                            __popcll(__ballot(64 + lane < cnt && lt(md1, mi1, d, id)));
-            const float cd = __shfl(md, 63);  // element 63 moves to 64
-            const int ci = __shfl(mi, 63);
-            const float upd = __shfl_up(md, 1), upd1 = __shfl_up(md1, 1);
-            const int upi = __shfl_up(mi, 1), upi1 = __shfl_up(mi1, 1);
-            if (lane > pos) { md = upd; mi = upi; }
-            if (lane == pos) { md = d; mi = id; }
-            if (64 + lane > pos) { md1 = lane == 0 ? cd : upd1; mi1 = lane == 0 ? ci : upi1; }
-            if (64 + lane == pos) { md1 = d; mi1 = id; }
+            int pos = 0;
+#pragma unroll
+            for (int j = 0; j < NE; ++j) pos += __popcll(__ballot(64 * j + lane < cnt && lt(md[j], mi[j], d, id)));
+            // shift elements >= pos up by one (element 64 j + 63 moves to 64 (j + 1))
+            float cd[NE], upd[NE];
+            int ci[NE], upi[NE];
+#pragma unroll
+            for (int j = 0; j < NE; ++j) {
+                cd[j] = __shfl(md[j], 63);
+                ci[j] = __shfl(mi[j], 63);
+                upd[j] = __shfl_up(md[j], 1);
+                upi[j] = __shfl_up(mi[j], 1);
+            }
+#pragma unroll
+            for (int j = 0; j < NE; ++j) {
+                const int e = 64 * j + lane;
+                const int jp = j > 0 ? j - 1 : 0;  // lane 0 of chunk j takes chunk j-1's last (e > pos >= 0: j > 0)
+                if (e > pos) {
+                    md[j] = lane == 0 ? cd[jp] : upd[j];
+                    mi[j] = lane == 0 ? ci[jp] : upi[j];
+                }
+                if (e == pos) { md[j] = d; mi[j] = id; }
+            }
             cnt = min(cnt + 1, cap);
         }
-        if (lane < cnt) { ds[lane] = md; ids[lane] = mi; }
-        if (64 + lane < cnt) { ds[64 + lane] = md1; ids[64 + lane] = mi1; }
+#pragma unroll
+        for (int j = 0; j < NE; ++j)
+            if (64 * j + lane < cnt) { ds[64 * j + lane] = md[j]; ids[64 * j + lane] = mi[j]; }
         if (lane == 0) { *cntp = cnt; a.rev_head[key] = -1; }
     }
 }
@@ -326,10 +357,10 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
                         int64_t batch_begin, int batch_n, int entry, int entry_level, unsigned nonempty_mask, int ef_c,
                         BuildScratch& s, float curv, int hyper) {
     if (batch_n <= 0) return;
-    RVX_REQUIRE(G.C0 <= MAX_C0 && G.M <= 64, RVX_ERR_UNSUPPORTED,
-                "GPU HNSW build supports layer-0 lists of <= 128 and upper lists of <= 64 neighbours");
+    RVX_REQUIRE(G.C0 <= MAX_C0 && G.M <= MAX_C0 / 2, RVX_ERR_UNSUPPORTED,
+                "GPU HNSW build supports layer-0 lists of <= 256 and upper lists of <= 128 neighbours");
     RVX_REQUIRE(ef_c >= 1 && ef_c <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER, "ef_construction out of range");
-    const unsigned vcap = visited_capacity(ef_c);
+    const unsigned vcap = visited_capacity(ef_c, G.C0);
     const int nslots = (int)std::min<int64_t>(std::min(batch_n, 8192),
                                               std::max<int64_t>(1024, ((int64_t)4 << 30) / ((int64_t)vcap * 8)));
     const int rev_cap = G.C0 + G.M * G.max_layer;
@@ -374,7 +405,9 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
         default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by the GPU HNSW build");
     }
     const int waves = (int)((nrec + 63) / 64);
-    RVX_LAUNCH("hnsw_build_merge", k_build_merge, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, a, (int)nrec);
+    const dim3 mgrid((unsigned)((waves + 3) / 4));
+    if (G.C0 <= 128) RVX_LAUNCH("hnsw_build_merge", k_build_merge<2>, mgrid, dim3(256), 0, a, (int)nrec);
+    else RVX_LAUNCH("hnsw_build_merge", k_build_merge<4>, mgrid, dim3(256), 0, a, (int)nrec);
     sync();
 }
 

@@ -30,6 +30,9 @@ struct GemmEpilogue {
     const float* bias1 = nullptr;
     const float* addend = nullptr;
     int64_t ld_addend = 0;
+    // gemm_nt_h2 only: then x /= |x| over each row of C (rows with norm 0 or NaN left as they
+    // are), bit-identical to normalize_rows(C, M, N, only_positive = true); see gemm_h2_rownorm_ok
+    bool normalize_rows = false;
 };
 // C[M][N] = epilogue(A0·B0^T [+ A1·B1^T])
 void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, const GemmEpilogue& ep, float* C,
@@ -43,6 +46,8 @@ void split_x3(const float* src, int64_t n, uint16_t* dst);
 // ([2][N][K], from split_h2_rows) with b_inv[n] its inverse column scale.
 bool gemm_h2_ok(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1);
 // persist: blocks per CU of a persistent grid (0 = one block per tile; -1 = RVX_GEMM_CAP, default 0)
+// ep.normalize_rows is honoured when this holds (N % 4 == 0, N <= 1024, aligned C rows, opt-in RVX_GEMM_ROWNORM=1)
+bool gemm_h2_rownorm_ok(int N, const float* C, int64_t ldc);
 void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
                 const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
                 int64_t ldc, const char* tag, int persist = -1);

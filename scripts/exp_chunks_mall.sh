@@ -3,9 +3,11 @@
 # (and GEMM output) within the 256 MB Infinity Cache between producer and consumer.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/chunks
+i=0
 for c in ${CHUNKS:-24 64 128 256}; do
-  RVX_SAGE_CHUNKS=$c timeout -k 10 300 python -u bench.py --steps 4 --warmup 2 --no-hnsw --no-scan --no-cpu > gpurun_out/chunks/c$c.log 2>&1 || exit 4
-  python - gpurun_out/chunks/c$c.log $c <<'PY'
+  i=$((i+1))
+  RVX_SAGE_CHUNKS=$c timeout -k 10 300 python -u bench.py --steps ${STEPS:-4} --warmup 2 --no-hnsw --no-scan --no-cpu > gpurun_out/chunks/r${i}_c$c.log 2>&1 || exit 4
+  python - gpurun_out/chunks/r${i}_c$c.log $c <<'PY'
 import json, sys
 for line in open(sys.argv[1]):
     if line.startswith("{"):

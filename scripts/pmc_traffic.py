@@ -17,9 +17,11 @@ from collections import defaultdict
 
 TAGS = {  # kernel symbol substring -> bench tag
     "k_aggregate_vec": "sage_aggregate",
-    "gemm_nt_mfma": "sage_gemm",
-    "gemm_nt_x3": "sage_gemm",
+    # one entry per GEMM kernel: the layer's split-f16 GEMM (h2g) alone under sage_gemm; the
+    # alternatives bench.py times (gemm_paths) under their own names
     "gemm_nt_h2g": "sage_gemm",
+    "gemm_nt_x3": "sage_gemm_alt_split_bf16x6",
+    "gemm_nt_mfma": "sage_gemm_alt_fp32_mfma",
     "k_normalize_rows": "sage_normalize",
     "k_scan_topk": "scan_topk",
     "k_scan_filter": "scan_filter",

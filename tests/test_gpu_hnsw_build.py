@@ -75,11 +75,11 @@ def test_recall_matches_cpu_build():
         assert r_gpu >= r_cpu - 0.02, (ef, r_gpu, r_cpu)
 
 
-@pytest.mark.parametrize("m", [48, 64])
+@pytest.mark.parametrize("m", [48, 64, 96, 128])
 def test_wide_lists_recall_and_invariants(m):
-    # M up to 64 (layer-0 lists of 2M = 128: two list elements per lane in the
-    # reverse-edge merge, selection over two chunks of selected points)
-    n, d, efc = 12000, 32, 120
+    # M up to 128 (layer-0 lists of 2M <= 256: two or four list elements per lane
+    # in the reverse-edge merge, selection over up to four chunks of selected points)
+    n, d, efc = 12000, 32, 120 if m <= 64 else 2 * m
     x = O.fill_uniform(n * d, 17).reshape(n, d)
     q = O.fill_uniform(200 * d, 18).reshape(200, d)
     gt, _ = O.flat_search(x, q, 10, "l2")
@@ -87,7 +87,10 @@ def test_wide_lists_recall_and_invariants(m):
     g = idx.export_graph()
     rp, col = g["row_ptr0"], g["col0"]
     deg = np.diff(rp)
+    print(f"m {m}: layer-0 degree max {deg.max()}, mean {deg.mean():.1f}")
     assert deg.max() <= 2 * m and deg.max() > 64  # lists past one wave's width exist
+    if m == 128:
+        assert deg.max() > 128  # and past two (four elements per lane)
     for i in range(0, n, 97):
         nb = col[rp[i]:rp[i + 1]]
         assert i not in nb.tolist() and len(set(nb.tolist())) == len(nb)

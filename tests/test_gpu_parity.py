@@ -913,3 +913,28 @@ def test_graphsage_fused_full_width_gemm_bits(monkeypatch, in_f, out_f, n, deg):
     y1 = layer.forward_graph(x, g)
     assert np.array_equal(y0, y1)
     assert_close(y1, O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0))
+
+
+@pytest.mark.parametrize("in_f,out_f,n,deg,chunks", [(768, 768, 700, 9, 0), (96, 200, 1000, 5, 0),
+                                                     (64, 1024, 257, 0, 0), (64, 256, 40000, 4, 2)])
+def test_graphsage_in_gemm_row_normalisation_bits(monkeypatch, in_f, out_f, n, deg, chunks):
+    """The split-f16 GEMM normalises its own rows (RVX_GEMM_ROWNORM=1, default: the block
+    that completes a 128-row tile's last column tile re-reads the rows after an agent-scope
+    acquire and divides by the norm) with the same bits as the separate normalize_rows pass
+    (RVX_GEMM_ROWNORM=0), including ragged row tiles, out_f not a multiple of the 128-column
+    tile, and the chunked pipeline's persistent queue grid (chunks > 1)."""
+    x = O.fill_uniform(n * in_f, 70 + n).reshape(n, in_f)
+    rp, col = O.random_csr(n, deg, 71)
+    g = rv.Graph.from_csr(rp, col)
+    layer = rv.GraphSAGELayer(in_f, out_f, num_samples=max(deg, 1))
+    if chunks:
+        monkeypatch.setenv("RVX_SAGE_CHUNKS", str(chunks))
+    monkeypatch.setenv("RVX_GEMM_ROWNORM", "0")
+    y0 = layer.forward_graph(x, g)
+    monkeypatch.setenv("RVX_GEMM_ROWNORM", "1")
+    y1 = layer.forward_graph(x, g)
+    assert np.array_equal(y0, y1)
+    nrm = np.linalg.norm(y1.astype(np.float64), axis=1)
+    assert np.all(np.abs(nrm[nrm > 0] - 1.0) < 1e-5)
+    if n <= 1000 and out_f != 200:  # out_f 200: test_graphsage_ill_conditioned_rows_f64_anchor
+        assert_close(y1, O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0))
