@@ -252,7 +252,35 @@ def hnsw_leg(a, rank, world, comm):
         qps = comm.allreduce([qps])[0]
     res["value"] = round(qps, 1)
     res["unit"] = "queries/s (recall@10 >= 0.95, replicas summed over GPUs)"
+    attach_hnsw_traffic(res)
     return res
+
+
+def attach_hnsw_traffic(res):
+    """C1's 51 MB table stays resident in L2 / the Infinity Cache, so `alg_GBps` (SURVEY.md
+    §8d bytes / kernel time) is not an HBM rate. The committed rocprofv3 --pmc passes of the
+    same search (scripts/hnsw_c1_traffic.sh -> profiles/pmc_traffic_hnsw_c1.json) give the
+    bytes that left L2 per launch (Infinity-Cache hits included, so an upper bound on HBM
+    bytes); the HBM fraction is capped by those bytes over the kernel time."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic_hnsw_c1.json")
+    row = next((s for s in res.get("sweep", []) if s["ef"] == 550), None)
+    if row is None or not os.path.exists(path):
+        return
+    try:
+        pmc = json.load(open(path))
+    except ValueError:
+        return
+    ent = pmc.get("kernels", {}).get("hnsw_search")
+    if not ent or (pmc.get("config") or {}).get("ef") != 550 or not row.get("kernel_ms"):
+        return
+    fab = ent["hbm_bytes_per_launch"]
+    rate = fab / (row["kernel_ms"] * 1e-3) / 1e9
+    res["traffic_ef550"] = {
+        "fabric_bytes_per_launch": round(fab, 0), "fabric_bytes_per_query": round(fab / 10_000, 1),
+        "algorithmic_GBps": row["alg_GBps"], "fabric_GBps": round(rate, 1), "hbm_frac_upper_bound": round(rate / 8000.0, 4),
+        "source": "rocprofv3 --pmc FETCH_SIZE(x2, gfx950) + WRITE_SIZE, profiles/pmc_traffic_hnsw_c1.json",
+        "caveat": "51 MB table resident in L2 / Infinity Cache: the algorithmic rate is served on die, "
+                  "FETCH counts L2 misses including Infinity-Cache hits, so HBM traffic is at most these bytes"}
 
 
 def scan_leg(a, x, n, d, rank, world, comm):
