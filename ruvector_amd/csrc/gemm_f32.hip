@@ -994,7 +994,7 @@ __device__ __forceinline__ void h2g_tile(const GemmArgs& g, int epi, int64_t wgi
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
         const int64_t row = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-        rinv[e] = row < g.M ? 1.0f / g.a_scale[row] : 0.0f;
+        rinv[e] = 1.0f / g.a_scale[std::min<int64_t>(row, g.M - 1)];  // unconditional loads: no per-load wait
     }
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
@@ -1239,6 +1239,237 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
     }
 }
 
+// Wide split-f16 GEMM ("h2w"): gemm_nt_h2g's arithmetic — per-row power-of-two A scale,
+// the in-register hi/lo split of A (split_h2_pair), three MFMA products per k16 in the
+// same order (a_lo b_hi, a_hi b_lo, a_hi b_hi), k ascending — so every output is
+// bit-identical to h2g, on a 256 x 256 x 32 tile: 8 waves (2 along M x 4 along N), 128 x 64
+// outputs and 8 accumulators per wave, half the LDS bytes per MFMA of the 128 x 128 tile
+// and one block (two 64 KB stages) per CU. Each K-tile opens with one vmcnt(0) + barrier
+// (this stage landed everywhere, the other stage fully read), then runs four phases, one
+// per 32-row block of the wave's rows: that block's A slice read and split in registers,
+// 12 MFMAs against the wave's B fragments (read once per K-tile), and 2 of the 16 LDS-DMA
+// pieces of the next K-tile issued between them, so the next stage's loads have a whole
+// K-tile of MFMA work to land (cdna_hip_programming.md §5.5 T3/T4, without per-phase
+// barriers). A and B stages keep h2g's layouts and source-side XOR swizzles.
+template <bool DUAL, int WN>
+__device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgid) {
+    constexpr int BM = 256, BN = 256;
+    constexpr int WMW = 8 / WN;                 // waves along M
+    constexpr int RB = BM / WMW / 32, NB = BN / WN / 32;  // 32-row / 32-column blocks per wave (RB * NB = 8)
+    constexpr int XA = BM * 128;       // f32 A tile bytes per stage (256 rows x 32 k)
+    constexpr int BPL = BN * 64;       // one f16 B plane tile (256 columns x 32 k)
+    constexpr int STG = XA + 2 * BPL;  // 64 KB
+    extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
+
+    const int64_t tm = wgid / g.tiles_n;
+    const int tn = (int)(wgid % g.tiles_n);
+    const int64_t m0 = tm * BM;
+    const int n0 = tn * BN;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int nk0 = g.K0 / 32;
+    const int nkt = nk0 + (DUAL ? g.K1 / 32 : 0);
+
+    auto sw_a = [](int row) { return (row >> 1) & 7; };
+    auto sw_b = [](int row) { return (row >> 2) & 3; };
+
+    // 64 DMA pieces of 1 KB per stage, 8 per wave: A pieces 4 wave + j (8 rows x 128 B),
+    // B pieces 4 wave + j of 32 (plane piece / 16, 16 rows x 64 B each)
+    // the host routes here only operands whose phase-1 strides equal phase 0's
+    // (lda, ldb, B plane stride), so one set of lane offsets serves both phases
+    uint32_t a_off[4], b_off[4];
+    const char* a_base[2];
+    const char* b_base[2];
+    a_base[0] = reinterpret_cast<const char*>(g.A0 + m0 * g.lda0);
+    b_base[0] = reinterpret_cast<const char*>(g.B0h + (int64_t)n0 * g.ldb0);
+    a_base[1] = DUAL ? reinterpret_cast<const char*>(g.A1 + m0 * g.lda0) : a_base[0];
+    b_base[1] = DUAL ? reinterpret_cast<const char*>(g.B1h + (int64_t)n0 * g.ldb0) : b_base[0];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = 8 * (4 * wave + j) + (lane >> 3);
+        const int chunk = (lane & 7) ^ sw_a(row);
+        const int64_t rr = std::min<int64_t>(m0 + row, g.M - 1) - m0;
+        a_off[j] = (uint32_t)((rr * g.lda0 + 4 * chunk) * 4);
+        const int piece = 4 * wave + j;
+        const int brow = 16 * (piece & 15) + (lane >> 2);
+        const int bchunk = (lane & 3) ^ sw_b(brow);
+        const int64_t rb = std::min<int64_t>(n0 + brow, (int64_t)g.N - 1) - n0;
+        b_off[j] = (uint32_t)(((piece >> 4) * g.B0h_plane + rb * g.ldb0 + 8 * bchunk) * 2);
+    }
+    // piece j (0..7) of K-tile t's fill into stage `base`
+    auto issue = [&](int t, unsigned char* base, int j) {
+        const bool p1 = DUAL && t >= nk0;
+        const int k0 = (t - (p1 ? nk0 : 0)) * 32;
+        if (j < 4) {
+            const char* src = (p1 ? a_base[1] : a_base[0]) + (int64_t)k0 * 4 + a_off[j];
+            __builtin_amdgcn_global_load_lds((const void*)src,
+                                             (__attribute__((address_space(3))) void*)(base + (4 * wave + j) * 1024),
+                                             16, 0, 0);
+        } else {
+            const int jj = j - 4, piece = 4 * wave + jj;
+            const char* src = (p1 ? b_base[1] : b_base[0]) + (int64_t)k0 * 2 + b_off[jj];
+            __builtin_amdgcn_global_load_lds(
+                (const void*)src,
+                (__attribute__((address_space(3))) void*)(base + XA + (piece >> 4) * BPL + (piece & 15) * 1024), 16,
+                0, 0);
+        }
+    };
+
+    // read offsets (the swizzle depends on the row only mod 32: row blocks and column
+    // blocks are immediate offsets 4096 / 2048)
+    const int arow = wm * (32 * RB) + lr;
+    const int bcol = wn * (32 * NB) + lr;
+    int a_rd[2][2], b_rd[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        a_rd[s][0] = arow * 128 + (((4 * s + 2 * lh) ^ sw_a(arow)) << 4);
+        a_rd[s][1] = arow * 128 + (((4 * s + 2 * lh + 1) ^ sw_a(arow)) << 4);
+        b_rd[s] = XA + bcol * 64 + (((2 * s + lh) ^ sw_b(bcol)) << 4);
+    }
+    float asc[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) asc[rb] = g.a_scale[std::min<int64_t>(m0 + arow + 32 * rb, g.M - 1)];
+
+    f32x16 acc[RB][NB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+#pragma unroll
+    for (int j = 0; j < 8; ++j) issue(0, xsm, j);
+    // one K-tile; restrict parameters give the stage pointers distinct alias scopes, so
+    // the ds_reads of `cur` do not wait for the LDS-DMA into `nxt` (vmcnt) in the phases
+    auto ktile = [&](const unsigned char* __restrict__ cur, unsigned char* __restrict__ nxt, int t) {
+        const bool more = t + 1 < nkt;
+#ifndef RVX_H2W_SPREAD
+        // all 16 KB of this wave's share of the next K-tile first: the loads get the whole
+        // K-tile of MFMA work to land before the next tile's wait
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) issue(t + 1, nxt, j);
+        }
+#endif
+        // B fragments [nb][s][plane]: held for the K-tile when the wave has 2 column blocks,
+        // read per use when it has 8 (WN = 1)
+        u32x4 bq[NB <= 2 ? NB : 1][2][2];
+        if constexpr (NB <= 2) {
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                    for (int p = 0; p < 2; ++p)
+                        bq[nb][s][p] = *reinterpret_cast<const u32x4*>(cur + b_rd[s] + nb * 2048 + p * BPL);
+        }
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+#ifdef RVX_H2W_SPREAD
+            if (more) {
+                issue(t + 1, nxt, 2 * rb);
+                issue(t + 1, nxt, 2 * rb + 1);
+            }
+#endif
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                // this k16 half of the row block's A slice, split in registers
+                const float4 alo = *reinterpret_cast<const float4*>(cur + a_rd[s][0] + rb * 4096);
+                const float4 ahi = *reinterpret_cast<const float4*>(cur + a_rd[s][1] + rb * 4096);
+                unsigned w[2][4];  // [hi, lo][pair]
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    split_h2_pair(f4_at(alo, ahi, 2 * j), f4_at(alo, ahi, 2 * j + 1), asc[rb], w[0][j], w[1][j]);
+                f16x8 af[2];
+#pragma unroll
+                for (int p = 0; p < 2; ++p) af[p] = __builtin_bit_cast(f16x8, u32x4{w[p][0], w[p][1], w[p][2], w[p][3]});
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb) {
+                    u32x4 q0, q1;
+                    if constexpr (NB <= 2) {
+                        q0 = bq[nb][s][0];
+                        q1 = bq[nb][s][1];
+                    } else {
+                        q0 = *reinterpret_cast<const u32x4*>(cur + b_rd[s] + nb * 2048);
+                        q1 = *reinterpret_cast<const u32x4*>(cur + b_rd[s] + nb * 2048 + BPL);
+                    }
+                    const f16x8 b0 = __builtin_bit_cast(f16x8, q0);
+                    const f16x8 b1 = __builtin_bit_cast(f16x8, q1);
+                    acc[rb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], b0, acc[rb][nb], 0, 0, 0);
+                    acc[rb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], b1, acc[rb][nb], 0, 0, 0);
+                    acc[rb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], b0, acc[rb][nb], 0, 0, 0);
+                }
+            }
+        }
+    };
+    for (int t = 0; t < nkt; ++t) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // stage t landed for every wave; stage t-1 fully read
+        asm volatile("" ::: "memory");
+        ktile(xsm + (t & 1) * STG, xsm + ((t + 1) & 1) * STG, t);
+    }
+
+    // epilogue as h2g: undo the row and column scales (powers of two: exact), then
+    // alpha / bias / addend / activation
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+        float rinv[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int64_t row = m0 + wm * (32 * RB) + rb * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+            rinv[e] = 1.0f / g.a_scale[std::min<int64_t>(row, g.M - 1)];  // unconditional loads: no per-load wait
+        }
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+            const int col = n0 + wn * (32 * NB) + nb * 32 + lr;
+            if (col >= g.N) continue;
+            const float cinv = g.b_inv[col];
+            float b = 0.0f;
+            if (g.bias0) b = g.bias0[col];
+            if (g.bias1) b += g.bias1[col];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int64_t row = m0 + wm * (32 * RB) + rb * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+                if (row < g.M) {
+                    float v = (acc[rb][nb][e] * rinv[e]) * cinv;
+                    if (g.alpha != 1.0f) v *= g.alpha;
+                    if (g.bias0 || g.bias1) v += b;
+                    if (g.addend) v += g.addend[row * g.ld_add + col];
+                    g.C[row * g.ldc + col] = epi_apply(epi, v);
+                }
+            }
+        }
+    }
+}
+
+// One tile per block (XCD-mapped tile order), or a persistent grid of one block per CU
+// taking tiles from per-XCD counters in row-tile-major order (g.queue, as gemm_nt_h2g):
+// beside the overlapped gather a persistent block keeps its LDS and registers.
+template <bool DUAL, int WN>
+__global__ __launch_bounds__(512, 1) void gemm_nt_h2w(GemmArgs g, int epi) {
+    if (g.queue) {
+        __shared__ int64_t s_t;
+        const int64_t xcd = blockIdx.x % 8;
+        const int64_t first = xcd_first(g.nblocks, xcd), cnt = xcd_count(g.nblocks, xcd);
+        for (;;) {
+            if (threadIdx.x == 0) s_t = (int64_t)atomicAdd(g.queue + 32 * xcd, 1u);
+            __syncthreads();
+            const int64_t t = s_t;
+            if (t >= cnt) break;
+            h2w_tile<DUAL, WN>(g, epi, first + t);
+            __syncthreads();  // LDS stages and s_t are reused by the next tile
+        }
+        return;
+    }
+    const int64_t nwg = g.nblocks, bid = blockIdx.x;
+    h2w_tile<DUAL, WN>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
+}
+
 // B rows n of one or two [N][K] matrices: common scale t_n, f16 planes of each
 // (plane stride N*K), inv[n] = 1 / t_n. One wave per row.
 __global__ __launch_bounds__(256) void k_split_h2_rows(const float* __restrict__ B0, const float* __restrict__ B1,
@@ -1424,6 +1655,52 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
         attr = true;
     }
     const char* t = tag ? tag : "gemm_nt_h2";
+    // 256 x 256 tiles (gemm_nt_h2w, bit-identical). Default for standalone launches (8 waves
+    // along M: 80.3 vs 87.2 ms for the 10M x 768 SAGE GEMM alone, scripts/exp_gemm_wide.sh); the
+    // overlapped GraphSAGE GEMM (persist > 0) keeps h2g, whose 2 x 4-wave blocks leave a gather
+    // wave room on every SIMD (h2w's 211-VGPR waves do not: 487 vs 454 ms/step).
+    // RVX_GEMM_WIDE (read per call; tests cover all): 0 off, 1 waves 2 x 4, 2 waves 8 x 1.
+    const int wide_mode = env_int("RVX_GEMM_WIDE", persist > 0 ? 0 : 2);
+    const bool same_strides = !s1 || (g.lda1 == g.lda0 && g.ldb1 == g.ldb0 && g.B1h_plane == g.B0h_plane);
+    const bool wide = !ep.normalize_rows && wide_mode && same_strides && (int64_t)256 * g.lda0 * 4 < ((int64_t)1 << 31) &&
+                      (!s1 || (int64_t)256 * g.lda1 * 4 < ((int64_t)1 << 31)) &&
+                      (g.B0h_plane + (int64_t)256 * g.ldb0) * 2 < ((int64_t)1 << 31) &&
+                      (!s1 || (g.B1h_plane + (int64_t)256 * g.ldb1) * 2 < ((int64_t)1 << 31));
+    if (wide) {
+        constexpr int wlds = 2 * (256 * 128 + 2 * 256 * 64);
+        static bool wattr = false;
+        if (!wattr) {
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, wlds));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, wlds));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, wlds));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, wlds));
+            wattr = true;
+        }
+        g.tiles_n = (N + 255) / 256;
+        g.nblocks = ((M + 255) / 256) * g.tiles_n;
+        RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
+        // persistent (one block per CU, per-XCD tile queue) when asked for, as h2g
+        const int wcap = persist >= 0 ? persist : env_int("RVX_GEMM_CAP", 0);
+        int64_t wgrid = g.nblocks;
+        if (wcap > 0) wgrid = std::min<int64_t>(wgrid, ((int64_t)active_cus() + 7) / 8 * 8);
+        if (wgrid < g.nblocks && wgrid % 8 == 0) {
+            g.queue = (unsigned*)scratch_bytes("gemm_h2_queue", 8 * 32 * 4);
+            RVX_HIP(hipMemsetAsync(g.queue, 0, 8 * 32 * 4, stream()));
+        } else {
+            wgrid = g.nblocks;
+        }
+        const dim3 wg((unsigned)wgrid), wb(512);
+        // RVX_GEMM_WIDE=1: waves 2 (M) x 4 (N), 128 x 64 each; 2: waves 8 x 1, 32 x 256 each
+        // (A converted once per row instead of by four waves)
+        if (wide_mode == 2) {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1>), wg, wb, wlds, g, ep.epi);
+        } else {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 4>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 4>), wg, wb, wlds, g, ep.epi);
+        }
+        return;
+    }
     // persistent grid of `cap` blocks per CU (a multiple of 8 blocks, so a block
     // keeps its XCD across the tiles it strides over). The overlapped GraphSAGE
     // GEMM asks for 2 (every resident slot, no block turnover beside the gather:

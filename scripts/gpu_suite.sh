@@ -14,5 +14,5 @@ if [ $rc -gt 1 ] || grep -qiE "illegal memory|memory access fault|HSA_STATUS_ERR
 fi
 timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests $ign > gpurun_out/${tag}_b.log 2>&1
 rc2=$?
-tail -3 gpurun_out/${tag}_a.log gpurun_out/${tag}_b.log
+tail -n 3 gpurun_out/${tag}_a.log gpurun_out/${tag}_b.log
 exit $(( rc > rc2 ? rc : rc2 ))

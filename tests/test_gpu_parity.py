@@ -938,3 +938,46 @@ def test_graphsage_in_gemm_row_normalisation_bits(monkeypatch, in_f, out_f, n, d
     assert np.all(np.abs(nrm[nrm > 0] - 1.0) < 1e-5)
     if n <= 1000 and out_f != 200:  # out_f 200: test_graphsage_ill_conditioned_rows_f64_anchor
         assert_close(y1, O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0))
+
+
+@pytest.mark.parametrize("wide", ["1", "2"])
+@pytest.mark.parametrize("in_f,out_f,n,deg,chunks", [(768, 768, 600, 9, 0), (96, 232, 1000, 5, 0),
+                                                     (64, 130, 257, 0, 0), (32, 32, 129, 3, 0),
+                                                     (128, 512, 40000, 4, 2)])
+def test_graphsage_wide_gemm_bits(monkeypatch, in_f, out_f, n, deg, chunks, wide):
+    """The 256 x 256-tile split-f16 GEMM (gemm_nt_h2w, RVX_GEMM_WIDE=1: waves 2 x 4, 2: 8 x 1) does h2g's
+    arithmetic in the same order: identical bits on ragged M and N (M < 256, N < 256,
+    N not a multiple of 32), all-empty neighbourhoods, and the chunked pipeline."""
+    x = O.fill_uniform(n * in_f, 80 + n).reshape(n, in_f)
+    rp, col = O.random_csr(n, deg, 81)
+    g = rv.Graph.from_csr(rp, col)
+    layer = rv.GraphSAGELayer(in_f, out_f, num_samples=max(deg, 1))
+    if chunks:
+        monkeypatch.setenv("RVX_SAGE_CHUNKS", str(chunks))
+    monkeypatch.setenv("RVX_GEMM_WIDE", "0")
+    y0 = layer.forward_graph(x, g)
+    monkeypatch.setenv("RVX_GEMM_WIDE", wide)
+    y1 = layer.forward_graph(x, g)
+    assert np.array_equal(y0, y1)
+    if n <= 1000:
+        assert_close(y1, O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0))
+
+
+@pytest.mark.parametrize("wide", ["1", "2"])
+@pytest.mark.parametrize("hidden,heads", [(64, 4), (768, 8), (96, 4)])
+def test_ruvector_layer_wide_gemm_bits(monkeypatch, hidden, heads, wide):
+    """RuvectorLayer's GEMMs (single and dual, bias / addend / sigmoid / tanh
+    epilogues, N = H and 2H) on the 256 x 256 tile: same bits as the 128 x 128 tile,
+    within 1e-5 of the oracle."""
+    n, deg = 300, 12
+    layer, W, _ = _layer_and_weights(hidden, hidden, heads, 0.1, seed=7)
+    x = O.fill_uniform(n * hidden, 4).reshape(n, hidden)
+    rp, col = O.random_csr(n, deg, 5)
+    ew = O.fill_uniform(n * deg, 6, 0.0, 1.0)
+    g = rv.Graph.from_csr(rp, col, ew)
+    monkeypatch.setenv("RVX_GEMM_WIDE", "0")
+    y0 = layer.forward_graph(x, g)
+    monkeypatch.setenv("RVX_GEMM_WIDE", wide)
+    y1 = layer.forward_graph(x, g)
+    assert np.array_equal(y0, y1)
+    assert_close(y1, O.rvl_forward_graph(W, x, rp, col, ew))
