@@ -49,6 +49,9 @@ void check_graph(const rvx_graph* g) {
     RVX_REQUIRE(g && g->row_ptr && (g->e == 0 || g->col), RVX_ERR_INVALID_PARAMETER, "null graph");
 }
 
+// hand-off events sage_forward_dev uses (callers that add their own take them after these)
+#define SAGE_PIPE_EVENTS(chunks) (2 * (chunks) + 3)
+
 // Row chunking of the layer pipeline (same on every rank for a given chunk count).
 int sage_chunks_for(int64_t n) {
     // 24 chunks with the gather capped at one block per CU (k_aggregate.hip):
@@ -242,7 +245,13 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
     if (chunks <= 0) chunks = sage_chunks_for(n);
     const int64_t step = chunk_step(n, chunks);
     Device& d = device();
-    hipEvent_t* ev = pipeline_events(chunks + 2);
+    hipEvent_t* ev = pipeline_events(SAGE_PIPE_EVENTS(chunks));
+    hipEvent_t* evg = ev + chunks + 2;  // GEMM of chunk c done (normalise stream hand-off)
+    // Opt-in (RVX_SAGE_NORM_STREAM=1, read per call): the row normalisation of chunk c on a
+    // third stream beside the GEMM of chunk c+1 instead of between the GEMMs. Three kernels
+    // at once slow the gather and the GEMM more than the pass costs in line: 488 vs
+    // 435-466 ms/step at 10M x 768 (scripts/exp_norm_stream.sh).
+    const bool norm_side = chunks > 1 && l->normalize && env_int("RVX_SAGE_NORM_STREAM", 0);
     // RVX_SAGE_CU_SPLIT (experiment, read per call): the GEMM and the gather on
     // two streams owning disjoint CU halves instead of sharing every CU
     const int split = chunks > 1 ? env_int("RVX_SAGE_CU_SPLIT", 0) : 0;
@@ -258,7 +267,31 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         RVX_HIP(hipEventRecord(ev[chunks], d.stream));  // aux may not overwrite agg before earlier work is done
         RVX_HIP(hipStreamWaitEvent(gath_s, ev[chunks], 0));
         if (main_s != d.stream) RVX_HIP(hipStreamWaitEvent(main_s, ev[chunks], 0));
+        if (norm_side) RVX_HIP(hipStreamWaitEvent(d.aux2, ev[chunks], 0));
     }
+    // chunk c's output finished by the GEMM: normalise it (third stream or in line), then
+    // the caller's hook on the stream that completed the rows
+    auto finish_chunk = [&](int cc, int64_t rr0, int64_t rrows, bool norm) {
+        if (norm && norm_side) {
+            RVX_HIP(hipEventRecord(evg[cc], main_s));
+            RVX_HIP(hipStreamWaitEvent(d.aux2, evg[cc], 0));
+            StreamScope on_norm(d.aux2);
+            normalize_rows(y + rr0 * l->out, rrows, l->out, true, "sage_normalize");
+            if (hook) hook(cc, rr0, rrows);
+            return;
+        }
+        if (norm) normalize_rows(y + rr0 * l->out, rrows, l->out, true, "sage_normalize");
+        if (hook) {
+            if (norm_side) {  // keep the hooks in chunk order on the normalise stream
+                RVX_HIP(hipEventRecord(evg[cc], main_s));
+                RVX_HIP(hipStreamWaitEvent(d.aux2, evg[cc], 0));
+                StreamScope on_norm(d.aux2);
+                hook(cc, rr0, rrows);
+            } else {
+                hook(cc, rr0, rrows);
+            }
+        }
+    };
     StreamScope on_main(main_s);
     CuScope main_cu(main_cus);
     int c = 0;
@@ -282,15 +315,14 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
             gemm_nt_h2p(rows, l->out, aplanes + r0 * 2 * l->in, 2 * l->in, a_plane, s0, l->wn_h2.as<_Float16>(), &s0,
                         l->ws_h2.as<_Float16>(), scale + r0, l->w_inv.as<float>(), ep, y + r0 * l->out, l->out,
                         "sage_gemm");
-            if (l->normalize) normalize_rows(y + r0 * l->out, rows, l->out, true, "sage_normalize");
-            if (hook) hook(c, r0, rows);
+            finish_chunk(c, r0, rows, l->normalize != 0);
             continue;
         }
         if (fused) {
             sage_gemm_fused(rows, l->out, agg + r0 * l->in, l->in, l->in, x + (row_offset + r0) * l->in, l->in, l->in,
                             l->wn_h2.as<_Float16>(), l->in, wplane, l->ws_h2.as<_Float16>(), l->in, wplane, scale + r0,
                             l->w_inv.as<float>(), y + r0 * l->out, l->out, l->normalize != 0, "sage_gemm");
-            if (hook) hook(c, r0, rows);
+            finish_chunk(c, r0, rows, false);
             continue;
         }
         GemmOperand s0{agg + r0 * l->in, l->in, l->wn_t.as<float>(), l->in, l->in, l->wn_x3.as<uint16_t>(), plane};
@@ -307,14 +339,19 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         else
             gemm_nt(rows, l->out, s0, &s1, ep, y + r0 * l->out, l->out, "sage_gemm");
 #ifndef RVX_AB_NO_NORMALIZE  // timing-only ablation build (scripts/exp_sage_ablate.sh): results wrong
-        if (l->normalize && !epn.normalize_rows) normalize_rows(y + r0 * l->out, rows, l->out, true, "sage_normalize");
+        finish_chunk(c, r0, rows, l->normalize && !epn.normalize_rows);
+#else
+        finish_chunk(c, r0, rows, false);
 #endif
-        if (hook) hook(c, r0, rows);
     }
-    for (; hook && c < chunks; ++c) hook(c, n, 0);
+    for (; hook && c < chunks; ++c) finish_chunk(c, n, 0, false);
     if (main_s != d.stream) {
         RVX_HIP(hipEventRecord(ev[chunks + 1], main_s));
         RVX_HIP(hipStreamWaitEvent(d.stream, ev[chunks + 1], 0));
+    }
+    if (norm_side) {  // the normalise stream's last chunk (and hooks) before anything after the layer
+        RVX_HIP(hipEventRecord(evg[chunks], d.aux2));
+        RVX_HIP(hipStreamWaitEvent(d.stream, evg[chunks], 0));
     }
 }
 
@@ -540,7 +577,7 @@ rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g
         const std::vector<ExchangeRound> plan = exchange_plan(PLAN_SAGE, offsets, world);
         const int chunks = (int)plan.size();
         Device& d = device();
-        hipEvent_t* ev = pipeline_events(2 * chunks + 3) + chunks + 2;  // after sage_forward_dev's chunks + 2
+        hipEvent_t* ev = pipeline_events(SAGE_PIPE_EVENTS(chunks) + chunks + 1) + SAGE_PIPE_EVENTS(chunks);  // after sage_forward_dev's
         auto hook = [&](int c, int64_t, int64_t) {
             RVX_HIP(hipEventRecord(ev[c], stream()));  // chunk c's rows are complete on the pipeline's main stream
             RVX_HIP(hipStreamWaitEvent(d.xfer, ev[c], 0));

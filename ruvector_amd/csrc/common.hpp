@@ -66,6 +66,7 @@ struct Device {
     hipStream_t stream = nullptr;  // every kernel of this device runs here ...
     hipStream_t aux = nullptr;     // ... except pipelined stages overlapped on this one
     hipStream_t xfer = nullptr;    // RCCL halo exchange overlapped with compute
+    hipStream_t aux2 = nullptr;    // a third pipeline stage (GraphSAGE row normalisation)
     std::vector<hipEvent_t> pipe_events;  // timing-free events for stream hand-offs
     // CU-partitioned stream pair (cu_split_streams): [0] the MFMA side, [1] the gather side
     hipStream_t cu_split[2] = {nullptr, nullptr};

@@ -32,6 +32,7 @@ static Device& device_for(int id) {
     RVX_HIP(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     RVX_HIP(hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking));
     RVX_HIP(hipStreamCreateWithFlags(&d->xfer, hipStreamNonBlocking));
+    RVX_HIP(hipStreamCreateWithFlags(&d->aux2, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     RVX_HIP(hipGetDeviceProperties(&prop, id));
     d->num_cus = prop.multiProcessorCount;
