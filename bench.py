@@ -99,6 +99,12 @@ def main():
     x = rv.Buffer(n_tot * d * 4)
     x.fill_normal(n_tot * d, 3)
     tables = [rv.Buffer(n_tot * d * 4) for _ in range(min(layers, 2))]
+    # Layer l's L2 normalisation is carried into layer l+1 (rvx_sage_forward_exchange2:
+    # the unnormalised rows and 1/|y| per row, exchanged together) instead of a pass that
+    # re-reads and re-writes the table; the last layer normalises in place. RVX_SAGE_DEFER=0
+    # runs every layer with its own pass.
+    defer = layers > 1 and os.environ.get("RVX_SAGE_DEFER", "1") != "0"
+    invs = [rv.Buffer(n_tot * 4) for _ in range(2)] if defer else None
     g = rv.Graph.random_shard(n_tot, r0, n_loc, deg, 4)
     sage = [rv.GraphSAGELayer(d, d, num_samples=deg) for _ in range(layers)]
     rv.synchronize()
@@ -107,7 +113,9 @@ def main():
         src = x
         for li, layer in enumerate(sage):
             dst = tables[li % 2]
-            rv._lib.call("rvx_sage_forward_exchange", layer._h, g.handle, src.handle, dst.handle, off_ptr,
+            xm = invs[(li - 1) % 2].handle if defer and li > 0 else None
+            yi = invs[li % 2].handle if defer and li < layers - 1 else None
+            rv._lib.call("rvx_sage_forward_exchange2", layer._h, g.handle, src.handle, xm, dst.handle, yi, off_ptr,
                          comm._h if comm else None, int(li < layers - 1))
             src = dst
 
@@ -153,9 +161,10 @@ def main():
     agg_bytes = n_loc * deg * (4 * d + 4) + n_loc * (8 + 4 * d)   # per layer
     gemm_flops = 2.0 * n_loc * d * (2 * d)
     norm_bytes = 2 * n_loc * d * 4
+    norm_layers = 1 if defer else layers  # carried normalisation: only the last layer runs the pass
     rls = {"sage_aggregate": rl("sage_aggregate", "GB/s", agg_bytes * layers, HBM_PEAK_GBS, "hbm"),
            "sage_gemm": rl("sage_gemm", "TFLOP/s", gemm_flops * layers, GEMM_PEAK_TFS, "mfma"),
-           "sage_normalize": rl("sage_normalize", "GB/s", norm_bytes * layers, HBM_PEAK_GBS, "hbm")}
+           "sage_normalize": rl("sage_normalize", "GB/s", norm_bytes * norm_layers, HBM_PEAK_GBS, "hbm")}
     if comm is not None:
         rls["halo_exchange"] = rl("halo_exchange", "GB/s", (n_tot - n_loc) * d * 4 * (layers - 1), XGMI_PEAK_GBS,
                                   "xgmi")
@@ -165,7 +174,7 @@ def main():
     # whole-layer floor: HBM and MFMA work overlap, so a layer cannot beat the
     # larger of the two floors
     layer_ms = elapsed / a.steps / layers * 1e3
-    hbm_floor = (agg_bytes + norm_bytes) / (HBM_PEAK_GBS * 1e9) * 1e3
+    hbm_floor = (agg_bytes + norm_bytes * norm_layers / layers) / (HBM_PEAK_GBS * 1e9) * 1e3
     mfma_floor = gemm_flops / (GEMM_PEAK_TFS * 1e12) * 1e3
     layer_rl = {"layer_ms": round(layer_ms, 3), "hbm_floor_ms": round(hbm_floor, 3),
                 "mfma_floor_ms": round(mfma_floor, 3), "frac": round(max(hbm_floor, mfma_floor) / layer_ms, 4)}
@@ -182,7 +191,10 @@ def main():
                                "metric's 10M scale); node-range shards + chunked RCCL p2p halo exchange for N>1",
                    "nodes_total": n_tot, "nodes_per_gpu": n_loc, "dim": d, "degree": deg, "layers": layers,
                    "edges_per_step": edges_per_step, "parallelism": f"node-range x{world}",
-                   "pipeline": PIPELINE},
+                   "pipeline": PIPELINE,
+                   "normalisation": ("layer l's L2 normalisation carried into layer l+1 as 1/|y| per row "
+                                     "(rvx_sage_forward_exchange2); the last layer normalises in place")
+                   if defer else "every layer normalises in place"},
         "roofline": dict(rls[dom], kernel=dom),
         "roofline_kernels": {k: v for k, v in rls.items() if v},
         "roofline_layer": layer_rl,
@@ -192,7 +204,7 @@ def main():
     if comm is not None:
         line["multi_gpu"] = exchange_report(a, kern, comm, world, rank, offsets, d, layers)
     if rank == 0 and world == 1 and not a.no_cpu:
-        line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, tables, n_tot, d, deg, layers)
+        line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, tables, n_tot, d, deg, layers, invs)
     if world == 1:
         line["gemm_paths"] = gemm_alternatives(g, x, tables[0], off_ptr, d, deg)
     if not a.no_scan:
@@ -374,7 +386,7 @@ def gemm_alternatives(g, x, y, off_ptr, d, deg):
     return out
 
 
-def cpu_baseline(a, x_buf, g, tables, n, d, deg, layers):
+def cpu_baseline(a, x_buf, g, tables, n, d, deg, layers, invs=None):
     """Oracle (reference algorithm, C++) on a bounded sample of layer-1 rows, plus
     per-layer parity of every layer: tables[i] holds the GPU's layer-(i+1) output of
     the last timed step; layer i+1 > 1 is checked on rows 0..8191 from the GPU's own
@@ -398,7 +410,16 @@ def cpu_baseline(a, x_buf, g, tables, n, d, deg, layers):
     ref = O.sage_forward(x, rp, col, wn, ws, rows=(0, rows), threads=threads)
     dt = time.perf_counter() - t0
     del x
-    got = tables[0].gather_rows(n, d, np.arange(rows))
+    # deferred normalisation: layer l's table holds unnormalised rows, invs[l] their 1/|y|
+    inv = [b.download(np.float32, (n,)) for b in invs] if invs else None
+
+    def rows_of(li, ids):
+        r = tables[li % 2].gather_rows(n, d, ids)
+        if inv is not None and li < layers - 1:
+            r = (r * inv[li % 2][ids][:, None]).astype(np.float32)
+        return r
+
+    got = rows_of(0, np.arange(rows))
     err, row_err = rel_errs(got, ref)
     del got, ref
     cpu = {"value": round(rows * deg / dt, 1), "unit": "edges/s", "cores": threads, "kind": "port", "host": tinfo,
@@ -408,10 +429,10 @@ def cpu_baseline(a, x_buf, g, tables, n, d, deg, layers):
     r2 = min(n, 8192)
     for li in range(1, layers):
         need = np.unique(np.concatenate([np.arange(r2), col[:rp[r2]]]))
-        h = tables[(li - 1) % 2].gather_rows(n, d, need)
+        h = rows_of(li - 1, need)
         ref = O.sage_forward(h, rp[:r2 + 1], np.searchsorted(need, col[:rp[r2]]).astype(np.int32), wn, ws,
                              rows=(0, r2), threads=threads)
-        got = tables[li % 2].gather_rows(n, d, np.arange(r2))
+        got = rows_of(li, np.arange(r2))
         e, re_ = rel_errs(got, ref)
         per_layer.append({"layer": li + 1, "rows": r2, "max_rel_err": e, "row_rel_l2_max": re_,
                           "input": f"GPU layer-{li} rows"})

@@ -182,6 +182,18 @@ rvx_status rvx_sage_forward_shard_device(const rvx_sage_layer* l, const rvx_grap
  * stream. x_full and y_full must differ. offsets has comm_size+1 entries. */
 rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g, const rvx_buffer* x_full,
                                      rvx_buffer* y_full, const int64_t* offsets, rvx_comm* comm, int32_t exchange);
+/* rvx_sage_forward_exchange for a stack with the L2 normalisation (graphsage.rs:177-182)
+ * carried between layers instead of materialised (an rvx extension; the values are the
+ * reference's within the 1e-5 bar). x_rowmul (NULL = none) [N] floats: row i of x_full
+ * enters the layer as x_full[i] * x_rowmul[i] (the previous layer's y_rowinv). y_rowinv
+ * (NULL = none) [N] floats: the owned rows of y_full are left unnormalised and
+ * y_rowinv[i] = 1 / |y_full[i]| (1 where the norm is 0 or NaN) is written instead, and
+ * exchanged with the rows. Where the layer's GEMM path cannot take it (not the split-f16
+ * h2g path), x_full is rescaled in place by x_rowmul and y_full normalised as usual, with
+ * y_rowinv set to 1. A stack's last layer passes y_rowinv = NULL. */
+rvx_status rvx_sage_forward_exchange2(const rvx_sage_layer* l, const rvx_graph* g, rvx_buffer* x_full,
+                                      const rvx_buffer* x_rowmul, rvx_buffer* y_full, rvx_buffer* y_rowinv,
+                                      const int64_t* offsets, rvx_comm* comm, int32_t exchange);
 
 
 /* ------------------------------------------------------------------ */

@@ -204,10 +204,55 @@ namespace {
 // library stream.
 using ChunkHook = std::function<void(int c, int64_t r0, int64_t rows)>;
 
+// The layer runs the in-register split-f16 dual GEMM (gemm_nt_h2, h2g) — the path that
+// can take a deferred normalisation (below) — rather than h2p, the fused kernel or the
+// split-bf16 / fp32 GEMMs. Same conditions as sage_forward_dev's choice.
+bool sage_defer_path(const rvx_sage_layer* l, int64_t n, const float* x, const float* y, int64_t row_offset) {
+    const GemmOperand w0{nullptr, 2 * l->in, nullptr, l->in, l->in, nullptr, 0, l->wn_h2.as<_Float16>(), 0, nullptr};
+    const int64_t a_plane = std::max<int64_t>(n, 1) * 2 * l->in;
+    const bool h2p = l->wn_h2.p && l->in <= 1024 && l->in % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
+                     gemm_h2p_ok(std::max<int64_t>(n, 1), l->out, 2 * l->in, a_plane, w0, &w0);
+    if (h2p || !l->wn_h2.p || l->in > 1024 || ((uintptr_t)x & 15) != 0 || l->in % 4 != 0) return false;
+    // the aggregate scratch is hipMalloc'd (aligned): x stands in for its alignment check
+    if (!gemm_h2_ok(std::max<int64_t>(n, 1), l->out, GemmOperand{x, l->in, nullptr, l->in, l->in}, nullptr)) return false;
+    const int64_t wplane = (int64_t)l->in * l->out;
+    return !sage_gemm_fused_ok(std::max<int64_t>(n, 1), l->out, l->in, l->in, l->in, l->in, l->in, l->in, wplane,
+                               wplane, l->out, x, x + row_offset * l->in, y);
+}
+
+__global__ void k_rows_inv_norm(const float* __restrict__ ssq, int tiles, int64_t rows, float* __restrict__ inv) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    float s = 0.0f;
+    for (int t = 0; t < tiles; ++t) s = __fadd_rn(s, ssq[r * tiles + t]);
+    const float norm = sqrtf(s);
+    inv[r] = norm > 0.0f ? 1.0f / norm : 1.0f;  // rows with norm 0 / NaN stay as they are (normalize_rows)
+}
+
+__global__ void k_fill_value(float* __restrict__ p, int64_t n, float v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+void fill_value(float* p, int64_t n, float v) {
+    if (n > 0) RVX_LAUNCH("fill_value", k_fill_value, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, p, n, v);
+}
+
+__global__ void k_scale_rows(float* __restrict__ x, int64_t rows, int dim, const float* __restrict__ mul) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows * dim) return;
+    x[i] *= mul[i / dim];
+}
+
 // x: node table indexed by the CSR columns; rows [row_offset, row_offset+g->n)
 // of it are this graph's destination (self) rows.
+// Deferred normalisation (h2g path only, sage_defer_path): x_mul (nullable) holds a
+// multiplier for every row of x (the previous layer's 1/|y|, applied as rows are gathered
+// and in the GEMM's self-operand split); y_inv (nullable) makes the layer leave its output
+// rows unnormalised and write 1/|y| per row instead (from the GEMM epilogue's per-tile
+// sums of squares) — the pass that re-reads and re-writes y is not run.
 void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* x, float* y, int64_t row_offset = 0,
-                      int chunks = 0, const ChunkHook& hook = nullptr) {
+                      int chunks = 0, const ChunkHook& hook = nullptr, const float* x_mul = nullptr,
+                      float* y_inv = nullptr) {
     // rows with more than num_samples neighbours aggregate the reference's
     // sample_neighbors subset (graphsage.rs:92-102, k_sample.hip)
     g = sampled_graph(g, l->num_samples);
@@ -238,6 +283,10 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
                                           wplane, wplane, l->out, agg, x + row_offset * l->in, y);
     GemmEpilogue ep;
     ep.epi = GEMM_EPI_RELU;
+    RVX_REQUIRE((!x_mul && !y_inv) || (h2 && !h2p && !fused), RVX_ERR_UNSUPPORTED,
+                "deferred normalisation needs the split-f16 GEMM path");
+    const int ntiles = (l->out + 127) / 128;
+    float* ssq = y_inv ? scratch_f32("sage_sumsq", std::max<int64_t>(n, 1) * ntiles) : nullptr;
     // Rows are independent, so the layer runs as a two-stage pipeline over
     // row chunks: the HBM-bound gather of chunk c+1 (aux stream) overlaps the
     // MFMA-bound GEMM + normalisation of chunk c (library stream). Every row
@@ -303,12 +352,13 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
             aggregate_rows(g->row_ptr + r0, g->col, nullptr, rows, x, l->in, a, /*empty_fill zeros*/ 0, 0,
                            h2p ? nullptr : agg + r0 * l->in, "sage_aggregate", /*overlapped*/ true,
                            x + (row_offset + r0) * l->in, h2 ? scale + r0 : nullptr,
-                           h2p ? aplanes + r0 * 2 * l->in : nullptr, a_plane);
+                           h2p ? aplanes + r0 * 2 * l->in : nullptr, a_plane, x_mul,
+                           x_mul ? x_mul + row_offset + r0 : nullptr);
             RVX_HIP(hipEventRecord(ev[c], gath_s));
             RVX_HIP(hipStreamWaitEvent(main_s, ev[c], 0));
         } else {
             aggregate_rows(g->row_ptr, g->col, nullptr, n, x, l->in, a, 0, 0, agg, "sage_aggregate", false,
-                           x + row_offset * l->in, scale, aplanes, a_plane);
+                           x + row_offset * l->in, scale, aplanes, a_plane, x_mul, x_mul ? x_mul + row_offset : nullptr);
         }
         if (h2p) {
             GemmOperand s0{nullptr, 2 * l->in, nullptr, l->in, l->in};
@@ -331,15 +381,25 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         // opt-in: the h2g GEMM normalises its own rows (last column tile of each 128-row
         // block, same bits as normalize_rows) instead of a separate pass over y
         GemmEpilogue epn = ep;
-        epn.normalize_rows = h2 && l->normalize && gemm_h2_rownorm_ok(l->out, y, l->out);
+        epn.normalize_rows = h2 && l->normalize && !y_inv && gemm_h2_rownorm_ok(l->out, y, l->out);
+        epn.a1_rowmul = x_mul ? x_mul + row_offset + r0 : nullptr;
+        epn.row_sumsq = y_inv ? ssq + r0 * ntiles : nullptr;
         if (h2)
             gemm_nt_h2(rows, l->out, s0, l->wn_h2.as<_Float16>(), &s1, l->ws_h2.as<_Float16>(), scale + r0,
                        l->w_inv.as<float>(), epn, y + r0 * l->out, l->out, "sage_gemm",
                        chunks > 1 ? env_int("RVX_SAGE_GEMM_CAP", 2) : -1);
         else
             gemm_nt(rows, l->out, s0, &s1, ep, y + r0 * l->out, l->out, "sage_gemm");
+        if (y_inv && rows > 0) {
+            if (l->normalize) {
+                RVX_LAUNCH("sage_inv_norm", k_rows_inv_norm, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
+                           ssq + r0 * ntiles, ntiles, rows, y_inv + r0);
+            } else {
+                fill_value(y_inv + r0, rows, 1.0f);
+            }
+        }
 #ifndef RVX_AB_NO_NORMALIZE  // timing-only ablation build (scripts/exp_sage_ablate.sh): results wrong
-        finish_chunk(c, r0, rows, l->normalize && !epn.normalize_rows);
+        finish_chunk(c, r0, rows, l->normalize && !epn.normalize_rows && !y_inv);
 #else
         finish_chunk(c, r0, rows, false);
 #endif
@@ -554,6 +614,14 @@ rvx_status rvx_sage_forward_shard_device(const rvx_sage_layer* l, const rvx_grap
 
 rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g, const rvx_buffer* x_full,
                                      rvx_buffer* y_full, const int64_t* offsets, rvx_comm* comm, int32_t exchange) {
+    // without x_rowmul the input is never rescaled
+    return rvx_sage_forward_exchange2(l, g, const_cast<rvx_buffer*>(x_full), nullptr, y_full, nullptr, offsets, comm,
+                                      exchange);
+}
+
+rvx_status rvx_sage_forward_exchange2(const rvx_sage_layer* l, const rvx_graph* g, rvx_buffer* x_full,
+                                      const rvx_buffer* x_rowmul, rvx_buffer* y_full, rvx_buffer* y_rowinv,
+                                      const int64_t* offsets, rvx_comm* comm, int32_t exchange) {
     return guard([&] {
         check_graph(g);
         RVX_REQUIRE(l && x_full && y_full && offsets, RVX_ERR_INVALID_PARAMETER, "null argument");
@@ -567,11 +635,30 @@ rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g
         const int64_t N = offsets[world];
         RVX_REQUIRE(x_full->mem.bytes >= N * l->in * 4, RVX_ERR_DIMENSION_MISMATCH, "x_full smaller than N*in");
         RVX_REQUIRE(y_full->mem.bytes >= N * l->out * 4, RVX_ERR_DIMENSION_MISMATCH, "y_full smaller than N*out");
+        RVX_REQUIRE(!x_rowmul || x_rowmul->mem.bytes >= N * 4, RVX_ERR_DIMENSION_MISMATCH, "x_rowmul smaller than N");
+        RVX_REQUIRE(!y_rowinv || y_rowinv->mem.bytes >= N * 4, RVX_ERR_DIMENSION_MISMATCH, "y_rowinv smaller than N");
         ComputeLock cl;
         float* y = y_full->mem.as<float>();
         const float* x = x_full->mem.as<float>();
+        // deferred normalisation where this layer's GEMM path takes it; otherwise the
+        // multiplied input is materialised in place and the output normalised as usual
+        // (then every 1/|y| is 1)
+        const bool can = sage_defer_path(l, g->n, x, y + offsets[me] * l->out, offsets[me]);
+        const float* xm = x_rowmul ? x_rowmul->mem.as<float>() : nullptr;
+        if (xm && !can) {
+            const int64_t tot = N * l->in;
+            RVX_LAUNCH("scale_rows", k_scale_rows, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                       x_full->mem.as<float>(), N, l->in, xm);
+            xm = nullptr;
+        }
+        float* yinv = y_rowinv ? y_rowinv->mem.as<float>() : nullptr;
+        if (yinv && !can) {
+            fill_value(yinv, N, 1.0f);
+            yinv = nullptr;
+        }
+        float* yinv_rows = yinv ? yinv + offsets[me] : nullptr;
         if (!exchange || world == 1) {
-            sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me]);
+            sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], 0, nullptr, xm, yinv_rows);
             return;
         }
         const std::vector<ExchangeRound> plan = exchange_plan(PLAN_SAGE, offsets, world);
@@ -584,8 +671,9 @@ rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g
             StreamScope on_xfer(d.xfer);
             ProfScope ps("halo_exchange");
             comm_exchange_rows(comm, y, l->out, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
+            if (yinv) comm_exchange_rows(comm, yinv, 1, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
         };
-        sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], chunks, hook);
+        sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], chunks, hook, xm, yinv_rows);
         RVX_HIP(hipEventRecord(ev[chunks], d.xfer));
         {
             // the exchange's tail the compute stream waits for: from the last chunk's

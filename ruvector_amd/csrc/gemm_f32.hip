@@ -56,6 +56,9 @@ struct GemmArgs {
     int xsplit;  // queue mode: XCD pair (2i, 2i+1) shares a row range, each XCD takes half the column tiles
     // in-launch row normalisation (h2g): one arrival ticket per 128-row tile, zeroed per launch
     unsigned* row_tickets;
+    // deferred normalisation (h2g): per-row partial sums of squares per column tile, and the
+    // phase-1 operand's per-row multiplier
+    float* row_sumsq; const float* a1_rowmul;
 };
 
 __device__ __forceinline__ float epi_apply(int epi, float v) {
@@ -921,7 +924,10 @@ __device__ __forceinline__ void h2g_tile(const GemmArgs& g, int epi, int64_t wgi
         for (int e = 0; e < 16; ++e) acc[j][e] = 0.0f;
 
     const int arow = wave * 32 + lr;
-    const float a_sc = g.a_scale[std::min<int64_t>(m0 + arow, g.M - 1)];
+    const float a_sc0 = g.a_scale[std::min<int64_t>(m0 + arow, g.M - 1)];
+    // phase 1 with a row multiplier m: v * (m * sc) == round(v * m) * sc bit for bit (sc is a
+    // power of two), i.e. the split of the multiplied row at no extra k-loop work
+    const float a_sc1 = g.a1_rowmul ? a_sc0 * g.a1_rowmul[std::min<int64_t>(m0 + arow, g.M - 1)] : a_sc0;
     int a_rd[2][2], b_rd[2][4];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -931,7 +937,8 @@ __device__ __forceinline__ void h2g_tile(const GemmArgs& g, int epi, int64_t wgi
         for (int ni = 0; ni < 4; ++ni) b_rd[s][ni] = XA + xb_sw(ni * 32 + lr, 2 * s + lh);
     }
 
-    auto tile = [&](const unsigned char* __restrict__ cur, unsigned char* __restrict__ nxt, int fph, int fk0) {
+    auto tile = [&](const unsigned char* __restrict__ cur, unsigned char* __restrict__ nxt, int fph, int fk0,
+                    float a_sc) {
         if (fph == 0) fill_ph(0, fk0, nxt);
         else if (DUAL && fph == 1) fill_ph(1, fk0, nxt);
         float4 alo[2], ahi[2];
@@ -982,38 +989,49 @@ __device__ __forceinline__ void h2g_tile(const GemmArgs& g, int epi, int64_t wgi
             int fph = -1, fk0 = 0;
             if (kt + 1 < nkp) { fph = ph; fk0 = (kt + 1) * 32; }
             else if (DUAL && ph == 0 && nk1 > 0) fph = 1;
-            tile(xsm + stage * STG, xsm + (stage ^ 1) * STG, fph, fk0);
+            tile(xsm + stage * STG, xsm + (stage ^ 1) * STG, fph, fk0, ph ? a_sc1 : a_sc0);
             __syncthreads();
             stage ^= 1;
         }
     }
 
     // epilogue: undo the row and column scales (powers of two: exact), then
-    // alpha / bias / addend / activation as the other kernels
-    float rinv[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-        const int64_t row = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-        rinv[e] = 1.0f / g.a_scale[std::min<int64_t>(row, g.M - 1)];  // unconditional loads: no per-load wait
-    }
+    // alpha / bias / addend / activation as the other kernels; row-outer so the deferred
+    // normalisation's per-row sum of squares needs one register
+    float cinv[4], cb[4];
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
-        const int col = n0 + ni * 32 + lr;
-        if (col >= g.N) continue;
-        const float cinv = g.b_inv[col];
+        const int col = std::min(n0 + ni * 32 + lr, g.N - 1);
+        cinv[ni] = g.b_inv[col];
         float b = 0.0f;
         if (g.bias0) b = g.bias0[col];
         if (g.bias1) b += g.bias1[col];
+        cb[ni] = b;
+    }
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int64_t row = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-            if (row < g.M) {
-                float v = (acc[ni][e] * rinv[e]) * cinv;
+    for (int e = 0; e < 16; ++e) {
+        const int64_t row = m0 + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        const float rinv = 1.0f / g.a_scale[std::min<int64_t>(row, g.M - 1)];  // unconditional loads: no per-load wait
+        float ssq = 0.0f;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int col = n0 + ni * 32 + lr;
+            if (col < g.N && row < g.M) {
+                float v = (acc[ni][e] * rinv) * cinv[ni];
                 if (g.alpha != 1.0f) v *= g.alpha;
-                if (g.bias0 || g.bias1) v += b;
+                if (g.bias0 || g.bias1) v += cb[ni];
                 if (g.addend) v += g.addend[row * g.ld_add + col];
-                g.C[row * g.ldc + col] = epi_apply(epi, v);
+                v = epi_apply(epi, v);
+                g.C[row * g.ldc + col] = v;
+                ssq = __fadd_rn(ssq, __fmul_rn(v, v));
             }
+        }
+        if (g.row_sumsq) {
+            // this tile's 128 columns of the row: lanes lr of one half hold columns
+            // ni * 32 + lr; a fixed xor tree over the 32 lanes of the half
+#pragma unroll
+            for (int off = 16; off > 0; off >>= 1) ssq += __shfl_xor(ssq, off);
+            if (lr == 0 && row < g.M) g.row_sumsq[row * g.tiles_n + tn] = ssq;
         }
     }
     if (g.row_tickets) h2g_rownorm(g, tm, m0, xsm);
@@ -1643,7 +1661,9 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
     }
     g.bias0 = ep.bias0; g.bias1 = ep.bias1; g.C = C; g.ldc = ldc; g.M = M; g.N = N; g.alpha = ep.alpha;
     g.a_scale = a_scale; g.b_inv = b_inv;
+    g.row_sumsq = ep.row_sumsq; g.a1_rowmul = ep.a1_rowmul;
     RVX_REQUIRE(gemm_h2_ok(M, N, s0, s1), RVX_ERR_INVALID_SHAPE, "shape not supported by the split-f16 GEMM");
+    RVX_REQUIRE(!ep.a1_rowmul || s1, RVX_ERR_INVALID_PARAMETER, "a1_rowmul needs a dual GEMM");
     g.tiles_n = (N + XBN - 1) / XBN;
     g.nblocks = ((M + 127) / 128) * g.tiles_n;
     RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
@@ -1662,7 +1682,7 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
     // RVX_GEMM_WIDE (read per call; tests cover all): 0 off, 1 waves 2 x 4, 2 waves 8 x 1.
     const int wide_mode = env_int("RVX_GEMM_WIDE", persist > 0 ? 0 : 2);
     const bool same_strides = !s1 || (g.lda1 == g.lda0 && g.ldb1 == g.ldb0 && g.B1h_plane == g.B0h_plane);
-    const bool wide = !ep.normalize_rows && wide_mode && same_strides && (int64_t)256 * g.lda0 * 4 < ((int64_t)1 << 31) &&
+    const bool wide = !ep.normalize_rows && !ep.row_sumsq && !ep.a1_rowmul && wide_mode && same_strides && (int64_t)256 * g.lda0 * 4 < ((int64_t)1 << 31) &&
                       (!s1 || (int64_t)256 * g.lda1 * 4 < ((int64_t)1 << 31)) &&
                       (g.B0h_plane + (int64_t)256 * g.ldb0) * 2 < ((int64_t)1 << 31) &&
                       (!s1 || (g.B1h_plane + (int64_t)256 * g.ldb1) * 2 < ((int64_t)1 << 31));

@@ -66,7 +66,9 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
                                                       const float* __restrict__ x, int dim, int empty_fill,
                                                       int post_scale, float* __restrict__ out,
                                                       const float* __restrict__ self_x, float* __restrict__ row_scale,
-                                                      _Float16* __restrict__ planes, int64_t pstride) {
+                                                      _Float16* __restrict__ planes, int64_t pstride,
+                                                      const float* __restrict__ row_mul,
+                                                      const float* __restrict__ self_mul) {
     const int lane = threadIdx.x & 63;
 #ifndef RVX_AGG_PRIO
 #define RVX_AGG_PRIO 0
@@ -93,6 +95,8 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
         const int my_c = lane < cnt ? col[e0 + lane] : 0;
         const float my_w = (W && lane < cnt) ? wts[e0 + lane] : 1.0f;
         int t = 0;
+        // deferred normalisation: one multiplier per gathered row (wave-uniform id)
+        const float my_m = (row_mul && lane < cnt) ? row_mul[my_c] : 1.0f;
         for (; t + U <= cnt; t += U) {
             float4 v[U][NV];
 #pragma unroll
@@ -107,6 +111,11 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
             for (int u = 0; u < U; ++u) {
                 float wu = 1.0f;
                 if (W) wu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), t + u));
+                if (row_mul) {
+                    const float mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_m), t + u));
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) v[u][j] = scale4(v[u][j], mu);
+                }
 #pragma unroll
                 for (int j = 0; j < NV; ++j) acc[j] = agg_op<AGG>(acc[j], W ? scale4(v[u][j], wu) : v[u][j]);
             }
@@ -116,9 +125,11 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
             const float* src = x + (int64_t)c * dim + 4 * lane;
             float wu = 1.0f;
             if (W) wu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), t));
+            const float mu = row_mul ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_m), t)) : 1.0f;
 #pragma unroll
             for (int j = 0; j < NV; ++j) {
                 float4 v = active[j] ? ld_row4<NT>(src + 256 * j) : make_float4(0, 0, 0, 0);
+                if (row_mul) v = scale4(v, mu);
                 acc[j] = agg_op<AGG>(acc[j], W ? scale4(v, wu) : v);
             }
         }
@@ -141,11 +152,13 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
     if (row_scale) {  // split-f16 GEMM operand scale over this row's aggregate and self rows
         float m = 0.0f;
         const float* sp = self_x + row * dim + 4 * lane;
+        const float smul = self_mul ? self_mul[row] : 1.0f;
         float4 sv[NV];
 #pragma unroll
         for (int j = 0; j < NV; ++j)
             if (active[j]) {
-                const float4 v = *reinterpret_cast<const float4*>(sp + 256 * j);
+                float4 v = *reinterpret_cast<const float4*>(sp + 256 * j);
+                if (self_mul) v = scale4(v, smul);
                 sv[j] = v;
                 m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
                 if (cnt_total > 0)
@@ -216,24 +229,26 @@ __global__ __launch_bounds__(256) void k_aggregate_scalar(const int64_t* rp, con
 template <int AGG, bool W>
 void launch_agg(const char* t, const int64_t* rp, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
                 int empty_fill, int post_scale, float* out, int cap_per_cu, bool deep, bool nt, const float* self_x,
-                float* row_scale, _Float16* planes, int64_t pstride) {
+                float* row_scale, _Float16* planes, int64_t pstride, const float* row_mul, const float* self_mul) {
     int64_t blocks = (n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
     if (cap_per_cu > 0) blocks = std::min<int64_t>(blocks, (int64_t)cap_per_cu * active_cus());
     const dim3 grid((unsigned)blocks), block(256);
     const bool vec = (dim % 4 == 0) && (((uintptr_t)x & 15) == 0) && (((uintptr_t)out & 15) == 0);
     RVX_REQUIRE(!planes || (vec && row_scale && self_x && empty_fill == 0), RVX_ERR_INVALID_SHAPE,
                 "planes need the vector gather with zero-filled empty rows");
+    RVX_REQUIRE(!row_mul || (vec && empty_fill == 0), RVX_ERR_INVALID_SHAPE,
+                "row multipliers need the vector gather with zero-filled empty rows");
 #define RVX_AGG_VEC(NV)                                                                                          \
     do {                                                                                                         \
         if (deep && nt)                                                                                        \
             RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 8, true>), grid, block, 0, rp, col, w, n, x, dim,         \
-                       empty_fill, post_scale, out, self_x, row_scale, planes, pstride);                         \
+                       empty_fill, post_scale, out, self_x, row_scale, planes, pstride, row_mul, self_mul);                         \
         else if (deep)                                                                                           \
             RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 8>), grid, block, 0, rp, col, w, n, x, dim, empty_fill,   \
-                       post_scale, out, self_x, row_scale, planes, pstride);                                     \
+                       post_scale, out, self_x, row_scale, planes, pstride, row_mul, self_mul);                                     \
         else                                                                                                     \
             RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 4>), grid, block, 0, rp, col, w, n, x, dim, empty_fill,   \
-                       post_scale, out, self_x, row_scale, planes, pstride);                                     \
+                       post_scale, out, self_x, row_scale, planes, pstride, row_mul, self_mul);                                     \
     } while (0)
     if (vec && dim <= 256) RVX_AGG_VEC(1);
     else if (vec && dim <= 512) RVX_AGG_VEC(2);
@@ -258,7 +273,8 @@ int g_agg_nt = env_int("RVX_AGG_NT", 1);
 
 void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, int64_t n, const float* x, int dim,
                     int agg, int empty_fill, int post_scale, float* out, const char* tag, bool overlapped,
-                    const float* self_x, float* row_scale, _Float16* planes, int64_t plane_stride) {
+                    const float* self_x, float* row_scale, _Float16* planes, int64_t plane_stride,
+                    const float* row_mul, const float* self_mul) {
     if (n <= 0) return;
     static const int standalone_deep = env_int("RVX_AGG_STANDALONE_DEEP", 0);  // experiment knob
     const int cap = overlapped ? g_agg_overlap_cap : 0;
@@ -268,12 +284,12 @@ void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, 
     const char* t = tag ? tag : "aggregate";
     const bool W = w != nullptr;
     switch (agg) {
-        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride)
-                        : launch_agg<AGG_SUM, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride); break;
-        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride)
-                         : launch_agg<AGG_MEAN, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride); break;
-        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride)
-                        : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride); break;
+        case AGG_SUM: W ? launch_agg<AGG_SUM, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride, row_mul, self_mul)
+                        : launch_agg<AGG_SUM, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride, row_mul, self_mul); break;
+        case AGG_MEAN: W ? launch_agg<AGG_MEAN, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride, row_mul, self_mul)
+                         : launch_agg<AGG_MEAN, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride, row_mul, self_mul); break;
+        case AGG_MAX: W ? launch_agg<AGG_MAX, true>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride, row_mul, self_mul)
+                        : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride, row_mul, self_mul); break;
         default: fail(RVX_ERR_INVALID_PARAMETER, "unknown aggregator");
     }
 }

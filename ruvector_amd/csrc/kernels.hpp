@@ -33,6 +33,12 @@ struct GemmEpilogue {
     // gemm_nt_h2 only: then x /= |x| over each row of C (rows with norm 0 or NaN left as they
     // are), bit-identical to normalize_rows(C, M, N, only_positive = true); see gemm_h2_rownorm_ok
     bool normalize_rows = false;
+    // gemm_nt_h2 (128 x 128 tile) only, for a normalisation deferred to the next layer:
+    // row_sumsq[row * ceil(N / 128) + t] receives sum of v^2 over output column tile t of the
+    // row (v after the activation; fixed order), and a1_rowmul[row] multiplies the phase-1
+    // (A1) operand row before the split (the previous layer's 1 / |y|)
+    float* row_sumsq = nullptr;
+    const float* a1_rowmul = nullptr;
 };
 // C[M][N] = epilogue(A0·B0^T [+ A1·B1^T])
 void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, const GemmEpilogue& ep, float* C,
@@ -102,6 +108,9 @@ void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, 
                     const float* self_x = nullptr, float* row_scale = nullptr,
                     // with row_scale: write [aggregate | self] * row_scale as f16 planes
                     // [2][n][2*dim] (plane stride plane_stride) instead of out
-                    _Float16* planes = nullptr, int64_t plane_stride = 0);
+                    _Float16* planes = nullptr, int64_t plane_stride = 0,
+                    // deferred normalisation of x: gathered row c is x[c] * row_mul[c], the
+                    // self row i (for row_scale) self_x[i] * self_mul[i]
+                    const float* row_mul = nullptr, const float* self_mul = nullptr);
 
 }  // namespace rvx

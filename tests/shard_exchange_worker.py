@@ -79,6 +79,24 @@ def main():
         res["sage_layer2_owned_equal"] = bool(np.array_equal(a2[o0:o1], b2[o0:o1]))
         ref = O.sage_forward(x, rp, col, O.sage_init(d, d, 0), O.sage_init(d, d, 1000), rows=(o0, min(o1 - o0, 500)))
         res["sage_layer1_vs_oracle"] = float(np.max(np.abs(a1[o0:o0 + len(ref)] - ref)) / np.max(np.abs(ref)))
+        # the same two layers with the normalisation deferred across the exchange
+        # (rvx_sage_forward_exchange2: unnormalised rows + 1/|y| exchanged together)
+        iv = rv.Buffer(N * 4)
+        y1d, y2d = rv.Buffer(N * d * 4), rv.Buffer(N * d * 4)
+        y1d.upload(np.full((N, d), np.nan, np.float32))
+        call("rvx_sage_forward_exchange2", layer._h, g_loc.handle, xb.handle, None, y1d.handle, iv.handle, off_p,
+             comm._h, 1)
+        call("rvx_sage_forward_exchange2", layer._h, g_loc.handle, y1d.handle, iv.handle, y2d.handle, None, off_p,
+             comm._h, 0)
+        inv = iv.download(np.float32, (N,))
+        a1d = y1d.download(np.float32, (N, d)).astype(np.float64) * inv[:, None]
+        a2d = y2d.download(np.float32, (N, d))
+        def row_rel(u, v):
+            v = np.asarray(v, np.float64)
+            nb = np.linalg.norm(v, axis=1)
+            return float(np.max(np.linalg.norm(np.asarray(u, np.float64) - v, axis=1) / np.where(nb > 0, nb, 1.0)))
+        res["sage_deferred_layer1_row_rel"] = row_rel(a1d, b1)
+        res["sage_deferred_layer2_row_rel"] = row_rel(a2d[o0:o1], b2[o0:o1])
 
         # ---- RuvectorLayer (M|K|V exchange) and the attention head (T exchange)
         n2 = int(offsets[-1])

@@ -981,3 +981,74 @@ def test_ruvector_layer_wide_gemm_bits(monkeypatch, hidden, heads, wide):
     y1 = layer.forward_graph(x, g)
     assert np.array_equal(y0, y1)
     assert_close(y1, O.rvl_forward_graph(W, x, rp, col, ew))
+
+
+def test_graphsage_norm_stream_bits(monkeypatch):
+    """The opt-in third-stream row normalisation of the chunked pipeline
+    (RVX_SAGE_NORM_STREAM=1) writes the same bits as the in-line pass."""
+    n, in_f, out_f, deg = 60000, 64, 128, 5
+    x = O.fill_uniform(n * in_f, 95).reshape(n, in_f)
+    rp, col = O.random_csr(n, deg, 96)
+    g = rv.Graph.from_csr(rp, col)
+    layer = rv.GraphSAGELayer(in_f, out_f, num_samples=deg)
+    monkeypatch.setenv("RVX_SAGE_CHUNKS", "3")
+    monkeypatch.setenv("RVX_SAGE_NORM_STREAM", "0")
+    y0 = layer.forward_graph(x, g)
+    monkeypatch.setenv("RVX_SAGE_NORM_STREAM", "1")
+    y1 = layer.forward_graph(x, g)
+    assert np.array_equal(y0, y1)
+    nrm = np.linalg.norm(y1.astype(np.float64), axis=1)
+    assert np.all(np.abs(nrm[nrm > 0] - 1.0) < 1e-5)
+
+
+def _sage_stack(layers, g, x, n, defer):
+    """Two-layer GraphSAGE stack through rvx_sage_forward_exchange2 (single GPU):
+    defer=True carries layer 1's normalisation into layer 2."""
+    import ctypes
+    from ruvector_amd import _lib as L
+    off = np.array([0, n], np.int64)
+    off_p = off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+    xb = rv.Buffer.from_numpy(x)
+    d1, d2 = layers[0].out_features, layers[1].out_features
+    t1, t2, iv = rv.Buffer(n * d1 * 4), rv.Buffer(n * d2 * 4), rv.Buffer(n * 4)
+    L.call("rvx_sage_forward_exchange2", layers[0]._h, g.handle, xb.handle, None, t1.handle,
+           iv.handle if defer else None, off_p, None, 0)
+    # layer 1's table as layer 1 left it (a layer 2 that cannot take the multipliers, e.g.
+    # in = 200 off the split-f16 path, rescales it in place)
+    y1 = t1.download(np.float32, (n, d1))
+    inv = iv.download(np.float32, (n,)) if defer else np.ones(n, np.float32)
+    L.call("rvx_sage_forward_exchange2", layers[1]._h, g.handle, t1.handle, iv.handle if defer else None,
+           t2.handle, None, off_p, None, 0)
+    return y1, inv, t2.download(np.float32, (n, d2))
+
+
+@pytest.mark.parametrize("gemm", ["h2", "x3"])
+@pytest.mark.parametrize("dims,n,deg,chunks", [((64, 96, 64), 1000, 7, 0), ((96, 200, 128), 700, 5, 0),
+                                               ((768, 768, 768), 600, 9, 0), ((64, 256, 128), 40000, 4, 2)])
+def test_graphsage_deferred_normalisation_stack(monkeypatch, gemm, dims, n, deg, chunks):
+    """rvx_sage_forward_exchange2: layer 1 leaves its rows unnormalised and hands 1/|y| to
+    layer 2, which applies it as rows are gathered and in the self operand's split. The
+    stack's output is the per-layer stack's within the 1e-5 per-row bar (and the carried
+    layer-1 rows within 1e-6); with the split-bf16 GEMM (no deferral there) the input is
+    rescaled in place and 1/|y| is 1. Ragged column tiles (96, 200), chunks, d = 768."""
+    if gemm == "x3":
+        monkeypatch.setenv("RVX_GEMM_H2", "0")
+    if chunks:
+        monkeypatch.setenv("RVX_SAGE_CHUNKS", str(chunks))
+    d0, d1, d2 = dims
+    x = O.fill_uniform(n * d0, 60 + n).reshape(n, d0)
+    rp, col = O.random_csr(n, deg, 61)
+    g = rv.Graph.from_csr(rp, col)
+    layers = [rv.GraphSAGELayer(d0, d1, num_samples=deg), rv.GraphSAGELayer(d1, d2, num_samples=deg)]
+    y1r, _, y2r = _sage_stack(layers, g, x, n, False)
+    y1d, inv, y2d = _sage_stack(layers, g, x, n, True)
+    if gemm == "x3":
+        assert np.all(inv == 1.0) and np.array_equal(y1d, y1r) and np.array_equal(y2d, y2r)
+        return
+    assert row_rel_err(y1d.astype(np.float64) * inv[:, None], y1r) <= 1e-6
+    assert row_rel_err(y2d, y2r) <= 1e-5
+    if n <= 1000 and d1 != 200:
+        r1 = O.sage_forward(x, rp, col, O.sage_init(d0, d1, 0), O.sage_init(d0, d1, 1000), 0)
+        ref = O.sage_forward(y1r, rp, col, O.sage_init(d1, d2, 0), O.sage_init(d1, d2, 1000), 0)
+        assert_close(y1r, r1)
+        assert_close(y2d, ref)

@@ -56,6 +56,8 @@ def test_exchange_entry_points_multi_rank(offsets, tmp_path):
         assert r["sage_layer1_all_rows_equal"] and r["sage_layer1_halo_rows"] > 0, r
         assert r["sage_layer2_owned_equal"], r
         assert r["sage_layer1_vs_oracle"] <= 1e-5, r
+        assert r["sage_deferred_layer1_row_rel"] <= 1e-6, r  # |y| carried, not applied: same rows
+        assert r["sage_deferred_layer2_row_rel"] <= 1e-5, r
         assert r["gnn_owned_equal"], r
         assert r["gnn_fold_owned_equal"] and r["gnn_fold_vs_oracle"] <= 1e-5, r
         assert r["efa_owned_equal"], r
