@@ -212,7 +212,8 @@ bool sage_defer_path(const rvx_sage_layer* l, int64_t n, const float* x, const f
     const int64_t a_plane = std::max<int64_t>(n, 1) * 2 * l->in;
     const bool h2p = l->wn_h2.p && l->in <= 1024 && l->in % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
                      gemm_h2p_ok(std::max<int64_t>(n, 1), l->out, 2 * l->in, a_plane, w0, &w0);
-    if (h2p || !l->wn_h2.p || l->in > 1024 || ((uintptr_t)x & 15) != 0 || l->in % 4 != 0) return false;
+    if (h2p || !l->wn_h2.p || l->in > 1024 || l->out > 1024 || ((uintptr_t)x & 15) != 0 || l->in % 4 != 0)
+        return false;
     // the aggregate scratch is hipMalloc'd (aligned): x stands in for its alignment check
     if (!gemm_h2_ok(std::max<int64_t>(n, 1), l->out, GemmOperand{x, l->in, nullptr, l->in, l->in}, nullptr)) return false;
     const int64_t wplane = (int64_t)l->in * l->out;
@@ -220,11 +221,12 @@ bool sage_defer_path(const rvx_sage_layer* l, int64_t n, const float* x, const f
                                wplane, l->out, x, x + row_offset * l->in, y);
 }
 
-__global__ void k_rows_inv_norm(const float* __restrict__ ssq, int tiles, int64_t rows, float* __restrict__ inv) {
+__global__ void k_rows_inv_norm(const float* __restrict__ ssq, int stride, int tiles, int64_t rows,
+                                float* __restrict__ inv) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= rows) return;
     float s = 0.0f;
-    for (int t = 0; t < tiles; ++t) s = __fadd_rn(s, ssq[r * tiles + t]);
+    for (int t = 0; t < tiles; ++t) s = __fadd_rn(s, ssq[r * stride + t]);
     const float norm = sqrtf(s);
     inv[r] = norm > 0.0f ? 1.0f / norm : 1.0f;  // rows with norm 0 / NaN stay as they are (normalize_rows)
 }
@@ -285,7 +287,7 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
     ep.epi = GEMM_EPI_RELU;
     RVX_REQUIRE((!x_mul && !y_inv) || (h2 && !h2p && !fused), RVX_ERR_UNSUPPORTED,
                 "deferred normalisation needs the split-f16 GEMM path");
-    const int ntiles = (l->out + 127) / 128;
+    const int ntiles = ROWSUMSQ_SLOTS;
     float* ssq = y_inv ? scratch_f32("sage_sumsq", std::max<int64_t>(n, 1) * ntiles) : nullptr;
     // Rows are independent, so the layer runs as a two-stage pipeline over
     // row chunks: the HBM-bound gather of chunk c+1 (aux stream) overlaps the
@@ -384,16 +386,17 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         epn.normalize_rows = h2 && l->normalize && !y_inv && gemm_h2_rownorm_ok(l->out, y, l->out);
         epn.a1_rowmul = x_mul ? x_mul + row_offset + r0 : nullptr;
         epn.row_sumsq = y_inv ? ssq + r0 * ntiles : nullptr;
+        int coltiles = 0;
         if (h2)
-            gemm_nt_h2(rows, l->out, s0, l->wn_h2.as<_Float16>(), &s1, l->ws_h2.as<_Float16>(), scale + r0,
-                       l->w_inv.as<float>(), epn, y + r0 * l->out, l->out, "sage_gemm",
-                       chunks > 1 ? env_int("RVX_SAGE_GEMM_CAP", 2) : -1);
+            coltiles = gemm_nt_h2(rows, l->out, s0, l->wn_h2.as<_Float16>(), &s1, l->ws_h2.as<_Float16>(), scale + r0,
+                                  l->w_inv.as<float>(), epn, y + r0 * l->out, l->out, "sage_gemm",
+                                  chunks > 1 ? env_int("RVX_SAGE_GEMM_CAP", 2) : -1);
         else
             gemm_nt(rows, l->out, s0, &s1, ep, y + r0 * l->out, l->out, "sage_gemm");
         if (y_inv && rows > 0) {
             if (l->normalize) {
                 RVX_LAUNCH("sage_inv_norm", k_rows_inv_norm, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
-                           ssq + r0 * ntiles, ntiles, rows, y_inv + r0);
+                           ssq + r0 * ntiles, ntiles, coltiles, rows, y_inv + r0);
             } else {
                 fill_value(y_inv + r0, rows, 1.0f);
             }

@@ -1031,7 +1031,7 @@ __device__ __forceinline__ void h2g_tile(const GemmArgs& g, int epi, int64_t wgi
             // ni * 32 + lr; a fixed xor tree over the 32 lanes of the half
 #pragma unroll
             for (int off = 16; off > 0; off >>= 1) ssq += __shfl_xor(ssq, off);
-            if (lr == 0 && row < g.M) g.row_sumsq[row * g.tiles_n + tn] = ssq;
+            if (lr == 0 && row < g.M) g.row_sumsq[row * ROWSUMSQ_SLOTS + tn] = ssq;
         }
     }
     if (g.row_tickets) h2g_rownorm(g, tm, m0, xsm);
@@ -1269,14 +1269,15 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
 // pieces of the next K-tile issued between them, so the next stage's loads have a whole
 // K-tile of MFMA work to land (cdna_hip_programming.md §5.5 T3/T4, without per-phase
 // barriers). A and B stages keep h2g's layouts and source-side XOR swizzles.
-template <bool DUAL, int WN>
+template <bool DUAL, int WN, int BN>
 __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgid) {
-    constexpr int BM = 256, BN = 256;
+    constexpr int BM = 256;
     constexpr int WMW = 8 / WN;                 // waves along M
-    constexpr int RB = BM / WMW / 32, NB = BN / WN / 32;  // 32-row / 32-column blocks per wave (RB * NB = 8)
+    constexpr int RB = BM / WMW / 32, NB = BN / WN / 32;  // 32-row / 32-column blocks per wave
+    constexpr int NBP = BN / 64;       // B DMA pieces per wave (2 planes x BN / 16 pieces over 8 waves)
     constexpr int XA = BM * 128;       // f32 A tile bytes per stage (256 rows x 32 k)
-    constexpr int BPL = BN * 64;       // one f16 B plane tile (256 columns x 32 k)
-    constexpr int STG = XA + 2 * BPL;  // 64 KB
+    constexpr int BPL = BN * 64;       // one f16 B plane tile (BN columns x 32 k)
+    constexpr int STG = XA + 2 * BPL;  // 64 KB (BN 256) / 56 KB (BN 192)
     extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
 
     const int64_t tm = wgid / g.tiles_n;
@@ -1299,7 +1300,7 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
     // B pieces 4 wave + j of 32 (plane piece / 16, 16 rows x 64 B each)
     // the host routes here only operands whose phase-1 strides equal phase 0's
     // (lda, ldb, B plane stride), so one set of lane offsets serves both phases
-    uint32_t a_off[4], b_off[4];
+    uint32_t a_off[4], b_off[NBP];
     const char* a_base[2];
     const char* b_base[2];
     a_base[0] = reinterpret_cast<const char*>(g.A0 + m0 * g.lda0);
@@ -1312,13 +1313,16 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
         const int chunk = (lane & 7) ^ sw_a(row);
         const int64_t rr = std::min<int64_t>(m0 + row, g.M - 1) - m0;
         a_off[j] = (uint32_t)((rr * g.lda0 + 4 * chunk) * 4);
-        const int piece = 4 * wave + j;
-        const int brow = 16 * (piece & 15) + (lane >> 2);
+    }
+#pragma unroll
+    for (int j = 0; j < NBP; ++j) {
+        const int piece = NBP * wave + j;
+        const int brow = 16 * (piece % (BN / 16)) + (lane >> 2);
         const int bchunk = (lane & 3) ^ sw_b(brow);
         const int64_t rb = std::min<int64_t>(n0 + brow, (int64_t)g.N - 1) - n0;
-        b_off[j] = (uint32_t)(((piece >> 4) * g.B0h_plane + rb * g.ldb0 + 8 * bchunk) * 2);
+        b_off[j] = (uint32_t)(((piece / (BN / 16)) * g.B0h_plane + rb * g.ldb0 + 8 * bchunk) * 2);
     }
-    // piece j (0..7) of K-tile t's fill into stage `base`
+    // piece j (0 .. 3 + NBP) of K-tile t's fill into stage `base`
     auto issue = [&](int t, unsigned char* base, int j) {
         const bool p1 = DUAL && t >= nk0;
         const int k0 = (t - (p1 ? nk0 : 0)) * 32;
@@ -1328,12 +1332,13 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
                                              (__attribute__((address_space(3))) void*)(base + (4 * wave + j) * 1024),
                                              16, 0, 0);
         } else {
-            const int jj = j - 4, piece = 4 * wave + jj;
+            const int jj = j - 4, piece = NBP * wave + jj;
             const char* src = (p1 ? b_base[1] : b_base[0]) + (int64_t)k0 * 2 + b_off[jj];
             __builtin_amdgcn_global_load_lds(
                 (const void*)src,
-                (__attribute__((address_space(3))) void*)(base + XA + (piece >> 4) * BPL + (piece & 15) * 1024), 16,
-                0, 0);
+                (__attribute__((address_space(3))) void*)(base + XA + (piece / (BN / 16)) * BPL +
+                                                           (piece % (BN / 16)) * 1024),
+                16, 0, 0);
         }
     };
 
@@ -1348,9 +1353,13 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
         a_rd[s][1] = arow * 128 + (((4 * s + 2 * lh + 1) ^ sw_a(arow)) << 4);
         b_rd[s] = XA + bcol * 64 + (((2 * s + lh) ^ sw_b(bcol)) << 4);
     }
-    float asc[RB];
+    float asc[RB], asc1[RB];  // phase 1: s * m with the deferred normalisation's row multiplier (as h2g)
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) asc[rb] = g.a_scale[std::min<int64_t>(m0 + arow + 32 * rb, g.M - 1)];
+    for (int rb = 0; rb < RB; ++rb) {
+        const int64_t r = std::min<int64_t>(m0 + arow + 32 * rb, g.M - 1);
+        asc[rb] = g.a_scale[r];
+        asc1[rb] = g.a1_rowmul ? asc[rb] * g.a1_rowmul[r] : asc[rb];
+    }
 
     f32x16 acc[RB][NB];
 #pragma unroll
@@ -1361,17 +1370,18 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
 #pragma unroll
-    for (int j = 0; j < 8; ++j) issue(0, xsm, j);
+    for (int j = 0; j < 4 + NBP; ++j) issue(0, xsm, j);
     // one K-tile; restrict parameters give the stage pointers distinct alias scopes, so
     // the ds_reads of `cur` do not wait for the LDS-DMA into `nxt` (vmcnt) in the phases
     auto ktile = [&](const unsigned char* __restrict__ cur, unsigned char* __restrict__ nxt, int t) {
         const bool more = t + 1 < nkt;
+        const bool p1 = DUAL && t >= nk0;  // this K-tile reads the A1 / B1 operands
 #ifndef RVX_H2W_SPREAD
         // all 16 KB of this wave's share of the next K-tile first: the loads get the whole
         // K-tile of MFMA work to land before the next tile's wait
         if (more) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) issue(t + 1, nxt, j);
+            for (int j = 0; j < 4 + NBP; ++j) issue(t + 1, nxt, j);
         }
 #endif
         // B fragments [nb][s][plane]: held for the K-tile when the wave has 2 column blocks,
@@ -1402,7 +1412,8 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
                 unsigned w[2][4];  // [hi, lo][pair]
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    split_h2_pair(f4_at(alo, ahi, 2 * j), f4_at(alo, ahi, 2 * j + 1), asc[rb], w[0][j], w[1][j]);
+                    split_h2_pair(f4_at(alo, ahi, 2 * j), f4_at(alo, ahi, 2 * j + 1), p1 ? asc1[rb] : asc[rb],
+                                  w[0][j], w[1][j]);
                 f16x8 af[2];
 #pragma unroll
                 for (int p = 0; p < 2; ++p) af[p] = __builtin_bit_cast(f16x8, u32x4{w[p][0], w[p][1], w[p][2], w[p][3]});
@@ -1433,32 +1444,43 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
     }
 
     // epilogue as h2g: undo the row and column scales (powers of two: exact), then
-    // alpha / bias / addend / activation
+    // alpha / bias / addend / activation; row-outer, and with WN = 1 (a wave holds whole
+    // tile rows) the deferred normalisation's per-row sum of squares of this tile
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
-        float rinv[16];
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int64_t row = m0 + wm * (32 * RB) + rb * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-            rinv[e] = 1.0f / g.a_scale[std::min<int64_t>(row, g.M - 1)];  // unconditional loads: no per-load wait
-        }
+        float cinv[NB], cb[NB];
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) {
-            const int col = n0 + wn * (32 * NB) + nb * 32 + lr;
-            if (col >= g.N) continue;
-            const float cinv = g.b_inv[col];
+            const int col = std::min(n0 + wn * (32 * NB) + nb * 32 + lr, g.N - 1);
+            cinv[nb] = g.b_inv[col];
             float b = 0.0f;
             if (g.bias0) b = g.bias0[col];
             if (g.bias1) b += g.bias1[col];
+            cb[nb] = b;
+        }
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int64_t row = m0 + wm * (32 * RB) + rb * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-                if (row < g.M) {
-                    float v = (acc[rb][nb][e] * rinv[e]) * cinv;
+        for (int e = 0; e < 16; ++e) {
+            const int64_t row = m0 + wm * (32 * RB) + rb * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+            const float rinv = 1.0f / g.a_scale[std::min<int64_t>(row, g.M - 1)];  // unconditional: no per-load wait
+            float ssq = 0.0f;
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) {
+                const int col = n0 + wn * (32 * NB) + nb * 32 + lr;
+                if (col < g.N && row < g.M) {
+                    float v = (acc[rb][nb][e] * rinv) * cinv[nb];
                     if (g.alpha != 1.0f) v *= g.alpha;
-                    if (g.bias0 || g.bias1) v += b;
+                    if (g.bias0 || g.bias1) v += cb[nb];
                     if (g.addend) v += g.addend[row * g.ld_add + col];
-                    g.C[row * g.ldc + col] = epi_apply(epi, v);
+                    v = epi_apply(epi, v);
+                    g.C[row * g.ldc + col] = v;
+                    ssq = __fadd_rn(ssq, __fmul_rn(v, v));
+                }
+            }
+            if constexpr (WN == 1) {
+                if (g.row_sumsq) {
+#pragma unroll
+                    for (int off = 16; off > 0; off >>= 1) ssq += __shfl_xor(ssq, off);
+                    if (lr == 0 && row < g.M) g.row_sumsq[row * ROWSUMSQ_SLOTS + tn] = ssq;
                 }
             }
         }
@@ -1468,7 +1490,7 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
 // One tile per block (XCD-mapped tile order), or a persistent grid of one block per CU
 // taking tiles from per-XCD counters in row-tile-major order (g.queue, as gemm_nt_h2g):
 // beside the overlapped gather a persistent block keeps its LDS and registers.
-template <bool DUAL, int WN>
+template <bool DUAL, int WN, int BN>
 __global__ __launch_bounds__(512, 1) void gemm_nt_h2w(GemmArgs g, int epi) {
     if (g.queue) {
         __shared__ int64_t s_t;
@@ -1479,13 +1501,13 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_h2w(GemmArgs g, int epi) {
             __syncthreads();
             const int64_t t = s_t;
             if (t >= cnt) break;
-            h2w_tile<DUAL, WN>(g, epi, first + t);
+            h2w_tile<DUAL, WN, BN>(g, epi, first + t);
             __syncthreads();  // LDS stages and s_t are reused by the next tile
         }
         return;
     }
     const int64_t nwg = g.nblocks, bid = blockIdx.x;
-    h2w_tile<DUAL, WN>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
+    h2w_tile<DUAL, WN, BN>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
 }
 
 // B rows n of one or two [N][K] matrices: common scale t_n, f16 planes of each
@@ -1646,10 +1668,10 @@ bool gemm_h2_rownorm_ok(int N, const float* C, int64_t ldc) {
     return env_int("RVX_GEMM_ROWNORM", 0) && N % 4 == 0 && N <= 1024 && ldc % 4 == 0 && aligned16(C);
 }
 
-void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
-                const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
-                int64_t ldc, const char* tag, int persist) {
-    if (M <= 0 || N <= 0) return;
+int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
+               const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
+               int64_t ldc, const char* tag, int persist) {
+    if (M <= 0 || N <= 0) return 0;
     GemmArgs g{};
     g.addend = ep.addend;
     g.ld_add = ep.ld_addend;
@@ -1675,29 +1697,37 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
         attr = true;
     }
     const char* t = tag ? tag : "gemm_nt_h2";
-    // 256 x 256 tiles (gemm_nt_h2w, bit-identical). Default for standalone launches (8 waves
-    // along M: 80.3 vs 87.2 ms for the 10M x 768 SAGE GEMM alone, scripts/exp_gemm_wide.sh); the
-    // overlapped GraphSAGE GEMM (persist > 0) keeps h2g, whose 2 x 4-wave blocks leave a gather
-    // wave room on every SIMD (h2w's 211-VGPR waves do not: 487 vs 454 ms/step).
-    // RVX_GEMM_WIDE (read per call; tests cover all): 0 off, 1 waves 2 x 4, 2 waves 8 x 1.
-    const int wide_mode = env_int("RVX_GEMM_WIDE", persist > 0 ? 0 : 2);
+    // Wide tiles (gemm_nt_h2w, bit-identical to h2g). Standalone launches: 256 x 256, 8 waves
+    // along M (78.7-80.3 vs 87.2 ms for the 10M x 768 SAGE GEMM alone). The persistent GEMM
+    // beside the gather (persist > 0): 256 x 192 (161 VGPRs, so two GEMM waves and a 152-VGPR
+    // gather wave share each SIMD; the 256-wide tile's 193+ VGPRs do not fit and lost, 487 vs
+    // 454 ms/step): 403-451 vs 455-470 ms/step for h2g (scripts/exp_wide3_pipe.sh).
+    // RVX_GEMM_WIDE (read per call; tests cover all): 0 h2g, 1 waves 2 x 4, 2 waves 8 x 1,
+    // 3 waves 8 x 1 on 256 x 192 tiles (32 x 192 per wave: 96 accumulator registers).
+    const int wide_mode = env_int("RVX_GEMM_WIDE", persist > 0 ? 3 : 2);
     const bool same_strides = !s1 || (g.lda1 == g.lda0 && g.ldb1 == g.ldb0 && g.B1h_plane == g.B0h_plane);
-    const bool wide = !ep.normalize_rows && !ep.row_sumsq && !ep.a1_rowmul && wide_mode && same_strides && (int64_t)256 * g.lda0 * 4 < ((int64_t)1 << 31) &&
+    const bool wide = !ep.normalize_rows && (wide_mode >= 2 || (!ep.row_sumsq && !ep.a1_rowmul)) && wide_mode &&
+                      same_strides && (int64_t)256 * g.lda0 * 4 < ((int64_t)1 << 31) &&
                       (!s1 || (int64_t)256 * g.lda1 * 4 < ((int64_t)1 << 31)) &&
                       (g.B0h_plane + (int64_t)256 * g.ldb0) * 2 < ((int64_t)1 << 31) &&
                       (!s1 || (g.B1h_plane + (int64_t)256 * g.ldb1) * 2 < ((int64_t)1 << 31));
     if (wide) {
-        constexpr int wlds = 2 * (256 * 128 + 2 * 256 * 64);
+        const int wbn = wide_mode == 3 ? 192 : 256;
+        const int wlds = 2 * (256 * 128 + 2 * wbn * 64);
         static bool wattr = false;
         if (!wattr) {
-            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, wlds));
-            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, wlds));
-            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, wlds));
-            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, wlds));
+            constexpr int l256 = 2 * (256 * 128 + 2 * 256 * 64), l192 = 2 * (256 * 128 + 2 * 192 * 64);
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 4, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 4, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
             wattr = true;
         }
-        g.tiles_n = (N + 255) / 256;
+        g.tiles_n = (N + wbn - 1) / wbn;
         g.nblocks = ((M + 255) / 256) * g.tiles_n;
+        RVX_REQUIRE(!ep.row_sumsq || g.tiles_n <= ROWSUMSQ_SLOTS, RVX_ERR_INVALID_SHAPE, "row sums: N too large");
         RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
         // persistent (one block per CU, per-XCD tile queue) when asked for, as h2g
         const int wcap = persist >= 0 ? persist : env_int("RVX_GEMM_CAP", 0);
@@ -1712,14 +1742,17 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
         const dim3 wg((unsigned)wgrid), wb(512);
         // RVX_GEMM_WIDE=1: waves 2 (M) x 4 (N), 128 x 64 each; 2: waves 8 x 1, 32 x 256 each
         // (A converted once per row instead of by four waves)
-        if (wide_mode == 2) {
-            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1>), wg, wb, wlds, g, ep.epi);
-            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1>), wg, wb, wlds, g, ep.epi);
+        if (wide_mode == 3) {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192>), wg, wb, wlds, g, ep.epi);
+        } else if (wide_mode == 2) {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 256>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 256>), wg, wb, wlds, g, ep.epi);
         } else {
-            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 4>), wg, wb, wlds, g, ep.epi);
-            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 4>), wg, wb, wlds, g, ep.epi);
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 4, 256>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 4, 256>), wg, wb, wlds, g, ep.epi);
         }
-        return;
+        return g.tiles_n;
     }
     // persistent grid of `cap` blocks per CU (a multiple of 8 blocks, so a block
     // keeps its XCD across the tiles it strides over). The overlapped GraphSAGE
@@ -1745,6 +1778,7 @@ void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, co
     }
     if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
     else RVX_LAUNCH(t, gemm_nt_h2g<false>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
+    return g.tiles_n;
 }
 
 bool gemm_h2p_ok(int64_t M, int N, int64_t lda, int64_t a_plane, const GemmOperand& s0, const GemmOperand* s1) {

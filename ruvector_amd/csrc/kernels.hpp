@@ -23,6 +23,7 @@ struct GemmOperand {
     const float* b_inv = nullptr;
 };
 // Epilogue: C = epi(alpha * acc + bias0 + bias1 + addend[row][col])
+constexpr int ROWSUMSQ_SLOTS = 8;  // per-row partial sums of squares (column tiles >= 128 wide, N <= 1024)
 struct GemmEpilogue {
     int epi = GEMM_EPI_STORE;
     float alpha = 1.0f;
@@ -33,10 +34,11 @@ struct GemmEpilogue {
     // gemm_nt_h2 only: then x /= |x| over each row of C (rows with norm 0 or NaN left as they
     // are), bit-identical to normalize_rows(C, M, N, only_positive = true); see gemm_h2_rownorm_ok
     bool normalize_rows = false;
-    // gemm_nt_h2 (128 x 128 tile) only, for a normalisation deferred to the next layer:
-    // row_sumsq[row * ceil(N / 128) + t] receives sum of v^2 over output column tile t of the
-    // row (v after the activation; fixed order), and a1_rowmul[row] multiplies the phase-1
-    // (A1) operand row before the split (the previous layer's 1 / |y|)
+    // gemm_nt_h2 only, for a normalisation deferred to the next layer (N <= 1024):
+    // row_sumsq[row * ROWSUMSQ_SLOTS + t] receives sum of v^2 over output column tile t of
+    // the row (v after the activation; fixed order; t < the tile count gemm_nt_h2 returns), and
+    // a1_rowmul[row] multiplies the phase-1 (A1) operand row before the split (the previous
+    // layer's 1 / |y|)
     float* row_sumsq = nullptr;
     const float* a1_rowmul = nullptr;
 };
@@ -54,9 +56,10 @@ bool gemm_h2_ok(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1);
 // persist: blocks per CU of a persistent grid (0 = one block per tile; -1 = RVX_GEMM_CAP, default 0)
 // ep.normalize_rows is honoured when this holds (N % 4 == 0, N <= 1024, aligned C rows, opt-in RVX_GEMM_ROWNORM=1)
 bool gemm_h2_rownorm_ok(int N, const float* C, int64_t ldc);
-void gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
-                const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
-                int64_t ldc, const char* tag, int persist = -1);
+// returns the number of output column tiles (the row_sumsq slots it wrote per row)
+int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, const GemmOperand* s1,
+               const _Float16* B1h, const float* a_scale, const float* b_inv, const GemmEpilogue& ep, float* C,
+               int64_t ldc, const char* tag, int persist = -1);
 // Pre-split A (gemm_nt_h2p): Ah holds A*a_scale as f16 planes [2][M][lda]
 // (plane stride a_plane), phase 0 in columns [0, s0.K), phase 1 (s1) in
 // [s0.K, s0.K + s1->K); s0/s1 give K and the B planes as for gemm_nt_h2.

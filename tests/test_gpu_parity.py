@@ -940,7 +940,7 @@ def test_graphsage_in_gemm_row_normalisation_bits(monkeypatch, in_f, out_f, n, d
         assert_close(y1, O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0))
 
 
-@pytest.mark.parametrize("wide", ["1", "2"])
+@pytest.mark.parametrize("wide", ["1", "2", "3"])
 @pytest.mark.parametrize("in_f,out_f,n,deg,chunks", [(768, 768, 600, 9, 0), (96, 232, 1000, 5, 0),
                                                      (64, 130, 257, 0, 0), (32, 32, 129, 3, 0),
                                                      (128, 512, 40000, 4, 2)])
@@ -963,7 +963,7 @@ def test_graphsage_wide_gemm_bits(monkeypatch, in_f, out_f, n, deg, chunks, wide
         assert_close(y1, O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0))
 
 
-@pytest.mark.parametrize("wide", ["1", "2"])
+@pytest.mark.parametrize("wide", ["1", "2", "3"])
 @pytest.mark.parametrize("hidden,heads", [(64, 4), (768, 8), (96, 4)])
 def test_ruvector_layer_wide_gemm_bits(monkeypatch, hidden, heads, wide):
     """RuvectorLayer's GEMMs (single and dual, bias / addend / sigmoid / tanh
@@ -1022,7 +1022,7 @@ def _sage_stack(layers, g, x, n, defer):
     return y1, inv, t2.download(np.float32, (n, d2))
 
 
-@pytest.mark.parametrize("gemm", ["h2", "x3"])
+@pytest.mark.parametrize("gemm", ["h2", "x3", "wide3"])
 @pytest.mark.parametrize("dims,n,deg,chunks", [((64, 96, 64), 1000, 7, 0), ((96, 200, 128), 700, 5, 0),
                                                ((768, 768, 768), 600, 9, 0), ((64, 256, 128), 40000, 4, 2)])
 def test_graphsage_deferred_normalisation_stack(monkeypatch, gemm, dims, n, deg, chunks):
@@ -1033,6 +1033,8 @@ def test_graphsage_deferred_normalisation_stack(monkeypatch, gemm, dims, n, deg,
     rescaled in place and 1/|y| is 1. Ragged column tiles (96, 200), chunks, d = 768."""
     if gemm == "x3":
         monkeypatch.setenv("RVX_GEMM_H2", "0")
+    if gemm == "wide3":  # the 256 x 192 tile in every GEMM of the stack, pipelined or not
+        monkeypatch.setenv("RVX_GEMM_WIDE", "3")
     if chunks:
         monkeypatch.setenv("RVX_SAGE_CHUNKS", str(chunks))
     d0, d1, d2 = dims
