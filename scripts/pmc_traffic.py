@@ -20,6 +20,7 @@ TAGS = {  # kernel symbol substring -> bench tag
     # one entry per GEMM kernel: the layer's split-f16 GEMM (h2g) alone under sage_gemm; the
     # alternatives bench.py times (gemm_paths) under their own names
     "gemm_nt_h2g": "sage_gemm",
+    "gemm_nt_h2w": "sage_gemm",
     "gemm_nt_x3": "sage_gemm_alt_split_bf16x6",
     "gemm_nt_mfma": "sage_gemm_alt_fp32_mfma",
     "k_normalize_rows": "sage_normalize",
