@@ -200,6 +200,120 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
     }
 }
 
+// Overlapped GraphSAGE gather (beside the GEMM, one block per CU) for rows of exactly
+// 256 NV floats: k_aggregate_vec's groups of U neighbour rows, with the latencies between
+// destination rows taken off the chain — the next row's CSR bounds and first 64 column ids
+// load while this row's neighbours stream, and this row's self row (operand scale) loads
+// with its first group (k_aggregate_vec waits for rp, then col, then the neighbours, then
+// the self row: four dependent round trips per destination row). Straight-line loads (no
+// per-load conditions, which would make the compiler wait for every load). Same
+// accumulation order (CSR order) and arithmetic as k_aggregate_vec: bit-identical outputs.
+// rows per group: eight at NV <= 3 (d 768: <= 176 VGPRs, so one wave fits on a SIMD beside
+// two waves of the 168-VGPR GEMM, 512 per SIMD)
+#define ROLL_U(NV) ((NV) <= 3 ? 8 : 4)
+template <int NV, int AGG, int U>
+__global__ __launch_bounds__(256) void k_aggregate_roll(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                       int64_t n, const float* __restrict__ x, int dim,
+                                                       float* __restrict__ out, const float* __restrict__ self_x,
+                                                       float* __restrict__ row_scale, const float* __restrict__ row_mul,
+                                                       const float* __restrict__ self_mul) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * ROWS_PER_BLOCK;
+    int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+    int64_t beg = 0, end = 0;
+    int c_lane = 0;
+    if (row < n) {
+        beg = rp[row];
+        end = rp[row + 1];
+        c_lane = lane < min<int64_t>(64, end - beg) ? col[beg + lane] : 0;
+    }
+    auto load_row_from = [&](float4 (&v)[NV], const float* base) {
+        const float* src = base + 4 * lane;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) v[j] = ld_row4<true>(src + 256 * j);
+    };
+    auto load_row = [&](float4 (&v)[NV], int c) { load_row_from(v, x + (int64_t)c * dim); };
+    while (row < n) {
+        const int cnt_total = (int)(end - beg);
+        const int64_t nxt = row + stride;
+        int64_t nbeg = 0, nend = 0;
+        if (nxt < n) {
+            nbeg = rp[nxt];
+            nend = rp[nxt + 1];
+        }
+        float4 sv[NV];  // this row's self row (operand scale), in flight with the neighbours
+        if (row_scale) load_row_from(sv, self_x + row * dim);
+        const float init = (AGG == AGG_MAX) ? -INFINITY : 0.0f;
+        float4 acc[NV];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) acc[j] = make_float4(init, init, init, init);
+        int ncl = 0;
+        bool ncl_done = false;
+        for (int64_t e0 = beg; e0 < end; e0 += 64) {
+            const int cnt = (int)min<int64_t>(64, end - e0);
+            const int my_c = e0 == beg ? c_lane : (lane < cnt ? col[e0 + lane] : 0);
+            const float my_m = (row_mul && lane < cnt) ? row_mul[my_c] : 1.0f;
+            auto take = [&](float4 (&v)[NV], int idx) {
+                if (row_mul) {
+                    const float mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_m), idx));
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) v[j] = scale4(v[j], mu);
+                }
+#pragma unroll
+                for (int j = 0; j < NV; ++j) acc[j] = agg_op<AGG>(acc[j], v[j]);
+            };
+            const int groups = cnt / U;
+            for (int gi = 0; gi < groups; ++gi) {
+                float4 v[U][NV];
+#pragma unroll
+                for (int u = 0; u < U; ++u) load_row(v[u], __builtin_amdgcn_readlane(my_c, gi * U + u));
+                if (!ncl_done && nxt < n) {  // next row's ids, behind this row's first loads
+                    ncl = lane < min<int64_t>(64, nend - nbeg) ? col[nbeg + lane] : 0;
+                    ncl_done = true;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) take(v[u], gi * U + u);
+            }
+            for (int t = groups * U; t < cnt; ++t) {  // the last cnt % U rows, one at a time
+                float4 v[NV];
+                load_row(v, __builtin_amdgcn_readlane(my_c, t));
+                take(v, t);
+            }
+        }
+        if (!ncl_done && nxt < n) ncl = lane < min<int64_t>(64, nend - nbeg) ? col[nbeg + lane] : 0;
+
+        if (cnt_total > 0 && AGG == AGG_MEAN) {
+            const float cntf = (float)cnt_total;  // mean_aggregate: x / count (aggregators.rs:64-67)
+#pragma unroll
+            for (int j = 0; j < NV; ++j)
+                acc[j] = make_float4(acc[j].x / cntf, acc[j].y / cntf, acc[j].z / cntf, acc[j].w / cntf);
+        }
+        if (row_scale) {  // split-f16 GEMM operand scale over this row's aggregate and self rows
+            float m = 0.0f;
+            const float smul = self_mul ? self_mul[row] : 1.0f;
+#pragma unroll
+            for (int j = 0; j < NV; ++j) {
+                float4 v = sv[j];
+                if (self_mul) v = scale4(v, smul);
+                m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+                if (cnt_total > 0)
+                    m = fmaxf(m, fmaxf(fmaxf(fabsf(acc[j].x), fabsf(acc[j].y)), fmaxf(fabsf(acc[j].z), fabsf(acc[j].w))));
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+            if (lane == 0) row_scale[row] = h2_scale_dev(m);
+        }
+        float* dst = out + row * dim + 4 * lane;
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+            *reinterpret_cast<float4*>(dst + 256 * j) = cnt_total > 0 ? acc[j] : make_float4(0, 0, 0, 0);
+        row = nxt;
+        beg = nbeg;
+        end = nend;
+        c_lane = ncl;
+    }
+}
+
 // Any dim: one wave per row, scalar columns; same sequential order.
 template <int AGG, bool W>
 __global__ __launch_bounds__(256) void k_aggregate_scalar(const int64_t* rp, const int32_t* col, const float* wts,
@@ -238,9 +352,18 @@ void launch_agg(const char* t, const int64_t* rp, const int32_t* col, const floa
                 "planes need the vector gather with zero-filled empty rows");
     RVX_REQUIRE(!row_mul || (vec && empty_fill == 0), RVX_ERR_INVALID_SHAPE,
                 "row multipliers need the vector gather with zero-filled empty rows");
+    // opt-in (RVX_AGG_ROLL=1, read per call; tests cover both): the overlapped gather with the
+    // next row's CSR data and the self row prefetched (k_aggregate_roll). Same bits; beside the
+    // 256 x 192 GEMM it slowed the GEMM more than it saved (401-427 vs 410 ms/step,
+    // scripts/exp_roll_ab.sh)
+    const bool roll = deep && nt && !W && empty_fill == 0 && post_scale == 0 && !planes && (!row_scale || self_x) &&
+                      dim % 256 == 0 && env_int("RVX_AGG_ROLL", 0);
 #define RVX_AGG_VEC(NV)                                                                                          \
     do {                                                                                                         \
-        if (deep && nt)                                                                                        \
+        if (roll)                                                                                                \
+            RVX_LAUNCH(t, (k_aggregate_roll<NV, AGG, ROLL_U(NV)>), grid, block, 0, rp, col, n, x, dim, out,      \
+                       self_x, row_scale, row_mul, self_mul);                                                    \
+        else if (deep && nt)                                                                                     \
             RVX_LAUNCH(t, (k_aggregate_vec<NV, AGG, W, 8, true>), grid, block, 0, rp, col, w, n, x, dim,         \
                        empty_fill, post_scale, out, self_x, row_scale, planes, pstride, row_mul, self_mul);                         \
         else if (deep)                                                                                           \

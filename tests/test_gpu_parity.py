@@ -1054,3 +1054,25 @@ def test_graphsage_deferred_normalisation_stack(monkeypatch, gemm, dims, n, deg,
         ref = O.sage_forward(y1r, rp, col, O.sage_init(d1, d2, 0), O.sage_init(d1, d2, 1000), 0)
         assert_close(y1r, r1)
         assert_close(y2d, ref)
+
+
+@pytest.mark.parametrize("in_f,deg", [(256, 5), (768, 9), (512, 70)])
+def test_graphsage_overlapped_gather_prefetch_bits(monkeypatch, in_f, deg):
+    """The overlapped gather with the next row's CSR bounds / column ids and the self row
+    prefetched (k_aggregate_roll, RVX_AGG_ROLL=1) writes the same bits as the grouped
+    gather (0): chunked pipeline, empty rows, and rows of more than 64 neighbours."""
+    n, out_f = 40000, 128
+    x = O.fill_uniform(n * in_f, 97).reshape(n, in_f)
+    rng = np.random.default_rng(deg)
+    degs = rng.integers(0, 2 * deg, n)
+    degs[::13] = 0
+    rp = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
+    col = rng.integers(0, n, int(rp[-1])).astype(np.int32)
+    g = rv.Graph.from_csr(rp, col)
+    layer = rv.GraphSAGELayer(in_f, out_f, num_samples=2 * deg)
+    monkeypatch.setenv("RVX_SAGE_CHUNKS", "2")
+    monkeypatch.setenv("RVX_AGG_ROLL", "0")
+    y0 = layer.forward_graph(x, g)
+    monkeypatch.setenv("RVX_AGG_ROLL", "1")
+    y1 = layer.forward_graph(x, g)
+    assert np.array_equal(y0, y1)
