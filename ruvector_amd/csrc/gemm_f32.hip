@@ -1269,13 +1269,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
 // pieces of the next K-tile issued between them, so the next stage's loads have a whole
 // K-tile of MFMA work to land (cdna_hip_programming.md §5.5 T3/T4, without per-phase
 // barriers). A and B stages keep h2g's layouts and source-side XOR swizzles.
-template <bool DUAL, int WN, int BN>
+template <bool DUAL, int WN, int BN, int NW>
 __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgid) {
-    constexpr int BM = 256;
-    constexpr int WMW = 8 / WN;                 // waves along M
+    constexpr int BM = 32 * NW;        // 256 rows with 8 waves, 128 with 4
+    constexpr int WMW = NW / WN;                // waves along M
     constexpr int RB = BM / WMW / 32, NB = BN / WN / 32;  // 32-row / 32-column blocks per wave
-    constexpr int NBP = BN / 64;       // B DMA pieces per wave (2 planes x BN / 16 pieces over 8 waves)
-    constexpr int XA = BM * 128;       // f32 A tile bytes per stage (256 rows x 32 k)
+    constexpr int NBP = BN / (8 * NW);  // B DMA pieces per wave (2 planes x BN / 16 pieces over NW waves)
+    constexpr int XA = BM * 128;       // f32 A tile bytes per stage (BM rows x 32 k)
     constexpr int BPL = BN * 64;       // one f16 B plane tile (BN columns x 32 k)
     constexpr int STG = XA + 2 * BPL;  // 64 KB (BN 256) / 56 KB (BN 192)
     extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
@@ -1490,8 +1490,8 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
 // One tile per block (XCD-mapped tile order), or a persistent grid of one block per CU
 // taking tiles from per-XCD counters in row-tile-major order (g.queue, as gemm_nt_h2g):
 // beside the overlapped gather a persistent block keeps its LDS and registers.
-template <bool DUAL, int WN, int BN>
-__global__ __launch_bounds__(512, 1) void gemm_nt_h2w(GemmArgs g, int epi) {
+template <bool DUAL, int WN, int BN, int NW = 8>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 3 : 1) void gemm_nt_h2w(GemmArgs g, int epi) {
     if (g.queue) {
         __shared__ int64_t s_t;
         const int64_t xcd = blockIdx.x % 8;
@@ -1501,13 +1501,13 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_h2w(GemmArgs g, int epi) {
             __syncthreads();
             const int64_t t = s_t;
             if (t >= cnt) break;
-            h2w_tile<DUAL, WN, BN>(g, epi, first + t);
+            h2w_tile<DUAL, WN, BN, NW>(g, epi, first + t);
             __syncthreads();  // LDS stages and s_t are reused by the next tile
         }
         return;
     }
     const int64_t nwg = g.nblocks, bid = blockIdx.x;
-    h2w_tile<DUAL, WN, BN>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
+    h2w_tile<DUAL, WN, BN, NW>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
 }
 
 // B rows n of one or two [N][K] matrices: common scale t_n, f16 planes of each
@@ -1712,8 +1712,9 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
                       (g.B0h_plane + (int64_t)256 * g.ldb0) * 2 < ((int64_t)1 << 31) &&
                       (!s1 || (g.B1h_plane + (int64_t)256 * g.ldb1) * 2 < ((int64_t)1 << 31));
     if (wide) {
-        const int wbn = wide_mode == 3 ? 192 : 256;
-        const int wlds = 2 * (256 * 128 + 2 * wbn * 64);
+        const int wbn = wide_mode >= 3 ? 192 : 256;
+        const int wbm = wide_mode == 4 ? 128 : 256;  // 4: 4-wave blocks (one GEMM wave per SIMD)
+        const int wlds = 2 * (wbm * 128 + 2 * wbn * 64);
         static bool wattr = false;
         if (!wattr) {
             constexpr int l256 = 2 * (256 * 128 + 2 * 256 * 64), l192 = 2 * (256 * 128 + 2 * 192 * 64);
@@ -1723,10 +1724,13 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
+            constexpr int l4 = 2 * (128 * 128 + 2 * 192 * 64);
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
             wattr = true;
         }
         g.tiles_n = (N + wbn - 1) / wbn;
-        g.nblocks = ((M + 255) / 256) * g.tiles_n;
+        g.nblocks = ((M + wbm - 1) / wbm) * g.tiles_n;
         RVX_REQUIRE(!ep.row_sumsq || g.tiles_n <= ROWSUMSQ_SLOTS, RVX_ERR_INVALID_SHAPE, "row sums: N too large");
         RVX_REQUIRE(g.nblocks < (int64_t)1 << 31, RVX_ERR_INVALID_SHAPE, "GEMM grid too large");
         // persistent (one block per CU, per-XCD tile queue) when asked for, as h2g
@@ -1739,10 +1743,13 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
         } else {
             wgrid = g.nblocks;
         }
-        const dim3 wg((unsigned)wgrid), wb(512);
+        const dim3 wg((unsigned)wgrid), wb(wide_mode == 4 ? 256 : 512);
         // RVX_GEMM_WIDE=1: waves 2 (M) x 4 (N), 128 x 64 each; 2: waves 8 x 1, 32 x 256 each
         // (A converted once per row instead of by four waves)
-        if (wide_mode == 3) {
+        if (wide_mode == 4) {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 4>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 4>), wg, wb, wlds, g, ep.epi);
+        } else if (wide_mode == 3) {
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192>), wg, wb, wlds, g, ep.epi);
             else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192>), wg, wb, wlds, g, ep.epi);
         } else if (wide_mode == 2) {
