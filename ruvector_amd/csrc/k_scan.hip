@@ -597,30 +597,52 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
             float2 qsp[2];
 #pragma unroll
             for (int fn = 0; fn < 2; ++fn) qsp[fn] = qfac[wn * 64 + fn * 32 + lr];
+            // rows (e & 3) of a run are consecutive: four float4 reads issued together per run
 #pragma unroll
             for (int fm = 0; fm < F_FM; ++fm)
 #pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    const float4 c = rowc4[wm * WROWS + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh];
+                for (int g = 0; g < 4; ++g) {
+                    float4 cr[4];
 #pragma unroll
-                    for (int fn = 0; fn < 2; ++fn) {
-                        const float v = __builtin_fmaf(
-                            c.w, qsp[fn].y, __builtin_fmaf(c.z, qsp[fn].x, __builtin_fmaf(acc[fm][fn][e] * c.x, qf_[fn], c.y)));
-                        acc[fm][fn][e] = v;
-                        vmin[fn] = fminf(vmin[fn], v);
+                    for (int w = 0; w < 4; ++w) cr[w] = rowc4[wm * WROWS + fm * 32 + w + 8 * g + 4 * lh];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const int e = 4 * g + w;
+                        const float4 c = cr[w];
+#pragma unroll
+                        for (int fn = 0; fn < 2; ++fn) {
+                            const float v = __builtin_fmaf(
+                                c.w, qsp[fn].y,
+                                __builtin_fmaf(c.z, qsp[fn].x, __builtin_fmaf(acc[fm][fn][e] * c.x, qf_[fn], c.y)));
+                            acc[fm][fn][e] = v;
+                            vmin[fn] = fminf(vmin[fn], v);
+                        }
                     }
                 }
         } else {
+            // the 16 rows of a 32-row block that one lane holds are 4 runs of 4 consecutive
+            // rows: 8 ds_read_b128 (two rows' {C, R} each) issued together per block, instead
+            // of 16 dependent 8-byte reads the compiler waited on one by one
+            const float4* rc4 = reinterpret_cast<const float4*>(rowc);
 #pragma unroll
-        for (int fm = 0; fm < F_FM; ++fm)
+            for (int fm = 0; fm < F_FM; ++fm) {
+                const int rbase = (wm * WROWS + fm * 32 + 4 * lh) >> 1;  // even row: a float4 holds rows 2i, 2i+1
+                float4 cc[8];
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const float2 c = rowc[wm * WROWS + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh];
+                for (int g = 0; g < 4; ++g) {
+                    cc[2 * g] = rc4[rbase + 4 * g];
+                    cc[2 * g + 1] = rc4[rbase + 4 * g + 1];
+                }
 #pragma unroll
-                for (int fn = 0; fn < 2; ++fn) {
-                    const float v = __builtin_fmaf(acc[fm][fn][e] * c.x, qf_[fn], c.y);
-                    acc[fm][fn][e] = v;
-                    vmin[fn] = fminf(vmin[fn], v);  // NaN-ignoring: an all-NaN lane stays NaN
+                for (int e = 0; e < 16; ++e) {
+                    const float4 q = cc[2 * (e >> 2) + ((e & 3) >> 1)];
+                    const float2 c = (e & 1) ? make_float2(q.z, q.w) : make_float2(q.x, q.y);
+#pragma unroll
+                    for (int fn = 0; fn < 2; ++fn) {
+                        const float v = __builtin_fmaf(acc[fm][fn][e] * c.x, qf_[fn], c.y);
+                        acc[fm][fn][e] = v;
+                        vmin[fn] = fminf(vmin[fn], v);  // NaN-ignoring: an all-NaN lane stays NaN
+                    }
                 }
             }
         }
