@@ -771,12 +771,16 @@ __global__ void k_split_x3(const float* __restrict__ src, int64_t n, uint16_t* _
 // stage fill with source-address XOR swizzle, 2 x 32 KB stages.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+// packed form: v_pk_mul_f32, v_cvt_pk_f16_f32 (RNE) for the high parts, the exact residual
+// x - f32(h) (v_pk_add_f32) rounded the same way for the low parts — 6 VALU per pair
 __device__ __forceinline__ void split_h2_pair(float a0, float a1, float sc, unsigned& w1, unsigned& w2) {
-    const float x0 = a0 * sc, x1 = a1 * sc;
-    const _Float16 h0 = (_Float16)x0, h1 = (_Float16)x1;
-    const _Float16 l0 = (_Float16)(x0 - (float)h0), l1 = (_Float16)(x1 - (float)h1);
-    w1 = (unsigned)__builtin_bit_cast(unsigned short, h0) | ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
-    w2 = (unsigned)__builtin_bit_cast(unsigned short, l0) | ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
+    const f32x2 x = f32x2{a0, a1} * sc;
+    const f16x2 h = __builtin_convertvector(x, f16x2);
+    const f16x2 l = __builtin_convertvector(x - __builtin_convertvector(h, f32x2), f16x2);
+    w1 = __builtin_bit_cast(unsigned, h);
+    w2 = __builtin_bit_cast(unsigned, l);
 }
 
 // XCD x (= block id % 8: workgroups are dealt round-robin over the 8 XCDs)
@@ -1269,7 +1273,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
 // pieces of the next K-tile issued between them, so the next stage's loads have a whole
 // K-tile of MFMA work to land (cdna_hip_programming.md §5.5 T3/T4, without per-phase
 // barriers). A and B stages keep h2g's layouts and source-side XOR swizzles.
-template <bool DUAL, int WN, int BN, int NW>
+#ifndef H2W_RING
+#define H2W_RING 4
+#endif
+template <bool DUAL, int WN, int BN, int NW, bool PIPE = false>
 __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgid) {
     constexpr int BM = 32 * NW;        // 256 rows with 8 waves, 128 with 4
     constexpr int WMW = NW / WN;                // waves along M
@@ -1371,6 +1378,98 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
 
 #pragma unroll
     for (int j = 0; j < 4 + NBP; ++j) issue(0, xsm, j);
+    if constexpr (PIPE) {
+        // Software-pipelined K loop. A wave owns 32 whole tile rows, so a K-tile is G = 2 NB
+        // MFMA groups (k16 half s, column block nb), 3 MFMAs each. B fragments come from a
+        // ring of R register pairs read L = R - 1 groups ahead of their MFMAs; the one barrier
+        // per K-tile sits where the reads cross into the next stage (after group G - L: this
+        // wave's reads of the stage are then all issued), and the DMA of tile t+2 into the
+        // freed stage follows it. A(t, s1) is read and split during the s0 groups, A(t+1, s0)
+        // during the s1 groups. Per accumulator the products keep h2w's order (s ascending;
+        // a_lo b_hi, a_hi b_lo, a_hi b_hi), so every output is bit-identical.
+        static_assert(WN == 1 && RB == 1, "pipelined form: a wave owns 32 whole tile rows");
+        constexpr int G = 2 * NB, R = H2W_RING, L = R - 1, G0 = G - L;
+        static_assert(G % R == 0 && G0 >= NB && G0 < G - 1, "ring slots are static per K-tile");
+        u32x4 ring[R][2];
+        float4 ra[2];
+        u32x4 fx[2], fy[2];  // split A words [hi, lo] of the s0 / s1 half
+        // pair j of the raw A slice into word j of af (one pair per MFMA group: the split's
+        // VALU runs in the MFMA shadow instead of as one block ahead of a group)
+        auto split_a = [&](float sc, u32x4 (&af)[2], int j) {
+            unsigned w0, w1;
+            split_h2_pair(f4_at(ra[0], ra[1], 2 * j), f4_at(ra[0], ra[1], 2 * j + 1), sc, w0, w1);
+            af[0][j] = w0;
+            af[1][j] = w1;
+        };
+        auto rd_a = [&](const unsigned char* st, int s) {
+            ra[0] = *reinterpret_cast<const float4*>(st + a_rd[s][0]);
+            ra[1] = *reinterpret_cast<const float4*>(st + a_rd[s][1]);
+        };
+        auto rd_b = [&](const unsigned char* st, int gg, u32x4 (&b)[2]) {
+            const int s = gg / NB, nb = gg % NB;
+            b[0] = *reinterpret_cast<const u32x4*>(st + b_rd[s] + nb * 2048);
+            b[1] = *reinterpret_cast<const u32x4*>(st + b_rd[s] + nb * 2048 + BPL);
+        };
+        auto mm = [&](const u32x4 (&af)[2], const u32x4 (&b)[2], f32x16& c) {
+            const f16x8 a0 = __builtin_bit_cast(f16x8, af[0]);
+            const f16x8 a1 = __builtin_bit_cast(f16x8, af[1]);
+            const f16x8 b0 = __builtin_bit_cast(f16x8, b[0]);
+            const f16x8 b1 = __builtin_bit_cast(f16x8, b[1]);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, c, 0, 0, 0);
+        };
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (nkt > 1) {
+#pragma unroll
+            for (int j = 0; j < 4 + NBP; ++j) issue(1, xsm + STG, j);
+        }
+        rd_a(xsm, 0);
+#pragma unroll
+        for (int gg = 0; gg < L; ++gg) rd_b(xsm, gg, ring[gg]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) split_a(DUAL && nk0 == 0 ? asc1[0] : asc[0], fx, j);
+        // tile t from `cur` (its stage), then the first reads of tile t+1 from `nxt`
+        auto body = [&](unsigned char* __restrict__ cur, const unsigned char* __restrict__ nxt, int t) {
+            const float sc = DUAL && t >= nk0 ? asc1[0] : asc[0];
+            const float scn = DUAL && t + 1 >= nk0 ? asc1[0] : asc[0];
+            const bool more = t + 1 < nkt;
+#pragma unroll
+            for (int gg = 0; gg < G; ++gg) {
+                mm(gg < NB ? fx : fy, ring[gg % R], acc[0][gg % NB]);
+                if (gg == 0) rd_a(cur, 1);
+                if (gg >= 2 && gg < 6) split_a(sc, fy, gg - 2);  // A(t, s1), before group NB
+                const int ng = gg + L;
+                if (ng < G) {
+                    rd_b(cur, ng, ring[ng % R]);
+                } else if (more) {
+                    if (ng == G) {
+                        // this wave's reads of tile t are all issued: wait for them and for its
+                        // DMA of tile t+1, then every wave's (barrier); tile t's stage is free
+                        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+                        __builtin_amdgcn_s_barrier();
+                        asm volatile("" ::: "memory");
+                        if (t + 2 < nkt) {
+#pragma unroll
+                            for (int j = 0; j < 4 + NBP; ++j) issue(t + 2, cur, j);
+                        }
+                        rd_a(nxt, 0);
+                    }
+                    rd_b(nxt, ng - G, ring[ng % R]);
+                }
+                if (gg > G0 && more) {  // A(t+1, s0): its pairs over the groups after the read
+                    constexpr int NS = G - 1 - G0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (j * NS / 4 == gg - G0 - 1) split_a(scn, fx, j);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        for (int t = 0; t < nkt; ++t) body(xsm + (t & 1) * STG, xsm + ((t + 1) & 1) * STG, t);
+    } else {
     // one K-tile; restrict parameters give the stage pointers distinct alias scopes, so
     // the ds_reads of `cur` do not wait for the LDS-DMA into `nxt` (vmcnt) in the phases
     auto ktile = [&](const unsigned char* __restrict__ cur, unsigned char* __restrict__ nxt, int t) {
@@ -1442,6 +1541,7 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
         asm volatile("" ::: "memory");
         ktile(xsm + (t & 1) * STG, xsm + ((t + 1) & 1) * STG, t);
     }
+    }
 
     // epilogue as h2g: undo the row and column scales (powers of two: exact), then
     // alpha / bias / addend / activation; row-outer, and with WN = 1 (a wave holds whole
@@ -1490,7 +1590,7 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
 // One tile per block (XCD-mapped tile order), or a persistent grid of one block per CU
 // taking tiles from per-XCD counters in row-tile-major order (g.queue, as gemm_nt_h2g):
 // beside the overlapped gather a persistent block keeps its LDS and registers.
-template <bool DUAL, int WN, int BN, int NW = 8>
+template <bool DUAL, int WN, int BN, int NW = 8, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 3 : 1) void gemm_nt_h2w(GemmArgs g, int epi) {
     if (g.queue) {
         __shared__ int64_t s_t;
@@ -1501,13 +1601,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 3 : 1) void gemm_nt_h2w(GemmArgs
             __syncthreads();
             const int64_t t = s_t;
             if (t >= cnt) break;
-            h2w_tile<DUAL, WN, BN, NW>(g, epi, first + t);
+            h2w_tile<DUAL, WN, BN, NW, PIPE>(g, epi, first + t);
             __syncthreads();  // LDS stages and s_t are reused by the next tile
         }
         return;
     }
     const int64_t nwg = g.nblocks, bid = blockIdx.x;
-    h2w_tile<DUAL, WN, BN, NW>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
+    h2w_tile<DUAL, WN, BN, NW, PIPE>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
 }
 
 // B rows n of one or two [N][K] matrices: common scale t_n, f16 planes of each
@@ -1712,7 +1812,7 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
                       (g.B0h_plane + (int64_t)256 * g.ldb0) * 2 < ((int64_t)1 << 31) &&
                       (!s1 || (g.B1h_plane + (int64_t)256 * g.ldb1) * 2 < ((int64_t)1 << 31));
     if (wide) {
-        const int wbn = wide_mode >= 3 ? 192 : 256;
+        const int wbn = wide_mode >= 3 && wide_mode <= 5 ? 192 : 256;  // 5 / 6: 256 x 192 / 256 x 256, software-pipelined K loop
         const int wbm = wide_mode == 4 ? 128 : 256;  // 4: 4-wave blocks (one GEMM wave per SIMD)
         const int wlds = 2 * (wbm * 128 + 2 * wbn * 64);
         static bool wattr = false;
@@ -1724,6 +1824,10 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 256, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 256, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
             constexpr int l4 = 2 * (128 * 128 + 2 * 192 * 64);
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
@@ -1746,7 +1850,13 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
         const dim3 wg((unsigned)wgrid), wb(wide_mode == 4 ? 256 : 512);
         // RVX_GEMM_WIDE=1: waves 2 (M) x 4 (N), 128 x 64 each; 2: waves 8 x 1, 32 x 256 each
         // (A converted once per row instead of by four waves)
-        if (wide_mode == 4) {
+        if (wide_mode == 6) {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 256, 8, true>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 256, 8, true>), wg, wb, wlds, g, ep.epi);
+        } else if (wide_mode == 5) {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 8, true>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 8, true>), wg, wb, wlds, g, ep.epi);
+        } else if (wide_mode == 4) {
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 4>), wg, wb, wlds, g, ep.epi);
             else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 4>), wg, wb, wlds, g, ep.epi);
         } else if (wide_mode == 3) {
