@@ -1590,16 +1590,20 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
 // One tile per block (XCD-mapped tile order), or a persistent grid of one block per CU
 // taking tiles from per-XCD counters in row-tile-major order (g.queue, as gemm_nt_h2g):
 // beside the overlapped gather a persistent block keeps its LDS and registers.
+// The tile ticket is passed through the first word of the (then idle) stage memory, so two
+// 80 KB 4-wave blocks fit one CU's 160 KB.
 template <bool DUAL, int WN, int BN, int NW = 8, bool PIPE = false>
-__global__ __launch_bounds__(64 * NW, NW == 4 ? 3 : 1) void gemm_nt_h2w(GemmArgs g, int epi) {
+__global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt_h2w(GemmArgs g, int epi) {
     if (g.queue) {
-        __shared__ int64_t s_t;
+        extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
+        int64_t* s_t = reinterpret_cast<int64_t*>(xsm);
         const int64_t xcd = blockIdx.x % 8;
         const int64_t first = xcd_first(g.nblocks, xcd), cnt = xcd_count(g.nblocks, xcd);
         for (;;) {
-            if (threadIdx.x == 0) s_t = (int64_t)atomicAdd(g.queue + 32 * xcd, 1u);
+            if (threadIdx.x == 0) *s_t = (int64_t)atomicAdd(g.queue + 32 * xcd, 1u);
             __syncthreads();
-            const int64_t t = s_t;
+            const int64_t t = *s_t;
+            __syncthreads();  // every wave holds t before the tile's DMA overwrites the word
             if (t >= cnt) break;
             h2w_tile<DUAL, WN, BN, NW, PIPE>(g, epi, first + t);
             __syncthreads();  // LDS stages and s_t are reused by the next tile
@@ -1803,8 +1807,12 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
     // gather wave share each SIMD; the 256-wide tile's 193+ VGPRs do not fit and lost, 487 vs
     // 454 ms/step): 403-451 vs 455-470 ms/step for h2g (scripts/exp_wide3_pipe.sh).
     // RVX_GEMM_WIDE (read per call; tests cover all): 0 h2g, 1 waves 2 x 4, 2 waves 8 x 1,
-    // 3 waves 8 x 1 on 256 x 192 tiles (32 x 192 per wave: 96 accumulator registers).
-    const int wide_mode = env_int("RVX_GEMM_WIDE", persist > 0 ? 3 : 2);
+    // 3 waves 8 x 1 on 256 x 192 tiles (32 x 192 per wave: 96 accumulator registers),
+    // 4 the same rows on 4-wave 128 x 192 blocks, 5 / 6 / 7 the software-pipelined K loop on
+    // 256 x 192 / 256 x 256 / 4-wave 128 x 192 (two blocks per CU, each its own barriers).
+    // Standalone default 7: C4 stack GEMMs 345 vs 356 ms per 2M step with 2, the 10M
+    // GraphSAGE GEMM 77.2 vs 78.1 ms (scripts/exp_gemm_pipe.sh, profiles/r03_gemm_pipe_ab.txt).
+    const int wide_mode = env_int("RVX_GEMM_WIDE", persist > 0 ? 3 : 7);
     const bool same_strides = !s1 || (g.lda1 == g.lda0 && g.ldb1 == g.ldb0 && g.B1h_plane == g.B0h_plane);
     const bool wide = !ep.normalize_rows && (wide_mode >= 2 || (!ep.row_sumsq && !ep.a1_rowmul)) && wide_mode &&
                       same_strides && (int64_t)256 * g.lda0 * 4 < ((int64_t)1 << 31) &&
@@ -1812,8 +1820,8 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
                       (g.B0h_plane + (int64_t)256 * g.ldb0) * 2 < ((int64_t)1 << 31) &&
                       (!s1 || (g.B1h_plane + (int64_t)256 * g.ldb1) * 2 < ((int64_t)1 << 31));
     if (wide) {
-        const int wbn = wide_mode >= 3 && wide_mode <= 5 ? 192 : 256;  // 5 / 6: 256 x 192 / 256 x 256, software-pipelined K loop
-        const int wbm = wide_mode == 4 ? 128 : 256;  // 4: 4-wave blocks (one GEMM wave per SIMD)
+        const int wbn = wide_mode == 3 || wide_mode == 4 || wide_mode == 5 || wide_mode == 7 ? 192 : 256;  // 5 / 6: 256 x 192 / 256 x 256, software-pipelined K loop
+        const int wbm = wide_mode == 4 || wide_mode == 7 ? 128 : 256;  // 4: 4-wave blocks (one GEMM wave per SIMD)
         const int wlds = 2 * (wbm * 128 + 2 * wbn * 64);
         static bool wattr = false;
         if (!wattr) {
@@ -1831,6 +1839,8 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
             constexpr int l4 = 2 * (128 * 128 + 2 * 192 * 64);
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
             wattr = true;
         }
         g.tiles_n = (N + wbn - 1) / wbn;
@@ -1840,17 +1850,20 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
         // persistent (one block per CU, per-XCD tile queue) when asked for, as h2g
         const int wcap = persist >= 0 ? persist : env_int("RVX_GEMM_CAP", 0);
         int64_t wgrid = g.nblocks;
-        if (wcap > 0) wgrid = std::min<int64_t>(wgrid, ((int64_t)active_cus() + 7) / 8 * 8);
+        if (wcap > 0) wgrid = std::min<int64_t>(wgrid, ((int64_t)(wbm == 128 ? 2 : 1) * active_cus() + 7) / 8 * 8);  // 4-wave blocks: two per CU
         if (wgrid < g.nblocks && wgrid % 8 == 0) {
             g.queue = (unsigned*)scratch_bytes("gemm_h2_queue", 8 * 32 * 4);
             RVX_HIP(hipMemsetAsync(g.queue, 0, 8 * 32 * 4, stream()));
         } else {
             wgrid = g.nblocks;
         }
-        const dim3 wg((unsigned)wgrid), wb(wide_mode == 4 ? 256 : 512);
+        const dim3 wg((unsigned)wgrid), wb(wide_mode == 4 || wide_mode == 7 ? 256 : 512);
         // RVX_GEMM_WIDE=1: waves 2 (M) x 4 (N), 128 x 64 each; 2: waves 8 x 1, 32 x 256 each
         // (A converted once per row instead of by four waves)
-        if (wide_mode == 6) {
+        if (wide_mode == 7) {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 4, true>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 4, true>), wg, wb, wlds, g, ep.epi);
+        } else if (wide_mode == 6) {
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 256, 8, true>), wg, wb, wlds, g, ep.epi);
             else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 256, 8, true>), wg, wb, wlds, g, ep.epi);
         } else if (wide_mode == 5) {

@@ -940,7 +940,7 @@ def test_graphsage_in_gemm_row_normalisation_bits(monkeypatch, in_f, out_f, n, d
         assert_close(y1, O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0))
 
 
-@pytest.mark.parametrize("wide", ["1", "2", "3", "4", "5", "6"])
+@pytest.mark.parametrize("wide", ["1", "2", "3", "4", "5", "6", "7"])
 @pytest.mark.parametrize("in_f,out_f,n,deg,chunks", [(768, 768, 600, 9, 0), (96, 232, 1000, 5, 0),
                                                      (64, 130, 257, 0, 0), (32, 32, 129, 3, 0),
                                                      (128, 512, 40000, 4, 2)])
@@ -963,7 +963,7 @@ def test_graphsage_wide_gemm_bits(monkeypatch, in_f, out_f, n, deg, chunks, wide
         assert_close(y1, O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0))
 
 
-@pytest.mark.parametrize("wide", ["1", "2", "3", "4", "5", "6"])
+@pytest.mark.parametrize("wide", ["1", "2", "3", "4", "5", "6", "7"])
 @pytest.mark.parametrize("hidden,heads", [(64, 4), (768, 8), (96, 4)])
 def test_ruvector_layer_wide_gemm_bits(monkeypatch, hidden, heads, wide):
     """RuvectorLayer's GEMMs (single and dual, bias / addend / sigmoid / tanh
