@@ -132,6 +132,94 @@ __global__ __launch_bounds__(256) void k_edge_feat_out(EfaArgs a) {
     }
 }
 
+// k_edge_feat_out's concat form with float4 rows: lane l of the node's wave owns columns
+// 4(l + 64 v) .. +3 (v < NV), all in one head (hd % 4 == 0), and U edges' rows are in
+// flight at once. Per column the sum is the same chain — edges ascending, product then
+// add, from 0 — so the output bits equal the scalar kernel's.
+template <int NV>
+__global__ __launch_bounds__(256) void k_edge_feat_out_vec(EfaArgs a) {
+    constexpr int U = NV <= 2 ? 8 : 4;
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    const int heads = a.heads, hd = a.hd, D4 = heads * hd / 4;
+    const int64_t ldv4 = a.ldv / 4;
+    const float4* __restrict__ tv4 = reinterpret_cast<const float4*>(a.tv);
+    const int64_t beg = a.rp[i], end = a.rp[i + 1];
+    int hv[NV];
+    bool ok[NV];
+    float4 acc[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int c4 = lane + 64 * v;
+        ok[v] = c4 < D4;
+        hv[v] = ok[v] ? 4 * c4 / hd : 0;
+        acc[v] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    auto add = [](float4& s, float w, const float4& t) {
+        s.x = s.x + w * t.x;
+        s.y = s.y + w * t.y;
+        s.z = s.z + w * t.z;
+        s.w = s.w + w * t.w;
+    };
+    int64_t e = beg;
+    for (; e + U <= end; e += U) {
+        float4 t[U][NV];
+        float w[U][NV];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = a.col[e + u];
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (ok[v]) {
+                    t[u][v] = tv4[j * ldv4 + lane + 64 * v];
+                    w[u][v] = a.scores[(e + u) * heads + hv[v]];
+                }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+                if (ok[v]) add(acc[v], w[u][v], t[u][v]);
+    }
+    for (; e < end; ++e) {
+        const int64_t j = a.col[e];
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (ok[v]) add(acc[v], a.scores[e * heads + hv[v]], tv4[j * ldv4 + lane + 64 * v]);
+    }
+    float4* o4 = reinterpret_cast<float4*>(a.out) + i * (int64_t)D4;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+        if (ok[v]) o4[lane + 64 * v] = acc[v];
+}
+
+// k_efa_row_dots with the rows staged through LDS: a block takes 8 rows (coalesced float4
+// copies), then lane (row, head) runs the same sequential chain over its head's hd values.
+__global__ __launch_bounds__(256) void k_efa_row_dots_lds(const float* __restrict__ t, int64_t ld, int64_t rows,
+                                                          int heads, int hd, const float* __restrict__ av,
+                                                          float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float rs[];  // [8][D + 1]
+    const int D = heads * hd, D4 = D / 4, st = D + 4;
+    const int64_t r0 = (int64_t)blockIdx.x * 8;
+    for (int idx = threadIdx.x; idx < 8 * D4; idx += blockDim.x) {
+        const int rr = idx / D4, c4 = idx % D4;
+        if (r0 + rr < rows)
+            *reinterpret_cast<float4*>(rs + rr * st + 4 * c4) =
+                reinterpret_cast<const float4*>(t + (r0 + rr) * ld)[c4];
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < 8 * heads; p += blockDim.x) {
+        const int rr = p / heads, h = p % heads;
+        if (r0 + rr >= rows) continue;
+        const float* tr = rs + rr * st + h * hd;
+        const float* ar = av + (int64_t)h * hd;
+        float s = 0.0f;
+        for (int c = 0; c < hd; ++c) s = s + tr[c] * ar[c];
+        out[(r0 + rr) * heads + h] = s;
+    }
+}
+
 // ---- differentiable_search -------------------------------------------------
 // One wave per query. cand rows of query qi start at cand + qi * cand_q_stride
 // (stride C*d: per-query candidate lists; 0: one table shared by every query,
@@ -238,11 +326,22 @@ __global__ __launch_bounds__(256) void k_hier_combine(const float* cur, int64_t 
 void edge_feat_attention(const EfaArgs& a) {
     if (a.n <= 0) return;
     const int64_t nq = a.n * a.heads, nkh = a.nk * a.heads;
-    RVX_LAUNCH("efa_node_dots", k_efa_row_dots, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, a.tq, a.ldq, a.n,
-               a.heads, a.hd, a.a_src, a.sq);
-    if (nkh > 0)
-        RVX_LAUNCH("efa_node_dots", k_efa_row_dots, dim3((unsigned)((nkh + 255) / 256)), dim3(256), 0, a.tk, a.ldk,
-                   a.nk, a.heads, a.hd, a.a_dst, a.sk);
+    const int D = a.heads * a.hd;
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    // row dots through LDS when rows are float4-aligned and 8 of them fit 64 KB (<= 2040 columns)
+    auto row_dots = [&](const float* t, int64_t ld, int64_t rows, const float* av, float* out) {
+        if (rows <= 0) return;
+        if (D % 4 == 0 && ld % 4 == 0 && al16(t) && D <= 2040 && env_int("RVX_EFA_VEC", 1)) {
+            const size_t lds = (size_t)8 * (D + 4) * sizeof(float);
+            RVX_LAUNCH("efa_node_dots", k_efa_row_dots_lds, dim3((unsigned)((rows + 7) / 8)), dim3(256), lds, t, ld,
+                       rows, a.heads, a.hd, av, out);
+        } else {
+            RVX_LAUNCH("efa_node_dots", k_efa_row_dots, dim3((unsigned)((rows * a.heads + 255) / 256)), dim3(256), 0, t,
+                       ld, rows, a.heads, a.hd, av, out);
+        }
+    };
+    row_dots(a.tq, a.ldq, a.n, a.a_src, a.sq);
+    if (nkh > 0) row_dots(a.tk, a.ldk, a.nk, a.a_dst, a.sk);
     if (a.edges && a.edge_dim > 0) {
         const int nu = a.heads * a.edge_dim;
         RVX_LAUNCH("efa_node_dots", k_efa_edge_u, dim3((unsigned)((nu + 255) / 256)), dim3(256), 0, a.w_edge, a.a_edge,
@@ -250,7 +349,14 @@ void edge_feat_attention(const EfaArgs& a) {
     }
     RVX_LAUNCH("efa_scores", k_edge_feat_scores, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, a);
     RVX_LAUNCH("efa_softmax", k_edge_feat_softmax, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, a);
-    RVX_LAUNCH("efa_out", k_edge_feat_out, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, a);
+    const bool vec = a.concat && a.hd % 4 == 0 && a.ldv % 4 == 0 && al16(a.tv) && al16(a.out) && D <= 1024 &&
+                     env_int("RVX_EFA_VEC", 1);
+    const dim3 og((unsigned)((a.n + 3) / 4)), ob(256);
+    if (vec && D <= 256) RVX_LAUNCH("efa_out", k_edge_feat_out_vec<1>, og, ob, 0, a);
+    else if (vec && D <= 512) RVX_LAUNCH("efa_out", k_edge_feat_out_vec<2>, og, ob, 0, a);
+    else if (vec && D <= 768) RVX_LAUNCH("efa_out", k_edge_feat_out_vec<3>, og, ob, 0, a);
+    else if (vec) RVX_LAUNCH("efa_out", k_edge_feat_out_vec<4>, og, ob, 0, a);
+    else RVX_LAUNCH("efa_out", k_edge_feat_out, og, ob, 0, a);
 }
 
 void differentiable_search(const float* q, int64_t nq, const float* cand, int C, int d, int k, float temperature,

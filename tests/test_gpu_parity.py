@@ -757,6 +757,37 @@ def test_edge_attention_graph_matches_per_node():
         assert_close(y[i], ref)
 
 
+@pytest.mark.parametrize("node_dim,heads", [(64, 4), (512, 8), (768, 8), (1024, 8), (100, 4), (200, 5)])
+def test_edge_attention_vector_kernels_bits(monkeypatch, node_dim, heads):
+    """The float4 output kernel (k_edge_feat_out_vec, 4 / 8 edges in flight) and the
+    LDS-staged per-head node dots write the same bits as the scalar kernels
+    (RVX_EFA_VEC=0): degrees 0 to 19 (remainders past the edge batches), hd % 4 != 0
+    (200 / 5 = 40 is vectorised, 100 / 4 = 25 falls back), D up to 1024."""
+    n = 400
+    att = rv.EdgeFeaturedAttention(rv.EdgeFeaturedConfig(node_dim=node_dim, edge_dim=1, num_heads=heads))
+    x = O.fill_uniform(n * node_dim, 31).reshape(n, node_dim)
+    rng = np.random.default_rng(node_dim)
+    degs = rng.integers(0, 20, n)
+    degs[::17] = 0
+    rp = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
+    col = rng.integers(0, n, int(rp[-1])).astype(np.int32)
+    ef = O.fill_uniform(int(rp[-1]), 32, 0.0, 1.0)
+    g = rv.Graph.from_csr(rp, col)
+    xb, eb = rv.Buffer.from_numpy(x), rv.Buffer.from_numpy(ef)
+    ys = []
+    for vec in ("0", "1"):
+        monkeypatch.setenv("RVX_EFA_VEC", vec)
+        yb = rv.Buffer(x.nbytes)
+        att.forward_graph_device(xb, g, eb, yb)
+        ys.append(yb.download(np.float32, x.shape))
+    assert np.array_equal(ys[0], ys[1])
+    for i in (1, 5, 33):
+        nb = col[rp[i]:rp[i + 1]]
+        if len(nb):
+            ref = O.efa_compute(node_dim, 1, heads, x[i], x[nb], x[nb], ef[rp[i]:rp[i + 1]].reshape(-1, 1))
+            assert_close(ys[1][i], ref)
+
+
 def test_edge_attention_forward_exchange_entry():
     """rvx_edge_attention_forward_exchange (node-range-sharded head: owned rows of
     T = x W_node^T into the whole table, p2p exchange, per-edge attention on owned
