@@ -35,8 +35,10 @@ __device__ __forceinline__ float norm_weight(int mode, const float* w, int64_t e
 }
 
 // Fast path: H = 64*CPL, lane owns columns [lane*CPL, lane*CPL+CPL), a head is
-// G = head_dim/CPL consecutive lanes (G a power of two).
-template <int CPL>
+// G = head_dim/CPL consecutive lanes (G a power of two). B edges' rows are loaded
+// together before their arithmetic (B = 1: one edge at a time); each edge's dot and every
+// running sum keep the same operations in the same order, so B does not change the bits.
+template <int CPL, int B>
 __global__ __launch_bounds__(256) void k_edge_attn_grouped(EdgeArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -67,49 +69,87 @@ __global__ __launch_bounds__(256) void k_edge_attn_grouped(EdgeArgs a) {
     const float scale = sqrtf((float)a.hd);
     float mx = -INFINITY;
     // pass 1: scores
-    for (int64_t e = beg; e < end; ++e) {
-        const int j = a.col[e];
-        const float* kr = a.k + (int64_t)j * a.ldkv + c0;
+    auto score_of = [&](int64_t e, const float4 (&kv)[CPL / 4]) {
         float p = 0.0f;
 #pragma unroll
         for (int c = 0; c < CPL; c += 4) {
-            const float4 v = ld4(kr + c);
+            const float4 v = kv[c / 4];
             p = p + q[c] * v.x; p = p + q[c + 1] * v.y; p = p + q[c + 2] * v.z; p = p + q[c + 3] * v.w;
         }
         for (int o = 1; o < G; o <<= 1) p += __shfl_xor(p, o);
         const float s = p / scale;
         mx = fmaxf(mx, s);
         if ((lane & (G - 1)) == 0) scores[e * a.heads + head] = s;
+    };
+    int64_t e = beg;
+    for (; e + B <= end; e += B) {
+        float4 kv[B][CPL / 4];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const float* kr = a.k + (int64_t)a.col[e + b] * a.ldkv + c0;
+#pragma unroll
+            for (int c = 0; c < CPL; c += 4) kv[b][c / 4] = ld4(kr + c);
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b) score_of(e + b, kv[b]);
+    }
+    for (; e < end; ++e) {
+        float4 kv[CPL / 4];
+        const float* kr = a.k + (int64_t)a.col[e] * a.ldkv + c0;
+#pragma unroll
+        for (int c = 0; c < CPL; c += 4) kv[c / 4] = ld4(kr + c);
+        score_of(e, kv);
     }
     __builtin_amdgcn_wave_barrier();
     __threadfence_block();
     // pass 2: sum of exp in neighbour order
     float sum = 0.0f;
-    for (int64_t e = beg; e < end; ++e) sum = sum + expf(scores[e * a.heads + head] - mx);
+    for (int64_t e2 = beg; e2 < end; ++e2) sum = sum + expf(scores[e2 * a.heads + head] - mx);
     sum = fmaxf(sum, 1e-10f);
     float wsum = 0.0f;
     if (a.wmode == 1) wsum = row_weight_sum(a.w, beg, end);
     // pass 3: weighted sums of values and messages
-    for (int64_t e = beg; e < end; ++e) {
-        const int j = a.col[e];
-        const float wt = expf(scores[e * a.heads + head] - mx) / sum;
-        const float* vr = a.v + (int64_t)j * a.ldkv + c0;
+    const bool msg = a.wmode != 0;
+    auto accumulate = [&](int64_t e3, const float4 (&vv)[CPL / 4], const float4 (&mv)[CPL / 4]) {
+        const float wt = expf(scores[e3 * a.heads + head] - mx) / sum;
 #pragma unroll
         for (int c = 0; c < CPL; c += 4) {
-            const float4 v = ld4(vr + c);
+            const float4 v = vv[c / 4];
             att[c] = att[c] + wt * v.x; att[c + 1] = att[c + 1] + wt * v.y;
             att[c + 2] = att[c + 2] + wt * v.z; att[c + 3] = att[c + 3] + wt * v.w;
         }
-        if (a.wmode != 0) {
-            const float ww = norm_weight(a.wmode, a.w, e, wsum, deg);
-            const float* mr = a.m + (int64_t)j * H + c0;
+        if (msg) {
+            const float ww = norm_weight(a.wmode, a.w, e3, wsum, deg);
 #pragma unroll
             for (int c = 0; c < CPL; c += 4) {
-                const float4 v = ld4(mr + c);
+                const float4 v = mv[c / 4];
                 agg[c] = agg[c] + ww * v.x; agg[c + 1] = agg[c + 1] + ww * v.y;
                 agg[c + 2] = agg[c + 2] + ww * v.z; agg[c + 3] = agg[c + 3] + ww * v.w;
             }
         }
+    };
+    auto load_vm = [&](int64_t e3, float4 (&vv)[CPL / 4], float4 (&mv)[CPL / 4]) {
+        const int j = a.col[e3];
+        const float* vr = a.v + (int64_t)j * a.ldkv + c0;
+        const float* mr = a.m + (int64_t)j * H + c0;
+#pragma unroll
+        for (int c = 0; c < CPL; c += 4) {
+            vv[c / 4] = ld4(vr + c);
+            mv[c / 4] = msg ? ld4(mr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    e = beg;
+    for (; e + B <= end; e += B) {
+        float4 vv[B][CPL / 4], mv[B][CPL / 4];
+#pragma unroll
+        for (int b = 0; b < B; ++b) load_vm(e + b, vv[b], mv[b]);
+#pragma unroll
+        for (int b = 0; b < B; ++b) accumulate(e + b, vv[b], mv[b]);
+    }
+    for (; e < end; ++e) {
+        float4 vv[CPL / 4], mv[CPL / 4];
+        load_vm(e, vv, mv);
+        accumulate(e, vv, mv);
     }
 #pragma unroll
     for (int c = 0; c < CPL; c += 4) {
@@ -360,10 +400,15 @@ void edge_attention(const EdgeArgs& a) {
     const char* t = "gnn_edge_attention";
     const bool aligned = (((uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v | (uintptr_t)a.m | (uintptr_t)a.att |
                            (uintptr_t)a.wagg) & 15) == 0 && a.ldq % 4 == 0 && a.ldkv % 4 == 0;
-    if (aligned && a.H % 64 == 0 && a.G > 0 && a.H / 64 == 4) RVX_LAUNCH(t, k_edge_attn_grouped<4>, grid, block, 0, a);
-    else if (aligned && a.H % 64 == 0 && a.G > 0 && a.H / 64 == 8) RVX_LAUNCH(t, k_edge_attn_grouped<8>, grid, block, 0, a);
-    else if (aligned && a.H % 64 == 0 && a.G > 0 && a.H / 64 == 12) RVX_LAUNCH(t, k_edge_attn_grouped<12>, grid, block, 0, a);
-    else if (aligned && a.H % 64 == 0 && a.G > 0 && a.H / 64 == 16) RVX_LAUNCH(t, k_edge_attn_grouped<16>, grid, block, 0, a);
+    // RVX_EDGE_BATCH: edges whose rows are loaded together (1 or 4; same bits). 4 costs
+    // occupancy (159 vs 80 VGPRs at CPL 12) and lost: 356-365 vs 330-337 ms of edge kernel per
+    // 2M C4 step (scripts/exp_edge_batch.sh), so 1 stays the default.
+    const bool b4 = env_int("RVX_EDGE_BATCH", 1) == 4;
+    const bool grp = aligned && a.H % 64 == 0 && a.G > 0;
+    if (grp && a.H / 64 == 4) RVX_LAUNCH(t, (b4 ? k_edge_attn_grouped<4, 4> : k_edge_attn_grouped<4, 1>), grid, block, 0, a);
+    else if (grp && a.H / 64 == 8) RVX_LAUNCH(t, (b4 ? k_edge_attn_grouped<8, 4> : k_edge_attn_grouped<8, 1>), grid, block, 0, a);
+    else if (grp && a.H / 64 == 12) RVX_LAUNCH(t, (b4 ? k_edge_attn_grouped<12, 4> : k_edge_attn_grouped<12, 1>), grid, block, 0, a);
+    else if (grp && a.H / 64 == 16) RVX_LAUNCH(t, (b4 ? k_edge_attn_grouped<16, 4> : k_edge_attn_grouped<16, 1>), grid, block, 0, a);
     else RVX_LAUNCH(t, k_edge_attn_generic, grid, block, 0, a);
 }
 

@@ -1014,6 +1014,29 @@ def test_ruvector_layer_wide_gemm_bits(monkeypatch, hidden, heads, wide):
     assert_close(y1, O.rvl_forward_graph(W, x, rp, col, ew))
 
 
+@pytest.mark.parametrize("hidden,heads", [(256, 4), (512, 8), (768, 8), (1024, 8)])
+def test_ruvector_edge_batch_bits(monkeypatch, hidden, heads):
+    """K5 with four edges' K / V / M rows loaded together (RVX_EDGE_BATCH=4, opt-in)
+    writes the same bits as one edge at a time (1): degrees 0 to 13 (remainders), weighted
+    aggregation, CPL 4 / 8 / 12 / 16."""
+    n = 300
+    layer, W, _ = _layer_and_weights(hidden, hidden, heads, 0.1, seed=9)
+    x = O.fill_uniform(n * hidden, 14).reshape(n, hidden)
+    rng = np.random.default_rng(hidden)
+    degs = rng.integers(0, 14, n)
+    degs[::11] = 0
+    rp = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
+    col = rng.integers(0, n, int(rp[-1])).astype(np.int32)
+    ew = O.fill_uniform(int(rp[-1]), 15, 0.0, 1.0)
+    g = rv.Graph.from_csr(rp, col, ew)
+    monkeypatch.setenv("RVX_EDGE_BATCH", "1")
+    y0 = layer.forward_graph(x, g)
+    monkeypatch.setenv("RVX_EDGE_BATCH", "4")
+    y1 = layer.forward_graph(x, g)
+    assert np.array_equal(y0, y1)
+    assert_close(y1, O.rvl_forward_graph(W, x, rp, col, ew))
+
+
 def test_graphsage_norm_stream_bits(monkeypatch):
     """The opt-in third-stream row normalisation of the chunked pipeline
     (RVX_SAGE_NORM_STREAM=1) writes the same bits as the in-line pass."""
