@@ -1810,9 +1810,10 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
     // 3 waves 8 x 1 on 256 x 192 tiles (32 x 192 per wave: 96 accumulator registers),
     // 4 the same rows on 4-wave 128 x 192 blocks, 5 / 6 / 7 the software-pipelined K loop on
     // 256 x 192 / 256 x 256 / 4-wave 128 x 192 (two blocks per CU, each its own barriers).
-    // Standalone default 7: C4 stack GEMMs 345 vs 356 ms per 2M step with 2, the 10M
-    // GraphSAGE GEMM 77.2 vs 78.1 ms (scripts/exp_gemm_pipe.sh, profiles/r03_gemm_pipe_ab.txt).
-    const int wide_mode = env_int("RVX_GEMM_WIDE", persist > 0 ? 3 : 7);
+    // Standalone defaults: 7 for one operand (C4's K = 768 GEMMs: msg 26.9 vs 28.2 ms per 2M
+    // step with 6), 6 for two (the dual zr / h GEMMs 95.5 / 46.7 vs 99.8 / 48.0 ms with 7, the
+    // 10M GraphSAGE GEMM 72.8 vs 77.2 ms; scripts/exp_gemm_pipe.sh, profiles/r03_gemm_pipe_ab.txt).
+    const int wide_mode = env_int("RVX_GEMM_WIDE", persist > 0 ? 3 : (s1 ? 6 : 7));
     const bool same_strides = !s1 || (g.lda1 == g.lda0 && g.ldb1 == g.ldb0 && g.B1h_plane == g.B0h_plane);
     const bool wide = !ep.normalize_rows && (wide_mode >= 2 || (!ep.row_sumsq && !ep.a1_rowmul)) && wide_mode &&
                       same_strides && (int64_t)256 * g.lda0 * 4 < ((int64_t)1 << 31) &&
