@@ -350,23 +350,29 @@ constexpr int FKP = RVX_SCAN_FKP;           // list length per (query, split)
 constexpr int FCB = RVX_SCAN_FCB;           // candidate slots per query per merge round
 constexpr int F_NSTAGE = RVX_SCAN_NSTAGE;   // LDS-DMA ring: F_NSTAGE - 1 k-steps in flight across the barrier
 // Tile shapes. Waves 2 (rows) x WQ (queries); each wave FM x 2 accumulators of
-// 32 x 32 (rows x queries). Each wave DMAs 2 row pieces and 2 query pieces (16
-// rows x 64 B each) per k-step, so FR = FQ = 32 x waves.
-//   WIDE: 256 x 256, 8 waves, one block per CU (149 KB LDS) — half the L2->LDS
+// 32 x 32 (rows x queries). Each wave DMAs RP row pieces and QP query pieces (16
+// rows x 64 B each) per k-step.
+//   1 (wide): 256 x 256, 8 waves, one block per CU (149 KB LDS) — half the L2->LDS
 //         bytes per MFMA; taken for d >= 512 (10M x 768: 78.6 -> 64.3 ms per launch)
-//   else: 128 x 128, 4 waves, two blocks per CU (74.5 KB) — shorter tile
+//   0: 128 x 128, 4 waves, two blocks per CU (74.5 KB) — shorter tile
 //         epilogues for short rows (100k x 128: 3.8 vs 5.7 ms)
-template <bool WIDE>
+//   2 (tall): 256 rows x 128 queries, 4 waves of the wide tile's 128 x 64 shape, a
+//         2-stage ring, two blocks per CU (79.5 KB): each block's tile epilogue and
+//         barriers can run beside the other block's MFMAs (opt-in, RVX_SCAN_WIDE=2)
+template <int C>
 struct FCfg {
-    static constexpr int WQ = WIDE ? 4 : 2, FM = WIDE ? 4 : 2;
-    static constexpr int THREADS = 64 * 2 * WQ;
+    static constexpr int WQ = C == 1 ? 4 : 2, FM = C == 0 ? 2 : 4;
+    static constexpr int THREADS = 64 * 2 * WQ, NW = THREADS / 64;
     static constexpr int FQ = 64 * WQ, FR = 64 * FM;
+    static constexpr int NST = C == 2 ? 2 : F_NSTAGE;  // LDS-DMA ring stages
+    static constexpr int RP = FR / 16 / NW, QP = FQ / 16 / NW;  // DMA pieces per wave and k-step
     static constexpr int STAGE = (FR + FQ) * FK * 2;  // f16 rows then f16 queries, 64 B per row
     // + row constants (float4) and per-query {Qs, P} of the per-row-bound metrics
     // + per-query shared bound B_q and eps_q (group insertion, RVX_SCAN_GROUP_INSERT)
-    static constexpr int LDS = F_NSTAGE * STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 16 + FQ * 8 + FQ * 8;
-    static constexpr int BLOCKS = WIDE ? 1 : 2;
-    static_assert(FQ == FR && FR == 32 * THREADS / 64, "DMA pieces assume FR = FQ = 32 x waves");
+    static constexpr int LDS = NST * STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 16 + FQ * 8 + FQ * 8;
+    static constexpr int BLOCKS = C == 1 ? 1 : 2;
+    static_assert(RP * 16 * NW == FR && QP * 16 * NW == FQ && RP >= QP, "DMA pieces cover the stage");
+    static_assert(BLOCKS * LDS <= 160 * 1024, "resident blocks fit the CU's LDS");
 };
 constexpr int F_MAXE = 32;                  // rerank: list entries per lane (nsplit_total * FKP <= 64 * F_MAXE)
 
@@ -436,14 +442,15 @@ __device__ __forceinline__ float query_factor(float qinv, float qn) {
 
 __device__ __forceinline__ bool lt_vr(float v, int r, float bv, int br) { return v < bv || (v == bv && r < br); }
 
-template <int METRIC, bool WIDE, bool GROUP>
-__global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_scan_filter(FilterArgs a) {
-    using Cf = FCfg<WIDE>;
+template <int METRIC, int CFG, bool GROUP>
+__global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_filter(FilterArgs a) {
+    using Cf = FCfg<CFG>;
     constexpr int FQ = Cf::FQ, FR = Cf::FR, F_STAGE = Cf::STAGE, F_FM = Cf::FM, F_THREADS = Cf::THREADS;
+    constexpr int NST = Cf::NST, RP = Cf::RP, QP = Cf::QP, PCS = RP + QP;
     // per-row bounds (Poincaré, squared L2; see rows_to_f16_pr): the lists rank lower bounds
     constexpr bool PRB = METRIC == RVX_METRIC_POINCARE || METRIC == METRIC_L2SQ;
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
-    float* best_v = reinterpret_cast<float*>(fsm + F_NSTAGE * F_STAGE);  // [FQ][FKP] ascending (v, row)
+    float* best_v = reinterpret_cast<float*>(fsm + NST * F_STAGE);  // [FQ][FKP] ascending (v, row)
     int32_t* best_r = reinterpret_cast<int32_t*>(best_v + FQ * FKP);
     float* cand_v = reinterpret_cast<float*>(best_r + FQ * FKP);  // [FQ][FCB]
     int32_t* cand_r = reinterpret_cast<int32_t*>(cand_v + FQ * FCB);
@@ -512,11 +519,16 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     // LDS-DMA fill: 1 KB pieces of 16 rows x 64 B; lane -> (row, 16-B chunk)
     // with the chunk XOR-swizzled by (row >> 2) & 3 on the source address, so
     // the fragment reads below are bank-conflict free.
-    int prow[2], pchunk[2];
+    int prow[RP], pchunk[RP], qrow[QP], qchunk[QP];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        prow[j] = 16 * (2 * wave + j) + (lane >> 2);
+    for (int j = 0; j < RP; ++j) {
+        prow[j] = 16 * (RP * wave + j) + (lane >> 2);
         pchunk[j] = (lane & 3) ^ ((prow[j] >> 2) & 3);
+    }
+#pragma unroll
+    for (int j = 0; j < QP; ++j) {
+        qrow[j] = 16 * (QP * wave + j) + (lane >> 2);
+        qchunk[j] = (lane & 3) ^ ((qrow[j] >> 2) & 3);
     }
     const int nk = a.d / FK;
     const int64_t ntile = r_end > r_beg ? (r_end - r_beg + FR - 1) / FR : 0;
@@ -525,30 +537,36 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     // the end clamp to the last row), so a k-step's fill is address-add free:
     // SGPR base + k, VGPR offset (the tile offsets change once per tile)
     const char* qbase = reinterpret_cast<const char*>(a.qh + q0 * a.d);
-    uint32_t qoff[2];
+    uint32_t qoff[QP];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-        qoff[j] = (uint32_t)(((int64_t)min<int64_t>(prow[j], a.nq - 1 - q0) * a.d + pchunk[j] * 8) * 2);
-    struct TileSrc { const char* base; uint32_t off[2]; };
+    for (int j = 0; j < QP; ++j)
+        qoff[j] = (uint32_t)(((int64_t)min<int64_t>(qrow[j], a.nq - 1 - q0) * a.d + qchunk[j] * 8) * 2);
+    struct TileSrc { const char* base; uint32_t off[RP]; };
     auto tile_src = [&](int64_t t) {  // t = first row of a tile in [r_beg, r_end)
         TileSrc ts;
         ts.base = reinterpret_cast<const char*>(a.xh + (t - a.row0) * a.d);
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < RP; ++j)
             ts.off[j] = (uint32_t)(((int64_t)min<int64_t>(prow[j], r_end - 1 - t) * a.d + pchunk[j] * 8) * 2);
         return ts;
     };
+    // DMA piece j of a k-step: rows and queries alternate while both last, then rows
+    auto dma_piece = [&](const TileSrc& ts, int k0, unsigned char* dst, int j) {
+        const bool qry = j < 2 * QP && (j & 1);
+        const int h = j < 2 * QP ? j >> 1 : j - QP;
+        if (qry)
+            __builtin_amdgcn_global_load_lds((const void*)(qbase + k0 * 2 + qoff[h]),
+                                             (__attribute__((address_space(3))) void*)(dst + FR * 64 +
+                                                                                      (QP * wave + h) * 1024),
+                                             16, 0, 0);
+        else
+            __builtin_amdgcn_global_load_lds((const void*)(ts.base + k0 * 2 + ts.off[h]),
+                                             (__attribute__((address_space(3))) void*)(dst + (RP * wave + h) * 1024),
+                                             16, 0, 0);
+    };
     auto fill = [&](const TileSrc& ts, int k0, unsigned char* dst) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            __builtin_amdgcn_global_load_lds((const void*)(ts.base + k0 * 2 + ts.off[j]),
-                                             (__attribute__((address_space(3))) void*)(dst + (2 * wave + j) * 1024),
-                                             16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void*)(qbase + k0 * 2 + qoff[j]),
-                                             (__attribute__((address_space(3))) void*)(dst + FR * 64 +
-                                                                                      (2 * wave + j) * 1024),
-                                             16, 0, 0);
-        }
+        for (int j = 0; j < PCS; ++j) dma_piece(ts, k0, dst, j);
     };
     constexpr int WROWS = 32 * F_FM;  // rows per wave
     // LDS read offsets of fragment 0 per k-half; the XOR swizzle depends on
@@ -790,7 +808,7 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     TileSrc cur_src = tile_src(r_beg);
     TileSrc nxt_src = cur_src;
 #pragma unroll
-    for (int f = 0; f < F_NSTAGE - 1; ++f)
+    for (int f = 0; f < NST - 1; ++f)
         if (f < iters) fill(f < nk ? cur_src : tile_src(r_beg + (f / nk) * FR), (f % nk) * FK, fsm + f * F_STAGE);
 
     // One k-step: global step it, ring stage st. Every step issues one DMA group
@@ -801,37 +819,35 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
     // the step's first MFMAs rather than ahead of them: both waves of a SIMD
     // leave the barrier together, and a piece issued beside a running MFMA
     // overlaps it instead of idling the matrix core.
-    const int64_t later_c = min((int64_t)F_NSTAGE - 2, iters - 1);
+    const int64_t later_c = min((int64_t)NST - 2, iters - 1);
     auto kstep = [&](int64_t it, int64_t rt, int kt, int st) {
-        if (later_c >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (later_c == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        static_assert(PCS == 4 || PCS == 6, "vmcnt immediates below");
+        if constexpr (PCS == 4) {
+            if (later_c >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (later_c == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            if (later_c >= 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            else if (later_c == 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        const int fk = kt + F_NSTAGE - 1;
-        const int fst = st == 0 ? F_NSTAGE - 1 : st - 1;
+        const int fk = kt + NST - 1;
+        const int fst = st == 0 ? NST - 1 : st - 1;
         TileSrc fs = cur_src;
         int fk0 = 0;
-        if (it + F_NSTAGE - 1 < iters) {
+        if (it + NST - 1 < iters) {
             if (fk < nk) fk0 = fk * FK;
             else if (fk < 2 * nk) { fs = nxt_src; fk0 = (fk - nk) * FK; }
             else { fs = tile_src(rt + (fk / nk) * FR); fk0 = (fk % nk) * FK; }  // d < 64
         }
         unsigned char* fdst = fsm + fst * F_STAGE;
-        auto piece = [&](int j) {  // j: 0 rows/0, 1 queries/0, 2 rows/1, 3 queries/1
-            const int h = j >> 1;
+        auto piece = [&](int j) {  // j: 0 rows/0, 1 queries/0, 2 rows/1, 3 queries/1 (then rows)
 #ifdef RVX_ABLATE_DMA
             return;
 #endif
-            if (j & 1)
-                __builtin_amdgcn_global_load_lds((const void*)(qbase + fk0 * 2 + qoff[h]),
-                                                 (__attribute__((address_space(3))) void*)(fdst + FR * 64 +
-                                                                                          (2 * wave + h) * 1024),
-                                                 16, 0, 0);
-            else
-                __builtin_amdgcn_global_load_lds((const void*)(fs.base + fk0 * 2 + fs.off[h]),
-                                                 (__attribute__((address_space(3))) void*)(fdst + (2 * wave + h) * 1024),
-                                                 16, 0, 0);
+            dma_piece(fs, fk0, fdst, j);
         };
         const unsigned char* cur = fsm + st * F_STAGE;
 #pragma unroll
@@ -848,17 +864,18 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
 #pragma unroll
                 for (int fn = 0; fn < 2; ++fn) {
                     acc[fm][fn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[fm], bf[fn], acc[fm][fn], 0, 0, 0);
-                    const int m = 2 * fm + fn;  // piece j follows MFMA j * F_FM / 2 of the step
-                    if (ks == 0 && m % (F_FM / 2) == 0 && m / (F_FM / 2) < 4) {
+                    constexpr int PS = 2 * F_FM / PCS > 1 ? 2 * F_FM / PCS : 1;
+                    const int m = 2 * fm + fn;  // piece j follows MFMA j * PS of the step
+                    if (ks == 0 && m % PS == 0 && m / PS < PCS) {
                         __builtin_amdgcn_sched_barrier(0);
-                        piece(m / (F_FM / 2));
+                        piece(m / PS);
                         __builtin_amdgcn_sched_barrier(0);
                     }
                 }
         }
     };
 
-    const bool unrolled = nk % F_NSTAGE == 0;  // every tile starts on ring stage 0
+    const bool unrolled = nk % NST == 0;  // every tile starts on ring stage 0
     int st = 0;
     int64_t it = 0;
     for (int64_t rt = r_beg; rt < r_end; rt += FR) {
@@ -872,13 +889,13 @@ __global__ __launch_bounds__(FCfg<WIDE>::THREADS, FCfg<WIDE>::BLOCKS) void k_sca
         }
         if (rt + FR < r_end) nxt_src = tile_src(rt + FR);
         if (unrolled) {
-            for (int kt = 0; kt < nk; kt += F_NSTAGE, it += F_NSTAGE)
+            for (int kt = 0; kt < nk; kt += NST, it += NST)
 #pragma unroll
-                for (int u = 0; u < F_NSTAGE; ++u) kstep(it + u, rt, kt + u, u);
+                for (int u = 0; u < NST; ++u) kstep(it + u, rt, kt + u, u);
         } else {
             for (int kt = 0; kt < nk; ++kt, ++it) {
                 kstep(it, rt, kt, st);
-                st = st == F_NSTAGE - 1 ? 0 : st + 1;
+                st = st == NST - 1 ? 0 : st + 1;
             }
         }
 #ifdef RVX_ABLATE_EPI
@@ -1337,12 +1354,14 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     const bool prb = metric == RVX_METRIC_POINCARE || metric == METRIC_L2SQ;  // per-row bounds
     if (metric != RVX_METRIC_L2 && metric != RVX_METRIC_COSINE && metric != RVX_METRIC_DOT && !prb) return false;
     if (metric == RVX_METRIC_POINCARE && !(curv > 0.0f)) return false;
-    // tile shape: RVX_SCAN_WIDE 0/1 forces it (tests), else 256^2 for d >= 512
+    // tile shape: RVX_SCAN_WIDE 0/1/2 forces it (tests, A/B), else 256^2 for d >= 512
     const int wide_env = env_int("RVX_SCAN_WIDE", -1);
-    const bool wide = wide_env >= 0 ? wide_env != 0 : d >= 512;
-    const int FR = wide ? FCfg<true>::FR : FCfg<false>::FR, FQ = wide ? FCfg<true>::FQ : FCfg<false>::FQ;
-    const int F_LDS = wide ? FCfg<true>::LDS : FCfg<false>::LDS;
-    const int F_THREADS = wide ? FCfg<true>::THREADS : FCfg<false>::THREADS;
+    const int cfg = wide_env >= 0 && wide_env <= 2 ? wide_env : (d >= 512 ? 1 : 0);
+    const int FR = cfg == 1 ? FCfg<1>::FR : cfg == 2 ? FCfg<2>::FR : FCfg<0>::FR;
+    const int FQ = cfg == 1 ? FCfg<1>::FQ : cfg == 2 ? FCfg<2>::FQ : FCfg<0>::FQ;
+    const int F_LDS = cfg == 1 ? FCfg<1>::LDS : cfg == 2 ? FCfg<2>::LDS : FCfg<0>::LDS;
+    const int F_THREADS = cfg == 1 ? FCfg<1>::THREADS : cfg == 2 ? FCfg<2>::THREADS : FCfg<0>::THREADS;
+    const int F_BLOCKS = cfg == 1 ? FCfg<1>::BLOCKS : cfg == 2 ? FCfg<2>::BLOCKS : FCfg<0>::BLOCKS;
     // k > FKP: the lists stay FKP long (no single split proves a k-th value, so the
     // shared bound is off) and the rerank's completeness test decides per query
     if (d % FK != 0 || k > SCAN_MAX_K || n >= ((int64_t)1 << 31) - FR || nq <= 0 || n <= 0) return false;
@@ -1371,7 +1390,7 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     // tiles of a split whose still-empty lists admit most values (~8 tiles'
     // worth): 10M x 768 / 10k queries takes 32 splits per chunk (1280 blocks =
     // 5 full waves, not 640 = 2.5), 100k x 128 takes 6 (one wave).
-    const int64_t slots = (int64_t)device().num_cus * (wide ? 1 : 2);
+    const int64_t slots = (int64_t)device().num_cus * F_BLOCKS;
     const int64_t tiles = (chunk_rows + FR - 1) / FR;
     const int64_t s_max = std::max<int64_t>(1, std::min<int64_t>(max_splits / nchunks, tiles / 8));
     int64_t s_c = 1;
@@ -1410,10 +1429,12 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
 #define RVX_FILTER_ATTR(M, W) \
         RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<M, W, false>, hipFuncAttributeMaxDynamicSharedMemorySize, FCfg<W>::LDS)); \
         RVX_HIP(hipFuncSetAttribute((const void*)k_scan_filter<M, W, true>, hipFuncAttributeMaxDynamicSharedMemorySize, FCfg<W>::LDS))
-        RVX_FILTER_ATTR(RVX_METRIC_L2, true); RVX_FILTER_ATTR(RVX_METRIC_COSINE, true); RVX_FILTER_ATTR(RVX_METRIC_DOT, true);
-        RVX_FILTER_ATTR(RVX_METRIC_L2, false); RVX_FILTER_ATTR(RVX_METRIC_COSINE, false); RVX_FILTER_ATTR(RVX_METRIC_DOT, false);
-        RVX_FILTER_ATTR(RVX_METRIC_POINCARE, true); RVX_FILTER_ATTR(METRIC_L2SQ, true);
-        RVX_FILTER_ATTR(RVX_METRIC_POINCARE, false); RVX_FILTER_ATTR(METRIC_L2SQ, false);
+        RVX_FILTER_ATTR(RVX_METRIC_L2, 1); RVX_FILTER_ATTR(RVX_METRIC_COSINE, 1); RVX_FILTER_ATTR(RVX_METRIC_DOT, 1);
+        RVX_FILTER_ATTR(RVX_METRIC_L2, 0); RVX_FILTER_ATTR(RVX_METRIC_COSINE, 0); RVX_FILTER_ATTR(RVX_METRIC_DOT, 0);
+        RVX_FILTER_ATTR(RVX_METRIC_POINCARE, 1); RVX_FILTER_ATTR(METRIC_L2SQ, 1);
+        RVX_FILTER_ATTR(RVX_METRIC_POINCARE, 0); RVX_FILTER_ATTR(METRIC_L2SQ, 0);
+        RVX_FILTER_ATTR(RVX_METRIC_L2, 2); RVX_FILTER_ATTR(RVX_METRIC_COSINE, 2); RVX_FILTER_ATTR(RVX_METRIC_DOT, 2);
+        RVX_FILTER_ATTR(RVX_METRIC_POINCARE, 2); RVX_FILTER_ATTR(METRIC_L2SQ, 2);
 #undef RVX_FILTER_ATTR
         attr = true;
     }
@@ -1441,23 +1462,18 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
         // slot per lane (1, opt-in: spills ~100 B/lane in the 256-register wide tile and ran
         // 225 vs 173 ms at 10M x 768 / 10k, scripts/exp_scan_group.sh); read per call
         const bool group = env_int("RVX_SCAN_GROUP", 0) != 0;
-        if (wide) {
-            switch (metric) {
-                case RVX_METRIC_L2: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, true, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, true, false>), grid, blk, F_LDS, fa); break;
-                case RVX_METRIC_COSINE: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, true, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, true, false>), grid, blk, F_LDS, fa); break;
-                case RVX_METRIC_POINCARE: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, true, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, true, false>), grid, blk, F_LDS, fa); break;
-                case METRIC_L2SQ: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, true, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, true, false>), grid, blk, F_LDS, fa); break;
-                default: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, true, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, true, false>), grid, blk, F_LDS, fa); break;
-            }
-        } else {
-            switch (metric) {
-                case RVX_METRIC_L2: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, false, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, false, false>), grid, blk, F_LDS, fa); break;
-                case RVX_METRIC_COSINE: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, false, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, false, false>), grid, blk, F_LDS, fa); break;
-                case RVX_METRIC_POINCARE: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, false, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, false, false>), grid, blk, F_LDS, fa); break;
-                case METRIC_L2SQ: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, false, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, false, false>), grid, blk, F_LDS, fa); break;
-                default: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, false, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, false, false>), grid, blk, F_LDS, fa); break;
-            }
-        }
+#define RVX_FILTER_LAUNCH(C)                                                                                          \
+    switch (metric) {                                                                                                 \
+        case RVX_METRIC_L2: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, C, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, C, false>), grid, blk, F_LDS, fa); break; \
+        case RVX_METRIC_COSINE: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, C, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_COSINE, C, false>), grid, blk, F_LDS, fa); break; \
+        case RVX_METRIC_POINCARE: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, C, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_POINCARE, C, false>), grid, blk, F_LDS, fa); break; \
+        case METRIC_L2SQ: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, C, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, C, false>), grid, blk, F_LDS, fa); break; \
+        default: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, C, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, C, false>), grid, blk, F_LDS, fa); break; \
+    }
+        if (cfg == 1) { RVX_FILTER_LAUNCH(1) }
+        else if (cfg == 2) { RVX_FILTER_LAUNCH(2) }
+        else { RVX_FILTER_LAUNCH(0) }
+#undef RVX_FILTER_LAUNCH
     }
     RerankArgs ra{q, qnorm, qc, x, xnorm, nq, d, k, nsplit_total, part_v, part_r, max_bits, id_offset, out_d, out_i,
                   unsure};
