@@ -233,15 +233,21 @@ bool use_fold(const rvx_layer* l, bool exchange_multi) {
 }
 
 // Phase 1 for `rows` rows: M = w_msg(x) and (KV non-null) K|V = M·[W_k;W_v]^T.
-void phase1_dev(const rvx_layer* l, int64_t rows, const float* x, float* M, float* KV) {
+// Mamax (nullable): M's per-row max |m| slots (GemmEpilogue::row_absmax), so the GEMMs
+// reading M (K|V here, Q and z|r in phase 2) take their split-f16 row scales from it
+// instead of a pass over M (RVX_GEMM_AMAX=0 restores the passes; same scales, same bits).
+void phase1_dev(const rvx_layer* l, int64_t rows, const float* x, float* M, float* KV, float* Mamax) {
     const int64_t H = l->H;
     GemmEpilogue ep;
     ep.bias0 = l->d_bmsg.as<float>();
+    ep.row_absmax = Mamax;
     gemm_auto(rows, (int)H, l->d_wmsg.op(x, l->in), nullptr, ep, M, H, "gnn_gemm_msg");
     if (!KV) return;
     ep = GemmEpilogue();
     ep.bias0 = l->d_bqkv.as<float>() + H;
-    gemm_auto(rows, (int)(2 * H), l->d_wqkv.op(M, H, H), nullptr, ep, KV, 2 * H, "gnn_gemm_kv");
+    GemmOperand a = l->d_wqkv.op(M, H, H);
+    a.amax = Mamax;
+    gemm_auto(rows, (int)(2 * H), a, nullptr, ep, KV, 2 * H, "gnn_gemm_kv");
 }
 
 // Phase 2 for destination rows [0, rows_out) of rp: neighbours index the whole
@@ -250,7 +256,8 @@ void phase1_dev(const rvx_layer* l, int64_t rows, const float* x, float* M, floa
 // KV == nullptr: folded attention (qt / u tables of heads*H floats per row, so
 // the row chunk is capped at 128k rows).
 void phase2_dev(const rvx_layer* l, int64_t rows_out, const int64_t* rp, const int32_t* col, int64_t max_deg,
-                const float* w, int wmode, const float* M, const float* KV, int64_t self_off, float* y) {
+                const float* w, int wmode, const float* M, const float* KV, int64_t self_off, float* y,
+                const float* Mamax) {
     const int64_t H = l->H, heads = l->heads, hd = l->hd;
     const bool fold = KV == nullptr;
     int64_t CHUNK = std::max<int64_t>(4096, env_int("RVX_GNN_CHUNK_ROWS", 1 << 20));  // read per call
@@ -264,13 +271,22 @@ void phase2_dev(const rvx_layer* l, int64_t rows_out, const int64_t* rp, const i
     float* S3 = scratch_f32("rvl_s3", chunk * H);
     float* S4 = scratch_f32("rvl_s4", chunk * H);
     float* scores = scratch_f32("rvl_scores", std::max<int64_t>(chunk * max_deg, 1) * l->heads);
+    // per-row max |a| slots of the chunk's GEMM operands (COMB, AGG, r ⊙ h), written by
+    // their producers: the consumers' split-f16 row scales without a pass over the rows
+    const bool amx = Mamax && env_int("RVX_GEMM_AMAX", 1);
+    float* S4amax = amx ? scratch_f32("rvl_s4_amax", chunk * ROWSUMSQ_SLOTS) : nullptr;
+    float* S2amax = amx ? scratch_f32("rvl_s2_amax", chunk * ROWSUMSQ_SLOTS) : nullptr;
+    float* S3amax = amx ? scratch_f32("rvl_s3_amax", chunk * ROWSUMSQ_SLOTS) : nullptr;
     GemmEpilogue ep;
     for (int64_t r0 = 0; r0 < rows_out; r0 += chunk) {
         const int64_t rows = std::min(chunk, rows_out - r0);
         const float* Mc = M + (self_off + r0) * H;
+        const float* Mcamax = amx ? Mamax + (self_off + r0) * ROWSUMSQ_SLOTS : nullptr;
         ep = GemmEpilogue();
         ep.bias0 = l->d_bqkv.as<float>();
-        gemm_auto(rows, (int)H, l->d_wqkv.op(Mc, H, 0), nullptr, ep, Q, H, "gnn_gemm_q");
+        GemmOperand qa = l->d_wqkv.op(Mc, H, 0);
+        qa.amax = Mcamax;
+        gemm_auto(rows, (int)H, qa, nullptr, ep, Q, H, "gnn_gemm_q");
 
         if (fold) {
             // qt_h = W_k,h^T q_h (one GEMM per head), edges over m_j, att_h = W_v,h u_h + b_v,h
@@ -301,19 +317,25 @@ void phase2_dev(const rvx_layer* l, int64_t rows_out, const int64_t* rp, const i
         ep = GemmEpilogue();
         ep.bias0 = l->d_bo.as<float>();
         ep.addend = S3; ep.ld_addend = H;
+        ep.row_absmax = S4amax;
         gemm_auto(rows, (int)H, l->d_wo.op(S2, H), nullptr, ep, S4, H, "gnn_gemm_out");  // COMB
         ep = GemmEpilogue();
         ep.bias0 = l->d_bagg.as<float>();
-        gemm_auto(rows, (int)H, l->d_wagg.op(S4, H), nullptr, ep, S2, H, "gnn_gemm_agg");  // AGG
+        ep.row_absmax = S2amax;
+        GemmOperand aa = l->d_wagg.op(S4, H);
+        aa.amax = S4amax;
+        gemm_auto(rows, (int)H, aa, nullptr, ep, S2, H, "gnn_gemm_agg");  // AGG
         ep = GemmEpilogue();
         ep.epi = GEMM_EPI_SIGMOID; ep.bias0 = l->d_bwzr.as<float>(); ep.bias1 = l->d_buzr.as<float>();
-        const GemmOperand zr_b = l->d_uzr.op(Mc, H);
-        gemm_auto(rows, (int)(2 * H), l->d_wzr.op(S2, H), &zr_b, ep, S1, 2 * H, "gnn_gemm_zr");
-        mul_rows(S1 + H, 2 * H, Mc, S3, rows, (int)H);  // RH = r ⊙ h
+        GemmOperand zr_a = l->d_wzr.op(S2, H), zr_b = l->d_uzr.op(Mc, H);
+        zr_a.amax = S2amax; zr_b.amax = Mcamax;
+        gemm_auto(rows, (int)(2 * H), zr_a, &zr_b, ep, S1, 2 * H, "gnn_gemm_zr");
+        mul_rows(S1 + H, 2 * H, Mc, S3, rows, (int)H, S3amax);  // RH = r ⊙ h
         ep = GemmEpilogue();
         ep.epi = GEMM_EPI_TANH; ep.bias0 = l->d_bwh.as<float>(); ep.bias1 = l->d_buh.as<float>();
-        const GemmOperand h_b = l->d_uh.op(S3, H);
-        gemm_auto(rows, (int)H, l->d_wh.op(S2, H), &h_b, ep, S4, H, "gnn_gemm_h");  // HT
+        GemmOperand h_a = l->d_wh.op(S2, H), h_b = l->d_uh.op(S3, H);
+        h_a.amax = S2amax; h_b.amax = S3amax;
+        gemm_auto(rows, (int)H, h_a, &h_b, ep, S4, H, "gnn_gemm_h");  // HT
 
         FinishArgs fa;
         fa.n = rows; fa.H = (int)H; fa.rp = rp + r0; fa.m = Mc; fa.zr = S1; fa.ht = S4;
@@ -330,8 +352,9 @@ void forward_dev(const rvx_layer* l, int64_t n, const int64_t* rp, const int32_t
     const int64_t rows_out = n_out < 0 ? n : std::min(n_out, n);
     float* M = scratch_f32("rvl_m", n * H);
     float* KV = use_fold(l, false) ? nullptr : scratch_f32("rvl_kv", n * 2 * H);
-    phase1_dev(l, n, x, M, KV);
-    phase2_dev(l, rows_out, rp, col, max_deg, w, wmode, M, KV, 0, y);
+    float* Mamax = env_int("RVX_GEMM_AMAX", 1) ? scratch_f32("rvl_m_amax", n * ROWSUMSQ_SLOTS) : nullptr;
+    phase1_dev(l, n, x, M, KV, Mamax);
+    phase2_dev(l, rows_out, rp, col, max_deg, w, wmode, M, KV, 0, y, Mamax);
 }
 
 // RuvectorLayer::forward(nodes[i], table[ids[i*c .. i*c+c)], weights[i*c ..]) for
@@ -636,10 +659,14 @@ rvx_status rvx_gnn_forward_exchange(const rvx_layer* l, const rvx_graph* g, cons
         std::vector<TableRef> tables{{M, H}};
         if (KV) tables.push_back({KV, 2 * H});
         const float* x = x_full->mem.as<float>();
+        // row maxima of M for the owned rows only (phase 2 reads no peer row through a GEMM)
+        float* Mamax = env_int("RVX_GEMM_AMAX", 1) ? scratch_f32("rvl_m_amax", N * ROWSUMSQ_SLOTS) : nullptr;
         produce_and_exchange(comm, offsets, tables, [&](int64_t r0, int64_t rows) {
-            phase1_dev(l, rows, x + r0 * l->in, M + r0 * H, KV ? KV + r0 * 2 * H : nullptr);
+            phase1_dev(l, rows, x + r0 * l->in, M + r0 * H, KV ? KV + r0 * 2 * H : nullptr,
+                       Mamax ? Mamax + r0 * ROWSUMSQ_SLOTS : nullptr);
         });
-        phase2_dev(l, g->n, g->row_ptr, g->col, g->max_deg, g->w, 1, M, KV, o, y_full->mem.as<float>() + o * H);
+        phase2_dev(l, g->n, g->row_ptr, g->col, g->max_deg, g->w, 1, M, KV, o, y_full->mem.as<float>() + o * H,
+                   Mamax);
     });
 }
 

@@ -343,12 +343,41 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
             }
         }
     };
+    // Dynamic gather (RVX_SAGE_HELP, default on; read per call, tests cover both): chunk c's
+    // gather takes its rows from a counter, and the persistent GEMM of chunk c-1 joins it once
+    // its tiles are done — without it the GEMM's CU slots idle for the last ~third of every
+    // chunk while the gather runs on one block per CU. Same rows, same arithmetic, same bits.
+    const bool help = chunks > 1 && h2 && !h2p && !fused && split == 0 &&
+                      env_int("RVX_SAGE_GEMM_CAP", 2) > 0 && env_int("RVX_GEMM_WIDE", 3) == 3 &&
+                      agg_help_ok(l->in, x, agg, x + row_offset * l->in);
+    unsigned* counters = nullptr;
+    if (help) {
+        counters = (unsigned*)scratch_bytes("sage_help_counters", (int64_t)chunks * 64);
+        RVX_HIP(hipMemsetAsync(counters, 0, (size_t)chunks * 64, d.stream));
+        // (recorded into ev[chunks] below, before the gather stream's first launch)
+        RVX_HIP(hipEventRecord(ev[chunks], d.stream));
+        RVX_HIP(hipStreamWaitEvent(gath_s, ev[chunks], 0));
+    }
+    auto help_of = [&](int64_t rr0) {
+        AggHelp h{};
+        h.rp = g->row_ptr + rr0; h.col = g->col; h.n = std::min(step, n - rr0);
+        h.x = x; h.dim = l->in; h.agg = a;
+        h.out = agg + rr0 * l->in; h.self_x = x + (row_offset + rr0) * l->in; h.row_scale = scale + rr0;
+        h.row_mul = x_mul; h.self_mul = x_mul ? x_mul + row_offset + rr0 : nullptr;
+        h.counter = counters + (rr0 / step) * 16;
+        return h;
+    };
     StreamScope on_main(main_s);
     CuScope main_cu(main_cus);
     int c = 0;
     for (int64_t r0 = 0; r0 < n; r0 += step, ++c) {
         const int64_t rows = std::min(step, n - r0);
-        if (chunks > 1) {
+        if (chunks > 1 && help) {
+            StreamScope on_aux(gath_s);
+            aggregate_rows_help(help_of(r0), "sage_aggregate");
+            RVX_HIP(hipEventRecord(ev[c], gath_s));
+            RVX_HIP(hipStreamWaitEvent(main_s, ev[c], 0));
+        } else if (chunks > 1) {
             StreamScope on_aux(gath_s);
             CuScope aux_cu(gath_cus);
             aggregate_rows(g->row_ptr + r0, g->col, nullptr, rows, x, l->in, a, /*empty_fill zeros*/ 0, 0,
@@ -386,6 +415,11 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         epn.normalize_rows = h2 && l->normalize && !y_inv && gemm_h2_rownorm_ok(l->out, y, l->out);
         epn.a1_rowmul = x_mul ? x_mul + row_offset + r0 : nullptr;
         epn.row_sumsq = y_inv ? ssq + r0 * ntiles : nullptr;
+        AggHelp next{};
+        if (help && r0 + step < n && env_int("RVX_SAGE_HELP", 1) != 2) {  // 2: dynamic gather alone
+            next = help_of(r0 + step);
+            epn.help = &next;
+        }
         int coltiles = 0;
         if (h2)
             coltiles = gemm_nt_h2(rows, l->out, s0, l->wn_h2.as<_Float16>(), &s1, l->ws_h2.as<_Float16>(), scale + r0,

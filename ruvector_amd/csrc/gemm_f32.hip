@@ -24,6 +24,7 @@
 #include "common.hpp"
 #include "graph.hpp"
 #include "kernels.hpp"
+#include "agg_row.hpp"
 
 namespace rvx {
 
@@ -59,7 +60,26 @@ struct GemmArgs {
     // deferred normalisation (h2g): per-row partial sums of squares per column tile, and the
     // phase-1 operand's per-row multiplier
     float* row_sumsq; const float* a1_rowmul;
+    // per-row max |v| per column tile for the next GEMM's row scale (h2g, h2w with WN = 1)
+    float* row_absmax;
+    // gemm_nt_h2w<..., HELP>: the next row chunk's gather, helped once the tiles run out
+    AggHelp help;
 };
+
+// One row's max |v| over this column tile: lanes lr = 0..31 of a half-wave hold the row's
+// columns; lane 0 writes slot tn, and the last column tile zeroes the slots past the tile
+// count so a consumer reduces all ROWSUMSQ_SLOTS. fmaxf ignores NaN as k_row_scale_h2 does,
+// and max is order-free, so the scale equals the one a pass over C computes.
+__device__ __forceinline__ void row_absmax_store(const GemmArgs& g, int64_t row, int tn, int lr, float amx) {
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) amx = fmaxf(amx, __shfl_xor(amx, off));
+    if (lr == 0 && row < g.M) {
+        float* p = g.row_absmax + row * ROWSUMSQ_SLOTS;
+        p[tn] = amx;
+        if (tn == g.tiles_n - 1)
+            for (int t = tn + 1; t < ROWSUMSQ_SLOTS; ++t) p[t] = 0.0f;
+    }
+}
 
 __device__ __forceinline__ float epi_apply(int epi, float v) {
     if (epi == GEMM_EPI_RELU) return fmaxf(v, 0.0f);
@@ -1276,7 +1296,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
 #ifndef H2W_RING
 #define H2W_RING 4
 #endif
-template <bool DUAL, int WN, int BN, int NW, bool PIPE = false>
+template <bool DUAL, int WN, int BN, int NW, bool PIPE = false, bool AMX = false>
 __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgid) {
     constexpr int BM = 32 * NW;        // 256 rows with 8 waves, 128 with 4
     constexpr int WMW = NW / WN;                // waves along M
@@ -1562,7 +1582,7 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
         for (int e = 0; e < 16; ++e) {
             const int64_t row = m0 + wm * (32 * RB) + rb * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
             const float rinv = 1.0f / g.a_scale[std::min<int64_t>(row, g.M - 1)];  // unconditional: no per-load wait
-            float ssq = 0.0f;
+            float ssq = 0.0f, amx = 0.0f;
 #pragma unroll
             for (int nb = 0; nb < NB; ++nb) {
                 const int col = n0 + wn * (32 * NB) + nb * 32 + lr;
@@ -1574,9 +1594,11 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
                     v = epi_apply(epi, v);
                     g.C[row * g.ldc + col] = v;
                     ssq = __fadd_rn(ssq, __fmul_rn(v, v));
+                    if constexpr (AMX) amx = fmaxf(amx, fabsf(v));
                 }
             }
             if constexpr (WN == 1) {
+                if constexpr (AMX) row_absmax_store(g, row, tn, lr, amx);
                 if (g.row_sumsq) {
 #pragma unroll
                     for (int off = 16; off > 0; off >>= 1) ssq += __shfl_xor(ssq, off);
@@ -1592,7 +1614,10 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
 // beside the overlapped gather a persistent block keeps its LDS and registers.
 // The tile ticket is passed through the first word of the (then idle) stage memory, so two
 // 80 KB 4-wave blocks fit one CU's 160 KB.
-template <bool DUAL, int WN, int BN, int NW = 8, bool PIPE = false>
+// HELP: after the last tile every wave takes destination rows of the next chunk's gather
+// (g.help, aggrow::agg_help_run) — the GEMM's CU slots would otherwise idle beside the gather's
+// one block per CU until the chunk's gather ends.
+template <bool DUAL, int WN, int BN, int NW = 8, bool PIPE = false, bool HELP = false, bool AMX = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt_h2w(GemmArgs g, int epi) {
     if (g.queue) {
         extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
@@ -1605,13 +1630,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt
             const int64_t t = *s_t;
             __syncthreads();  // every wave holds t before the tile's DMA overwrites the word
             if (t >= cnt) break;
-            h2w_tile<DUAL, WN, BN, NW, PIPE>(g, epi, first + t);
+            h2w_tile<DUAL, WN, BN, NW, PIPE, AMX>(g, epi, first + t);
             __syncthreads();  // LDS stages and s_t are reused by the next tile
         }
+        if constexpr (HELP) aggrow::agg_help_run(g.help);
         return;
     }
     const int64_t nwg = g.nblocks, bid = blockIdx.x;
-    h2w_tile<DUAL, WN, BN, NW, PIPE>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
+    h2w_tile<DUAL, WN, BN, NW, PIPE, AMX>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
+    if constexpr (HELP) aggrow::agg_help_run(g.help);
 }
 
 // B rows n of one or two [N][K] matrices: common scale t_n, f16 planes of each
@@ -1833,6 +1860,10 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 256, 8, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 256, 8, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 8, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 8, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 256, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 256, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
@@ -1842,6 +1873,8 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 4, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 4, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
             wattr = true;
         }
         g.tiles_n = (N + wbn - 1) / wbn;
@@ -1858,10 +1891,20 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
         } else {
             wgrid = g.nblocks;
         }
+        // row maxima from the epilogue on the standalone defaults (6, 7); other tiles: a pass
+        g.row_absmax = (ep.row_absmax && (wide_mode == 6 || wide_mode == 7) && g.tiles_n <= ROWSUMSQ_SLOTS)
+                           ? ep.row_absmax : nullptr;
+        const bool amx = g.row_absmax != nullptr;
         const dim3 wg((unsigned)wgrid), wb(wide_mode == 4 || wide_mode == 7 ? 256 : 512);
         // RVX_GEMM_WIDE=1: waves 2 (M) x 4 (N), 128 x 64 each; 2: waves 8 x 1, 32 x 256 each
         // (A converted once per row instead of by four waves)
-        if (wide_mode == 7) {
+        if (wide_mode == 7 && amx) {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 4, true, false, true>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 4, true, false, true>), wg, wb, wlds, g, ep.epi);
+        } else if (wide_mode == 6 && amx) {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 256, 8, true, false, true>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 256, 8, true, false, true>), wg, wb, wlds, g, ep.epi);
+        } else if (wide_mode == 7) {
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 4, true>), wg, wb, wlds, g, ep.epi);
             else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 4, true>), wg, wb, wlds, g, ep.epi);
         } else if (wide_mode == 6) {
@@ -1873,6 +1916,10 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
         } else if (wide_mode == 4) {
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 4>), wg, wb, wlds, g, ep.epi);
             else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 4>), wg, wb, wlds, g, ep.epi);
+        } else if (wide_mode == 3 && ep.help && ep.help->n > 0) {
+            g.help = *ep.help;
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 8, false, true>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 8, false, true>), wg, wb, wlds, g, ep.epi);
         } else if (wide_mode == 3) {
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192>), wg, wb, wlds, g, ep.epi);
             else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192>), wg, wb, wlds, g, ep.epi);
@@ -1883,6 +1930,7 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 4, 256>), wg, wb, wlds, g, ep.epi);
             else RVX_LAUNCH(t, (gemm_nt_h2w<false, 4, 256>), wg, wb, wlds, g, ep.epi);
         }
+        if (ep.row_absmax && !g.row_absmax) row_absmax_pass(C, ldc, M, N, ep.row_absmax);
         return g.tiles_n;
     }
     // persistent grid of `cap` blocks per CU (a multiple of 8 blocks, so a block
@@ -1907,8 +1955,10 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
         g.row_tickets = (unsigned*)scratch_bytes("gemm_h2_row_tickets", tiles_m * 4);
         RVX_HIP(hipMemsetAsync(g.row_tickets, 0, (size_t)tiles_m * 4, stream()));
     }
+    g.row_absmax = nullptr;  // h2g: row maxima by a pass over C
     if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
     else RVX_LAUNCH(t, gemm_nt_h2g<false>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
+    if (ep.row_absmax && !g.row_absmax) row_absmax_pass(C, ldc, M, N, ep.row_absmax);
     return g.tiles_n;
 }
 
@@ -1998,6 +2048,46 @@ __global__ __launch_bounds__(256) void k_row_scale_h2(const float* __restrict__ 
 }
 }  // namespace
 
+namespace {
+// Row scales from the producers' per-row partial maxima (GemmOperand::amax): one thread
+// per row, max over both operands' ROWSUMSQ_SLOTS slots -> h2_scale_dev, the value
+// k_row_scale_h2 computes from the rows themselves.
+__global__ __launch_bounds__(256) void k_row_scale_amax(const float* __restrict__ a0, const float* __restrict__ a1,
+                                                       int64_t M, float* __restrict__ scale) {
+    const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (row >= M) return;
+    static_assert(ROWSUMSQ_SLOTS == 8, "two float4 per row");
+    const float4* p = reinterpret_cast<const float4*>(a0 + row * ROWSUMSQ_SLOTS);
+    float4 u = p[0], v = p[1];
+    float m = fmaxf(fmaxf(fmaxf(u.x, u.y), fmaxf(u.z, u.w)), fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+    if (a1) {
+        p = reinterpret_cast<const float4*>(a1 + row * ROWSUMSQ_SLOTS);
+        u = p[0]; v = p[1];
+        m = fmaxf(m, fmaxf(fmaxf(fmaxf(u.x, u.y), fmaxf(u.z, u.w)), fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w))));
+    }
+    scale[row] = h2_scale_dev(fmaxf(m, 0.0f));
+}
+
+// Fallback for GEMM paths without the epilogue form: one wave per row of C, max |v| into
+// slot 0, the other slots 0.
+__global__ __launch_bounds__(256) void k_row_absmax(const float* __restrict__ C, int64_t ldc, int64_t M, int N,
+                                                   float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    float m = 0.0f;
+    for (int k = lane; k < N; k += 64) m = fmaxf(m, fabsf(C[row * ldc + k]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane < ROWSUMSQ_SLOTS) out[row * ROWSUMSQ_SLOTS + lane] = lane == 0 ? m : 0.0f;
+}
+}  // namespace
+
+void row_absmax_pass(const float* C, int64_t ldc, int64_t M, int N, float* out) {
+    if (M <= 0) return;
+    RVX_LAUNCH("gemm_row_absmax", k_row_absmax, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, C, ldc, M, N, out);
+}
+
 void row_scale_h2(const float* A0, int64_t lda0, int K0, const float* A1, int64_t lda1, int K1, int64_t M,
                   float* scale) {
     if (M <= 0) return;
@@ -2010,11 +2100,16 @@ void gemm_auto(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, c
     const bool planes = s0.Bh && s0.b_inv && (!s1 || (s1->Bh && s1->b_inv == s0.b_inv));
     if (planes && env_int("RVX_GNN_H2", 1) && gemm_h2_ok(M, N, s0, s1)) {  // read per call: tests cover both
         float* scale = scratch_f32("gemm_auto_scale", M);
-        row_scale_h2(s0.A, s0.lda, s0.K, s1 ? s1->A : nullptr, s1 ? s1->lda : 0, s1 ? s1->K : 0, M, scale);
+        if (s0.amax && (!s1 || s1->amax) && env_int("RVX_GEMM_AMAX", 1))  // read per call: tests cover both
+            RVX_LAUNCH("gemm_row_scale_amax", k_row_scale_amax, dim3((unsigned)((M + 255) / 256)), dim3(256), 0,
+                       s0.amax, s1 ? s1->amax : nullptr, M, scale);
+        else
+            row_scale_h2(s0.A, s0.lda, s0.K, s1 ? s1->A : nullptr, s1 ? s1->lda : 0, s1 ? s1->K : 0, M, scale);
         gemm_nt_h2(M, N, s0, s0.Bh, s1, s1 ? s1->Bh : nullptr, scale, s0.b_inv, ep, C, ldc, tag);
         return;
     }
     gemm_nt(M, N, s0, s1, ep, C, ldc, tag);
+    if (ep.row_absmax) row_absmax_pass(C, ldc, M, N, ep.row_absmax);
 }
 
 void split_h2_rows(const float* B0, const float* B1, int N, int K, _Float16* P0, _Float16* P1, float* inv) {

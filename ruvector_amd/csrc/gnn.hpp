@@ -64,7 +64,8 @@ struct EdgeFoldArgs {
 bool edge_fold_ok(int H, int heads);
 void edge_attention_fold(const EdgeFoldArgs& a);
 int edge_group_lanes(int H, int heads);  // 0 when the grouped kernel does not apply
-void mul_rows(const float* r, int64_t ldr, const float* h, float* out, int64_t n, int H);
+// out = r ⊙ h per row; amax (optional): the rows' max |out| as GemmOperand::amax slots
+void mul_rows(const float* r, int64_t ldr, const float* h, float* out, int64_t n, int H, float* amax = nullptr);
 void gru_finish(const FinishArgs& a);
 
 // Star tables for batched per-node calls (RuvectorLayer::forward(node,

@@ -18,45 +18,14 @@
 #include "common.hpp"
 #include "graph.hpp"
 #include "kernels.hpp"
+#include "agg_row.hpp"
 
 namespace rvx {
 namespace {
 
 constexpr int ROWS_PER_BLOCK = 4;  // 4 waves
 
-template <int AGG>
-__device__ __forceinline__ float4 agg_op(float4 a, float4 v) {
-    if (AGG == AGG_MAX) return make_float4(fmaxf(a.x, v.x), fmaxf(a.y, v.y), fmaxf(a.z, v.z), fmaxf(a.w, v.w));
-    return make_float4(a.x + v.x, a.y + v.y, a.z + v.z, a.w + v.w);
-}
-__device__ __forceinline__ float4 scale4(float4 v, float w) { return make_float4(v.x * w, v.y * w, v.z * w, v.w * w); }
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-
-// v*t as f16 hi = rn(v*t) at p[0..3] and lo = rn(v*t - hi) at p[pstride..]
-__device__ __forceinline__ void split_store4(float4 v, float t, _Float16* p, int64_t pstride) {
-    const float x[4] = {v.x * t, v.y * t, v.z * t, v.w * t};
-    f16x4 hi, lo;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        hi[i] = (_Float16)x[i];
-        lo[i] = (_Float16)(x[i] - (float)hi[i]);
-    }
-    *reinterpret_cast<f16x4*>(p) = hi;
-    *reinterpret_cast<f16x4*>(p + pstride) = lo;
-}
-// Gathered rows are touched once per edge at random, so they never hit in L2
-// on a large table; NT loads keep them from evicting the working set of a
-// GEMM running beside the gather.
-template <bool NT>
-__device__ __forceinline__ float4 ld_row4(const float* p) {
-    if (NT) {
-        const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
-        return make_float4(v.x, v.y, v.z, v.w);
-    }
-    return *reinterpret_cast<const float4*>(p);
-}
+using namespace aggrow;
 
 // NV = float4 slots per lane (dim <= 256*NV; dim % 4 == 0); U = neighbour
 // rows in flight per wave (more when the grid is capped to few waves per CU).
@@ -79,124 +48,8 @@ __global__ __launch_bounds__(256) void k_aggregate_vec(const int64_t* __restrict
     // leaves CU slots to a concurrently running GEMM
     for (int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6); row < n;
          row += (int64_t)gridDim.x * ROWS_PER_BLOCK) {
-    const int64_t beg = rp[row], end = rp[row + 1];
-    const int cnt_total = (int)(end - beg);
-
-    const float init = (AGG == AGG_MAX) ? -INFINITY : 0.0f;
-    float4 acc[NV];
-#pragma unroll
-    for (int j = 0; j < NV; ++j) acc[j] = make_float4(init, init, init, init);
-    bool active[NV];
-#pragma unroll
-    for (int j = 0; j < NV; ++j) active[j] = (4 * lane + 256 * j) < dim;
-
-    for (int64_t e0 = beg; e0 < end; e0 += 64) {
-        const int cnt = (int)min<int64_t>(64, end - e0);
-        const int my_c = lane < cnt ? col[e0 + lane] : 0;
-        const float my_w = (W && lane < cnt) ? wts[e0 + lane] : 1.0f;
-        int t = 0;
-        // deferred normalisation: one multiplier per gathered row (wave-uniform id)
-        const float my_m = (row_mul && lane < cnt) ? row_mul[my_c] : 1.0f;
-        for (; t + U <= cnt; t += U) {
-            float4 v[U][NV];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int c = __builtin_amdgcn_readlane(my_c, t + u);
-                const float* src = x + (int64_t)c * dim + 4 * lane;
-#pragma unroll
-                for (int j = 0; j < NV; ++j)
-                    v[u][j] = active[j] ? ld_row4<NT>(src + 256 * j) : make_float4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                float wu = 1.0f;
-                if (W) wu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), t + u));
-                if (row_mul) {
-                    const float mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_m), t + u));
-#pragma unroll
-                    for (int j = 0; j < NV; ++j) v[u][j] = scale4(v[u][j], mu);
-                }
-#pragma unroll
-                for (int j = 0; j < NV; ++j) acc[j] = agg_op<AGG>(acc[j], W ? scale4(v[u][j], wu) : v[u][j]);
-            }
-        }
-        for (; t < cnt; ++t) {
-            const int c = __builtin_amdgcn_readlane(my_c, t);
-            const float* src = x + (int64_t)c * dim + 4 * lane;
-            float wu = 1.0f;
-            if (W) wu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), t));
-            const float mu = row_mul ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_m), t)) : 1.0f;
-#pragma unroll
-            for (int j = 0; j < NV; ++j) {
-                float4 v = active[j] ? ld_row4<NT>(src + 256 * j) : make_float4(0, 0, 0, 0);
-                if (row_mul) v = scale4(v, mu);
-                acc[j] = agg_op<AGG>(acc[j], W ? scale4(v, wu) : v);
-            }
-        }
-    }
-
-    float* dst = out + row * dim + 4 * lane;
-    if (cnt_total > 0) {
-        if (AGG == AGG_MEAN) {
-            const float cntf = (float)cnt_total;  // mean_aggregate: x / count (aggregators.rs:64-67)
-#pragma unroll
-            for (int j = 0; j < NV; ++j)
-                acc[j] = make_float4(acc[j].x / cntf, acc[j].y / cntf, acc[j].z / cntf, acc[j].w / cntf);
-        }
-        if (post_scale == 1) {  // GCN: aggregated *= 1/sqrt(degree) (gcn.rs:127-134)
-            const float nrm = 1.0f / sqrtf((float)cnt_total);
-#pragma unroll
-            for (int j = 0; j < NV; ++j) acc[j] = scale4(acc[j], nrm);
-        }
-    }
-    if (row_scale) {  // split-f16 GEMM operand scale over this row's aggregate and self rows
-        float m = 0.0f;
-        const float* sp = self_x + row * dim + 4 * lane;
-        const float smul = self_mul ? self_mul[row] : 1.0f;
-        float4 sv[NV];
-#pragma unroll
-        for (int j = 0; j < NV; ++j)
-            if (active[j]) {
-                float4 v = *reinterpret_cast<const float4*>(sp + 256 * j);
-                if (self_mul) v = scale4(v, smul);
-                sv[j] = v;
-                m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-                if (cnt_total > 0)
-                    m = fmaxf(m, fmaxf(fmaxf(fabsf(acc[j].x), fabsf(acc[j].y)), fmaxf(fabsf(acc[j].z), fabsf(acc[j].w))));
-            }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-        const float t = h2_scale_dev(m);
-        if (lane == 0) row_scale[row] = t;
-        if (planes) {
-            // the GEMM operand itself: [aggregate | self] * t split into two f16
-            // planes, rounding exactly as the in-GEMM split (split_h2_pair)
-            _Float16* p0 = planes + row * 2 * dim + 4 * lane;
-#pragma unroll
-            for (int j = 0; j < NV; ++j)
-                if (active[j]) {
-                    const float4 a = cnt_total > 0 ? acc[j] : make_float4(0, 0, 0, 0);
-                    split_store4(a, t, p0 + 256 * j, pstride);
-                    split_store4(sv[j], t, p0 + dim + 256 * j, pstride);
-                }
-            continue;
-        }
-    }
-    if (cnt_total == 0) {
-        const float* self = x + row * dim + 4 * lane;
-#pragma unroll
-        for (int j = 0; j < NV; ++j)
-            if (active[j])
-                *reinterpret_cast<float4*>(dst + 256 * j) =
-                    empty_fill == 1 ? *reinterpret_cast<const float4*>(self + 256 * j) : make_float4(0, 0, 0, 0);
-        continue;
-    }
-#ifdef RVX_AB_NO_AGG_WRITE  // timing-only ablation build (scripts/exp_sage_ablate.sh): results wrong
-    if (NT && acc[0].x == 12345.0f)
-#endif
-#pragma unroll
-    for (int j = 0; j < NV; ++j)
-        if (active[j]) *reinterpret_cast<float4*>(dst + 256 * j) = acc[j];
+    aggrow::agg_vec_row<NV, AGG, W, U, NT>(rp, col, wts, x, dim, empty_fill, post_scale, out, self_x, row_scale, planes,
+                                           pstride, row_mul, self_mul, row, lane);
     }
 }
 
@@ -415,6 +268,25 @@ void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, 
                         : launch_agg<AGG_MAX, false>(t, row_ptr, col, w, n, x, dim, empty_fill, post_scale, out, cap, deep, nt, self_x, row_scale, planes, plane_stride, row_mul, self_mul); break;
         default: fail(RVX_ERR_INVALID_PARAMETER, "unknown aggregator");
     }
+}
+
+namespace {
+__global__ __launch_bounds__(256) void k_aggregate_help(AggHelp h) { aggrow::agg_help_run(h); }
+}  // namespace
+
+bool agg_help_ok(int dim, const float* x, const float* out, const float* self_x) {
+    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    return env_int("RVX_SAGE_HELP", 1) && g_agg_overlap_unroll >= 8 && g_agg_nt && !env_int("RVX_AGG_ROLL", 0) &&
+           dim > 0 && dim % 4 == 0 && dim <= 768 && al(x) && al(out) && self_x && al(self_x);
+}
+
+void aggregate_rows_help(const AggHelp& h, const char* tag) {
+    if (h.n <= 0) return;
+    RVX_REQUIRE(h.counter && h.agg >= AGG_SUM && h.agg <= AGG_MAX && h.dim % 4 == 0 && h.dim <= 768,
+                RVX_ERR_INVALID_SHAPE, "dynamic gather: bad arguments");
+    const int64_t blocks = std::min<int64_t>((h.n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK,
+                                             (int64_t)std::max(1, g_agg_overlap_cap) * active_cus());
+    RVX_LAUNCH(tag ? tag : "aggregate", k_aggregate_help, dim3((unsigned)blocks), dim3(256), 0, h);
 }
 
 }  // namespace rvx

@@ -16,6 +16,7 @@
 // Traffic per edge: 3*H floats (k_j, v_j, m_j rows) + 4 B index (+4 B weight).
 #include "common.hpp"
 #include "gnn.hpp"
+#include "kernels.hpp"
 
 namespace rvx {
 namespace {
@@ -358,6 +359,26 @@ __global__ void k_mul(const float* r, int64_t ldr, const float* h, float* out, i
     out[idx] = r[i * ldr + c] * h[idx];
 }
 
+// The same products one wave per row, also writing the row's max |out| (slot 0 of
+// ROWSUMSQ_SLOTS, the others 0) for the next split-f16 GEMM's row scale.
+__global__ __launch_bounds__(256) void k_mul_amax(const float* __restrict__ r, int64_t ldr, const float* __restrict__ h,
+                                                 float* __restrict__ out, int64_t n, int H, float* __restrict__ amax) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= n) return;
+    float m = 0.0f;
+    for (int c = 4 * lane; c < H; c += 256) {
+        const float4 a = *reinterpret_cast<const float4*>(r + i * ldr + c);
+        const float4 b = *reinterpret_cast<const float4*>(h + i * (int64_t)H + c);
+        const float4 o = make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
+        *reinterpret_cast<float4*>(out + i * (int64_t)H + c) = o;
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w))));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane < ROWSUMSQ_SLOTS) amax[i * ROWSUMSQ_SLOTS + lane] = lane == 0 ? m : 0.0f;
+}
+
 // (1-z)⊙h + z⊙h~, ×(1-dropout), LayerNorm; deg==0 rows: LayerNorm(m_i).
 __global__ __launch_bounds__(256) void k_gru_finish(FinishArgs a) {
     const int lane = threadIdx.x & 63;
@@ -447,10 +468,16 @@ int edge_group_lanes(int H, int heads) {
     return g;
 }
 
-void mul_rows(const float* r, int64_t ldr, const float* h, float* out, int64_t n, int H) {
+void mul_rows(const float* r, int64_t ldr, const float* h, float* out, int64_t n, int H, float* amax) {
     const int64_t total = n * H;
     if (total <= 0) return;
+    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (amax && H % 4 == 0 && ldr % 4 == 0 && al(r) && al(h) && al(out)) {
+        RVX_LAUNCH("gnn_gate_mul", k_mul_amax, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, r, ldr, h, out, n, H, amax);
+        return;
+    }
     RVX_LAUNCH("gnn_gate_mul", k_mul, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, r, ldr, h, out, n, H);
+    if (amax) row_absmax_pass(out, H, n, H, amax);
 }
 
 void gru_finish(const FinishArgs& a) {

@@ -21,6 +21,22 @@ struct GemmOperand {
     const _Float16* Bh = nullptr;
     int64_t Bh_plane = 0;
     const float* b_inv = nullptr;
+    // optional per-row max |a| of this operand, written by its producer (GemmEpilogue
+    // row_absmax, mul_rows): [M][ROWSUMSQ_SLOTS] partial maxima (unused slots 0) that
+    // gemm_auto turns into the split-f16 row scales instead of re-reading A
+    const float* amax = nullptr;
+};
+// One row chunk of the overlapped GraphSAGE gather in its dynamic form (aggregate_rows_help):
+// destination rows are taken from *counter (zeroed before either kernel starts), both by the
+// chunk's own gather kernel and by the previous chunk's persistent GEMM once its tiles are done
+// (GemmEpilogue::help). Arguments as aggregate_rows with the vector path's overlapped settings
+// (no edge weights, zero-filled empty rows, no post-scale, no planes).
+struct AggHelp {
+    const int64_t* rp; const int32_t* col; int64_t n;
+    const float* x; int dim; int agg;
+    float* out; const float* self_x; float* row_scale;
+    const float* row_mul; const float* self_mul;
+    unsigned* counter;
 };
 // Epilogue: C = epi(alpha * acc + bias0 + bias1 + addend[row][col])
 constexpr int ROWSUMSQ_SLOTS = 8;  // per-row partial sums of squares (column tiles >= 128 wide, N <= 1024)
@@ -41,6 +57,13 @@ struct GemmEpilogue {
     // layer's 1 / |y|)
     float* row_sumsq = nullptr;
     const float* a1_rowmul = nullptr;
+    // gemm_auto / gemm_nt_h2: row_absmax[row * ROWSUMSQ_SLOTS + t] receives max |v| over
+    // output column tile t of the row (v as stored), every other slot 0 — the next GEMM's
+    // row scale from the producer (GemmOperand::amax) instead of a pass over C
+    float* row_absmax = nullptr;
+    // gemm_nt_h2, persistent 256 x 192 tiles only: after the tile queue runs dry the blocks
+    // take rows of this gather (the next row chunk's) — see AggHelp
+    const AggHelp* help = nullptr;
 };
 // C[M][N] = epilogue(A0·B0^T [+ A1·B1^T])
 void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, const GemmEpilogue& ep, float* C,
@@ -72,6 +95,9 @@ void gemm_nt_h2p(int64_t M, int N, const _Float16* Ah, int64_t lda, int64_t a_pl
 void gemm_auto(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, const GemmEpilogue& ep, float* C,
                int64_t ldc, const char* tag);
 // scale[r] = power of two putting max(|A0 row r|, |A1 row r|) in [2^14, 2^15).
+// max |C[row][:]| into row_absmax slot 0 (slots 1.. zeroed): GemmEpilogue::row_absmax for
+// GEMM paths whose epilogue does not write it
+void row_absmax_pass(const float* C, int64_t ldc, int64_t M, int N, float* out);
 void row_scale_h2(const float* A0, int64_t lda0, int K0, const float* A1, int64_t lda1, int K1, int64_t M,
                   float* scale);
 // Common power-of-two scale t_n per row n of B0 (and B1), planes P = [hi][lo]
@@ -115,5 +141,11 @@ void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, 
                     // deferred normalisation of x: gathered row c is x[c] * row_mul[c], the
                     // self row i (for row_scale) self_x[i] * self_mul[i]
                     const float* row_mul = nullptr, const float* self_mul = nullptr);
+// The overlapped gather in its dynamic form (AggHelp; same rows, same bits as aggregate_rows
+// overlapped with row_scale): agg_help_ok says whether the settings allow it (vector path,
+// dim <= 768 so the helping GEMM keeps its register budget, the overlapped kernel's U = 8 NT
+// loads, RVX_SAGE_HELP != 0).
+bool agg_help_ok(int dim, const float* x, const float* out, const float* self_x);
+void aggregate_rows_help(const AggHelp& h, const char* tag);
 
 }  // namespace rvx

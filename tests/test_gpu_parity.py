@@ -1014,6 +1014,35 @@ def test_ruvector_layer_wide_gemm_bits(monkeypatch, hidden, heads, wide):
     assert_close(y1, O.rvl_forward_graph(W, x, rp, col, ew))
 
 
+@pytest.mark.parametrize("fold", ["0", "2"])
+@pytest.mark.parametrize("wide", ["0", "1", "6", "7"])
+@pytest.mark.parametrize("hidden,heads,chunk", [(768, 8, 4096), (96, 4, 0), (64, 4, 4096)])
+def test_ruvector_layer_producer_row_maxima_bits(monkeypatch, hidden, heads, chunk, wide, fold):
+    """The split-f16 row scales of RuvectorLayer's GEMM operands (M, COMB, AGG, r ⊙ h) taken
+    from per-row maxima their producers write (GEMM epilogue slots, the gate multiply;
+    RVX_GEMM_AMAX=1, default) equal the scales of a pass over the rows (RVX_GEMM_AMAX=0): same
+    bits on every GEMM tiling (incl. the 2 x 4-wave tile and h2g, which fall back to a pass
+    over C or write from the epilogue), the folded attention, and row chunks with a ragged
+    last chunk (4096-row chunks of 9000 rows)."""
+    n, deg = (9000 if chunk else 300), 12
+    layer, W, _ = _layer_and_weights(hidden, hidden, heads, 0.1, seed=17)
+    x = O.fill_uniform(n * hidden, 14).reshape(n, hidden)
+    rp, col = O.random_csr(n, deg, 15)
+    ew = O.fill_uniform(n * deg, 16, 0.0, 1.0)
+    g = rv.Graph.from_csr(rp, col, ew)
+    if chunk:
+        monkeypatch.setenv("RVX_GNN_CHUNK_ROWS", str(chunk))
+    monkeypatch.setenv("RVX_GEMM_WIDE", wide)
+    monkeypatch.setenv("RVX_GNN_FOLD", fold)
+    monkeypatch.setenv("RVX_GEMM_AMAX", "0")
+    y0 = layer.forward_graph(x, g)
+    monkeypatch.setenv("RVX_GEMM_AMAX", "1")
+    y1 = layer.forward_graph(x, g)
+    assert np.array_equal(y0, y1)
+    if n <= 300:
+        assert_close(y1, O.rvl_forward_graph(W, x, rp, col, ew))
+
+
 @pytest.mark.parametrize("hidden,heads", [(256, 4), (512, 8), (768, 8), (1024, 8)])
 def test_ruvector_edge_batch_bits(monkeypatch, hidden, heads):
     """K5 with four edges' K / V / M rows loaded together (RVX_EDGE_BATCH=4, opt-in)
@@ -1130,3 +1159,27 @@ def test_graphsage_overlapped_gather_prefetch_bits(monkeypatch, in_f, deg):
     monkeypatch.setenv("RVX_AGG_ROLL", "1")
     y1 = layer.forward_graph(x, g)
     assert np.array_equal(y0, y1)
+
+
+@pytest.mark.parametrize("aggregator", ["mean", "maxpool"])
+@pytest.mark.parametrize("dims,n,deg,chunks", [((768, 768, 768), 20000, 9, 4), ((96, 200, 128), 9000, 5, 3),
+                                               ((512, 256, 512), 8000, 6, 5), ((64, 64, 64), 3000, 0, 2)])
+def test_graphsage_gemm_helps_gather_bits(monkeypatch, aggregator, dims, n, deg, chunks):
+    """The dynamic overlapped gather (RVX_SAGE_HELP=1, default): chunk c's gather takes its
+    rows from a counter and the persistent GEMM of chunk c-1 computes some of them once its
+    tiles are done. Same rows, same per-row code (agg_row.hpp), so the stack — deferred
+    normalisation factors included — is bit-identical to the static gather (RVX_SAGE_HELP=0),
+    on d 768 / 512 / <= 256 rows, ragged chunk ends and all-empty neighbourhoods."""
+    monkeypatch.setenv("RVX_SAGE_CHUNKS", str(chunks))
+    d0, d1, d2 = dims
+    x = O.fill_uniform(n * d0, 90 + n).reshape(n, d0)
+    rp, col = O.random_csr(n, deg, 91)
+    g = rv.Graph.from_csr(rp, col)
+    layers = [rv.GraphSAGELayer(d0, d1, num_samples=max(deg, 1), aggregator=aggregator),
+              rv.GraphSAGELayer(d1, d2, num_samples=max(deg, 1), aggregator=aggregator)]
+    monkeypatch.setenv("RVX_SAGE_HELP", "0")
+    a = _sage_stack(layers, g, x, n, True)
+    monkeypatch.setenv("RVX_SAGE_HELP", "1")
+    b = _sage_stack(layers, g, x, n, True)
+    for u, v in zip(a, b):
+        assert np.array_equal(u, v)
