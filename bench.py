@@ -350,7 +350,15 @@ def attach_pmc_traffic(rls, cfg):
         return
     for tag, r in rls.items():
         ent = pmc.get("kernels", {}).get(tag)
-        if r is not None and ent and r["unit"] == "GB/s":
+        pair = pmc.get("kernels", {}).get("sage_chunk_gather_gemm")
+        if tag == "sage_aggregate" and r is not None and pair:
+            # the chunk's gather rows are split between the gather kernel and the helping GEMM
+            r["traffic"] = round(pair["hbm_bytes_per_launch"], 0)
+            r["traffic_gather_kernel_only"] = round(ent["hbm_bytes_per_launch"], 0) if ent else None
+            r["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE(x2, gfx950) + WRITE_SIZE, profiles/pmc_traffic_latest.json: "
+                                   "gather kernel + the GEMM kernel that took part of its rows, per chunk (includes "
+                                   "the GEMM's own A / W / y bytes)")
+        elif r is not None and ent and r["unit"] == "GB/s":
             r["traffic"] = round(ent["hbm_bytes_per_launch"], 0)
             r["traffic_source"] = "rocprofv3 --pmc FETCH_SIZE(x2, gfx950) + WRITE_SIZE, profiles/pmc_traffic_latest.json"
         elif r is not None and ent:

@@ -311,6 +311,7 @@ void phase2_dev(const rvx_layer* l, int64_t rows_out, const int64_t* rp, const i
             ea.rp = rp + r0; ea.col = col; ea.w = w; ea.wmode = w ? wmode : 0;
             ea.q = Q; ea.ldq = H; ea.k = KV; ea.v = KV + H; ea.ldkv = 2 * H; ea.m = M;
             ea.scores = scores; ea.att = S2; ea.wagg = S3;
+            ea.att_amax = S2amax;  // att's row maxima for the out GEMM (S2amax is rewritten by AGG below)
             edge_attention(ea);
         }
 
@@ -318,7 +319,9 @@ void phase2_dev(const rvx_layer* l, int64_t rows_out, const int64_t* rp, const i
         ep.bias0 = l->d_bo.as<float>();
         ep.addend = S3; ep.ld_addend = H;
         ep.row_absmax = S4amax;
-        gemm_auto(rows, (int)H, l->d_wo.op(S2, H), nullptr, ep, S4, H, "gnn_gemm_out");  // COMB
+        GemmOperand oa = l->d_wo.op(S2, H);
+        oa.amax = fold ? nullptr : S2amax;
+        gemm_auto(rows, (int)H, oa, nullptr, ep, S4, H, "gnn_gemm_out");  // COMB
         ep = GemmEpilogue();
         ep.bias0 = l->d_bagg.as<float>();
         ep.row_absmax = S2amax;

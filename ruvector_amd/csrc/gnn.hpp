@@ -23,6 +23,7 @@ struct EdgeArgs {
     float* scores = nullptr;     // [chunk edges][heads] scratch
     float* att = nullptr;        // [n][H]   concat of head outputs
     float* wagg = nullptr;       // [n][H]   weighted message aggregate
+    float* att_amax = nullptr;   // optional [n][ROWSUMSQ_SLOTS]: max |att| per row (slot 0, others 0)
 };
 
 struct FinishArgs {

@@ -59,6 +59,7 @@ __global__ __launch_bounds__(256) void k_edge_attn_grouped(EdgeArgs a) {
             *reinterpret_cast<float4*>(a.att + i * H + c0 + c) = make_float4(0.f, 0.f, 0.f, 0.f);
             *reinterpret_cast<float4*>(a.wagg + i * H + c0 + c) = make_float4(0.f, 0.f, 0.f, 0.f);
         }
+        if (a.att_amax && lane < ROWSUMSQ_SLOTS) a.att_amax[i * ROWSUMSQ_SLOTS + lane] = 0.0f;
         return;
     }
     float q[CPL];
@@ -156,6 +157,14 @@ __global__ __launch_bounds__(256) void k_edge_attn_grouped(EdgeArgs a) {
     for (int c = 0; c < CPL; c += 4) {
         *reinterpret_cast<float4*>(a.att + i * H + c0 + c) = make_float4(att[c], att[c + 1], att[c + 2], att[c + 3]);
         *reinterpret_cast<float4*>(a.wagg + i * H + c0 + c) = make_float4(agg[c], agg[c + 1], agg[c + 2], agg[c + 3]);
+    }
+    if (a.att_amax) {  // the out GEMM's split-f16 row scale, without a pass over att
+        float mx2 = 0.0f;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) mx2 = fmaxf(mx2, fabsf(att[c]));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx2 = fmaxf(mx2, __shfl_xor(mx2, o));
+        if (lane < ROWSUMSQ_SLOTS) a.att_amax[i * ROWSUMSQ_SLOTS + lane] = lane == 0 ? mx2 : 0.0f;
     }
 }
 
@@ -413,6 +422,56 @@ __global__ __launch_bounds__(256) void k_gru_finish(FinishArgs a) {
     for (int c = lane; c < H; c += 64) y[c] = a.gamma[c] * ((y[c] - mean) / den) + a.beta[c];
 }
 
+// k_gru_finish with the row in registers (H = 64 NJ): element c = lane + 64 j as above, the
+// three loads of every element issued before any arithmetic, the sums in the same j order and
+// the same xor trees, y written once — the same bits as k_gru_finish.
+template <int NJ>
+__global__ __launch_bounds__(256) void k_gru_finish_reg(FinishArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= a.n) return;
+    constexpr int H = 64 * NJ;
+    const bool iso = a.rp[i + 1] == a.rp[i];
+    const float* __restrict__ mr = a.m + i * H;
+    const float* __restrict__ zr = a.zr + i * 2 * (int64_t)H;
+    const float* __restrict__ hr = a.ht + i * H;
+    float v[NJ];
+    float s = 0.0f;
+    if (iso) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) v[j] = mr[lane + 64 * j];
+    } else {
+        float hm[NJ], z[NJ], ht[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            hm[j] = mr[lane + 64 * j];
+            z[j] = zr[lane + 64 * j];
+            ht[j] = hr[lane + 64 * j];
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const float t1 = (1.0f - z[j]) * hm[j];
+            const float t2 = z[j] * ht[j];
+            v[j] = (t1 + t2) * a.keep;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) s += v[j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / (float)H;
+    float var = 0.0f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) { const float d = v[j] - mean; var += d * d; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) var += __shfl_xor(var, o);
+    var = var / (float)H;
+    const float den = sqrtf(var + a.eps);
+    float* y = a.y + i * H;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) y[lane + 64 * j] = a.gamma[lane + 64 * j] * ((v[j] - mean) / den) + a.beta[lane + 64 * j];
+}
+
 }  // namespace
 
 void edge_attention(const EdgeArgs& a) {
@@ -430,7 +489,10 @@ void edge_attention(const EdgeArgs& a) {
     else if (grp && a.H / 64 == 8) RVX_LAUNCH(t, (b4 ? k_edge_attn_grouped<8, 4> : k_edge_attn_grouped<8, 1>), grid, block, 0, a);
     else if (grp && a.H / 64 == 12) RVX_LAUNCH(t, (b4 ? k_edge_attn_grouped<12, 4> : k_edge_attn_grouped<12, 1>), grid, block, 0, a);
     else if (grp && a.H / 64 == 16) RVX_LAUNCH(t, (b4 ? k_edge_attn_grouped<16, 4> : k_edge_attn_grouped<16, 1>), grid, block, 0, a);
-    else RVX_LAUNCH(t, k_edge_attn_generic, grid, block, 0, a);
+    else {
+        RVX_LAUNCH(t, k_edge_attn_generic, grid, block, 0, a);
+        if (a.att_amax) row_absmax_pass(a.att, a.H, a.n, a.H, a.att_amax);
+    }
 }
 
 bool edge_fold_ok(int H, int heads) {
@@ -482,7 +544,19 @@ void mul_rows(const float* r, int64_t ldr, const float* h, float* out, int64_t n
 
 void gru_finish(const FinishArgs& a) {
     if (a.n <= 0) return;
-    RVX_LAUNCH("gnn_finish", k_gru_finish, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, a);
+    const dim3 grid((unsigned)((a.n + 3) / 4)), block(256);
+    // registers-resident row for H = 64 NJ (RVX_GNN_FINISH_REG=0 restores the loop form; same bits)
+    const int nj = a.H % 64 == 0 && env_int("RVX_GNN_FINISH_REG", 1) ? a.H / 64 : 0;
+    switch (nj) {
+        case 1: RVX_LAUNCH("gnn_finish", k_gru_finish_reg<1>, grid, block, 0, a); return;
+        case 2: RVX_LAUNCH("gnn_finish", k_gru_finish_reg<2>, grid, block, 0, a); return;
+        case 4: RVX_LAUNCH("gnn_finish", k_gru_finish_reg<4>, grid, block, 0, a); return;
+        case 8: RVX_LAUNCH("gnn_finish", k_gru_finish_reg<8>, grid, block, 0, a); return;
+        case 12: RVX_LAUNCH("gnn_finish", k_gru_finish_reg<12>, grid, block, 0, a); return;
+        case 16: RVX_LAUNCH("gnn_finish", k_gru_finish_reg<16>, grid, block, 0, a); return;
+        default: break;
+    }
+    RVX_LAUNCH("gnn_finish", k_gru_finish, grid, block, 0, a);
 }
 
 namespace {

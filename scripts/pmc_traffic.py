@@ -16,7 +16,12 @@ import sys
 from collections import defaultdict
 
 TAGS = {  # kernel symbol substring -> bench tag
-    "k_aggregate_vec": "sage_aggregate",
+    # the overlapped gather takes its rows from a counter (RVX_SAGE_HELP=1) and the previous
+    # chunk's GEMM takes some of them: its bytes are split between the two kernels, so the pair
+    # is also reported per chunk (sage_chunk_gather_gemm); the static gathers are the bench's
+    # gemm_paths alternatives (no help)
+    "k_aggregate_help": "sage_aggregate",
+    "k_aggregate_vec": "sage_aggregate_static",
     # one entry per GEMM kernel: the layer's split-f16 GEMM (h2g) alone under sage_gemm; the
     # alternatives bench.py times (gemm_paths) under their own names
     "gemm_nt_h2g": "sage_gemm",
@@ -70,6 +75,13 @@ def main():
         e["read_bytes_per_launch_corrected"] = rd
         e["write_bytes_per_launch"] = wr
         e["hbm_bytes_per_launch"] = rd + wr
+    if "sage_aggregate" in res and "sage_gemm" in res:
+        a, g = res["sage_aggregate"], res["sage_gemm"]
+        res["sage_chunk_gather_gemm"] = {
+            "kernels": a["kernels"] + g["kernels"],
+            "hbm_bytes_per_launch": a["hbm_bytes_per_launch"] + g["hbm_bytes_per_launch"],
+            "note": "per row chunk: the gather kernel plus the GEMM kernel that took part of the next "
+                    "chunk's gather rows; the GEMM's own A / W / y traffic is included"}
     # the bench configuration these counters belong to (bench JSON of the same command)
     cfg = None
     if len(sys.argv) > 4:

@@ -1043,6 +1043,25 @@ def test_ruvector_layer_producer_row_maxima_bits(monkeypatch, hidden, heads, chu
         assert_close(y1, O.rvl_forward_graph(W, x, rp, col, ew))
 
 
+@pytest.mark.parametrize("deg", [12, 0])
+@pytest.mark.parametrize("hidden,heads", [(768, 8), (64, 4), (1024, 8), (96, 4)])
+def test_ruvector_finish_in_registers_bits(monkeypatch, hidden, heads, deg):
+    """GRU blend + LayerNorm with the row held in registers (k_gru_finish_reg, H % 64 == 0;
+    RVX_GNN_FINISH_REG=1, default) against the loop form (0): same bits, incl. isolated rows
+    (deg 0: LayerNorm of the message) and H = 96, which keeps the loop form."""
+    n = 500
+    layer, W, _ = _layer_and_weights(hidden, hidden, heads, 0.1, seed=27)
+    x = O.fill_uniform(n * hidden, 24).reshape(n, hidden)
+    rp, col = O.random_csr(n, deg, 25)
+    ew = O.fill_uniform(max(n * deg, 1), 26, 0.0, 1.0)[: n * deg]
+    g = rv.Graph.from_csr(rp, col, ew if deg else None)
+    monkeypatch.setenv("RVX_GNN_FINISH_REG", "0")
+    y0 = layer.forward_graph(x, g)
+    monkeypatch.setenv("RVX_GNN_FINISH_REG", "1")
+    y1 = layer.forward_graph(x, g)
+    assert np.array_equal(y0, y1)
+
+
 @pytest.mark.parametrize("hidden,heads", [(256, 4), (512, 8), (768, 8), (1024, 8)])
 def test_ruvector_edge_batch_bits(monkeypatch, hidden, heads):
     """K5 with four edges' K / V / M rows loaded together (RVX_EDGE_BATCH=4, opt-in)
