@@ -332,8 +332,17 @@ void phase2_dev(const rvx_layer* l, int64_t rows_out, const int64_t* rp, const i
         ep.epi = GEMM_EPI_SIGMOID; ep.bias0 = l->d_bwzr.as<float>(); ep.bias1 = l->d_buzr.as<float>();
         GemmOperand zr_a = l->d_wzr.op(S2, H), zr_b = l->d_uzr.op(Mc, H);
         zr_a.amax = S2amax; zr_b.amax = Mcamax;
+        // RH = r ⊙ h. Opt-in (RVX_GNN_GATE_EPI=1, read per call; tests cover both): from the
+        // z|r GEMM's epilogue (r never stored; the same product as mul_rows). It needs the 4-wave
+        // 128 x 192 tile (registers), whose z|r GEMM is 10% slower than the 256 x 256 default:
+        // 10M C4 step 3.67 / 3.69 vs 3.65 / 3.75 s (zr 522 vs 473 ms + gate 49 ms; a wash)
+        const bool gate_epi = amx && env_int("RVX_GNN_GATE_EPI", 0);
+        if (gate_epi) {
+            ep.row_absmax = S3amax;
+            ep.gate_h = Mc; ep.ld_gate_h = H; ep.gate_out = S3; ep.ld_gate_out = H; ep.gate_col0 = (int)H;
+        }
         gemm_auto(rows, (int)(2 * H), zr_a, &zr_b, ep, S1, 2 * H, "gnn_gemm_zr");
-        mul_rows(S1 + H, 2 * H, Mc, S3, rows, (int)H, S3amax);  // RH = r ⊙ h
+        if (!gate_epi) mul_rows(S1 + H, 2 * H, Mc, S3, rows, (int)H, S3amax);
         ep = GemmEpilogue();
         ep.epi = GEMM_EPI_TANH; ep.bias0 = l->d_bwh.as<float>(); ep.bias1 = l->d_buh.as<float>();
         GemmOperand h_a = l->d_wh.op(S2, H), h_b = l->d_uh.op(S3, H);

@@ -25,6 +25,7 @@
 #include "graph.hpp"
 #include "kernels.hpp"
 #include "agg_row.hpp"
+#include "gnn.hpp"
 
 namespace rvx {
 
@@ -64,6 +65,8 @@ struct GemmArgs {
     float* row_absmax;
     // gemm_nt_h2w<..., HELP>: the next row chunk's gather, helped once the tiles run out
     AggHelp help;
+    // AMX tiles: the gate columns (GemmEpilogue::gate_*)
+    const float* gate_h; int64_t ld_gate_h; float* gate_out; int64_t ld_gate_out; int gate_col0;
 };
 
 // One row's max |v| over this column tile: lanes lr = 0..31 of a half-wave hold the row's
@@ -1296,7 +1299,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
 #ifndef H2W_RING
 #define H2W_RING 4
 #endif
-template <bool DUAL, int WN, int BN, int NW, bool PIPE = false, bool AMX = false>
+template <bool DUAL, int WN, int BN, int NW, bool PIPE = false, bool AMX = false, bool GATE = false>
 __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgid) {
     constexpr int BM = 32 * NW;        // 256 rows with 8 waves, 128 with 4
     constexpr int WMW = NW / WN;                // waves along M
@@ -1595,6 +1598,13 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
 #pragma unroll
                 for (int nb = 0; nb < NB; ++nb)
                     addv[nb] = g.addend[arow * g.ld_add + std::min(n0 + wn * (32 * NB) + nb * 32 + lr, g.N - 1)];
+            } else if (GATE) {  // the gate's h values, same preload
+                const int64_t arow = std::min<int64_t>(row, g.M - 1);
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb) {
+                    const int cc = std::min(n0 + wn * (32 * NB) + nb * 32 + lr, g.N - 1);
+                    addv[nb] = cc >= g.gate_col0 ? g.gate_h[arow * g.ld_gate_h + (cc - g.gate_col0)] : 0.0f;
+                }
             }
 #pragma unroll
             for (int nb = 0; nb < NB; ++nb) {
@@ -1605,9 +1615,15 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
                     if (g.bias0 || g.bias1) v += cb[nb];
                     if (g.addend) v += AMX ? addv[nb] : g.addend[row * g.ld_add + col];
                     v = epi_apply(epi, v);
-                    g.C[row * g.ldc + col] = v;
-                    ssq = __fadd_rn(ssq, __fmul_rn(v, v));
-                    if constexpr (AMX) amx = fmaxf(amx, fabsf(v));
+                    if (GATE && col >= g.gate_col0) {
+                        const float o = v * addv[nb];
+                        g.gate_out[row * g.ld_gate_out + (col - g.gate_col0)] = o;
+                        amx = fmaxf(amx, fabsf(o));
+                    } else {
+                        g.C[row * g.ldc + col] = v;
+                        ssq = __fadd_rn(ssq, __fmul_rn(v, v));
+                        if constexpr (AMX && !GATE) amx = fmaxf(amx, fabsf(v));
+                    }
                 }
             }
             if constexpr (WN == 1) {
@@ -1630,7 +1646,8 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
 // HELP: after the last tile every wave takes destination rows of the next chunk's gather
 // (g.help, aggrow::agg_help_run) — the GEMM's CU slots would otherwise idle beside the gather's
 // one block per CU until the chunk's gather ends.
-template <bool DUAL, int WN, int BN, int NW = 8, bool PIPE = false, bool HELP = false, bool AMX = false>
+template <bool DUAL, int WN, int BN, int NW = 8, bool PIPE = false, bool HELP = false, bool AMX = false,
+          bool GATE = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt_h2w(GemmArgs g, int epi) {
     if (g.queue) {
         extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
@@ -1643,14 +1660,14 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt
             const int64_t t = *s_t;
             __syncthreads();  // every wave holds t before the tile's DMA overwrites the word
             if (t >= cnt) break;
-            h2w_tile<DUAL, WN, BN, NW, PIPE, AMX>(g, epi, first + t);
+            h2w_tile<DUAL, WN, BN, NW, PIPE, AMX, GATE>(g, epi, first + t);
             __syncthreads();  // LDS stages and s_t are reused by the next tile
         }
         if constexpr (HELP) aggrow::agg_help_run(g.help);
         return;
     }
     const int64_t nwg = g.nblocks, bid = blockIdx.x;
-    h2w_tile<DUAL, WN, BN, NW, PIPE, AMX>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
+    h2w_tile<DUAL, WN, BN, NW, PIPE, AMX, GATE>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
     if constexpr (HELP) aggrow::agg_help_run(g.help);
 }
 
@@ -1853,7 +1870,7 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
     // Standalone defaults: 7 for one operand (C4's K = 768 GEMMs: msg 26.9 vs 28.2 ms per 2M
     // step with 6), 6 for two (the dual zr / h GEMMs 95.5 / 46.7 vs 99.8 / 48.0 ms with 7, the
     // 10M GraphSAGE GEMM 72.8 vs 77.2 ms; scripts/exp_gemm_pipe.sh, profiles/r03_gemm_pipe_ab.txt).
-    const int wide_mode = env_int("RVX_GEMM_WIDE", persist > 0 ? 3 : (s1 ? 6 : 7));
+    const int wide_mode = env_int("RVX_GEMM_WIDE", persist > 0 ? 3 : (s1 && !ep.gate_out ? 6 : 7));  // gate: 7 (registers)
     const bool same_strides = !s1 || (g.lda1 == g.lda0 && g.ldb1 == g.ldb0 && g.B1h_plane == g.B0h_plane);
     const bool wide = !ep.normalize_rows && (wide_mode >= 2 || (!ep.row_sumsq && !ep.a1_rowmul)) && wide_mode &&
                       same_strides && (int64_t)256 * g.lda0 * 4 < ((int64_t)1 << 31) &&
@@ -1887,6 +1904,8 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 4, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 4, true, false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 4, true, false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 4, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l4));
             wattr = true;
         }
@@ -1908,10 +1927,18 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
         g.row_absmax = (ep.row_absmax && (wide_mode == 6 || wide_mode == 7) && g.tiles_n <= ROWSUMSQ_SLOTS)
                            ? ep.row_absmax : nullptr;
         const bool amx = g.row_absmax != nullptr;
+        const bool gate = amx && ep.gate_out && wide_mode == 7;  // the 4-wave tile has the registers for it
+        if (gate) {
+            g.gate_h = ep.gate_h; g.ld_gate_h = ep.ld_gate_h; g.gate_out = ep.gate_out;
+            g.ld_gate_out = ep.ld_gate_out; g.gate_col0 = ep.gate_col0;
+        }
         const dim3 wg((unsigned)wgrid), wb(wide_mode == 4 || wide_mode == 7 ? 256 : 512);
         // RVX_GEMM_WIDE=1: waves 2 (M) x 4 (N), 128 x 64 each; 2: waves 8 x 1, 32 x 256 each
         // (A converted once per row instead of by four waves)
-        if (wide_mode == 7 && amx) {
+        if (gate) {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 4, true, false, true, true>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 4, true, false, true, true>), wg, wb, wlds, g, ep.epi);
+        } else if (wide_mode == 7 && amx) {
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 4, true, false, true>), wg, wb, wlds, g, ep.epi);
             else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 4, true, false, true>), wg, wb, wlds, g, ep.epi);
         } else if (wide_mode == 6 && amx) {
@@ -1943,7 +1970,10 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 4, 256>), wg, wb, wlds, g, ep.epi);
             else RVX_LAUNCH(t, (gemm_nt_h2w<false, 4, 256>), wg, wb, wlds, g, ep.epi);
         }
-        if (ep.row_absmax && !g.row_absmax) row_absmax_pass(C, ldc, M, N, ep.row_absmax);
+        if (ep.gate_out && !g.gate_out)
+            mul_rows(C + ep.gate_col0, ldc, ep.gate_h, ep.gate_out, M, N - ep.gate_col0, ep.row_absmax);
+        else if (ep.row_absmax && !g.row_absmax)
+            row_absmax_pass(C, ldc, M, N, ep.row_absmax);
         return g.tiles_n;
     }
     // persistent grid of `cap` blocks per CU (a multiple of 8 blocks, so a block
@@ -1971,7 +2001,10 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
     g.row_absmax = nullptr;  // h2g: row maxima by a pass over C
     if (s1) RVX_LAUNCH(t, gemm_nt_h2g<true>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
     else RVX_LAUNCH(t, gemm_nt_h2g<false>, dim3((unsigned)grid), dim3(256), lds, g, ep.epi);
-    if (ep.row_absmax && !g.row_absmax) row_absmax_pass(C, ldc, M, N, ep.row_absmax);
+    if (ep.gate_out)
+        mul_rows(C + ep.gate_col0, ldc, ep.gate_h, ep.gate_out, M, N - ep.gate_col0, ep.row_absmax);
+    else if (ep.row_absmax && !g.row_absmax)
+        row_absmax_pass(C, ldc, M, N, ep.row_absmax);
     return g.tiles_n;
 }
 
@@ -2122,7 +2155,10 @@ void gemm_auto(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, c
         return;
     }
     gemm_nt(M, N, s0, s1, ep, C, ldc, tag);
-    if (ep.row_absmax) row_absmax_pass(C, ldc, M, N, ep.row_absmax);
+    if (ep.gate_out)
+        mul_rows(C + ep.gate_col0, ldc, ep.gate_h, ep.gate_out, M, N - ep.gate_col0, ep.row_absmax);
+    else if (ep.row_absmax)
+        row_absmax_pass(C, ldc, M, N, ep.row_absmax);
 }
 
 void split_h2_rows(const float* B0, const float* B1, int N, int K, _Float16* P0, _Float16* P1, float* inv) {

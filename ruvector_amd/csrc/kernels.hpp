@@ -64,6 +64,12 @@ struct GemmEpilogue {
     // gemm_nt_h2, persistent 256 x 192 tiles only: after the tile queue runs dry the blocks
     // take rows of this gather (the next row chunk's) — see AggHelp
     const AggHelp* help = nullptr;
+    // gemm_auto with row_absmax (C4's z|r GEMM): columns >= gate_col0 are not stored in C;
+    // gate_out[row][c - gate_col0] = v * gate_h[row][c - gate_col0] is (RuvectorLayer's r ⊙ h,
+    // the same product as mul_rows), and row_absmax then holds the maxima of those products
+    const float* gate_h = nullptr; int64_t ld_gate_h = 0;
+    float* gate_out = nullptr; int64_t ld_gate_out = 0;
+    int gate_col0 = 0;
 };
 // C[M][N] = epilogue(A0·B0^T [+ A1·B1^T])
 void gemm_nt(int64_t M, int N, const GemmOperand& s0, const GemmOperand* s1, const GemmEpilogue& ep, float* C,

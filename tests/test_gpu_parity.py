@@ -1014,10 +1014,11 @@ def test_ruvector_layer_wide_gemm_bits(monkeypatch, hidden, heads, wide):
     assert_close(y1, O.rvl_forward_graph(W, x, rp, col, ew))
 
 
+@pytest.mark.parametrize("gate", ["0", "1"])
 @pytest.mark.parametrize("fold", ["0", "2"])
 @pytest.mark.parametrize("wide", ["0", "1", "6", "7"])
 @pytest.mark.parametrize("hidden,heads,chunk", [(768, 8, 4096), (96, 4, 0), (64, 4, 4096)])
-def test_ruvector_layer_producer_row_maxima_bits(monkeypatch, hidden, heads, chunk, wide, fold):
+def test_ruvector_layer_producer_row_maxima_bits(monkeypatch, hidden, heads, chunk, wide, fold, gate):
     """The split-f16 row scales of RuvectorLayer's GEMM operands (M, COMB, AGG, r ⊙ h) taken
     from per-row maxima their producers write (GEMM epilogue slots, the gate multiply;
     RVX_GEMM_AMAX=1, default) equal the scales of a pass over the rows (RVX_GEMM_AMAX=0): same
@@ -1034,6 +1035,7 @@ def test_ruvector_layer_producer_row_maxima_bits(monkeypatch, hidden, heads, chu
         monkeypatch.setenv("RVX_GNN_CHUNK_ROWS", str(chunk))
     monkeypatch.setenv("RVX_GEMM_WIDE", wide)
     monkeypatch.setenv("RVX_GNN_FOLD", fold)
+    monkeypatch.setenv("RVX_GNN_GATE_EPI", gate)  # r ⊙ h from the z|r GEMM's epilogue (opt-in)
     monkeypatch.setenv("RVX_GEMM_AMAX", "0")
     y0 = layer.forward_graph(x, g)
     monkeypatch.setenv("RVX_GEMM_AMAX", "1")
