@@ -374,7 +374,9 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         const int64_t rows = std::min(step, n - r0);
         if (chunks > 1 && help) {
             StreamScope on_aux(gath_s);
-            aggregate_rows_help(help_of(r0), "sage_aggregate");
+            // the layer's first chunk has no GEMM beside it: a wider grid (RVX_AGG_FIRST_CAP
+            // blocks per CU, read per call; same rows, same bits)
+            aggregate_rows_help(help_of(r0), "sage_aggregate", c == 0 ? env_int("RVX_AGG_FIRST_CAP", 4) : 0);
             RVX_HIP(hipEventRecord(ev[c], gath_s));
             RVX_HIP(hipStreamWaitEvent(main_s, ev[c], 0));
         } else if (chunks > 1) {

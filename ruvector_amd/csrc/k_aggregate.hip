@@ -280,12 +280,13 @@ bool agg_help_ok(int dim, const float* x, const float* out, const float* self_x)
            dim > 0 && dim % 4 == 0 && dim <= 768 && al(x) && al(out) && self_x && al(self_x);
 }
 
-void aggregate_rows_help(const AggHelp& h, const char* tag) {
+void aggregate_rows_help(const AggHelp& h, const char* tag, int blocks_per_cu) {
     if (h.n <= 0) return;
     RVX_REQUIRE(h.counter && h.agg >= AGG_SUM && h.agg <= AGG_MAX && h.dim % 4 == 0 && h.dim <= 768,
                 RVX_ERR_INVALID_SHAPE, "dynamic gather: bad arguments");
+    const int cap = blocks_per_cu > 0 ? blocks_per_cu : std::max(1, g_agg_overlap_cap);
     const int64_t blocks = std::min<int64_t>((h.n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK,
-                                             (int64_t)std::max(1, g_agg_overlap_cap) * active_cus());
+                                             (int64_t)cap * active_cus());
     RVX_LAUNCH(tag ? tag : "aggregate", k_aggregate_help, dim3((unsigned)blocks), dim3(256), 0, h);
 }
 

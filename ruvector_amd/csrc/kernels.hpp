@@ -152,6 +152,8 @@ void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, 
 // dim <= 768 so the helping GEMM keeps its register budget, the overlapped kernel's U = 8 NT
 // loads, RVX_SAGE_HELP != 0).
 bool agg_help_ok(int dim, const float* x, const float* out, const float* self_x);
-void aggregate_rows_help(const AggHelp& h, const char* tag);
+// blocks_per_cu > 0 overrides the overlapped cap (RVX_AGG_BLOCKS_PER_CU): the first chunk of a
+// layer has no GEMM beside it
+void aggregate_rows_help(const AggHelp& h, const char* tag, int blocks_per_cu = 0);
 
 }  // namespace rvx
