@@ -54,7 +54,7 @@ GEMM_DESC = ("split-f16 MFMA (per-row/column power-of-two operand scaling, two f
              "f32 GEMM to within 2^-23 per product), peak = 2.5 PF bf16 / 6" if GEMM_X3 else
              "FP32 MFMA v_mfma_f32_32x32x2_f32")
 XGMI_PEAK_GBS = 7 * 153.0    # 7 xGMI links x ~153 GB/s per direction per GPU
-PIPELINE = ("row chunks x24 (>=393216 rows), gather (1 block/CU, rows from a per-chunk counter) on aux stream "
+PIPELINE = ("row chunks x48 (>=786432 rows), gather (1 block/CU, rows from a per-chunk counter) on aux stream "
             "overlapping the GEMM (persistent 256x192 tiles, 1 block/CU) of the previous chunk, whose blocks take "
             "rows of that gather once their tiles are done (RVX_SAGE_HELP=1): sage_aggregate's duration is the "
             "chunk's gather completion and sage_gemm's includes the gather rows it took, so its TFLOP/s understates "

@@ -55,8 +55,11 @@ void check_graph(const rvx_graph* g) {
 // Row chunking of the layer pipeline (same on every rank for a given chunk count).
 int sage_chunks_for(int64_t n) {
     // 24 chunks with the gather capped at one block per CU (k_aggregate.hip):
-    // 1.46G vs 1.37G edges/s for 16 uncapped at 10M x 768 (scripts/exp_sweep3.sh)
-    const int pipe_chunks = std::max(1, env_int("RVX_SAGE_CHUNKS", 24));
+    // 1.46G vs 1.37G edges/s for 16 uncapped at 10M x 768 (scripts/exp_sweep3.sh); 48 once
+    // the GEMM helps the gather (smaller lone first gather / last GEMM per layer): 399.7 /
+    // 425.8 / 401.2 / 406.0 vs 433.7 / 427.5 / 419.9 / 427.9 ms/step for 24
+    // (scripts/exp_help_chunks.sh, profiles/r03_help_chunks.txt)
+    const int pipe_chunks = std::max(1, env_int("RVX_SAGE_CHUNKS", 48));
     return n >= (int64_t)pipe_chunks * 16384 ? pipe_chunks : 1;
 }
 int64_t chunk_step(int64_t n, int chunks) { return ((n + chunks - 1) / chunks + 127) / 128 * 128; }

@@ -157,7 +157,7 @@ class RcclComm:
             pass
 
 
-PIPE_CHUNKS = 24         # RVX_SAGE_CHUNKS default (api_graph.cpp sage_chunks_for)
+PIPE_CHUNKS = 48         # RVX_SAGE_CHUNKS default (api_graph.cpp sage_chunks_for)
 PIPE_MIN_ROWS = 16384    # rows per chunk below which a layer is not chunked
 
 
