@@ -107,7 +107,7 @@ def _exchange_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         # ragged shards, one far below the pipelining threshold
-        sizes = [450_000, 150_001, 5_000][:world]
+        sizes = [900_000, 150_001, 5_000][:world]  # the largest shard above PIPE_CHUNKS * PIPE_MIN_ROWS
         offsets = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
         n, d = int(offsets[-1]), 3
         full = np.arange(n * d, dtype=np.float32).reshape(n, d)
