@@ -403,10 +403,12 @@ def test_graphsage_ill_conditioned_rows_f64_anchor(monkeypatch, gemm, in_f, out_
           f"{n - good.sum()} ill-conditioned rows")
 
 
-def test_graphsage_chunked_pipeline_and_exchange_entry():
-    """n >= 24*16384 rows runs the two-stream row-chunk pipeline (api_graph.cpp
-    sage_forward_dev); rvx_sage_forward_exchange at world 1 writes the same rows."""
+def test_graphsage_chunked_pipeline_and_exchange_entry(monkeypatch):
+    """n >= chunks*16384 rows runs the two-stream row-chunk pipeline (api_graph.cpp
+    sage_forward_dev; 24 chunks here, the default 48 needs 786k rows); rvx_sage_forward_exchange
+    at world 1 writes the same rows."""
     import ctypes
+    monkeypatch.setenv("RVX_SAGE_CHUNKS", "24")
     n, d, deg = 400_000, 64, 8
     x = rv.Buffer(n * d * 4)
     x.fill_uniform(n * d, 21, -1.0, 1.0)
