@@ -8,10 +8,15 @@ out-degree-32 CSR, 2-layer ruvector-gnn GraphSAGE-mean forward
 (crates/ruvector-postgres/src/gnn/graphsage.rs:118-187) with the reference's
 deterministic weights. A step = one full 2-layer forward over every node.
 
-Multi-GPU (one process per GPU, launched by torch.distributed.run; the
-processes themselves use no torch: RCCL id over a TCP rendezvous, barriers and
-the max-over-ranks clock as RCCL all-reduces): the 10M nodes are
-split into contiguous node-id ranges (strong scaling). The input node table is
+Multi-GPU (one process per GPU: `--gpus N` starts the N ranks itself as child
+processes, or a launcher such as torch.distributed.run does and sets WORLD_SIZE;
+the processes use no torch: RCCL id over a TCP rendezvous, barriers and the
+max-over-ranks clock as RCCL all-reduces; `--transport host` moves the same
+exchange rounds through host memory and stdlib sockets so N ranks can share one
+GPU): the 10M nodes are split into contiguous node-id ranges (strong scaling).
+At N > 1 the run checks itself: every rank's copy of the exchanged layer-1 table
+must have the same checksum, and the last rank's rows are compared with the
+oracle (layer 1 on rank 0 from its exchanged copy, layer 2 on the last rank). The input node table is
 resident on every GPU; each layer writes its owned rows of the next table and
 ships them to every peer over RCCL p2p (xGMI) chunk by chunk while the
 remaining chunks compute (rvx_sage_forward_exchange); the last layer's rows
@@ -74,18 +79,26 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-hnsw", action="store_true", help="skip the HNSW queries/s@recall95 leg")
     p.add_argument("--no-scan", action="store_true", help="skip the 10M x 768 exact-scan queries/s leg")
+    p.add_argument("--transport", choices=("rccl", "host"), default="rccl",
+                   help="N>1 exchange: RCCL over xGMI, or host memory + stdlib sockets (ranks may share a GPU)")
+    p.add_argument("--check-rows", type=int, default=8192, help="N>1: oracle-checked rows of the last rank")
     return p.parse_args()
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N ranks here, before anything touches the GPU
+        from benchutil import spawn_ranks
+        sys.exit(spawn_ranks(a.gpus, os.path.abspath(__file__), sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import ruvector_amd as rv
-    from ruvector_amd.shard import REDUCE_MAX, RcclComm, ShardPlan
+    from ruvector_amd.shard import REDUCE_MAX, ShardPlan, comm_from_env
 
-    rv.set_device(local)
+    # host transport: ranks may outnumber the GPUs and share them
+    rv.set_device(local % max(rv.device_count(), 1) if a.transport == "host" else local)
     n_tot, d, deg, layers = a.nodes, a.dim, a.degree, a.layers
     plan = ShardPlan(n_tot, world)
     r0, r1 = plan.rows(rank)
@@ -94,8 +107,9 @@ def main():
     off_ptr = offsets.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
 
     # RCCL communicator: id over a stdlib TCP rendezvous, barriers and the
-    # max-over-ranks clock as RCCL all-reduces (no other collective library)
-    comm = RcclComm.from_env() if world > 1 else None
+    # max-over-ranks clock as RCCL all-reduces (no other collective library);
+    # or the host-staged socket transport
+    comm = comm_from_env(a.transport)
 
     # ---- inputs resident in HBM: the node table (same on every GPU), this
     # rank's CSR rows (global column ids), two full tables for layer outputs
@@ -206,6 +220,9 @@ def main():
 
     if comm is not None:
         line["multi_gpu"] = exchange_report(a, kern, comm, world, rank, offsets, d, layers)
+        line["multi_gpu"]["transport"] = ("rccl (p2p over xGMI)" if a.transport == "rccl" else
+                                          "host-staged (host memory + stdlib TCP sockets)")
+        line["parity"] = multi_rank_check(a, comm, rank, world, offsets, x, tables, invs, n_tot, d, deg, layers)
     if rank == 0 and world == 1 and not a.no_cpu:
         line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, tables, n_tot, d, deg, layers, invs)
     if world == 1:
@@ -220,6 +237,67 @@ def main():
         print(json.dumps(line), flush=True)
     if comm is not None:
         comm.barrier()
+
+
+def multi_rank_check(a, comm, rank, world, offsets, x, tables, invs, n_tot, d, deg, layers):
+    """Self-check of a multi-rank run (after the timed steps, on the last step's tables):
+    * agreement: every rank's copy of the exchanged layer-1 table (and its 1/|y| column
+      when the normalisation is carried) has the same 64-bit checksum (device kernel);
+    * layer 1: rank 0 compares `check_rows` rows owned by the LAST rank, as they arrived
+      over the exchange, with the oracle (per-row and normwise, tests/parity.py metrics);
+    * layer 2: the last rank compares the same rows of its own output, computed from its
+      exchanged layer-1 table.
+    Inputs: x rows gathered from HBM; the CSR rows from the oracle's own generator."""
+    from ruvector_amd.shard import REDUCE_MAX, REDUCE_MIN
+    if layers < 2:
+        return {"ok": None, "note": "one layer: nothing is exchanged"}
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as O
+    from benchutil import host_threads
+
+    cs = [tables[0].checksum(n_tot * d * 4)] + ([invs[0].checksum(n_tot * 4)] if invs else [])
+    halves = [float(v) for c in cs for v in (c & 0xFFFFFFFF, c >> 32)]
+    agree = comm.allreduce(halves, REDUCE_MAX) == comm.allreduce(halves, REDUCE_MIN)
+
+    last = world - 1
+    a0 = int(offsets[last])
+    rows = int(min(a.check_rows, int(offsets[last + 1]) - a0))
+    errs = [0.0, 0.0, 0.0, 0.0]
+    if rank in (0, last) and rows > 0:
+        threads, _ = host_threads()
+        rp, col = O.random_csr(n_tot, deg, 4)
+        wn, ws = O.sage_init(d, d, 0), O.sage_init(d, d, 1000)
+        nb = col[rp[a0]:rp[a0 + rows]].astype(np.int64)
+        need = np.concatenate([np.arange(a0, a0 + rows, dtype=np.int64), nb])
+        rp_sub = (rp[a0:a0 + rows + 1] - rp[a0]).astype(np.int64)
+        col_sub = (rows + np.arange(nb.size)).astype(np.int32)
+        inv = invs[0].download(np.float32, (n_tot,)) if invs else None
+
+        def layer1_rows(ids):
+            r = tables[0].gather_rows(n_tot, d, ids)
+            return (r * inv[ids][:, None]).astype(np.float32) if inv is not None and layers > 1 else r
+
+        if rank == 0:  # layer 1 of the last rank's rows, as rank 0 received them
+            ref = O.sage_forward(x.gather_rows(n_tot, d, need), rp_sub, col_sub, wn, ws, rows=(0, rows),
+                                 threads=threads)
+            errs[0], errs[1] = rel_errs(layer1_rows(np.arange(a0, a0 + rows)), ref)
+        if rank == last and layers > 1:  # layer 2 of its own rows from its exchanged layer-1 table
+            ref = O.sage_forward(layer1_rows(need), rp_sub, col_sub, wn, ws, rows=(0, rows), threads=threads)
+            got = tables[1 % len(tables)].gather_rows(n_tot, d, np.arange(a0, a0 + rows))
+            errs[2], errs[3] = rel_errs(got, ref)
+    errs = comm.allreduce(errs, REDUCE_MAX)
+    worst = max(errs)
+    return {"ok": bool(agree and worst <= 1e-5), "tol": 1e-5, "max_rel_err": max(errs[0], errs[2]),
+            "row_rel_l2_max": max(errs[1], errs[3]),
+            "tables_agree": bool(agree), "table_checksums": [f"{c:016x}" for c in cs],
+            "checked_rows": {"owner_rank": last, "rows": [a0, a0 + rows]},
+            "per_layer": [{"layer": 1, "checked_on_rank": 0, "max_rel_err": errs[0], "row_rel_l2_max": errs[1],
+                           "input": "x (HBM); rows received over the exchange"},
+                          {"layer": 2, "checked_on_rank": last, "max_rel_err": errs[2], "row_rel_l2_max": errs[3],
+                           "input": "the last rank's exchanged layer-1 table"}],
+            "metrics": "max_rel_err = max|gpu-ref| / max|ref|; row_rel_l2_max = max over rows of "
+                       "||gpu_r-ref_r||_2 / ||ref_r||_2 (tests/parity.py); tables_agree: every rank's "
+                       "exchanged layer-1 table (and 1/|y|) has the same checksum"}
 
 
 def exchange_report(a, kern, comm, world, rank, offsets, d, layers):

@@ -41,22 +41,27 @@ def main():
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--gpus", type=int, default=1, help="ranks to start when no launcher set WORLD_SIZE")
+    p.add_argument("--transport", choices=("rccl", "host"), default="rccl")
     a = p.parse_args()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        from benchutil import spawn_ranks  # N ranks as child processes, before any GPU call
+        sys.exit(spawn_ranks(a.gpus, os.path.abspath(__file__), sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import ruvector_amd as rv
     from ruvector_amd.attention import EdgeFeaturedAttention, EdgeFeaturedConfig
-    from ruvector_amd.shard import REDUCE_MAX, RcclComm, ShardPlan
+    from ruvector_amd.shard import REDUCE_MAX, ShardPlan, comm_from_env
 
-    rv.set_device(local)
+    rv.set_device(local % max(rv.device_count(), 1) if a.transport == "host" else local)
     n, d, deg, H = a.nodes, a.dim, a.degree, a.dim
     plan = ShardPlan(n, world)
     r0, r1 = plan.rows(rank)
     n_loc = r1 - r0
     offsets = np.array([plan.rows(p)[0] for p in range(world)] + [n], dtype=np.int64)
-    comm = RcclComm.from_env() if world > 1 else None  # TCP rendezvous for the RCCL id
+    comm = comm_from_env(a.transport)  # RCCL (TCP rendezvous for the id) or the host socket transport
 
     # node-range shards: every rank holds the whole-table buffers but reads and
     # writes only its own rows; its CSR rows (global column ids) and their slice
@@ -160,11 +165,14 @@ def cpu_baseline(a, x_buf, g, ew_buf, layer, n, d, deg, offsets):
     ref = O.rvl_forward_graph(W, x, rp, col, ew, rows=(0, rows), threads=threads)
     dt = time.perf_counter() - t0
     got = y1.download(np.float32, (rows, layer.hidden_dim))
-    err = float(np.max(np.abs(got.astype(np.float64) - ref)) / max(float(np.max(np.abs(ref))), 1e-30))
+    from bench import rel_errs
+    err, row_err = rel_errs(got, ref)
     cpu = {"value": round(rows * deg / dt, 1), "unit": "edges/s", "cores": threads, "kind": "port",
            "sample": f"oracle RuvectorLayer::forward per node (layer.rs:379-451 restated, {threads} threads) on rows "
                      f"0..{rows} of layer 1, {dt:.1f} s"}
-    return cpu, {"rows": rows, "max_rel_err": err, "tol": 1e-5, "ok": err <= 1e-5}
+    return cpu, {"rows": rows, "max_rel_err": err, "row_rel_l2_max": row_err, "tol": 1e-5,
+                 "ok": err <= 1e-5 and row_err <= 1e-5,
+                 "metrics": "normwise max|gpu-ref|/max|ref| and per-row ||gpu_r-ref_r||/||ref_r|| (tests/parity.py)"}
 
 
 if __name__ == "__main__":

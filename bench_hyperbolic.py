@@ -10,8 +10,9 @@ scan order). Reports build time, recall@10 / QPS over an ef sweep, QPS at
 recall >= 0.95, tangent-pruned search, and the oracle's CPU search on the same
 graph (bounded sample) with an id-equality check.
 
---gpus N (one process per GPU, launched like bench.py by torch.distributed.run;
-RANK / WORLD_SIZE / LOCAL_RANK from the environment): the C5 configuration itself,
+--gpus N (one process per GPU: started here as child processes when no launcher set
+WORLD_SIZE, else RANK / WORLD_SIZE / LOCAL_RANK from the launcher; `--transport host`
+lets the ranks share one GPU): the C5 configuration itself,
 node-range shards of --per-gpu points each (default 6.25M = 50M / 8; weak scaling,
 so N = 8 is the full 50M x 1024 corpus), every rank generating exactly its rows of
 the corpus on the GPU (rvx_fill_ball_rows). Each query batch runs
@@ -21,6 +22,10 @@ local shard searched (exact Poincaré scan, tangent-pruned search, graph search)
 one all-gather of every rank's top-10 and the GPU merge. Ground truth = the exact
 mode (global exact top-10). Reports QPS per mode, recall@10 against the exact
 mode, the broadcast / all-gather / merge time, and the build time (max over ranks).
+The exact mode is itself checked against the CPU at full scale: every rank streams its
+shard through the oracle's Poincaré scan for `--cpu-queries` queries, the per-shard
+top-10 lists are merged on rank 0 (shard.rs:354-373 order) and compared with the GPU's
+ids and distances bit for bit.
 """
 import argparse
 import json
@@ -53,13 +58,14 @@ def recall(gt, got):
 def main_sharded(a):
     """C5 across GPUs: node-range shards + broadcast / all-gather / merge per query batch."""
     import ruvector_amd as rv
-    from ruvector_amd.shard import REDUCE_MAX, RcclComm
+    from ruvector_amd.shard import REDUCE_MAX, comm_from_env
 
     import benchutil
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    rv.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    comm = RcclComm.from_env() if world > 1 else None
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rv.set_device(local % max(rv.device_count(), 1) if a.transport == "host" else local)
+    comm = comm_from_env(a.transport)
     log = (lambda s: print(f"[rank {rank}] {s}", file=sys.stderr, flush=True))  # noqa: E731
     n, d, nq, k = a.per_gpu, a.dim, a.queries, 10
     r0 = rank * n
@@ -85,6 +91,7 @@ def main_sharded(a):
         h.insert_device(xb, n, d)
         rv.synchronize()
     build_s = vmax(time.perf_counter() - t0)
+    cpu_check = oracle_scan_shard(a, xb, n, d, r0, rank, world, comm, log) if a.cpu_queries > 0 else None
     del xb
     t0 = time.perf_counter()
     h.build_tangent_cache()
@@ -107,6 +114,11 @@ def main_sharded(a):
         ids = gid.download(np.int64, (nq, k))
         if mode == "exact":
             gt = ids
+            if cpu_check is not None and rank == 0:
+                m = cpu_check["ids"].shape[0]
+                cpu_check["ids_equal"] = bool(np.array_equal(ids[:m], cpu_check["ids"]))
+                cpu_check["distances_equal"] = bool(np.array_equal(dist.download(np.float32, (nq, k))[:m],
+                                                                   cpu_check["dist"]))
         phases = {t: round(prof.query(t)[0], 2) for t in ("shard_bcast", "shard_allgather", "shard_merge")}
         key = mode if mode != "search" else f"search_ef{ef}"
         out_modes[key] = {"qps": round(nq / dt, 1), "recall_at_10": round(recall(gt, ids), 4), "wall_ms": round(dt * 1e3, 1),
@@ -120,7 +132,44 @@ def main_sharded(a):
                                                       f"shards of {n}, {nq} queries, k={k}, M=16 M0=32 ef_c=200"},
             "build_s": round(build_s, 2), "tangent_cache_s": round(cache_s, 2), "modes": out_modes,
             "ground_truth": "exact mode: global exact Poincaré top-10 over every shard",
+            "exact_vs_oracle": None if cpu_check is None else
+            {k2: v for k2, v in cpu_check.items() if k2 not in ("ids", "dist")},
             "data": "synthetic (rvx_fill_ball_rows, seed 7 points / 8 queries)"}), flush=True)
+
+
+def oracle_scan_shard(a, xb, n, d, r0, rank, world, comm, log):
+    """Exact Poincaré top-10 of the first `cpu_queries` queries over this rank's shard on
+    the CPU (oracle/hyperbolic.cpp orc_hyp_scan_rows, rows streamed from HBM in chunks),
+    then every rank's lists merged on rank 0 in ShardedHyperbolicHnsw::search order
+    (ascending distance, lower global id first on ties)."""
+    import ruvector_amd as rv
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as O
+    from benchutil import host_threads
+    m, k = a.cpu_queries, 10
+    q = rv.Buffer(m * d * 4)
+    q.fill_ball(m, d, 8, 0)  # the first m rows of the query batch
+    qh = q.download(np.float32, (m, d))
+    threads, _ = host_threads()
+    ids = dist = None
+    t0 = time.perf_counter()
+    chunk = 1 << 18
+    for s0 in range(0, n, chunk):
+        rows = min(chunk, n - s0)
+        xs = xb.download(np.float32, (rows, d), offset=s0 * d * 4)
+        ids, dist = O.hyp_scan_rows(xs, qh, k, id_base=r0 + s0, ids=ids, dist=dist, threads=threads)
+    cpu_s = time.perf_counter() - t0
+    log(f"oracle exact scan of {m} queries over {n} rows: {cpu_s:.1f} s")
+    if comm is not None:  # one-hot all-reduce sums move every rank's lists to every rank
+        flat = np.zeros((world, m, k, 2))
+        flat[rank, :, :, 0] = ids
+        flat[rank, :, :, 1] = dist
+        flat = np.asarray(comm.allreduce(flat.reshape(-1).tolist())).reshape(world, m, k, 2)
+        parts = [(flat[p, :, :, 0].astype(np.int64), flat[p, :, :, 1].astype(np.float32)) for p in range(world)]
+        from ruvector_amd.shard import merge_topk
+        ids, dist = merge_topk(parts, k)
+    return {"ids": ids, "dist": dist, "queries": m, "rows_per_rank": n, "cpu_s_rank0": round(cpu_s, 2),
+            "threads": threads}
 
 
 def main():
@@ -133,7 +182,12 @@ def main():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--gpus", type=int, default=0, help="node-range-sharded C5 across GPUs (see module doc)")
     p.add_argument("--per-gpu", type=int, default=6_250_000, help="points per GPU shard with --gpus")
+    p.add_argument("--transport", choices=("rccl", "host"), default="rccl")
+    p.add_argument("--cpu-queries", type=int, default=4, help="with --gpus: queries checked against the oracle scan")
     a = p.parse_args()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        import benchutil  # N ranks as child processes, before any GPU call
+        sys.exit(benchutil.spawn_ranks(a.gpus, os.path.abspath(__file__), sys.argv[1:]))
     if a.gpus or int(os.environ.get("WORLD_SIZE", "1")) > 1:
         if a.ef == "50,100,200,400,800":
             a.ef = "50,200"

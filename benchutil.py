@@ -53,3 +53,62 @@ class heartbeat:
     def __exit__(self, *exc):
         self._stop.set()
         self._t.join()
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, script, argv):
+    """`--gpus N` without a launcher: run N copies of `script` as ranks 0..N-1 of one job
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set, as
+    torch.distributed.run would), each a child process of this one — this process has
+    not touched the GPU and never execs. Rank 0 writes to this process's stdout (the
+    bench's JSON line); the other ranks' stdout goes to stderr. When a rank fails the
+    others are stopped (they would wait in a collective) and its status is returned."""
+    import signal
+    import subprocess
+    import sys
+    import time
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env,
+                                      stdout=None if r == 0 else sys.stderr, start_new_session=True))
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except OSError:
+                    pass
+        t_end = time.monotonic() + 20
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                r, c = bad[0]
+                print(f"[spawn_ranks] rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                stop_all()
+                return c if c > 0 else 1
+            if all(c == 0 for c in codes):
+                return 0
+            time.sleep(0.2)
+    except KeyboardInterrupt:
+        stop_all()
+        raise

@@ -82,6 +82,10 @@ void*      rvx_buffer_device_ptr(rvx_buffer* buf);
 rvx_status rvx_buffer_upload(rvx_buffer* buf, const void* src, int64_t bytes, int64_t offset);
 rvx_status rvx_buffer_download(const rvx_buffer* buf, void* dst, int64_t bytes, int64_t offset);
 rvx_status rvx_buffer_zero(rvx_buffer* buf);
+/* Position-keyed 64-bit checksum of bytes [offset, offset + bytes) of a buffer (integer
+ * arithmetic, launch-independent): multi-rank runs compare the exchanged node tables of
+ * every rank with it. Not part of the reference API. */
+rvx_status rvx_buffer_checksum(const rvx_buffer* buf, int64_t offset, int64_t bytes, uint64_t* out);
 /* Rows ids[0..n) of a [rows][dim] f32 table to host out [n][dim] (one device gather per
  * 256 MB; parity checks and stored-row export). Errors: IndexError for an id outside [0, rows). */
 rvx_status rvx_buffer_gather_rows_f32(const rvx_buffer* table, int64_t rows, int32_t dim, const int64_t* ids,
@@ -488,6 +492,13 @@ rvx_status rvx_feature_file_store(const char* path, int32_t layout, const rvx_bu
  * scalar accumulation order. */
 rvx_status rvx_distance_matrix(int32_t metric, const float* q, int64_t nq, const float* x, int64_t n,
                                int32_t d, float curvature, float* out);
+
+/* Self-test of the device libm restatements that make Poincaré distances, log maps and
+ * exp maps bit-identical to the reference (f32::ln -> glibc logf, f32::ln_1p -> log1pf,
+ * f32::tanh -> tanhf, f32::atanh -> Rust std's 0.5 * ln_1p(2x / (1 - x)); poincare.rs:259-276,
+ * :407-451): out[i] = f(bits(start + i * stride)) evaluated on the GPU, f = 0 logf,
+ * 1 log1pf, 2 expm1f, 3 tanhf, 4 atanh. Not part of the reference API. */
+rvx_status rvx_selftest_libm(int32_t fn, uint64_t start, uint64_t stride, int64_t count, float* out);
 
 /* ------------------------------------------------------------------ */
 /* HyperbolicHnsw: Poincaré-ball HNSW                                  */

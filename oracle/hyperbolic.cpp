@@ -8,10 +8,12 @@
 //                 poincare_distance_from_norms :238-255, fast_acosh :259-276,
 //                 mobius_add :310-356, exp_map :407-428, log_map :431-451,
 //                 frechet_mean :463-538 (PoincareConfig defaults :40-50)
-//   hnsw.rs       distance :172-180, random_level :186-189, insert :192-251,
-//                 search_layer_single :264-289, search_layer :292-364,
-//                 prune_connections :367-388, search :390-413,
-//                 search_with_pruning :416-471, build_tangent_cache :474-485
+//   hnsw.rs       distance :175-207, random_level :220-224, insert :226-293,
+//                 search_layer_single :304-327, search_layer :329-402,
+//                 prune_connections :404-425, search :427-448,
+//                 search_with_pruning :450-489, build_tangent_cache :492-503
+//   libm          f32::ln -> glibc logf, f32::tanh -> glibc tanhf, f32::atanh -> Rust
+//                 std's 0.5 * ln_1p(2x / (1 - x)) over glibc log1pf (rust_atanh)
 //   tangent.rs    TangentCache::new :47-73, tangent_distance_squared :109-119
 // Deviations (documented, test-visible only through exact ties):
 //   * rand::random levels -> a seeded counter stream (same formula as the GPU
@@ -67,6 +69,10 @@ void fused_norms(const float* u, const float* v, int d, float& diff_sq, float& n
         nv += v[i] * v[i];
     }
 }
+
+// Rust std's f32::atanh (library/std/src/f32.rs): 0.5 * ((2x) / (1 - x)).ln_1p(), with
+// ln_1p = libm log1pf — not libm atanhf, which rounds differently.
+float rust_atanh(float x) { return 0.5f * std::log1p((2.0f * x) / (1.0f - x)); }
 
 float fast_acosh(float x) {
     if (x <= 1.0f) return 0.0f;
@@ -131,7 +137,7 @@ std::vector<float> log_map(const float* y, const float* p, int d, float c) {
     if (norm_diff < EPS) return std::vector<float>(d, 0.0f);
     const float lambda_p = 2.0f / std::max(1.0f - c * norm_squared(p, d), EPS);
     const float arg = std::min(sqrt_c * norm_diff, 1.0f - EPS);
-    const float coef = (2.0f / (sqrt_c * lambda_p)) * std::atanh(arg) / norm_diff;
+    const float coef = (2.0f / (sqrt_c * lambda_p)) * rust_atanh(arg) / norm_diff;
     for (float& v : diff) v = coef * v;
     return diff;
 }
@@ -305,7 +311,7 @@ void* orc_hyp_new(int32_t d, int32_t M, int32_t M0, int32_t efc, int32_t efs, fl
     return h;
 }
 void orc_hyp_free(void* hp) { delete static_cast<OHyp*>(hp); }
-// HyperbolicHnswConfig.metric: 0 Poincaré, 1 Euclidean (hnsw.rs:23-32, 173-185)
+// HyperbolicHnswConfig.metric: 0 Poincaré, 1 Euclidean (hnsw.rs:21-31, 175-185)
 void orc_hyp_set_metric(void* hp, int32_t euclid) { static_cast<OHyp*>(hp)->euclid = euclid != 0; }
 int64_t orc_hyp_len(void* hp) { return (int64_t)static_cast<OHyp*>(hp)->level.size(); }
 
@@ -319,7 +325,7 @@ void orc_hyp_get_vector(void* hp, int64_t id, float* out) {
     std::memcpy(out, h.v(id), sizeof(float) * h.d);
 }
 
-// search (hnsw.rs:390-413); ef_arg 0 -> ef_search. ids -1 past the end.
+// search (hnsw.rs:427-448); ef_arg 0 -> ef_search. ids -1 past the end.
 void orc_hyp_search(void* hp, const float* q, int64_t nq, int32_t k, int32_t ef_arg, int64_t* ids, float* dist,
                     int32_t* counts, int32_t threads) {
     const OHyp& h = *static_cast<OHyp*>(hp);
@@ -358,7 +364,34 @@ void orc_hyp_brute_force(void* hp, const float* q, int64_t nq, int32_t k, int64_
     });
 }
 
-// build_tangent_cache (hnsw.rs:474-485) -> TangentCache::new (tangent.rs:47-73)
+// Exact scan of raw rows for a bench's spot check at scale: merges the (distance, id)
+// top-k of rows x[0..n) (ids id_base + i) into ids_io / dist_io, which hold k ascending
+// entries per query (-1 / inf when empty). Called once per row chunk, so a caller can
+// stream a large shard through host memory. Rows must already lie in the ball (the
+// projection is the identity then); queries are projected as in orc_hyp_brute_force.
+void orc_hyp_scan_rows(const float* x, int64_t n, int32_t d, float c, const float* q, int64_t nq, int32_t k,
+                       int64_t id_base, int64_t* ids_io, float* dist_io, int32_t threads) {
+    OHyp h;
+    h.d = d;
+    h.c = c;
+    pfor(nq, threads, [&](int64_t qi) {
+        std::vector<float> xq(q + qi * d, q + (qi + 1) * d);
+        project_inplace(xq, c, EPS);
+        std::vector<R> all;
+        all.reserve((size_t)(n + k));
+        for (int s = 0; s < k; ++s)
+            if (ids_io[qi * k + s] >= 0) all.push_back({dist_io[qi * k + s], ids_io[qi * k + s]});
+        for (int64_t i = 0; i < n; ++i) all.push_back({h.dist(xq.data(), x + i * d), id_base + i});
+        const int take = (int)std::min<int64_t>(k, (int64_t)all.size());
+        std::partial_sort(all.begin(), all.begin() + take, all.end(), r_less);
+        for (int s = 0; s < k; ++s) {
+            ids_io[qi * k + s] = s < take ? all[(size_t)s].id : -1;
+            dist_io[qi * k + s] = s < take ? all[(size_t)s].d : INFINITY;
+        }
+    });
+}
+
+// build_tangent_cache (hnsw.rs:492-503) -> TangentCache::new (tangent.rs:47-73)
 // -> frechet_mean (poincare.rs:463-538), PoincareConfig defaults.
 void orc_hyp_build_tangent(void* hp) {
     OHyp& h = *static_cast<OHyp*>(hp);
@@ -397,7 +430,7 @@ void orc_hyp_centroid(void* hp, float* out) {
     std::copy(h.centroid.begin(), h.centroid.end(), out);
 }
 
-// search_with_pruning (hnsw.rs:416-471)
+// search_with_pruning (hnsw.rs:450-489)
 void orc_hyp_search_pruning(void* hp, const float* q, int64_t nq, int32_t k, int64_t* ids, float* dist, int32_t threads) {
     const OHyp& h = *static_cast<OHyp*>(hp);
     if (!h.has_cache) {
@@ -429,7 +462,7 @@ void orc_hyp_search_pruning(void* hp, const float* q, int64_t nq, int32_t k, int
     });
 }
 
-// set_curvature (hnsw.rs:505-528)
+// set_curvature (hnsw.rs:511-530)
 void orc_hyp_set_curvature(void* hp, float c) {
     OHyp& h = *static_cast<OHyp*>(hp);
     h.c = c;

@@ -192,6 +192,8 @@ SIGNATURES = {
     "rvx_feature_file_load": (None, [C.c_char_p, I32, I64, I64, I64, P, I64]),
     "rvx_feature_file_store": (None, [C.c_char_p, I32, P, I64, I64, I64]),
     "rvx_distance_matrix": (None, [I32, PF32, I64, PF32, I64, I32, F32, PF32]),
+    "rvx_selftest_libm": (None, [I32, U64, U64, I64, PF32]),
+    "rvx_buffer_checksum": (None, [P, I64, I64, C.POINTER(C.c_uint64)]),
     "rvx_profile_enable": (None, [I32]),
     "rvx_profile_reset": (None, []),
     "rvx_profile_query": (None, [C.c_char_p, C.POINTER(C.c_double), PI64]),

@@ -130,8 +130,10 @@ void search_dev(const rvx_hyperbolic* h, const float* dq, int64_t nq, int k, int
 
 // TangentCache::new (tangent.rs:47-73): centroid = frechet_mean (poincare.rs:463-538,
 // PoincareConfig defaults: max_iter 100, tol 1e-6, learning rate 0.1), then
-// log_centroid of every point. The gradient sums run on the GPU in a fixed
-// order (not the reference's point-major f32 order).
+// log_centroid of every point. The weighted sums run in the reference's point-major f32
+// order (col_chain: one sequential chain per dimension, continued across row chunks) and
+// the log / exp maps use the glibc transcendentals, so the centroid and every tangent
+// coordinate equal the reference's bit for bit.
 void build_tangent(rvx_hyperbolic* h) {
     rvx_index* ix = &h->ix;
     const int64_t n = ix->n;
@@ -140,10 +142,11 @@ void build_tangent(rvx_hyperbolic* h) {
     const float c = ix->curv;
     const float w = 1.0f / (float)n;
     const float* x = ix->vecs.as<float>();
-    float* dsum = scratch_f32("hyp_fm_sum", d);
-    std::vector<float> mean((size_t)d), grad((size_t)d), part((size_t)d), tmp((size_t)d), upd((size_t)d), negp((size_t)d);
-    col_sum(x, n, d, w, dsum);
-    RVX_HIP(hipMemcpyAsync(mean.data(), dsum, (size_t)d * 4, hipMemcpyDeviceToHost, stream()));
+    float* dacc = scratch_f32("hyp_fm_acc", d);
+    std::vector<float> mean((size_t)d), grad((size_t)d), tmp((size_t)d), upd((size_t)d), negp((size_t)d);
+    RVX_HIP(hipMemsetAsync(dacc, 0, (size_t)d * 4, stream()));
+    col_chain(x, n, d, w, dacc);  // mean[i] += weight * val (poincare.rs:501-506)
+    RVX_HIP(hipMemcpyAsync(mean.data(), dacc, (size_t)d * 4, hipMemcpyDeviceToHost, stream()));
     sync();
     pdev::project_inplace(mean.data(), d, c, pdev::EPS);
     const int64_t chunk = std::min<int64_t>(n, (int64_t)1 << 20);
@@ -153,15 +156,14 @@ void build_tangent(rvx_hyperbolic* h) {
         for (int i = 0; i < d; ++i) negp[(size_t)i] = -mean[(size_t)i];
         RVX_HIP(hipMemcpyAsync(dnegp, negp.data(), (size_t)d * 4, hipMemcpyHostToDevice, stream()));
         const float np_sq = pdev::norm_sq(mean.data(), d);
-        std::fill(grad.begin(), grad.end(), 0.0f);
+        RVX_HIP(hipMemsetAsync(dacc, 0, (size_t)d * 4, stream()));
         for (int64_t r0 = 0; r0 < n; r0 += chunk) {
             const int64_t rows = std::min(chunk, n - r0);
             log_map_rows(x + r0 * d, rows, d, dnegp, np_sq, c, logs);
-            col_sum(logs, rows, d, w, dsum);
-            RVX_HIP(hipMemcpyAsync(part.data(), dsum, (size_t)d * 4, hipMemcpyDeviceToHost, stream()));
-            sync();
-            for (int i = 0; i < d; ++i) grad[(size_t)i] = grad[(size_t)i] + part[(size_t)i];
+            col_chain(logs, rows, d, w, dacc);  // grad[i] += weight * val (:519-525)
         }
+        RVX_HIP(hipMemcpyAsync(grad.data(), dacc, (size_t)d * 4, hipMemcpyDeviceToHost, stream()));
+        sync();
         if (std::sqrt(pdev::norm_sq(grad.data(), d)) < 1e-6f) break;
         for (int i = 0; i < d; ++i) upd[(size_t)i] = 0.1f * grad[(size_t)i];
         std::vector<float> next((size_t)d);

@@ -509,6 +509,18 @@ rvx_status rvx_distance_matrix(int32_t metric, const float* q, int64_t nq, const
     });
 }
 
+rvx_status rvx_selftest_libm(int32_t fn, uint64_t start, uint64_t stride, int64_t count, float* out) {
+    return guard([&] {
+        RVX_REQUIRE(fn >= 0 && fn <= 4 && count >= 0 && out, RVX_ERR_INVALID_PARAMETER, "bad selftest arguments");
+        if (count == 0) return;
+        ComputeLock cl;
+        float* dout = scratch_f32("libm_out", count);
+        libm_eval(fn, start, stride, count, dout);
+        RVX_HIP(hipMemcpyAsync(out, dout, (size_t)count * 4, hipMemcpyDeviceToHost, stream()));
+        sync();
+    });
+}
+
 rvx_status rvx_scan_last_stats(int64_t* mfma_queries, int64_t* valu_queries, int64_t* fallback_queries) {
     return guard([&] {
         const ScanStats& s = last_scan_stats();

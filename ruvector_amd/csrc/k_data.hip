@@ -142,6 +142,30 @@ __global__ void k_transpose(const float* in, int64_t rows, int64_t cols, float* 
     }
 }
 
+// sum over 8-byte words i of mix64(w_i + (i + 1) * golden) mod 2^64: order-free integer
+// arithmetic, so the result does not depend on the launch, and a permutation or a
+// single flipped bit changes it (rvx_buffer_checksum; cross-rank table agreement)
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__global__ __launch_bounds__(256) void k_checksum(const uint64_t* w, int64_t words, const uint8_t* tail, int tail_bytes,
+                                                  unsigned long long* out) {
+    uint64_t acc = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride)
+        acc += mix64(__builtin_nontemporal_load(w + i) + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && tail_bytes > 0) {
+        uint64_t t = 0;
+        for (int b = 0; b < tail_bytes; ++b) t |= (uint64_t)tail[b] << (8 * b);
+        acc += mix64(t + (uint64_t)(words + 1) * 0x9E3779B97F4A7C15ull);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)acc);
+}
+
 unsigned grid_for(int64_t n, int block) {
     int64_t g = (n + block - 1) / block;
     if (g > 65536) g = 65536;
@@ -150,6 +174,15 @@ unsigned grid_for(int64_t n, int block) {
 }
 
 }  // namespace
+
+void checksum(const void* p, int64_t bytes, uint64_t* out_dev) {
+    RVX_HIP(hipMemsetAsync(out_dev, 0, 8, stream()));
+    if (bytes <= 0) return;
+    const int64_t words = bytes / 8;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, (words + 255) / 256));
+    RVX_LAUNCH("checksum", k_checksum, dim3(grid), dim3(256), 0, (const uint64_t*)p, words,
+               (const uint8_t*)p + words * 8, (int)(bytes - words * 8), (unsigned long long*)out_dev);
+}
 
 void fill_uniform(float* p, int64_t n, uint64_t seed, float lo, float hi) {
     ProfScope ps("fill_uniform");

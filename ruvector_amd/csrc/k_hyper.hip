@@ -4,7 +4,8 @@
 //   poincare_topk     exact top-k with HyperbolicHnsw::distance (ground truth, K8) on
 //                     the tiled scan of k_scan.hip
 //   log_map_rows      TangentCache coordinates log_c(x) (tangent.rs:57-62)
-//   frechet_grad      sum_i w log_mean(p_i) for frechet_mean's gradient step (poincare.rs:463-538)
+//   col_chain         frechet_mean's point-major sums sum_i w x_i and sum_i w log_mean(p_i)
+//                     in the reference's f32 order (poincare.rs:463-538)
 //   rerank            search_with_pruning phase 2: exact distance of the tangent
 //                     candidates, stable ascending sort, first k (hnsw.rs:471-482)
 // Every per-point distance / map is one thread's sequential chain in the
@@ -33,23 +34,86 @@ __global__ void k_log_map_rows(const float* x, int64_t n, int d, const float* ne
     pdev::log_map_negp(x + r * d, negp, np_sq, d, c, out + r * d);
 }
 
-// Column sums of w * rows[i][j]: blockIdx.y takes a contiguous run of rows
-// (index order inside the run), then the runs are added in order —
-// deterministic for a given n.
-__global__ void k_col_sum_part(const float* rows, int64_t n, int d, float w, int64_t run, float* part) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= d) return;
-    const int64_t i0 = (int64_t)blockIdx.y * run, i1 = min<int64_t>(n, i0 + run);
-    float s = 0.0f;
-    for (int64_t i = i0; i < i1; ++i) s = s + w * rows[i * d + j];
-    part[(int64_t)blockIdx.y * d + j] = s;
+// acc[j] = (((acc[j] + w*rows[0][j]) + w*rows[1][j]) + ...): the reference's point-major
+// f32 accumulation, `mean[i] += weight * val` and `grad[i] += weight * val` over the
+// points in order (frechet_mean, poincare.rs:501-506, :519-525) — one sequential chain
+// per dimension, continued across calls through acc. A block owns CH_DIMS dimensions:
+// its 256 threads stage CH_ROWS rows of them (the products w*x, rounded as the reference
+// rounds them) into LDS, transposed so a chain lane reads four consecutive rows of its
+// dimension with one ds_read_b128; lanes 0..3 of wave 0 run the chains of tile t while
+// every thread's loads of tile t+1 are in flight (two LDS buffers, one barrier per tile).
+// Blocks of one XCD (block id mod 8) take adjacent dimension groups, so a row's cache
+// line is fetched from HBM once per XCD.
+constexpr int CH_DIMS = 4;
+constexpr int CH_ROWS = 1024;
+constexpr int CH_PER_THREAD = CH_ROWS / 256;
+
+template <bool VEC>
+__device__ __forceinline__ void chain_load(const float* rows, int64_t n, int d, int j0, float w, int64_t r0, int t,
+                                           float (&v)[CH_PER_THREAD][CH_DIMS]) {
+#pragma unroll
+    for (int u = 0; u < CH_PER_THREAD; ++u) {
+        const int64_t r = r0 + t + 256 * u;
+        if (r < n) {
+            const float* p = rows + r * d + j0;
+            if constexpr (VEC) {
+                const float4 q = *reinterpret_cast<const float4*>(p);
+                v[u][0] = q.x; v[u][1] = q.y; v[u][2] = q.z; v[u][3] = q.w;
+            } else {
+#pragma unroll
+                for (int c = 0; c < CH_DIMS; ++c) v[u][c] = (j0 + c < d) ? p[c] : 0.0f;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < CH_DIMS; ++c) v[u][c] = 0.0f;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < CH_PER_THREAD; ++u)
+#pragma unroll
+        for (int c = 0; c < CH_DIMS; ++c) v[u][c] = w * v[u][c];
 }
-__global__ void k_col_sum_final(const float* part, int runs, int d, float* out) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= d) return;
-    float s = 0.0f;
-    for (int r = 0; r < runs; ++r) s = s + part[(int64_t)r * d + j];
-    out[j] = s;
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_col_chain(const float* rows, int64_t n, int d, float w, float* acc) {
+    __shared__ float4 st[2][CH_DIMS][CH_ROWS / 4];  // [buffer][dim][row / 4]: 32 KB
+    const int groups = (d + CH_DIMS - 1) / CH_DIMS;
+    const int per_xcd = (groups + 7) / 8;
+    const int g = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
+    if (g >= groups) return;  // uniform over the block, before any barrier
+    const int j0 = g * CH_DIMS;
+    const int t = threadIdx.x;
+    const bool chain = t < CH_DIMS && j0 + t < d;
+    float s = chain ? acc[j0 + t] : 0.0f;
+    const int64_t tiles = (n + CH_ROWS - 1) / CH_ROWS;
+    float v[CH_PER_THREAD][CH_DIMS];
+    chain_load<VEC>(rows, n, d, j0, w, 0, t, v);
+    for (int64_t k = 0; k < tiles; ++k) {
+        float* buf = reinterpret_cast<float*>(st[k & 1]);
+#pragma unroll
+        for (int u = 0; u < CH_PER_THREAD; ++u)
+#pragma unroll
+            for (int c = 0; c < CH_DIMS; ++c) buf[c * CH_ROWS + t + 256 * u] = v[u][c];
+        __syncthreads();
+        if (k + 1 < tiles) chain_load<VEC>(rows, n, d, j0, w, (k + 1) * CH_ROWS, t, v);
+        if (chain) {
+            const int cnt = (int)min<int64_t>(CH_ROWS, n - k * CH_ROWS);
+            const float4* col = st[k & 1][t];
+            int i = 0;
+            for (; i + 4 <= cnt; i += 4) {
+                const float4 q = col[i / 4];
+                s = s + q.x;
+                s = s + q.y;
+                s = s + q.z;
+                s = s + q.w;
+            }
+            const float* tail = reinterpret_cast<const float*>(col);
+            for (; i < cnt; ++i) s = s + tail[i];
+        }
+        // the next iteration writes the other buffer; the one after writes this one
+        // only after the next barrier, which every chain lane reaches after its reads
+    }
+    if (chain) acc[j0 + t] = s;
 }
 
 // one wave per query: exact distances of its candidates (ids from the tangent
@@ -122,14 +186,15 @@ void log_map_rows(const float* x, int64_t n, int d, const float* negp_dev, float
                c, out);
 }
 
-void col_sum(const float* rows, int64_t n, int d, float w, float* out) {
+void col_chain(const float* rows, int64_t n, int d, float w, float* acc) {
     if (n <= 0 || d <= 0) return;
-    const int runs = (int)std::min<int64_t>(1024, std::max<int64_t>(1, n / 256));
-    const int64_t run = (n + runs - 1) / runs;
-    float* part = scratch_f32("hyp_colsum_part", (int64_t)runs * d);
-    RVX_LAUNCH("hyp_col_sum", k_col_sum_part, dim3((unsigned)((d + 255) / 256), (unsigned)runs), dim3(256), 0, rows, n, d,
-               w, run, part);
-    RVX_LAUNCH("hyp_col_sum", k_col_sum_final, dim3((unsigned)((d + 255) / 256)), dim3(256), 0, part, runs, d, out);
+    const int groups = (d + CH_DIMS - 1) / CH_DIMS;
+    const unsigned blocks = (unsigned)(8 * ((groups + 7) / 8));
+    const bool vec = d % 4 == 0 && ((uintptr_t)rows & 15) == 0;
+    if (vec)
+        RVX_LAUNCH("hyp_col_chain", k_col_chain<true>, dim3(blocks), dim3(256), 0, rows, n, d, w, acc);
+    else
+        RVX_LAUNCH("hyp_col_chain", k_col_chain<false>, dim3(blocks), dim3(256), 0, rows, n, d, w, acc);
 }
 
 void rerank(const float* q, int64_t nq, const float* x, int d, float c, const int64_t* cand, int nc, int k,

@@ -4,34 +4,18 @@
 // in 4-wide chunks, each chunk's a0*a0+a1*a1+a2*a2+a3*a3 summed left to right and
 // then added to its accumulator, remainder sequential; then
 // poincare_distance_from_norms (:238-255) with fast_acosh (:259-276).
-// The three sums follow the reference order exactly; logf/sqrtf come from the
-// device math library (<=1 ulp from glibc), so distances agree to ~1e-6 rel.
+// The three sums follow the reference order exactly; fast_acosh's logf is the
+// glibc restatement of libm_f32.hpp and sqrtf is correctly rounded, so every
+// distance equals the reference's bit for bit.
 #include "common.hpp"
+#include "hyper.hpp"
+#include "poincare_dev.hpp"
 #include "scan.hpp"
 
 namespace rvx {
 namespace {
 
-constexpr float PEPS = 1e-5f;  // poincare.rs EPS
-
-__device__ __forceinline__ float fast_acosh(float x) {
-    if (x <= 1.0f) return 0.0f;
-    const float delta = x - 1.0f;
-    if (delta < 1e-4f) return sqrtf(2.0f * delta);
-    if (x < 1e6f) return logf(x + sqrtf(x * x - 1.0f));
-    return logf(2.0f * x);
-}
-
-__device__ __forceinline__ float from_norms(float diff_sq, float nu, float nv, float c) {
-    const float sqrt_c = sqrtf(c);
-    const float lu = fmaxf(1.0f - c * nu, PEPS);
-    const float lv = fmaxf(1.0f - c * nv, PEPS);
-    const float num = 2.0f * c * diff_sq;
-    const float den = lu * lv;
-    const float arg = 1.0f + num / den;
-    if (arg <= 1.0f) return 0.0f;
-    return (1.0f / sqrt_c) * fast_acosh(arg);
-}
+constexpr float PEPS = pdev::EPS;
 
 __global__ void k_poincare_matrix(const float* q, int64_t nq, const float* x, int64_t n, int d, float c, float* out) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -55,10 +39,33 @@ __global__ void k_poincare_matrix(const float* q, int64_t nq, const float* x, in
         nu = nu + ui * ui;
         nv = nv + vi * vi;
     }
-    out[idx] = from_norms(ds, nu, nv, c);
+    out[idx] = pdev::from_norms(ds, nu, nv, c);
+}
+
+// rvx_selftest_libm: out[i] = f(bits(start + i * stride)) for the libm_f32.hpp
+// restatements, so tests can compare the device's bits with the host's glibc
+__global__ void k_libm_eval(int fn, uint64_t start, uint64_t stride, int64_t count, float* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const float x = glibc::u2f((uint32_t)(start + (uint64_t)i * stride));
+    float y;
+    switch (fn) {
+        case 0: y = glibc::logf(x); break;
+        case 1: y = glibc::log1pf(x); break;
+        case 2: y = glibc::expm1f(x); break;
+        case 3: y = glibc::tanhf(x); break;
+        default: y = glibc::rust_atanhf(x); break;
+    }
+    out[i] = y;
 }
 
 }  // namespace
+
+void libm_eval(int fn, uint64_t start, uint64_t stride, int64_t count, float* out) {
+    if (count <= 0) return;
+    RVX_LAUNCH("libm_eval", k_libm_eval, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, fn, start, stride, count,
+               out);
+}
 
 void poincare_matrix(const float* q, int64_t nq, const float* x, int64_t n, int d, float c, float* out) {
     const int64_t total = nq * n;

@@ -123,6 +123,8 @@ void sage_gemm_fused(int64_t M, int N, const float* A0, int64_t lda0, int K0, co
                      int64_t plane1, const float* a_scale, const float* b_inv, float* C, int64_t ldc, bool normalize,
                      const char* tag);
 void fill_normal(float* p, int64_t n, uint64_t seed);
+// *out_dev = sum over the 8-byte words of p of a position-keyed 64-bit mix (mod 2^64)
+void checksum(const void* p, int64_t bytes, uint64_t* out_dev);
 void fill_ball_rows(float* p, int64_t rows, int dim, uint64_t seed, int64_t first_row, float rmax);
 void normalize_rows(float* p, int64_t rows, int dim, bool divide_only_if_positive, const char* tag);
 void random_csr(int64_t n, int deg, uint64_t seed, int64_t* row_ptr, int32_t* col);

@@ -5,10 +5,15 @@
 // four products are summed left to right, ((a0*a0 + a1*a1) + a2*a2) + a3*a3, and
 // that is added to the running sum; the remainder is sequential
 // (norm_squared :77-103, dot :112-131, fused_norms :135-168, mobius_add :310-356).
+// Transcendentals are the glibc restatements of libm_f32.hpp (Rust's f32::ln,
+// f32::tanh and std's f32::atanh formula), so host and device return the reference's
+// bits; sqrtf and the f32 arithmetic are correctly rounded IEEE operations.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+
+#include "libm_f32.hpp"
 
 namespace rvx {
 namespace pdev {
@@ -47,8 +52,8 @@ __host__ __device__ inline float fast_acosh(float x) {  // poincare.rs:259-276
     if (x <= 1.0f) return 0.0f;
     const float delta = x - 1.0f;
     if (delta < 1e-4f) return sqrtf(2.0f * delta);
-    if (x < 1e6f) return logf(x + sqrtf(x * x - 1.0f));
-    return logf(2.0f * x);
+    if (x < 1e6f) return glibc::logf(x + sqrtf(x * x - 1.0f));
+    return glibc::logf(2.0f * x);
 }
 
 // poincare_distance_from_norms (:238-255); c is used as given
@@ -126,7 +131,7 @@ __host__ __device__ inline void log_map(const float* y, const float* p, int d, f
     }
     const float lambda_p = 2.0f / fmaxf(1.0f - c * norm_sq(p, d), EPS);
     const float arg = fminf(sqrt_c * norm_diff, 1.0f - EPS);
-    const float coef = (2.0f / (sqrt_c * lambda_p)) * atanhf(arg) / norm_diff;
+    const float coef = (2.0f / (sqrt_c * lambda_p)) * glibc::rust_atanhf(arg) / norm_diff;
     for (int i = 0; i < d; ++i) out[i] = coef * out[i];
 }
 
@@ -142,7 +147,7 @@ __host__ __device__ inline void log_map_negp(const float* y, const float* negp, 
     }
     const float lambda_p = 2.0f / fmaxf(1.0f - c * np_sq, EPS);
     const float arg = fminf(sqrt_c * norm_diff, 1.0f - EPS);
-    const float coef = (2.0f / (sqrt_c * lambda_p)) * atanhf(arg) / norm_diff;
+    const float coef = (2.0f / (sqrt_c * lambda_p)) * glibc::rust_atanhf(arg) / norm_diff;
     for (int i = 0; i < d; ++i) out[i] = coef * out[i];
 }
 
@@ -157,7 +162,7 @@ __host__ __device__ inline void exp_map(const float* v, const float* p, int d, f
         return;
     }
     const float scaled = sqrt_c * lambda_p * norm_v / 2.0f;
-    const float coef = tanhf(scaled) / (sqrt_c * norm_v);
+    const float coef = glibc::tanhf(scaled) / (sqrt_c * norm_v);
     for (int i = 0; i < d; ++i) tmp[i] = coef * v[i];
     mobius_add(p, tmp, d, c, out);
 }

@@ -7,6 +7,8 @@
 #include <vector>
 
 #include "common.hpp"
+#include "graph.hpp"
+#include "kernels.hpp"
 
 namespace rvx {
 
@@ -279,6 +281,17 @@ rvx_status rvx_buffer_download(const rvx_buffer* buf, void* dst, int64_t bytes, 
 rvx_status rvx_buffer_zero(rvx_buffer* buf) {
     return guard([&] {
         if (buf->mem.bytes) RVX_HIP(hipMemsetAsync(buf->mem.p, 0, (size_t)buf->mem.bytes, stream()));
+    });
+}
+
+rvx_status rvx_buffer_checksum(const rvx_buffer* buf, int64_t offset, int64_t bytes, uint64_t* out) {
+    return guard([&] {
+        RVX_REQUIRE(buf && out && offset >= 0 && bytes >= 0 && offset + bytes <= buf->mem.bytes,
+                    RVX_ERR_INVALID_PARAMETER, "checksum range outside the buffer");
+        auto* d = (uint64_t*)scratch_bytes("checksum", 8);
+        checksum((const uint8_t*)buf->mem.p + offset, bytes, d);
+        RVX_HIP(hipMemcpyAsync(out, d, 8, hipMemcpyDeviceToHost, stream()));
+        sync();
     });
 }
 

@@ -72,6 +72,13 @@ class Buffer:
     def zero(self) -> None:
         L.call("rvx_buffer_zero", self._h)
 
+    def checksum(self, nbytes: int = None, offset: int = 0) -> int:
+        """Position-keyed 64-bit checksum of bytes [offset, offset + nbytes) (device kernel)."""
+        out = C.c_uint64(0)
+        L.call("rvx_buffer_checksum", self._h, int(offset), int(self.nbytes - offset if nbytes is None else nbytes),
+               C.byref(out))
+        return int(out.value)
+
     def fill_uniform(self, n: int, seed: int, lo: float = -1.0, hi: float = 1.0) -> None:
         L.call("rvx_fill_uniform", self._h, int(n), int(seed), float(lo), float(hi))
 

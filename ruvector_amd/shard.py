@@ -157,6 +157,165 @@ class RcclComm:
             pass
 
 
+class SocketComm:
+    """librvx communicator over the host-staged transport (rvx_comm_init_host) with a
+    stdlib TCP full mesh between the ranks: the *_forward_exchange rounds, sharded-search
+    broadcasts and all-gathers move through host memory and sockets, and the scalar
+    all-reduces (barrier, max-over-ranks clock, sums) go through rank 0. No torch, no
+    RCCL: it lets several ranks share one GPU (RCCL refuses two ranks on one device), so
+    the multi-rank path runs end to end where only one GPU exists. Same interface as
+    RcclComm (_h, allreduce, max, barrier)."""
+
+    PORT_OFFSET = 23  # MASTER_PORT + 23 + rank: clear of the launcher store and the RCCL rendezvous
+
+    @classmethod
+    def from_env(cls) -> "SocketComm":
+        import os
+        return cls(int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+                   os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ.get("MASTER_PORT", "29500")))
+
+    def __init__(self, world: int, rank: int, addr: str = "127.0.0.1", port: int = 29500, timeout: float = 300.0):
+        import socket
+        import time
+        self.world, self.rank = world, rank
+        self._peers = {}
+        base = port + self.PORT_OFFSET
+        srv = socket.create_server((addr, base + rank)) if rank < world - 1 else None
+        try:
+            # connect to every lower rank (announcing our rank), accept every higher one
+            for p in range(rank):
+                deadline = time.monotonic() + timeout
+                while True:
+                    try:
+                        s = socket.create_connection((addr, base + p), timeout=10.0)
+                        break
+                    except OSError:
+                        if time.monotonic() > deadline:
+                            raise
+                        time.sleep(0.1)
+                s.sendall(rank.to_bytes(4, "little"))
+                self._peers[p] = s
+            if srv is not None:
+                srv.settimeout(timeout)
+                for _ in range(world - 1 - rank):
+                    s, _a = srv.accept()
+                    p = int.from_bytes(self._recv(s, 4), "little")
+                    self._peers[p] = s
+        finally:
+            if srv is not None:
+                srv.close()
+        for s in self._peers.values():
+            s.settimeout(None)
+            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        self._fn = HOST_EXCHANGE_FN(self._exchange)  # keep the trampoline alive
+        h = C.c_void_p()
+        L.call("rvx_comm_init_host", int(world), int(rank), self._fn, None, C.byref(h))
+        self._h = h
+
+    @staticmethod
+    def _recv(s, n: int, out=None):
+        buf = out if out is not None else bytearray(n)
+        view = memoryview(buf)
+        got = 0
+        while got < n:
+            k = s.recv_into(view[got:], n - got)
+            if k == 0:
+                raise ConnectionError("peer closed the connection")
+            got += k
+        return buf
+
+    def _exchange(self, _user, send, send_bytes, recv, recv_bytes) -> int:
+        """rvx_host_exchange_fn: ship send[0:send_bytes) to every peer, fill recv[p] with
+        recv_bytes[p] from peer p. Frames carry their length; sends run on threads so no
+        pair of ranks waits on each other's full socket buffers."""
+        import threading
+        try:
+            errs = []
+            payload = (C.c_char * send_bytes).from_address(send) if send_bytes else None
+
+            def ship(s):
+                try:
+                    s.sendall(int(send_bytes).to_bytes(8, "little"))
+                    s.sendall(memoryview(payload).cast("B"))
+                except Exception as e:  # noqa: BLE001
+                    errs.append(e)
+
+            ts = [threading.Thread(target=ship, args=(s,)) for p, s in sorted(self._peers.items())] if send_bytes else []
+            for t in ts:
+                t.start()
+            for p, s in sorted(self._peers.items()):
+                nb = int(recv_bytes[p])
+                if nb == 0:
+                    continue
+                hdr = int.from_bytes(self._recv(s, 8), "little")
+                if hdr != nb:
+                    raise ValueError(f"rank {self.rank}: expected {nb} bytes from rank {p}, got a frame of {hdr}")
+                dst = (C.c_char * nb).from_address(recv[p])
+                self._recv(s, nb, memoryview(dst).cast("B"))
+            for t in ts:
+                t.join()
+            if errs:
+                raise errs[0]
+            return 0
+        except Exception:  # a status, never an exception through the C frames
+            import traceback
+            traceback.print_exc()
+            return 1
+
+    def allreduce(self, values: Sequence[float], op: int = REDUCE_SUM) -> List[float]:
+        """Element-wise sum / max / min of float64 values over the ranks (through rank 0)."""
+        import struct
+        vals = [float(v) for v in values]
+        n = len(vals)
+        fmt = f"<{n}d"
+        if self.rank == 0:
+            acc = list(vals)
+            for p in sorted(self._peers):
+                got = struct.unpack(fmt, bytes(self._recv(self._peers[p], 8 * n)))
+                for i, v in enumerate(got):
+                    acc[i] = acc[i] + v if op == REDUCE_SUM else max(acc[i], v) if op == REDUCE_MAX else min(acc[i], v)
+            out = struct.pack(fmt, *acc)
+            for p in sorted(self._peers):
+                self._peers[p].sendall(out)
+            return acc
+        s = self._peers[0]
+        s.sendall(struct.pack(fmt, *vals))
+        return list(struct.unpack(fmt, bytes(self._recv(s, 8 * n))))
+
+    def max(self, value: float) -> float:
+        return self.allreduce([value], REDUCE_MAX)[0]
+
+    def barrier(self) -> None:
+        """Every rank's library stream drained and every rank arrived."""
+        L.call("rvx_synchronize")
+        self.allreduce([0.0])
+
+    def close(self) -> None:
+        try:
+            if getattr(self, "_h", None):
+                L.call("rvx_comm_destroy", self._h)
+                self._h = None
+        finally:
+            for s in self._peers.values():
+                s.close()
+            self._peers = {}
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_from_env(transport: str = "rccl"):
+    """The communicator of a launched rank (None at world 1): RCCL over xGMI, or the
+    stdlib-socket host transport (`transport="host"`, several ranks per GPU)."""
+    import os
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return None
+    return SocketComm.from_env() if transport == "host" else RcclComm.from_env()
+
+
 PIPE_CHUNKS = 48         # RVX_SAGE_CHUNKS default (api_graph.cpp sage_chunks_for)
 PIPE_MIN_ROWS = 16384    # rows per chunk below which a layer is not chunked
 

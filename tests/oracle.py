@@ -72,6 +72,8 @@ _SIG = {
     "orc_hyp_brute_force": (None, [P, PF, I64, I32, PI64, PF, I32]),
     "orc_hyp_build_tangent": (None, [P]),
     "orc_hyp_centroid": (None, [P, PF]),
+    "orc_hyp_scan_rows": (None, [PF, I64, I32, F32, PF, I64, I32, I64, PI64, PF, I32]),
+    "orc_libm_check": (I64, [I32, U64, U64, U64, PF, I32, C.POINTER(C.c_uint32)]),
     "orc_hyp_search_pruning": (None, [P, PF, I64, I32, PI64, PF, I32]),
     "orc_hyp_set_curvature": (None, [P, F32]),
     "orc_hyp_set_metric": (None, [P, I32]),
@@ -559,3 +561,29 @@ def dual_space_search(hyp, euc, query, k, fusion_weight, curvature=1.0):
                                     (np.float32(1.0) - w) * (np.float32(1.0) / np.float32(rank + 1)))
     top = sorted(scores.items(), key=lambda t: -t[1])[:k]
     return [(i, poincare_distance(q[0], hyp.get_vector(i), curvature)) for i, _ in top]
+
+
+LIBM_FNS = ("logf", "log1pf", "expm1f", "tanhf", "atanh")
+
+
+def libm_check(fn, start=0, stride=1, count=1 << 32, dev=None, threads=None):
+    """Mismatches of the libm restatements (ruvector_amd/csrc/libm_f32.hpp) against the
+    host glibc over x = bits(start + i*stride), i < count: the host-compiled restatement
+    when dev is None, else the device outputs dev[i]. Returns (mismatches, first bad bits)."""
+    fb = C.c_uint32()
+    threads = threads or min(16, os.cpu_count() or 8)
+    dev = None if dev is None else np.ascontiguousarray(dev, np.float32)
+    ptr = None if dev is None else fp(dev)
+    bad = lib().orc_libm_check(LIBM_FNS.index(fn), start, stride, count, ptr, threads, C.byref(fb))
+    return int(bad), int(fb.value)
+
+
+def hyp_scan_rows(x, q, k, id_base=0, ids=None, dist=None, c=1.0, threads=8):
+    """Merge the exact Poincaré top-k of rows x (ids id_base + i) into (ids, dist)
+    (orc_hyp_scan_rows); start from ids=None for a fresh scan."""
+    x, q = f32(x), f32(q)
+    nq = q.shape[0]
+    if ids is None:
+        ids, dist = np.full((nq, k), -1, np.int64), np.full((nq, k), np.inf, np.float32)
+    lib().orc_hyp_scan_rows(fp(x), x.shape[0], x.shape[1], c, fp(q), nq, k, id_base, ip64(ids), fp(dist), threads)
+    return ids, dist

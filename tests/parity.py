@@ -42,23 +42,3 @@ def row_rel_vs(a, ref64):
     a = np.asarray(a, np.float64)
     nb = np.linalg.norm(ref64, axis=1)
     return np.linalg.norm(a - ref64, axis=1) / np.where(nb > 0, nb, max(float(nb.max()), 1e-30))
-
-
-def same_topk_poincare(ids, dist, rids, rd, q, x, c=1.0, tol=4e-6):
-    """ids / dist (GPU) against the oracle's rids / rd (exact Poincaré top-k): identical,
-    or a valid top-k under the ORACLE's own distances up to near-ties — device logf /
-    sqrtf are within 1 ulp of glibc, so two rows whose distances differ by ~1 ulp may
-    swap places: every GPU id re-scored with the oracle's poincare_distance lies within
-    tol of the oracle's distance at that position, and the GPU's distances within tol of
-    the oracle's."""
-    import oracle as O
-    ids, rids = np.asarray(ids), np.asarray(rids)
-    dist, rd = np.asarray(dist, np.float64), np.asarray(rd, np.float64)
-    relerr = lambda a, b: float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-30))) if b.size else 0.0  # noqa: E731
-    if np.array_equal(ids, rids):
-        return relerr(dist, rd) <= 1e-6
-    for i in np.where(~np.all(ids == rids, axis=1))[0]:
-        od = np.array([O.poincare_distance(q[i], x[j], c) for j in ids[i]], np.float64)
-        if relerr(od, rd[i]) > tol:
-            return False
-    return relerr(dist, rd) <= tol

@@ -38,7 +38,7 @@ def merge(parts, k):
     return np.take_along_axis(ids, order, 1), np.take_along_axis(d, order, 1)
 
 
-def close(a, b, tol=1e-6):
+def close(a, b, tol=0.0):  # bit-exact distances by default (glibc-identical device libm)
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     fin = np.isfinite(b)
     return bool(np.array_equal(np.isfinite(a), fin) and
@@ -117,6 +117,8 @@ def main():
         rec = np.mean([len(set(a.tolist()) & set(b.tolist())) / 10 for a, b in zip(ei, gid)])
         res["pruned_recall_vs_oracle"] = float(rec)
         checks["pruned_sorted"] = bool(np.all(np.diff(gd, axis=1) >= 0))
+        # every shard's centroid and tangent coordinates equal the oracle's bits
+        checks["pruned_exact"] = bool(np.array_equal(gid, ei) and close(gd, ed))
         # nq = 0 is a no-op on every rank
         e = grp.search_batch(np.zeros((0, d), np.float32) if rank == 0 else 0, 10)
         checks["empty"] = e[0].shape == (0, 10)

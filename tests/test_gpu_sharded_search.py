@@ -8,8 +8,8 @@ World 2 and 3 share GPU 0 through the host-staged transport (rvx_comm_init_host)
 the same broadcast / all-gather calls RCCL serves in production
 (tests/sharded_search_worker.py): graph search on oracle-built shard graphs, exact
 scans and the VectorIndex shards must equal the merge of the per-shard oracle searches
-(ids bit-exact; Poincaré distances within 1e-6 relative, L2 distances bit-exact);
-pruned search is recall-checked (its centroid comes from a different summation order).
+(ids and distances bit-exact, pruned search included: every shard's Fréchet centroid
+and tangent coordinates equal the oracle's bits).
 Ragged shards include one smaller than k. The RCCL transport itself is the driver's
 8-GPU run.
 """
