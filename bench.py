@@ -79,6 +79,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-hnsw", action="store_true", help="skip the HNSW queries/s@recall95 leg")
     p.add_argument("--no-scan", action="store_true", help="skip the 10M x 768 exact-scan queries/s leg")
+    p.add_argument("--no-c4", action="store_true", help="skip the C4 leg (3 x RuvectorLayer + graph-attention head)")
+    p.add_argument("--c4-nodes", type=int, default=0, help="C4 leg nodes (default: --nodes)")
     p.add_argument("--transport", choices=("rccl", "host"), default="rccl",
                    help="N>1 exchange: RCCL over xGMI, or host memory + stdlib sockets (ranks may share a GPU)")
     p.add_argument("--check-rows", type=int, default=8192, help="N>1: oracle-checked rows of the last rank")
@@ -227,11 +229,15 @@ def main():
         line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, tables, n_tot, d, deg, layers, invs)
     if world == 1:
         line["gemm_paths"] = gemm_alternatives(g, x, tables[0], off_ptr, d, deg)
+    del tables, g, invs
     if not a.no_scan:
-        del tables, g
         line["exact_scan"] = scan_leg(a, x, n_tot, d, rank, world, comm)
+    del x
+    rv.release_scratch()  # the C4 leg needs ~235 GB of the 288 GB at 10M x 768
+    if not a.no_c4:
+        line["c4"] = c4_leg(a, comm, rank, world)
+        rv.release_scratch()
     if not a.no_hnsw:
-        del x
         line["hnsw"] = hnsw_leg(a, rank, world, comm)
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -327,6 +333,19 @@ def exchange_report(a, kern, comm, world, rank, offsets, d, layers):
             "exchange_wait_ms_per_layer": [round(v, 3) for v in wait],
             "note": "exchange_ms: transfer-stream time of the chunked RCCL p2p rounds (overlapped with compute); "
                     "exchange_wait: the part the compute stream waited for after its last chunk"}
+
+
+def c4_leg(a, comm, rank, world):
+    """configs[3] at the metric's scale: 3 x RuvectorLayer(768, h 8) + EdgeFeaturedAttention
+    (8 heads, edge_dim 1) over the --nodes x 768 table and a uniform random out-degree-32
+    graph with U[0,1) edge features (bench_gnn.run; `bench_gnn.py --graph hnsw` runs it on
+    a GPU-built HNSW layer-0 graph), node-range sharded at N > 1 with the M|K|V and T rows
+    exchanged per layer. 1 warm-up + 2 timed forwards; roofline of the layer GEMMs and
+    the edge kernel; CPU baseline and per-row parity of layer 1 on rank 0 at N = 1."""
+    import bench_gnn
+    n = a.c4_nodes or a.nodes
+    return bench_gnn.run(n, a.dim, a.degree, 8, 3, steps=2, warmup=1, comm=comm, rank=rank, world=world,
+                         graph="random", cpu=(rank == 0 and world == 1 and not a.no_cpu), cpu_seconds=8.0)
 
 
 def hnsw_leg(a, rank, world, comm):

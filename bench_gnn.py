@@ -1,19 +1,25 @@
 #!/usr/bin/env python3
 """C4 benchmark: multi-layer ruvector-gnn RuvectorLayer stack +
-EdgeFeaturedAttention head over a graph, one process per GPU (node-range shards,
-launched with torch.distributed.run for N>1 — the processes use no torch; rows exchanged over RCCL p2p).
+EdgeFeaturedAttention head over a graph, one process per GPU (node-range shards;
+`--gpus N` starts the N ranks itself, or a launcher sets WORLD_SIZE — the processes
+use no torch; rows exchanged over RCCL p2p, or the host socket transport).
 
-Workload: N x 768 node table (N(0,1), seed 5), uniform random out-degree-32
-CSR (seed 6) with edge weights uniform [0,1) (seed 7) standing in for the HNSW
-layer-0 graph; `--layers` x RuvectorLayer(768, 768, heads=8, dropout=0, seeded
-init) (crates/ruvector-gnn/src/layer.rs:313-457), then EdgeFeaturedAttention
-(node_dim 768, edge_dim 1 = the edge weight, 8 heads, concat, slope 0.2;
-crates/ruvector-attention/src/graph/edge_featured.rs:87-320).
+Workload: N x 768 node table (N(0,1), seed 5); `--layers` x RuvectorLayer(768, 768,
+heads=8, dropout=0, seeded init) (crates/ruvector-gnn/src/layer.rs:313-457), then
+EdgeFeaturedAttention (node_dim 768, edge_dim 1, 8 heads, concat, slope 0.2;
+crates/ruvector-attention/src/graph/edge_featured.rs:87-320). Graph (`--graph`):
+  random  uniform random out-degree-32 CSR (seed 6), edge feature = weight U[0,1)
+          (seed 7) — the default, shardable at any N;
+  hnsw    the layer-0 CSR of an HNSW built on the GPU over the same table (M 32,
+          ef_c 200, hnsw_rs rules; up to 64 neighbours per node in stored order) with
+          edge feature = the stored HNSW edge distance, as §8(d) C4 names it
+          (rvx_index_export_layer0; one GPU).
 
 value = (edges x (layers + 1)) / wall time of one forward of the stack, inputs
 resident in HBM. Per-kernel times are HIP events stamped by the dispatch
 packets. CPU baseline: the oracle's RuvectorLayer restatement on a bounded
-sample of layer-1 rows (16 threads), with a parity check on the same rows.
+sample of layer-1 rows (16 threads), with a per-row parity check on the same rows.
+bench.py runs the same leg (run()) at 10M x 768 on the random graph.
 """
 import argparse
 import json
@@ -30,50 +36,58 @@ HBM_PEAK_GBS = 8000.0
 GEMM_PEAK_TFS = 2500.0 / 3  # split-f16 (3 f16 MFMA products per f32 FMA) ceiling, as in bench.py
 
 
-def main():
-    p = argparse.ArgumentParser()
-    p.add_argument("--nodes", type=int, default=2_000_000)
-    p.add_argument("--dim", type=int, default=768)
-    p.add_argument("--degree", type=int, default=32)
-    p.add_argument("--heads", type=int, default=8)
-    p.add_argument("--layers", type=int, default=3)
-    p.add_argument("--steps", type=int, default=2)
-    p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--gpus", type=int, default=1, help="ranks to start when no launcher set WORLD_SIZE")
-    p.add_argument("--transport", choices=("rccl", "host"), default="rccl")
-    a = p.parse_args()
-    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        from benchutil import spawn_ranks  # N ranks as child processes, before any GPU call
-        sys.exit(spawn_ranks(a.gpus, os.path.abspath(__file__), sys.argv[1:]))
+def hnsw_layer0_graph(x, n, d, m=32, efc=200, log=None):
+    """Build an HNSW over the n x d HBM table on the GPU and return (Graph with the
+    layer-0 lists and their stored distances as edge weights, [E][1] edge-feature
+    buffer, host (row_ptr, col, dist), build seconds)."""
+    import ruvector_amd as rv
+    idx = rv.HnswIndex(d, rv.DistanceMetric.Euclidean, rv.HnswConfig(m=m, ef_construction=efc), seed=5)
+    t0 = time.perf_counter()
+    idx.add_device(x, n)
+    rv.synchronize()
+    build_s = time.perf_counter() - t0
+    if log:
+        log(f"HNSW over {n} x {d} (M {m}, ef_c {efc}): {build_s:.1f} s")
+    rp, col, dist = idx.layer0()
+    del idx
+    g = rv.Graph.from_csr(rp, col, dist)
+    ew = rv.Buffer.from_numpy(dist.reshape(-1, 1))
+    return g, ew, (rp, col, dist), build_s
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+def run(n, d=768, deg=32, heads=8, nlayers=3, steps=2, warmup=1, comm=None, rank=0, world=1, graph="random",
+        cpu=True, cpu_seconds=10.0, log=None):
+    """One C4 measurement; returns the bench line (dict). Every rank calls it."""
     import ruvector_amd as rv
     from ruvector_amd.attention import EdgeFeaturedAttention, EdgeFeaturedConfig
-    from ruvector_amd.shard import REDUCE_MAX, ShardPlan, comm_from_env
+    from ruvector_amd.shard import REDUCE_MAX, ShardPlan
 
-    rv.set_device(local % max(rv.device_count(), 1) if a.transport == "host" else local)
-    n, d, deg, H = a.nodes, a.dim, a.degree, a.dim
+    H = d
     plan = ShardPlan(n, world)
     r0, r1 = plan.rows(rank)
     n_loc = r1 - r0
     offsets = np.array([plan.rows(p)[0] for p in range(world)] + [n], dtype=np.int64)
-    comm = comm_from_env(a.transport)  # RCCL (TCP rendezvous for the id) or the host socket transport
 
     # node-range shards: every rank holds the whole-table buffers but reads and
     # writes only its own rows; its CSR rows (global column ids) and their slice
     # of the edge-weight stream are generated in place, so the sharded job is
     # the same graph as the 1-GPU one
-    E = n * deg
     x = rv.Buffer(n * d * 4)
     x.fill_normal(n * d, 5)
-    g = rv.Graph.random_shard(n, r0, n_loc, deg, 6, weight_seed=7)
-    ew = g._keep[2]  # [E_local][1] edge features = the edge weights
-    layers = [rv.RuvectorLayer(d, H, a.heads, 0.0, seed=100 + i) for i in range(a.layers)]
-    head = EdgeFeaturedAttention(EdgeFeaturedConfig(node_dim=H, edge_dim=1, num_heads=a.heads))
+    host_csr, hnsw_s = None, None
+    if graph == "hnsw":
+        if world > 1:
+            raise ValueError("--graph hnsw runs on one GPU")
+        g, ew, host_csr, hnsw_s = hnsw_layer0_graph(x, n, d, log=log)
+        E = int(host_csr[0][-1])
+        e_loc = E
+    else:
+        g = rv.Graph.random_shard(n, r0, n_loc, deg, 6, weight_seed=7)
+        ew = g._keep[2]  # [E_local][1] edge features = the edge weights
+        E = n * deg
+        e_loc = n_loc * deg
+    layers = [rv.RuvectorLayer(d, H, heads, 0.0, seed=100 + i) for i in range(nlayers)]
+    head = EdgeFeaturedAttention(EdgeFeaturedConfig(node_dim=H, edge_dim=1, num_heads=heads))
     bufs = [rv.Buffer(n * H * 4) for _ in range(2)]
     out = rv.Buffer(n * H * 4)
     rv.synchronize()
@@ -90,89 +104,148 @@ def main():
         if comm is not None:
             comm.barrier()
 
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         step()
     barrier()
     prof = rv.Profiler()
     with prof:
         barrier()
         t0 = time.perf_counter()
-        for _ in range(a.steps):
+        for _ in range(steps):
             step()
         rv.synchronize()
         t1 = time.perf_counter()
         barrier()
-    dt = (t1 - t0) / a.steps
+    dt = (t1 - t0) / steps
     kern = prof.summary()
     if comm is not None:
         dt = comm.allreduce([dt], REDUCE_MAX)[0]
-    n_own = n_loc  # per-launch work below is this rank's rows
 
-    # algorithmic work per layer
-    layer_flops = 2.0 * n_own * (d * H + 11 * H * H)
-    edge_bytes = n_own * deg * (3 * 4 * H + 8) + n_own * (8 + 4 * H + 2 * 4 * H)
-    gemm_ms = sum(v["total_ms"] for k, v in kern.items() if k.startswith("gnn_gemm")) / a.steps / a.layers
-    edge_ms = kern.get("gnn_edge_attention", {"total_ms": 0})["total_ms"] / a.steps / a.layers
+    # algorithmic work per layer, this rank's rows and edges
+    layer_flops = 2.0 * n_loc * (d * H + 11 * H * H)
+    edge_bytes = e_loc * (3 * 4 * H + 8) + n_loc * (8 + 4 * H + 2 * 4 * H)
+    gemm_ms = sum(v["total_ms"] for k, v in kern.items() if k.startswith("gnn_gemm")) / steps / nlayers
+    edge_ms = kern.get("gnn_edge_attention", {"total_ms": 0})["total_ms"] / steps / nlayers
     roof = {
         "gnn_gemm (all dense layers of one RuvectorLayer)": {
             "bound": "mfma", "achieved": round(layer_flops / (gemm_ms / 1e3) / 1e12, 2), "peak": round(GEMM_PEAK_TFS, 1),
             "unit": "TFLOP/s", "frac": round(layer_flops / (gemm_ms / 1e3) / 1e12 / GEMM_PEAK_TFS, 4),
-            "ms_per_layer": round(gemm_ms, 3)},
+            "ms_per_layer": round(gemm_ms, 3), "work_per_layer": layer_flops, "traffic": None},
         "gnn_edge_attention": {
             "bound": "hbm", "achieved": round(edge_bytes / (edge_ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(edge_bytes / (edge_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-            "ms_per_layer": round(edge_ms, 3)},
+            "ms_per_layer": round(edge_ms, 3), "work_per_layer": edge_bytes, "traffic": None,
+            "bytes": "per edge 3*4*H (k, v, m rows of the neighbour) + 8; per node 8 + 4H (q) + 2*4H (out, h)"},
     }
     line = {
         "metric": "GNN-layer edges/sec (RuvectorLayer stack + graph-attention head)",
-        "value": round(E * (a.layers + 1) / dt, 1), "unit": "edges/s", "n_gpus": world, "steps": a.steps,
-        "warmup": a.warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "strong", "dtype": "f32",
-        "config": {"workload": f"configs[3] stack on {world} GPU(s): {n} x {d}, {a.layers} x RuvectorLayer(h={a.heads})"
-                               " + EdgeFeaturedAttention(8 heads, edge_dim 1)", "nodes": n, "degree": deg,
-                   "edges": E, "layers": a.layers, "parallelism": f"node-range x{world}",
+        "value": round(E * (nlayers + 1) / dt, 1), "unit": "edges/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+        "dtype": "f32", "gemm_dtype": "split-f16x3",
+        "config": {"workload": f"configs[3] stack on {world} GPU(s): {n} x {d}, {nlayers} x RuvectorLayer(h={heads})"
+                               " + EdgeFeaturedAttention(8 heads, edge_dim 1)", "nodes": n, "edges": E,
+                   "graph": ("uniform random out-degree 32 CSR (seed 6), edge feature U[0,1) (seed 7)" if graph == "random"
+                             else "layer 0 of a GPU-built HNSW (M 32, ef_c 200) over the table, edge feature = "
+                                  "stored HNSW edge distance"),
+                   "layers": nlayers, "parallelism": f"node-range x{world}",
                    "exchange": "per layer: M|K|V rows (RuvectorLayer), T rows (attention head), "
-                               "one grouped RCCL p2p round each" if world > 1 else "none"},
-        "data": "synthetic: X ~ N(0,1) seed 5; uniform random out-degree CSR seed 6; edge weights U[0,1) seed 7",
+                               "chunked p2p rounds" if world > 1 else "none"},
+        "data": "synthetic: X ~ N(0,1) seed 5" + ("; uniform random out-degree CSR seed 6; edge weights U[0,1) seed 7"
+                                                   if graph == "random" else "; HNSW layer-0 graph built on the GPU"),
         "roofline": roof,
-        "kernel_ms_per_step": {k: round(v["total_ms"] / a.steps, 3) for k, v in kern.items()},
+        "kernel_ms_per_step": {k: round(v["total_ms"] / steps, 3) for k, v in kern.items()},
     }
-    if rank == 0 and world == 1 and not a.no_cpu:
-        line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, ew, layers[0], n, d, deg, offsets)
+    if hnsw_s is not None:
+        line["hnsw_build_s"] = round(hnsw_s, 2)
+    if rank == 0 and world == 1 and cpu:
+        line["cpu_baseline"], line["parity"] = cpu_baseline(cpu_seconds, x, g, layers[0], n, d, deg, offsets,
+                                                             host_csr)
+    del bufs, out, x, g, ew, layers, head
+    rv.synchronize()
+    return line
+
+
+def cpu_baseline(cpu_seconds, x_buf, g, layer, n, d, deg, offsets, host_csr=None):
+    """Oracle RuvectorLayer::forward on a bounded sample of layer-1 rows (the CPU
+    baseline) and the per-row parity of the GPU's layer 1 on the same rows."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as O
+    import ruvector_amd as rv
+    from bench import rel_errs
+    from benchutil import host_threads
+
+    threads, tinfo = host_threads()
+    W = O.RvlWeights(json.loads(layer.to_json()))
+    if host_csr is None:
+        rp, col = O.random_csr(n, deg, 6)
+        ew = O.fill_uniform(n * deg, 7, 0.0, 1.0)
+    else:
+        rp, col, ew = host_csr
+    y1 = rv.Buffer(n * layer.hidden_dim * 4)
+    layer.forward_exchange(g, x_buf, y1, offsets)
+
+    def ref_rows(r):
+        # only the sample's rows and their neighbours leave HBM
+        nb = col[:rp[r]].astype(np.int64)
+        need = np.concatenate([np.arange(r, dtype=np.int64), nb])
+        h = x_buf.gather_rows(n, d, need)
+        return O.rvl_forward_graph(W, h, rp[:r + 1], (r + np.arange(nb.size)).astype(np.int32), ew[:rp[r]],
+                                   rows=(0, r), threads=threads)
+
+    rows = 64
+    t0 = time.perf_counter()
+    ref_rows(rows)
+    dt = time.perf_counter() - t0
+    rows = int(min(n, max(rows, rows * cpu_seconds / max(dt, 1e-3))))
+    t0 = time.perf_counter()
+    ref = ref_rows(rows)
+    dt = time.perf_counter() - t0
+    got = y1.download(np.float32, (rows, layer.hidden_dim))
+    del y1
+    err, row_err = rel_errs(got, ref)
+    edges = int(rp[rows])
+    cpu = {"value": round(edges / dt, 1), "unit": "edges/s", "cores": threads, "kind": "port", "host": tinfo,
+           "sample": f"oracle RuvectorLayer::forward per node (layer.rs:379-451 restated, {threads} threads) on rows "
+                     f"0..{rows} of layer 1 ({edges} edges), {dt:.1f} s"}
+    return cpu, {"rows": rows, "max_rel_err": err, "row_rel_l2_max": row_err, "tol": 1e-5,
+                 "ok": err <= 1e-5 and row_err <= 1e-5,
+                 "metrics": "normwise max|gpu-ref|/max|ref| and per-row ||gpu_r-ref_r||/||ref_r|| (tests/parity.py)"}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--nodes", type=int, default=2_000_000)
+    p.add_argument("--dim", type=int, default=768)
+    p.add_argument("--degree", type=int, default=32)
+    p.add_argument("--heads", type=int, default=8)
+    p.add_argument("--layers", type=int, default=3)
+    p.add_argument("--steps", type=int, default=2)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--graph", choices=("random", "hnsw"), default="random")
+    p.add_argument("--gpus", type=int, default=1, help="ranks to start when no launcher set WORLD_SIZE")
+    p.add_argument("--transport", choices=("rccl", "host"), default="rccl")
+    a = p.parse_args()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        from benchutil import spawn_ranks  # N ranks as child processes, before any GPU call
+        sys.exit(spawn_ranks(a.gpus, os.path.abspath(__file__), sys.argv[1:]))
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import ruvector_amd as rv
+    from ruvector_amd.shard import comm_from_env
+
+    rv.set_device(local % max(rv.device_count(), 1) if a.transport == "host" else local)
+    comm = comm_from_env(a.transport)  # RCCL (TCP rendezvous for the id) or the host socket transport
+    log = (lambda s: print(f"[rank {rank}] {s}", file=sys.stderr, flush=True))  # noqa: E731
+    line = run(a.nodes, a.dim, a.degree, a.heads, a.layers, a.steps, a.warmup, comm, rank, world, a.graph,
+               cpu=not a.no_cpu, cpu_seconds=a.cpu_seconds, log=log)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if comm is not None:
         comm.barrier()
-
-
-def cpu_baseline(a, x_buf, g, ew_buf, layer, n, d, deg, offsets):
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle as O
-    import ruvector_amd as rv
-
-    threads = min(16, os.cpu_count() or 1)
-    W = O.RvlWeights(json.loads(layer.to_json()))
-    x = x_buf.download(np.float32, (n, d))
-    rp, col = O.random_csr(n, deg, 6)
-    ew = O.fill_uniform(n * deg, 7, 0.0, 1.0)
-    y1 = rv.Buffer(n * layer.hidden_dim * 4)
-    layer.forward_exchange(g, x_buf, y1, offsets)
-    rows = 64
-    t0 = time.perf_counter()
-    O.rvl_forward_graph(W, x, rp, col, ew, rows=(0, rows), threads=threads)
-    dt = time.perf_counter() - t0
-    rows = int(min(n, max(rows, rows * a.cpu_seconds / max(dt, 1e-3))))
-    t0 = time.perf_counter()
-    ref = O.rvl_forward_graph(W, x, rp, col, ew, rows=(0, rows), threads=threads)
-    dt = time.perf_counter() - t0
-    got = y1.download(np.float32, (rows, layer.hidden_dim))
-    from bench import rel_errs
-    err, row_err = rel_errs(got, ref)
-    cpu = {"value": round(rows * deg / dt, 1), "unit": "edges/s", "cores": threads, "kind": "port",
-           "sample": f"oracle RuvectorLayer::forward per node (layer.rs:379-451 restated, {threads} threads) on rows "
-                     f"0..{rows} of layer 1, {dt:.1f} s"}
-    return cpu, {"rows": rows, "max_rel_err": err, "row_rel_l2_max": row_err, "tol": 1e-5,
-                 "ok": err <= 1e-5 and row_err <= 1e-5,
-                 "metrics": "normwise max|gpu-ref|/max|ref| and per-row ||gpu_r-ref_r||/||ref_r|| (tests/parity.py)"}
 
 
 if __name__ == "__main__":

@@ -68,6 +68,9 @@ rvx_status rvx_set_device(int32_t device);
 rvx_status rvx_get_device(int32_t* device);
 /* Wait for all work the library queued on the current device. */
 rvx_status rvx_synchronize(void);
+/* Free the per-device scratch pool (pipeline chunk buffers, scan images, ...) that compute
+ * calls keep for reuse; the next call re-allocates what it needs. */
+rvx_status rvx_scratch_release(void);
 /* Device properties: CU count, HBM bytes, arch name (e.g. "gfx950"). */
 rvx_status rvx_device_info(int32_t* num_cus, int64_t* hbm_bytes, char* arch, size_t arch_len);
 

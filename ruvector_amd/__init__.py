@@ -9,7 +9,7 @@ from . import _lib
 _lib.load()
 
 from ._lib import RvxError  # noqa: E402
-from .device import Buffer, Profiler, device_count, device_info, set_device, synchronize  # noqa: E402
+from .device import Buffer, Profiler, device_count, device_info, release_scratch, set_device, synchronize  # noqa: E402
 from .graph import Graph  # noqa: E402
 from .core import (DistanceMetric, FlatIndex, HnswConfig, HnswIndex, RuvectorError, SearchResult,  # noqa: E402
                    batch_distances, distance, distance_matrix, hnsw_last_search_stats, scan_last_stats)
@@ -25,7 +25,7 @@ from .query import NeuralSearch, QueryMode, RuvectorQuery  # noqa: E402
 from .vector_db import DbOptions, SearchQuery, VectorDB, VectorEntry  # noqa: E402
 
 __all__ = [
-    "RvxError", "Buffer", "Profiler", "device_count", "device_info", "set_device", "synchronize", "Graph",
+    "RvxError", "Buffer", "Profiler", "device_count", "device_info", "release_scratch", "set_device", "synchronize", "Graph",
     "DistanceMetric", "FlatIndex", "HnswConfig", "HnswIndex", "RuvectorError", "SearchResult", "batch_distances",
     "distance", "distance_matrix", "GCNLayer", "GnnError", "GraphSAGELayer", "RuvectorLayer", "aggregate",
     "differentiable_search", "differentiable_search_batch", "hierarchical_forward", "EdgeFeaturedAttention",

@@ -91,6 +91,7 @@ SIGNATURES = {
     "rvx_set_device": (None, [I32]),
     "rvx_get_device": (None, [PI32]),
     "rvx_synchronize": (None, []),
+    "rvx_scratch_release": (None, []),
     "rvx_device_info": (None, [PI32, PI64, C.c_char_p, SZ]),
     "rvx_buffer_alloc": (None, [I64, PP]),
     "rvx_buffer_free": (None, [P]),

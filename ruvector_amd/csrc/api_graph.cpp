@@ -26,6 +26,15 @@ void* scratch_bytes(const std::string& slot, int64_t bytes) {
     return m->p;
 }
 float* scratch_f32(const std::string& slot, int64_t count) { return (float*)scratch_bytes(slot, count * 4); }
+void scratch_release_all() {
+    const int dev = device().id;
+    RVX_HIP(hipDeviceSynchronize());
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (auto it = g_scratch.begin(); it != g_scratch.end();) {
+        if (it->first.first == dev) it = g_scratch.erase(it);
+        else ++it;
+    }
+}
 int64_t scratch_held(const std::string& slot) {
     const int dev = device().id;
     std::lock_guard<std::mutex> lk(g_scratch_mu);
@@ -489,6 +498,14 @@ void gcn_forward_dev(const rvx_gcn_layer* l, const rvx_graph* g, bool use_w, con
 }  // namespace
 
 extern "C" {
+
+rvx_status rvx_scratch_release(void) {
+    return guard([&] {
+        ComputeLock cl;
+        scratch_release_all();
+    });
+}
+
 
 rvx_status rvx_graph_from_edges(int64_t n, const int64_t* src, const int64_t* dst, int64_t ne, const float* ew,
                                 rvx_graph** out) {

@@ -32,6 +32,8 @@ namespace rvx {
 // lock (ComputeLock) for the duration of the op that uses them.
 float* scratch_f32(const std::string& slot, int64_t count);
 void* scratch_bytes(const std::string& slot, int64_t bytes);
+// Frees every scratch slot of the calling thread's device (after a device sync).
+void scratch_release_all();
 // Bytes the slot holds now (0 if never used).
 int64_t scratch_held(const std::string& slot);
 

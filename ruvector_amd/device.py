@@ -8,6 +8,11 @@ import numpy as np
 from . import _lib as L
 
 
+def release_scratch() -> None:
+    """Free librvx's per-device scratch pool (kept between calls for reuse)."""
+    L.call("rvx_scratch_release")
+
+
 def device_count() -> int:
     n = C.c_int32(0)
     L.call("rvx_device_count", C.byref(n))
