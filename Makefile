@@ -39,8 +39,32 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# Host-side sanitizer build (tests/test_asan.py): the translation units that parse
+# caller-supplied files and text — hnsw_rs dumps (api_hnswio.cpp), feature files
+# (api_io.cpp), RuvectorLayer JSON (api_gnn.cpp + json.hpp) — and the error plumbing
+# (runtime.cpp) compiled with ASan + UBSan on the host side only (-Xarch_host: device
+# code is never instrumented), linked with the normal objects of every other file.
+# Loaded through RVX_LIB with the clang ASan runtime preloaded; never shipped.
+ASAN_DIR   := $(BUILD)/asan
+ASAN_SRCS  := api_hnswio.cpp api_io.cpp api_gnn.cpp runtime.cpp
+ASANFLAGS  := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+              -Xarch_host -fno-sanitize-recover=undefined -Xarch_host -fno-omit-frame-pointer
+ASAN_OBJS  := $(patsubst %,$(ASAN_DIR)/%.o,$(ASAN_SRCS))
+PLAIN_OBJS := $(filter-out $(patsubst %,$(BUILD)/%.o,$(ASAN_SRCS)),$(OBJS))
+ASAN_LIB   := $(ASAN_DIR)/librvx_asan.so
+
+$(ASAN_DIR)/%.o: $(CSRC)/% $(HDRS)
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) $(HIPFLAGS) $(ASANFLAGS) -DRVX_SRC_HASH=\"$(SRC_HASH)\" -x hip -c $< -o $@
+
+$(ASAN_LIB): $(ASAN_OBJS) $(PLAIN_OBJS)
+	$(HIPCC) $(LDFLAGS) -fsanitize=address,undefined -shared-libsan -o $@ $(ASAN_OBJS) $(PLAIN_OBJS)
+
+asan: $(ASAN_LIB)
+	$(MAKE) -C oracle asan
+
 clean:
 	rm -rf $(BUILD) $(LIB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean asan

@@ -171,8 +171,18 @@ std::vector<float> arr_data(const json::Value* a, std::vector<int64_t>& dim) {
     RVX_REQUIRE(d && d->kind == json::Value::Array && data && data->kind == json::Value::Array, RVX_ERR_SERIALIZATION,
                 "ndarray needs dim and data");
     dim.clear();
+    // dims are untrusted numbers: integral, in [0, 2^31), and their product bounded by
+    // the data actually present before any arithmetic that could overflow
     int64_t total = 1;
-    for (auto& x : d->arr) { dim.push_back((int64_t)x.num); total *= (int64_t)x.num; }
+    for (auto& x : d->arr) {
+        RVX_REQUIRE(x.kind == json::Value::Number && x.num >= 0.0 && x.num < 2147483648.0 && x.num == std::floor(x.num),
+                    RVX_ERR_SERIALIZATION, "ndarray dim must be a non-negative integer");
+        const int64_t e = (int64_t)x.num;
+        dim.push_back(e);
+        RVX_REQUIRE(e == 0 || total <= (int64_t)data->arr.size() / e, RVX_ERR_SERIALIZATION,
+                    "ndarray data length != prod(dim)");
+        total *= e;
+    }
     RVX_REQUIRE((int64_t)data->arr.size() == total, RVX_ERR_SERIALIZATION, "ndarray data length != prod(dim)");
     std::vector<float> v(total);
     for (int64_t i = 0; i < total; ++i)
@@ -448,8 +458,13 @@ rvx_status rvx_gnn_layer_from_json(const char* text, rvx_layer** out) {
         l->w_h = linear_from(up->get("w_h"), "w_h"); l->u_h = linear_from(up->get("u_h"), "u_h");
         const json::Value* at = root.get("attention");
         RVX_REQUIRE(at && at->get("num_heads") && at->get("head_dim"), RVX_ERR_SERIALIZATION, "missing attention");
-        l->heads = (int)at->get("num_heads")->num;
-        l->hd = (int)at->get("head_dim")->num;
+        auto small_int = [](const json::Value* v, const char* what) {  // untrusted: check before the cast
+            RVX_REQUIRE(v->kind == json::Value::Number && v->num >= 0.0 && v->num <= 65536.0 && v->num == std::floor(v->num),
+                        RVX_ERR_SERIALIZATION, std::string(what) + " must be an integer in [0, 65536]");
+            return (int)v->num;
+        };
+        l->heads = small_int(at->get("num_heads"), "num_heads");
+        l->hd = small_int(at->get("head_dim"), "head_dim");
         l->q = linear_from(at->get("q_linear"), "q_linear"); l->k = linear_from(at->get("k_linear"), "k_linear");
         l->v = linear_from(at->get("v_linear"), "v_linear"); l->o = linear_from(at->get("out_linear"), "out_linear");
         const json::Value* nm = root.get("norm");
@@ -463,7 +478,7 @@ rvx_status rvx_gnn_layer_from_json(const char* text, rvx_layer** out) {
         l->dropout = (float)dr->num;
         l->in = l->w_msg.in;
         l->H = l->w_msg.out;
-        RVX_REQUIRE(l->heads * l->hd == l->H, RVX_ERR_SERIALIZATION, "num_heads*head_dim != hidden_dim");
+        RVX_REQUIRE((int64_t)l->heads * l->hd == l->H, RVX_ERR_SERIALIZATION, "num_heads*head_dim != hidden_dim");
         validate(l.get());
         upload_layer(l.get());
         *out = l.release();

@@ -710,7 +710,12 @@ rvx_status rvx_sage_forward_exchange2(const rvx_sage_layer* l, const rvx_graph* 
                        x_full->mem.as<float>(), N, l->in, xm);
             xm = nullptr;
         }
-        float* yinv = y_rowinv ? y_rowinv->mem.as<float>() : nullptr;
+        // `can` is this rank's own decision (its GEMM path and alignment). Whenever the
+        // caller passed y_rowinv, every rank exchanges it: a rank that normalises in place
+        // ships 1.0 for its rows, so the ranks' collective sequences stay identical
+        // whatever each one decided.
+        float* yinv_xchg = y_rowinv ? y_rowinv->mem.as<float>() : nullptr;
+        float* yinv = yinv_xchg;
         if (yinv && !can) {
             fill_value(yinv, N, 1.0f);
             yinv = nullptr;
@@ -730,7 +735,7 @@ rvx_status rvx_sage_forward_exchange2(const rvx_sage_layer* l, const rvx_graph* 
             StreamScope on_xfer(d.xfer);
             ProfScope ps("halo_exchange");
             comm_exchange_rows(comm, y, l->out, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
-            if (yinv) comm_exchange_rows(comm, yinv, 1, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
+            if (yinv_xchg) comm_exchange_rows(comm, yinv_xchg, 1, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
         };
         sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], chunks, hook, xm, yinv_rows);
         RVX_HIP(hipEventRecord(ev[chunks], d.xfer));

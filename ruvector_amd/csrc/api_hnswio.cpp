@@ -103,6 +103,21 @@ int metric_of(const std::string& name) {
     return -1;
 }
 
+// The names are Rust Strings in hnsw_rs (load_description decodes them as UTF-8 and
+// errors otherwise, hnswio.rs:937-1040); a damaged dump is rejected the same way.
+bool valid_utf8(const unsigned char* s, size_t n) {
+    size_t i = 0;
+    while (i < n) {
+        const unsigned c = s[i];
+        const int len = c < 0x80 ? 1 : (c >> 5) == 0x6 ? 2 : (c >> 4) == 0xE ? 3 : (c >> 3) == 0x1E ? 4 : 0;
+        if (len == 0 || i + (size_t)len > n) return false;
+        for (int k = 1; k < len; ++k)
+            if ((s[i + k] & 0xC0) != 0x80) return false;
+        i += (size_t)len;
+    }
+    return true;
+}
+
 void read_description(File& g, rvx_hnswio_description* d) {
     std::memset(d, 0, sizeof *d);
     const uint32_t magic = g.r<uint32_t>();
@@ -122,6 +137,8 @@ void read_description(File& g, rvx_hnswio_description* d) {
         RVX_REQUIRE(len <= 256, RVX_ERR_SERIALIZATION, "name longer than 256 bytes");
         g.get(dst, (size_t)len);
         dst[len] = 0;
+        RVX_REQUIRE(valid_utf8(reinterpret_cast<const unsigned char*>(dst), (size_t)len), RVX_ERR_SERIALIZATION,
+                    "name in the dump description is not UTF-8");
     }
 }
 
@@ -266,8 +283,10 @@ rvx_status rvx_index_file_load(const char* dir, const char* basename, int32_t me
                     "only Full-mode dumps reload (hnswio.rs load_point_graph reads PointIds unconditionally)");
         RVX_REQUIRE(std::string(ds.t_name) == "f32", RVX_ERR_SERIALIZATION, "data type is not f32");
         RVX_REQUIRE(ds.format_version >= 3, RVX_ERR_UNSUPPORTED, "format 2 (bincode point data) is not supported");
-        RVX_REQUIRE(ds.dimension > 0 && ds.nb_layer >= 1 && ds.nb_layer <= NB_LAYER_MAX, RVX_ERR_SERIALIZATION,
-                    "bad description");
+        // description fields are untrusted: bound them before sizing anything by them
+        RVX_REQUIRE(ds.dimension > 0 && ds.dimension <= ((int64_t)1 << 24) && ds.nb_layer >= 1 &&
+                        ds.nb_layer <= NB_LAYER_MAX && ds.nb_point >= 0 && ds.nb_point <= ((int64_t)1 << 40),
+                    RVX_ERR_SERIALIZATION, "bad description");
         if (metric < 0) metric = metric_of(ds.distname);
         RVX_REQUIRE(metric >= 0, RVX_ERR_INVALID_PARAMETER,
                     std::string("distance '") + ds.distname + "' does not name a metric; pass one");

@@ -183,9 +183,10 @@ void build_tangent(rvx_hyperbolic* h) {
 
 void check_cfg(const rvx_hyperbolic_config* c) {
     RVX_REQUIRE(c->dim > 0, RVX_ERR_INVALID_PARAMETER, "dimension must be positive");
-    RVX_REQUIRE(c->max_connections >= 1 && c->max_connections <= 64 && c->max_connections_0 >= 1 &&
-                    c->max_connections_0 <= 64,
-                RVX_ERR_UNSUPPORTED, "max_connections / max_connections_0 must be in [1, 64]");
+    // the GPU builder's list capacities (k_hnsw_build.hip: MAX_C0 = 256 layer-0 slots)
+    RVX_REQUIRE(c->max_connections >= 1 && c->max_connections <= 128 && c->max_connections_0 >= 1 &&
+                    c->max_connections_0 <= 256,
+                RVX_ERR_UNSUPPORTED, "max_connections must be in [1, 128] and max_connections_0 in [1, 256]");
     RVX_REQUIRE(c->ef_construction >= 1 && c->ef_construction <= HNSW_MAX_EF && c->ef_search >= 1,
                 RVX_ERR_INVALID_PARAMETER, "ef out of range");
     RVX_REQUIRE(c->curvature > 0.0f, RVX_ERR_INVALID_PARAMETER, "invalid curvature (must be > 0)");
@@ -324,6 +325,29 @@ rvx_status rvx_hyperbolic_search_device(const rvx_hyperbolic* h, const rvx_buffe
     });
 }
 
+// The shard-dependent conditions search_dev enforces (pruned: Poincaré metric and
+// k * prune_factor <= 128 on this shard's size; graph: a fresh graph and ef in range;
+// exact: k <= 128), checked locally before the sharded entry points enter any collective.
+static void hyp_shard_precheck(const rvx_hyperbolic* h, int64_t nq, int k, int ef, int mode) {
+    RVX_REQUIRE(h && nq >= 0 && k >= 1 && mode >= 0 && mode <= 2, RVX_ERR_INVALID_PARAMETER,
+                "bad sharded search arguments");
+    const rvx_index* ix = &h->ix;
+    if (ix->n == 0 || nq == 0) return;
+    const int m = (mode == 2 && !ix->tan_valid) ? 0 : mode;
+    if (m == 2) {
+        RVX_REQUIRE(ix->cfg.metric == RVX_METRIC_POINCARE, RVX_ERR_UNSUPPORTED,
+                    "search_with_pruning is implemented for the Poincaré metric");
+        RVX_REQUIRE(std::min<int64_t>((int64_t)k * h->cfg.prune_factor, ix->n) <= SCAN_MAX_K, RVX_ERR_UNSUPPORTED,
+                    "k * prune_factor must be <= 128");
+    } else if (m == 1) {
+        RVX_REQUIRE(k <= SCAN_MAX_K, RVX_ERR_INVALID_PARAMETER, "k must be in [1, 128]");
+    } else {
+        RVX_REQUIRE(ix->has_graph && ix->graph_n == ix->n, RVX_ERR_INDEX, "HNSW graph missing or stale");
+        const int e = std::max(ef > 0 ? ef : ix->cfg.ef_search, k);
+        RVX_REQUIRE(e >= 1 && e <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER, "ef out of range");
+    }
+}
+
 // ShardedHyperbolicHnsw::search across processes (shard.rs:354-373): rank 0's
 // queries are broadcast, every rank searches its node-range shard (local ids +
 // id_base = global ids), one all-gather moves every rank's top-k, and each rank
@@ -353,10 +377,18 @@ rvx_status rvx_hyperbolic_sharded_search(const rvx_hyperbolic* h, rvx_comm* comm
                                          int64_t nq, int32_t k, int32_t ef, int32_t mode, int64_t* out_gid,
                                          int64_t* out_lid, float* out_dist, int32_t* out_count) {
     return guard([&] {
-        RVX_REQUIRE(h && nq >= 0 && k >= 1 && mode >= 0 && mode <= 2 && id_base >= 0, RVX_ERR_INVALID_PARAMETER,
-                    "bad sharded search arguments");
-        RVX_REQUIRE(nq == 0 || (out_gid && out_dist && (comm_rank(comm) != 0 || q)), RVX_ERR_INVALID_PARAMETER,
-                    "null argument");
+        rvx_status st = RVX_OK;
+        std::string why;
+        try {  // local verdict first; every rank learns every verdict before any data moves
+            hyp_shard_precheck(h, nq, k, ef, mode);
+            RVX_REQUIRE(id_base >= 0, RVX_ERR_INVALID_PARAMETER, "bad sharded search arguments");
+            RVX_REQUIRE(nq == 0 || (out_gid && out_dist && (comm_rank(comm) != 0 || q)), RVX_ERR_INVALID_PARAMETER,
+                        "null argument");
+        } catch (const Error& e) {
+            st = e.code;
+            why = e.what();
+        }
+        shard_agree(comm, st, why, {nq, (int64_t)k, (int64_t)ef, (int64_t)mode, h ? (int64_t)h->cfg.dim : 0});
         if (nq == 0) return;
         std::shared_lock<std::shared_mutex> lk(h->ix.mu);
         ComputeLock cl;
@@ -381,13 +413,21 @@ rvx_status rvx_hyperbolic_sharded_search_device(const rvx_hyperbolic* h, rvx_com
                                                 const rvx_buffer* q, int64_t nq, int32_t k, int32_t ef, int32_t mode,
                                                 rvx_buffer* out_gid, rvx_buffer* out_lid, rvx_buffer* out_dist) {
     return guard([&] {
-        RVX_REQUIRE(h && nq >= 0 && k >= 1 && mode >= 0 && mode <= 2 && id_base >= 0 && out_gid && out_dist,
-                    RVX_ERR_INVALID_PARAMETER, "bad sharded search arguments");
-        RVX_REQUIRE(comm_rank(comm) != 0 || (q && q->mem.bytes >= nq * h->cfg.dim * 4), RVX_ERR_DIMENSION_MISMATCH,
-                    "query buffer too small");
-        RVX_REQUIRE(out_gid->mem.bytes >= nq * k * 8 && out_dist->mem.bytes >= nq * k * 4 &&
-                        (!out_lid || out_lid->mem.bytes >= nq * k * 8),
-                    RVX_ERR_DIMENSION_MISMATCH, "output buffer too small");
+        rvx_status st = RVX_OK;
+        std::string why;
+        try {  // local verdict first; every rank learns every verdict before any data moves
+            hyp_shard_precheck(h, nq, k, ef, mode);
+            RVX_REQUIRE(id_base >= 0 && out_gid && out_dist, RVX_ERR_INVALID_PARAMETER, "bad sharded search arguments");
+            RVX_REQUIRE(comm_rank(comm) != 0 || (q && q->mem.bytes >= nq * h->cfg.dim * 4), RVX_ERR_DIMENSION_MISMATCH,
+                        "query buffer too small");
+            RVX_REQUIRE(out_gid->mem.bytes >= nq * k * 8 && out_dist->mem.bytes >= nq * k * 4 &&
+                            (!out_lid || out_lid->mem.bytes >= nq * k * 8),
+                        RVX_ERR_DIMENSION_MISMATCH, "output buffer too small");
+        } catch (const Error& e) {
+            st = e.code;
+            why = e.what();
+        }
+        shard_agree(comm, st, why, {nq, (int64_t)k, (int64_t)ef, (int64_t)mode, h ? (int64_t)h->cfg.dim : 0});
         if (nq == 0) return;
         std::shared_lock<std::shared_mutex> lk(h->ix.mu);
         ComputeLock cl;

@@ -117,6 +117,21 @@ void check_query_args(const rvx_index* ix, int64_t nq, int k) {
     RVX_REQUIRE(nq >= 0 && k >= 1, RVX_ERR_INVALID_PARAMETER, "nq >= 0 and k >= 1 required");
 }
 
+// The shard-dependent conditions search_rows enforces, checked locally before the
+// sharded entry points enter any collective (shard_agree).
+void index_shard_precheck(const rvx_index* ix, int64_t nq, int k, int ef, bool exact) {
+    check_query_args(ix, nq, k);
+    if (ix->n == 0 || nq == 0) return;
+    if (exact || ix->cfg.kind == RVX_INDEX_FLAT) {
+        RVX_REQUIRE(k <= SCAN_MAX_K, RVX_ERR_INVALID_PARAMETER, "k must be in [1, " + std::to_string(SCAN_MAX_K) + "]");
+        return;
+    }
+    RVX_REQUIRE(ix->has_graph && ix->graph_n == ix->n, RVX_ERR_INDEX, "HNSW graph missing or stale");
+    const int e = std::max(ef > 0 ? ef : ix->cfg.ef_search, k);
+    RVX_REQUIRE(e >= 1 && e <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER,
+                "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
+}
+
 }  // namespace
 
 namespace rvx {
@@ -366,9 +381,17 @@ rvx_status rvx_index_sharded_search(const rvx_index* ix, rvx_comm* comm, const f
                                     int32_t ef, int32_t exact, uint64_t* out_ids, float* out_dist,
                                     int32_t* out_count) {
     return guard([&] {
-        check_query_args(ix, nq, k);
-        RVX_REQUIRE(nq == 0 || (out_ids && out_dist && (comm_rank(comm) != 0 || q)), RVX_ERR_INVALID_PARAMETER,
-                    "null argument");
+        rvx_status st = RVX_OK;
+        std::string why;
+        try {  // local verdict first; every rank learns every verdict before any data moves
+            index_shard_precheck(ix, nq, k, ef, exact != 0);
+            RVX_REQUIRE(nq == 0 || (out_ids && out_dist && (comm_rank(comm) != 0 || q)), RVX_ERR_INVALID_PARAMETER,
+                        "null argument");
+        } catch (const Error& e) {
+            st = e.code;
+            why = e.what();
+        }
+        shard_agree(comm, st, why, {nq, (int64_t)k, (int64_t)ef, (int64_t)exact, ix ? (int64_t)ix->cfg.dim : 0});
         if (nq == 0) return;
         std::shared_lock<std::shared_mutex> lk(ix->mu);
         ComputeLock cl;
@@ -391,12 +414,20 @@ rvx_status rvx_index_sharded_search_device(const rvx_index* ix, rvx_comm* comm, 
                                            int32_t k, int32_t ef, int32_t exact, rvx_buffer* out_ids,
                                            rvx_buffer* out_dist) {
     return guard([&] {
-        check_query_args(ix, nq, k);
-        RVX_REQUIRE(out_ids && out_dist, RVX_ERR_INVALID_PARAMETER, "null buffer");
-        RVX_REQUIRE(comm_rank(comm) != 0 || (q && q->mem.bytes >= nq * ix->cfg.dim * 4), RVX_ERR_DIMENSION_MISMATCH,
-                    "query buffer too small");
-        RVX_REQUIRE(out_ids->mem.bytes >= nq * k * 8 && out_dist->mem.bytes >= nq * k * 4, RVX_ERR_DIMENSION_MISMATCH,
-                    "output buffers too small");
+        rvx_status st = RVX_OK;
+        std::string why;
+        try {  // local verdict first; every rank learns every verdict before any data moves
+            index_shard_precheck(ix, nq, k, ef, exact != 0);
+            RVX_REQUIRE(out_ids && out_dist, RVX_ERR_INVALID_PARAMETER, "null buffer");
+            RVX_REQUIRE(comm_rank(comm) != 0 || (q && q->mem.bytes >= nq * ix->cfg.dim * 4),
+                        RVX_ERR_DIMENSION_MISMATCH, "query buffer too small");
+            RVX_REQUIRE(out_ids->mem.bytes >= nq * k * 8 && out_dist->mem.bytes >= nq * k * 4,
+                        RVX_ERR_DIMENSION_MISMATCH, "output buffers too small");
+        } catch (const Error& e) {
+            st = e.code;
+            why = e.what();
+        }
+        shard_agree(comm, st, why, {nq, (int64_t)k, (int64_t)ef, (int64_t)exact, ix ? (int64_t)ix->cfg.dim : 0});
         if (nq == 0) return;
         std::shared_lock<std::shared_mutex> lk(ix->mu);
         ComputeLock cl;

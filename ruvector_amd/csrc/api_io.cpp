@@ -66,8 +66,9 @@ struct Layout {
 
 Layout layout_of(const Fd& f, int32_t layout, int64_t dim) {
     Layout L;
+    constexpr int64_t MAX_DIM = (int64_t)1 << 28, MAX_BLOCK = (int64_t)1 << 36;  // keep every product in int64
     if (layout == RVX_FEATURE_RAW) {
-        RVX_REQUIRE(dim > 0, RVX_ERR_INVALID_PARAMETER, "raw feature files need the dimension");
+        RVX_REQUIRE(dim > 0 && dim <= MAX_DIM, RVX_ERR_INVALID_PARAMETER, "raw feature files need a dimension in [1, 2^28]");
         L.dim = dim;
         L.block = dim * 4;
         L.rows = f.size() / L.block;
@@ -79,7 +80,12 @@ Layout layout_of(const Fd& f, int32_t layout, int64_t dim) {
         L.rows = (int64_t)h[1];
         L.block = (int64_t)h[2];
         L.base = COLD_HEADER;
-        RVX_REQUIRE(L.dim > 0 && L.block >= L.dim * 4, RVX_ERR_SERIALIZATION, "bad cold-tier header");
+        // header fields are untrusted: bound them before any arithmetic on them
+        RVX_REQUIRE(h[0] > 0 && h[0] <= (uint64_t)MAX_DIM && h[2] <= (uint64_t)MAX_BLOCK && h[1] <= (uint64_t)INT64_MAX,
+                    RVX_ERR_SERIALIZATION, "bad cold-tier header");
+        RVX_REQUIRE(L.block >= L.dim * 4, RVX_ERR_SERIALIZATION, "bad cold-tier header");
+        RVX_REQUIRE(L.rows <= (f.size() - COLD_HEADER) / L.block, RVX_ERR_SERIALIZATION,
+                    "cold-tier header claims more rows than the file holds");
         RVX_REQUIRE(dim <= 0 || dim == L.dim, RVX_ERR_DIMENSION_MISMATCH, "dimension differs from the file header");
     } else {
         fail(RVX_ERR_INVALID_PARAMETER, "unknown feature-file layout");
@@ -120,9 +126,10 @@ rvx_status rvx_feature_file_load(const char* path, int32_t layout, int64_t dim, 
         RVX_REQUIRE(path && dst && row0 >= 0 && nrows >= 0 && dst_row0 >= 0, RVX_ERR_INVALID_PARAMETER, "bad argument");
         Fd f(path, O_RDONLY);
         const Layout L = layout_of(f, layout, dim);
-        RVX_REQUIRE(row0 + nrows <= L.rows, RVX_ERR_INDEX, "rows past the end of the file");
+        RVX_REQUIRE(row0 <= L.rows && nrows <= L.rows - row0, RVX_ERR_INDEX, "rows past the end of the file");
         const int64_t rb = L.dim * 4;
-        RVX_REQUIRE((dst_row0 + nrows) * rb <= dst->mem.bytes, RVX_ERR_DIMENSION_MISMATCH, "buffer smaller than rows*dim");
+        RVX_REQUIRE(dst_row0 <= dst->mem.bytes / rb && nrows <= dst->mem.bytes / rb - dst_row0,
+                    RVX_ERR_DIMENSION_MISMATCH, "buffer smaller than rows*dim");
         RVX_REQUIRE(f.size() >= L.base + (row0 + nrows - 1) * L.block + rb || nrows == 0, RVX_ERR_SERIALIZATION,
                     "file shorter than its rows");
         if (nrows == 0) return;

@@ -10,12 +10,14 @@ using namespace rvx;
 
 namespace {
 
-// One hit as it travels between ranks (24 B).
+// One hit as it travels between ranks (24 B): the reported distance and the merge key
+// (the distance with NaN — e.g. cosine against a zero row — and empty slots at +inf, so
+// every rank's list is totally ordered and each output slot is written exactly once).
 struct Hit {
     int64_t gid;
     int64_t lid;
     float d;
-    int32_t pad;
+    float key;
 };
 
 __global__ void k_pack_hits(const int64_t* gid, const int64_t* lid, const float* d, int64_t total, Hit* out) {
@@ -25,7 +27,7 @@ __global__ void k_pack_hits(const int64_t* gid, const int64_t* lid, const float*
     h.gid = gid[i];
     h.lid = lid ? lid[i] : 0;
     h.d = h.gid == -1 ? INFINITY : d[i];
-    h.pad = 0;
+    h.key = isnan(h.d) ? INFINITY : h.d;
     out[i] = h;
 }
 
@@ -34,7 +36,7 @@ __device__ __forceinline__ int count_before(const Hit* l, int k, float v, bool i
     int lo = 0, hi = k;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        const float x = l[mid].d;
+        const float x = l[mid].key;
         if (inclusive ? (x <= v) : (x < v)) lo = mid + 1;
         else hi = mid;
     }
@@ -58,7 +60,7 @@ __global__ void k_merge_hits(const Hit* all, int w, int64_t nq, int k, int64_t* 
     int pos = j;
     for (int p = 0; p < w && pos < k; ++p) {
         if (p == r) continue;
-        pos += count_before(all + (int64_t)p * per_rank + q * k, k, h.d, p < r);
+        pos += count_before(all + (int64_t)p * per_rank + q * k, k, h.key, p < r);
     }
     if (pos < k) {
         out_gid[q * k + pos] = h.gid;
@@ -78,6 +80,34 @@ __global__ void k_merge_hits(const Hit* all, int w, int64_t nq, int k, int64_t* 
 }  // namespace
 
 namespace rvx {
+
+void shard_agree(rvx_comm* c, rvx_status status, const std::string& why, const int64_t (&args)[5]) {
+    const int w = comm_size(c), me = comm_rank(c);
+    if (w <= 1) {
+        if (status != RVX_OK) fail(status, why);
+        return;
+    }
+    // fixed-size all-gather: {status, args...} per rank, so ranks that disagree on the
+    // arguments (or failed before any collective) still exchange the same byte count
+    constexpr int F = 8;
+    int64_t mine[F] = {(int64_t)status, args[0], args[1], args[2], args[3], args[4], 0, 0};
+    auto* dev = (int64_t*)scratch_bytes("shard_agree", (int64_t)(w + 1) * F * 8);
+    RVX_HIP(hipMemcpyAsync(dev, mine, sizeof mine, hipMemcpyHostToDevice, stream()));
+    comm_allgather_bytes(c, dev, dev + F, F * 8, stream());
+    std::vector<int64_t> all((size_t)w * F);
+    RVX_HIP(hipMemcpyAsync(all.data(), dev + F, all.size() * 8, hipMemcpyDeviceToHost, stream()));
+    sync();
+    for (int p = 0; p < w; ++p)
+        if (all[(size_t)p * F] != RVX_OK)
+            fail((rvx_status)all[(size_t)p * F],
+                 p == me ? why : "sharded search failed on rank " + std::to_string(p) + " (status " +
+                                     std::to_string(all[(size_t)p * F]) + ")");
+    for (int p = 1; p < w; ++p)
+        for (int f = 1; f <= 5; ++f)
+            RVX_REQUIRE(all[(size_t)p * F + f] == all[(size_t)f], RVX_ERR_INVALID_PARAMETER,
+                        "sharded search arguments (nq, k, ef, mode, dim) differ between rank 0 and rank " +
+                            std::to_string(p));
+}
 
 void sharded_merge(rvx_comm* c, const int64_t* gid, const int64_t* lid, const float* dist, int64_t nq, int k,
                    int64_t* out_gid, int64_t* out_lid, float* out_dist, int32_t* out_count) {

@@ -37,6 +37,12 @@ void comm_allgather_bytes(rvx_comm* c, const void* send, void* recv, int64_t byt
 void sharded_merge(rvx_comm* c, const int64_t* gid, const int64_t* lid, const float* dist, int64_t nq, int k,
                    int64_t* out_gid, int64_t* out_lid, float* out_dist, int32_t* out_count);
 
+// Collective precondition check of a sharded search, before any other collective: every
+// rank passes its local verdict (status, message) and its {nq, k, ef, mode, dim}; a fixed-
+// size all-gather lets every rank see every verdict, and all ranks throw the same way when
+// any rank failed or the arguments differ — no rank is left waiting in a collective.
+void shard_agree(rvx_comm* c, rvx_status status, const std::string& why, const int64_t (&args)[5]);
+
 // Exchange round plan (rvx_exchange_plan): plan[c] = {r0[p], rows[p]} of round c.
 enum { PLAN_SAGE = 0, PLAN_WHOLE = 1 };
 struct ExchangeRound {

@@ -298,8 +298,8 @@ class ShardedHyperbolicSearch:
         else:
             q = L.f32c(queries).reshape(-1, d)
             nq = q.shape[0]
-        if self.rank == 0 and q is None:
-            raise HyperbolicError(2, "rank 0 must pass the queries")
+        # rank 0 without queries is reported by the library on every rank (a Python-side
+        # raise on one rank would leave the others waiting in the collective)
         gid = np.empty((nq, k), np.int64)
         lid = np.empty((nq, k), np.int64)
         dist = np.empty((nq, k), np.float32)

@@ -95,14 +95,18 @@ class VectorDB:
             raise RuvectorError(1, f"DimensionMismatch expected {self.options.dimensions} actual {v.size}")
 
     def _store(self, entries: Sequence[VectorEntry]) -> List[str]:
-        """MemoryStorage::insert_batch (storage_memory.rs:68-99): entries are stored one
-        at a time and the first one of the wrong dimension returns DimensionMismatch;
-        the entries before it stay stored (and, as VectorDB::insert_batch returns
-        before index.add_batch, vector_db.rs:154-165, are never indexed)."""
-        ids = []
-        for e in entries:
-            v = L.f32c(e.vector).reshape(-1)
+        """VectorStorage::insert_batch of the reference's default build (features
+        "storage" = redb, ruvector-core Cargo.toml:89; storage.rs:168-206): the batch is
+        one write transaction, and an entry of the wrong dimension returns
+        DimensionMismatch before the commit — nothing of the batch is stored (and, as
+        VectorDB::insert_batch returns before index.add_batch, vector_db.rs:154-165,
+        nothing is indexed). The memory-only build (storage_memory.rs:68-99) would keep
+        the entries before the bad one; this mirrors the default."""
+        vecs = [L.f32c(e.vector).reshape(-1) for e in entries]
+        for v in vecs:
             self._check_dim(v)
+        ids = []
+        for e, v in zip(entries, vecs):
             if e.id is not None:
                 vid = e.id
             else:

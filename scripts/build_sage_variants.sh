@@ -1,5 +1,5 @@
 #!/bin/bash
-# Timing-only ablation builds of librvx.so (same sources, one -D each) for scripts/exp_sage_ablate.sh:
+# Timing-only ablation builds of librvx.so (same sources, one -D each) for scripts/exp/exp_sage_ablate.sh:
 #   nonorm  = no normalisation pass; noaggw = the overlapped gather stores no aggregate.
 set -e
 cd "$(dirname "$0")/.."

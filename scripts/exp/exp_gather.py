@@ -1,6 +1,6 @@
 """Standalone gather-aggregate bandwidth vs node-table size (d=768, deg=32,
 mean): separates the per-launch HBM rate from table-size effects (address
-translation reach). Usage: python scripts/exp_gather.py [n ...]"""
+translation reach). Usage: python scripts/exp/exp_gather.py [n ...]"""
 import os
 import sys
 

@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+# RVX_ORACLE_LIB: the sanitizer build (oracle/_asan/liboracle_asan.so, tests/test_asan.py)
+LIB_PATH = os.environ.get("RVX_ORACLE_LIB") or os.path.join(ROOT, "oracle", "liboracle.so")
 
 P, I32, I64, U64, F32 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_float
 PF = C.POINTER(C.c_float)

@@ -97,6 +97,40 @@ def main():
             return float(np.max(np.linalg.norm(np.asarray(u, np.float64) - v, axis=1) / np.where(nb > 0, nb, 1.0)))
         res["sage_deferred_layer1_row_rel"] = row_rel(a1d, b1)
         res["sage_deferred_layer2_row_rel"] = row_rel(a2d[o0:o1], b2[o0:o1])
+        # ranks that decide differently: rank 1 takes the split-bf16 GEMM, which cannot carry
+        # the factors, so it normalises in place and ships 1.0 for its rows; the others
+        # defer. The collective sequences must still match (no hang) and every row agree.
+        if rank == 1:
+            os.environ["RVX_GEMM_H2"] = "0"
+        y1d.upload(np.full((N, d), np.nan, np.float32))
+        iv.upload(np.full(N, np.nan, np.float32))
+        call("rvx_sage_forward_exchange2", layer._h, g_loc.handle, xb.handle, None, y1d.handle, iv.handle, off_p,
+             comm._h, 1)
+        # read layer 1 now: a rank that cannot take the factors in layer 2 rescales its
+        # input table in place (x_rowmul materialised), as documented for exchange2
+        inv = iv.download(np.float32, (N,))
+        a1d = y1d.download(np.float32, (N, d)).astype(np.float64) * inv[:, None]
+        call("rvx_sage_forward_exchange2", layer._h, g_loc.handle, y1d.handle, iv.handle, y2d.handle, None, off_p,
+             comm._h, 0)
+        os.environ.pop("RVX_GEMM_H2", None)
+        lo1, hi1 = int(offsets[1]), int(offsets[2])
+        res["sage_mixed_defer_rank1_factors_one"] = bool(np.all(inv[lo1:hi1] == 1.0))
+        a2d = y2d.download(np.float32, (N, d))
+        # expected tables: rank 1's layer-1 rows from the split-bf16 path, the others from the
+        # default path; layer 2 over that table with the owner's GEMM path (one process)
+        os.environ["RVX_GEMM_H2"] = "0"
+        call("rvx_sage_forward_exchange", layer._h, g_full.handle, xb.handle, r1.handle, one_p, None, 0)
+        os.environ.pop("RVX_GEMM_H2", None)
+        e1 = b1.copy()
+        e1[lo1:hi1] = r1.download(np.float32, (N, d))[lo1:hi1]
+        r1.upload(e1)
+        if rank == 1:
+            os.environ["RVX_GEMM_H2"] = "0"
+        call("rvx_sage_forward_exchange", layer._h, g_full.handle, r1.handle, r2.handle, one_p, None, 0)
+        os.environ.pop("RVX_GEMM_H2", None)
+        e2 = r2.download(np.float32, (N, d))
+        res["sage_mixed_defer_layer1_row_rel"] = row_rel(a1d, e1)
+        res["sage_mixed_defer_layer2_row_rel"] = row_rel(a2d[o0:o1], e2[o0:o1])
 
         # ---- RuvectorLayer (M|K|V exchange) and the attention head (T exchange)
         n2 = int(offsets[-1])

@@ -102,6 +102,7 @@ def main():
                  for s, o in enumerate(orc) for oi, od in [o.brute_force(q, 10)]]
         ei, ed = merge(parts, 10)
         checks["exact_k10"] = bool(np.array_equal(gid, ei) and close(gd, ed))
+        expect_exact = (gid.copy(), gd.copy())
         one = grp.search(q[3] if rank == 0 else None, 10)  # shard.search = graph search (hnsw.rs:427)
         e10 = expect[(10, 0)]
         checks["shape"] = all(g == int(e10[3, j]) and r.id == g - offsets[int(np.searchsorted(offsets, g, "right")) - 1]
@@ -119,6 +120,22 @@ def main():
         checks["pruned_sorted"] = bool(np.all(np.diff(gd, axis=1) >= 0))
         # every shard's centroid and tangent coordinates equal the oracle's bits
         checks["pruned_exact"] = bool(np.array_equal(gid, ei) and close(gd, ed))
+        # a precondition that fails on some shards only (k * prune_factor = 200 > 128 where a
+        # shard holds more than 128 points; a 7-point shard passes) fails on EVERY rank
+        # instead of leaving the passing ranks waiting in a collective, and so do
+        # arguments that differ between ranks; the group stays usable afterwards
+        def fails(*args):
+            try:
+                grp.search_batch(*args)
+                return False
+            except rv.RvxError:
+                return True
+        checks["one_shard_failure_fails_all"] = fails(qa, 20, 0, "pruned")
+        checks["arg_mismatch_fails_all"] = fails(qa, 10 if rank == 0 else 9, 0, "exact")
+        checks["rank0_without_queries_fails_all"] = fails(nq, 10, 0, "exact")
+        gid2, _, gd2, _ = grp.search_batch(qa, 10, 0, "exact")
+        checks["usable_after_failures"] = bool(np.array_equal(gid2[:, :10], expect_exact[0]) and
+                                               np.array_equal(gd2[:, :10], expect_exact[1]))
         # nq = 0 is a no-op on every rank
         e = grp.search_batch(np.zeros((0, d), np.float32) if rank == 0 else 0, 10)
         checks["empty"] = e[0].shape == (0, 10)

@@ -112,6 +112,32 @@ def test_gpu_build_matches_oracle_graph_rules_and_recall():
     assert r_gpu >= r_cpu - 0.02, (r_gpu, r_cpu)
 
 
+def test_wide_lists_m128_m0_256_build_and_search():
+    """The GPU builder's list capacities (M <= 128, M0 <= 256) reach HyperbolicHnsw:
+    same seeded levels as the oracle's sequential build with the same config, lists
+    within capacity, recall at least the oracle build's; search on the oracle's graph
+    returns the oracle's ids and distances."""
+    n, d = 4000, 16
+    x = ball_points(n, d, 61)
+    q = ball_points(200, d, 62)
+    cfg = rv.HyperbolicHnswConfig(max_connections=128, max_connections_0=256, ef_construction=300, seed=4)
+    h = rv.HyperbolicHnsw(cfg)
+    h.insert_batch(x)
+    o = O.Hyp(d, m=128, m0=256, ef_construction=300, seed=4)
+    o.insert(x)
+    g, og = h.export_graph(), o.export()
+    assert np.array_equal(g["levels"], og["levels"])
+    assert np.all(np.diff(g["row_ptr0"]) <= 256) and np.max(np.diff(g["row_ptr0"])) > 64
+    gt, _ = o.brute_force(q, 10)
+    assert recall(gt, h.search_batch(q, 10, 300)[0]) >= recall(gt, o.search(q, 10, 300)[0]) - 0.02
+    h.load_graph(og)
+    ids, dist, _ = h.search_batch(q, 10, 300)
+    rids, rd, _ = o.search(q, 10, 300)
+    assert np.array_equal(ids, rids) and np.array_equal(dist, rd)
+    with pytest.raises(rv.HyperbolicError):
+        rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(max_connections=129), dim=d)
+
+
 def test_brute_force_matches_oracle():
     x = ball_points(70_000, 32, 31)  # > one 65536-row segment
     q = ball_points(40, 32, 32)

@@ -58,6 +58,9 @@ def test_exchange_entry_points_multi_rank(offsets, tmp_path):
         assert r["sage_layer1_vs_oracle"] <= 1e-5, r
         assert r["sage_deferred_layer1_row_rel"] <= 1e-6, r  # |y| carried, not applied: same rows
         assert r["sage_deferred_layer2_row_rel"] <= 1e-5, r
+        # one rank normalising in place while the others defer: same rows
+        assert r["sage_mixed_defer_rank1_factors_one"], r
+        assert r["sage_mixed_defer_layer1_row_rel"] <= 1e-6 and r["sage_mixed_defer_layer2_row_rel"] <= 1e-5, r
         assert r["gnn_owned_equal"], r
         assert r["gnn_fold_owned_equal"] and r["gnn_fold_vs_oracle"] <= 1e-5, r
         assert r["efa_owned_equal"], r

@@ -81,3 +81,20 @@ def test_dimension_mismatch():
     db.insert(VectorEntry(vector=[1.0, 0.0, 0.0, 0.0]))
     with pytest.raises(rv.RuvectorError):
         db.search(SearchQuery(vector=[1.0, 0.0], k=1))
+
+
+@pytest.mark.parametrize("hnsw", [True, False])
+def test_failed_batch_leaves_earlier_rows_alone(hnsw):
+    """storage.rs:168-206 (default redb build): a failing batch commits nothing; rows
+    stored before it stay stored and indexed, and the valid entries go in together."""
+    opts = DbOptions(dimensions=4) if hnsw else DbOptions(dimensions=4, hnsw_config=None)
+    db = VectorDB(opts)
+    db.insert(VectorEntry(vector=[0.0, 0.0, 0.0, 1.0], id="before"))
+    batch = [VectorEntry(vector=[1.0, 2.0, 3.0, 4.0], id="a"), VectorEntry(vector=[1.0, 2.0, 3.0]),
+             VectorEntry(vector=[9.0, 9.0, 9.0, 9.0], id="d")]
+    with pytest.raises(rv.RuvectorError):
+        db.insert_batch(batch)
+    assert db.keys() == ["before"] and db.index.len() == 1
+    ids = db.insert_batch([b for b in batch if len(b.vector) == 4])
+    assert ids == ["a", "d"] and len(db) == 3 and db.index.len() == 3
+    assert db.search(SearchQuery(vector=[9.0, 9.0, 9.0, 9.0], k=1))[0].id == "d"
