@@ -20,6 +20,7 @@
 // that beat the current k-th distance are appended to a per-query buffer and
 // merged by one lane per query after each row tile.
 #include <cfloat>
+#include <type_traits>
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -338,6 +339,7 @@ size_t scan_lds_bytes(int k) {
 // leave f32 range) send the whole call to the VALU scan.
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 #ifndef RVX_SCAN_FKP
@@ -359,9 +361,13 @@ constexpr int F_NSTAGE = RVX_SCAN_NSTAGE;   // LDS-DMA ring: F_NSTAGE - 1 k-step
 //   2 (tall): 256 rows x 128 queries, 4 waves of the wide tile's 128 x 64 shape, a
 //         2-stage ring, two blocks per CU (79.5 KB): each block's tile epilogue and
 //         barriers can run beside the other block's MFMAs (opt-in, RVX_SCAN_WIDE=2)
+//   3 (wide, 16x16x32): the wide tile with v_mfma_f32_16x16x32_f16 — the same cycles per
+//         flop and LDS bytes, 8 x 4 accumulators of 16 x 16 per wave; the chip holds a
+//         higher clock under the smaller MFMA shape (MI355X_MICROARCH.md, DVFS item 7)
 template <int C>
 struct FCfg {
-    static constexpr int WQ = C == 1 ? 4 : 2, FM = C == 0 ? 2 : 4;
+    static constexpr bool M16 = C == 3;
+    static constexpr int WQ = (C == 1 || C == 3) ? 4 : 2, FM = C == 0 ? 2 : 4;
     static constexpr int THREADS = 64 * 2 * WQ, NW = THREADS / 64;
     static constexpr int FQ = 64 * WQ, FR = 64 * FM;
     static constexpr int NST = C == 2 ? 2 : F_NSTAGE;  // LDS-DMA ring stages
@@ -370,7 +376,7 @@ struct FCfg {
     // + row constants (float4) and per-query {Qs, P} of the per-row-bound metrics
     // + per-query shared bound B_q and eps_q (group insertion, RVX_SCAN_GROUP_INSERT)
     static constexpr int LDS = NST * STAGE + FQ * FKP * 8 + FQ * FCB * 8 + FQ * 12 + 16 + FR * 16 + FQ * 8 + FQ * 8;
-    static constexpr int BLOCKS = C == 1 ? 1 : 2;
+    static constexpr int BLOCKS = (C == 1 || C == 3) ? 1 : 2;
     static_assert(RP * 16 * NW == FR && QP * 16 * NW == FQ && RP >= QP, "DMA pieces cover the stage");
     static_assert(BLOCKS * LDS <= 160 * 1024, "resident blocks fit the CU's LDS");
 };
@@ -447,6 +453,11 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
     using Cf = FCfg<CFG>;
     constexpr int FQ = Cf::FQ, FR = Cf::FR, F_STAGE = Cf::STAGE, F_FM = Cf::FM, F_THREADS = Cf::THREADS;
     constexpr int NST = Cf::NST, RP = Cf::RP, QP = Cf::QP, PCS = RP + QP;
+    // accumulator geometry: AM x AN tiles of TT x TT per wave, AE values per lane each
+    constexpr bool M16 = Cf::M16;
+    constexpr int AM = M16 ? 2 * F_FM : F_FM, AN = M16 ? 4 : 2, AE = M16 ? 4 : 16, TT = M16 ? 16 : 32;
+    using AccT = typename std::conditional<M16, f32x4v, f32x16>::type;
+    using OffT = typename std::conditional<M16, uint32_t, uint64_t>::type;
     // per-row bounds (Poincaré, squared L2; see rows_to_f16_pr): the lists rank lower bounds
     constexpr bool PRB = METRIC == RVX_METRIC_POINCARE || METRIC == METRIC_L2SQ;
     extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
@@ -462,6 +473,8 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lr = lane & 31, lh = lane >> 5, wm = wave & 1, wn = wave >> 1;
+    const int lc = lane & 15, lg = lane >> 4;  // 16x16x32 lane roles: query / row-group
+    const int lq = M16 ? lc : lr;              // the lane's query column inside an accumulator tile
     // consecutive blocks share a row split (and, 8 at a time, an XCD's L2)
     const int qt = (int)(blockIdx.x % (unsigned)a.qtiles);
     const int sl = (int)(blockIdx.x / (unsigned)a.qtiles);
@@ -479,11 +492,11 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
     if (tid < FQ) { cand_n[tid] = 0; thr[tid] = INFINITY; fillc[tid] = 0; }
     if (tid < 4) ovf[tid] = 0;
 
-    float qf_[2];  // query factor Q
-    bool qv_[2];
+    float qf_[AN];  // query factor Q
+    bool qv_[AN];
 #pragma unroll
-    for (int fn = 0; fn < 2; ++fn) {
-        const int64_t qg = q0 + wn * 64 + fn * 32 + lr;
+    for (int fn = 0; fn < AN; ++fn) {
+        const int64_t qg = q0 + wn * 64 + fn * TT + lq;
         qv_[fn] = qg < a.nq;
         const int64_t qc = min(qg, a.nq - 1);
         const float2 c = a.qc[qc];
@@ -519,16 +532,20 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
     // LDS-DMA fill: 1 KB pieces of 16 rows x 64 B; lane -> (row, 16-B chunk)
     // with the chunk XOR-swizzled by (row >> 2) & 3 on the source address, so
     // the fragment reads below are bank-conflict free.
+    // swizzle of a row's four 16-B chunks by g = (row >> 2) & 3: g for the 32x32x16 reads;
+    // (4 - g) & 3 for the 16x16x32 reads (lane (lc, lg) reads row lc, chunk lg), which keeps
+    // each of ds_read_b128's four 16-lane bank groups on 16 distinct 4-bank quads
+    auto swz = [](int g) { return M16 ? ((4 - g) & 3) : g; };
     int prow[RP], pchunk[RP], qrow[QP], qchunk[QP];
 #pragma unroll
     for (int j = 0; j < RP; ++j) {
         prow[j] = 16 * (RP * wave + j) + (lane >> 2);
-        pchunk[j] = (lane & 3) ^ ((prow[j] >> 2) & 3);
+        pchunk[j] = (lane & 3) ^ swz((prow[j] >> 2) & 3);
     }
 #pragma unroll
     for (int j = 0; j < QP; ++j) {
         qrow[j] = 16 * (QP * wave + j) + (lane >> 2);
-        qchunk[j] = (lane & 3) ^ ((qrow[j] >> 2) & 3);
+        qchunk[j] = (lane & 3) ^ swz((qrow[j] >> 2) & 3);
     }
     const int nk = a.d / FK;
     const int64_t ntile = r_end > r_beg ? (r_end - r_beg + FR - 1) / FR : 0;
@@ -575,18 +592,24 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
     int a_rd[2], b_rd[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-        const int sw = ((2 * ks + lh) ^ ((lr >> 2) & 3)) << 4;
-        a_rd[ks] = (wm * WROWS + lr) * 64 + sw;
-        b_rd[ks] = FR * 64 + (wn * 64 + lr) * 64 + sw;
+        if constexpr (M16) {  // one K = 32 step: row lc, chunk lg (fragments 16 rows = 1 KiB apart)
+            const int sw = (lg ^ swz((lc >> 2) & 3)) << 4;
+            a_rd[ks] = (wm * WROWS + lc) * 64 + sw;
+            b_rd[ks] = FR * 64 + (wn * 64 + lc) * 64 + sw;
+        } else {
+            const int sw = ((2 * ks + lh) ^ ((lr >> 2) & 3)) << 4;
+            a_rd[ks] = (wm * WROWS + lr) * 64 + sw;
+            b_rd[ks] = FR * 64 + (wn * 64 + lr) * 64 + sw;
+        }
     }
 
-    f32x16 acc[F_FM][2];
+    AccT acc[AM][AN];
 #pragma unroll
-    for (int i = 0; i < F_FM; ++i)
+    for (int i = 0; i < AM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < AN; ++j)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+            for (int e = 0; e < AE; ++e) acc[i][j][e] = 0.0f;
 
     // Tile epilogue. The accumulators are overwritten in place by the
     // approximate values v; invalid rows (past the split, deleted: 1/scale =
@@ -610,8 +633,33 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
             else rowc[tid] = row_factors<METRIC>(make_float2(pre.x, pre.y));
         }
         __syncthreads();
-        float vmin[2] = {INFINITY, INFINITY};
-        if constexpr (PRB) {
+        float vmin[AN];
+#pragma unroll
+        for (int fn = 0; fn < AN; ++fn) vmin[fn] = INFINITY;
+        if constexpr (PRB && M16) {
+            float2 qsp[AN];
+#pragma unroll
+            for (int fn = 0; fn < AN; ++fn) qsp[fn] = qfac[wn * 64 + fn * TT + lq];
+            // the lane's 4 values of a 16 x 16 tile are 4 consecutive rows: four float4 reads
+#pragma unroll
+            for (int fm = 0; fm < AM; ++fm) {
+                float4 cr[4];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) cr[w] = rowc4[wm * WROWS + fm * 16 + 4 * lg + w];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float4 c = cr[e];
+#pragma unroll
+                    for (int fn = 0; fn < AN; ++fn) {
+                        const float v = __builtin_fmaf(
+                            c.w, qsp[fn].y,
+                            __builtin_fmaf(c.z, qsp[fn].x, __builtin_fmaf(acc[fm][fn][e] * c.x, qf_[fn], c.y)));
+                        acc[fm][fn][e] = v;
+                        vmin[fn] = fminf(vmin[fn], v);
+                    }
+                }
+            }
+        } else if constexpr (PRB) {
             float2 qsp[2];
 #pragma unroll
             for (int fn = 0; fn < 2; ++fn) qsp[fn] = qfac[wn * 64 + fn * 32 + lr];
@@ -637,6 +685,25 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
                         }
                     }
                 }
+        } else if constexpr (M16) {
+            // 4 consecutive rows per lane and tile: two float4 reads (two rows' {R, C} each)
+            const float4* rc4 = reinterpret_cast<const float4*>(rowc);
+#pragma unroll
+            for (int fm = 0; fm < AM; ++fm) {
+                const int rbase = (wm * WROWS + fm * 16 + 4 * lg) >> 1;
+                const float4 cc[2] = {rc4[rbase], rc4[rbase + 1]};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float4 q = cc[e >> 1];
+                    const float2 c = (e & 1) ? make_float2(q.z, q.w) : make_float2(q.x, q.y);
+#pragma unroll
+                    for (int fn = 0; fn < AN; ++fn) {
+                        const float v = __builtin_fmaf(acc[fm][fn][e] * c.x, qf_[fn], c.y);
+                        acc[fm][fn][e] = v;
+                        vmin[fn] = fminf(vmin[fn], v);
+                    }
+                }
+            }
         } else {
             // the 16 rows of a 32-row block that one lane holds are 4 runs of 4 consecutive
             // rows: 8 ds_read_b128 (two rows' {C, R} each) issued together per block, instead
@@ -669,7 +736,7 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
         // admit something).
         bool any = false;
 #pragma unroll
-        for (int fn = 0; fn < 2; ++fn) any = any || vmin[fn] < thr[wn * 64 + fn * 32 + lr];
+        for (int fn = 0; fn < AN; ++fn) any = any || vmin[fn] < thr[wn * 64 + fn * TT + lq];
         // block vote: one flag per tile parity, one LDS barrier (no VMEM drain)
         const int vp = 2 + (int)(((rt - r_beg) / FR) & 1);
         if (__ballot(any) && lane == 0) ovf[vp] = 1;
@@ -680,28 +747,30 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
 #ifdef RVX_COUNT_SLOW
         if (tid == 0) atomicAdd((unsigned*)a.xsq_max_bits + 2, 1u);
 #endif
-        static_assert(F_FM * 16 <= 64, "offered-value mask holds one bit per (fm, e)");
-        uint64_t offered[2] = {0ull, 0ull};  // per fn: values already handed to the list
+        static_assert(AM * AE <= 8 * (int)sizeof(OffT), "offered-value mask holds one bit per (fm, e)");
+        OffT offered[AN];  // per fn: values already handed to the list
+#pragma unroll
+        for (int fn = 0; fn < AN; ++fn) offered[fn] = 0;
         for (int round = 0;; ++round) {
 #pragma unroll
-            for (int fn = 0; fn < 2; ++fn) {
-                const int ql = wn * 64 + fn * 32 + lr;
+            for (int fn = 0; fn < AN; ++fn) {
+                const int ql = wn * 64 + fn * TT + lq;
                 const float t = thr[ql];
-                if (!__ballot(vmin[fn] < t)) continue;  // none of the wave's 32 queries has a value below its threshold
+                if (!__ballot(vmin[fn] < t)) continue;  // none of the wave's queries has a value below its threshold
 #pragma unroll
-                for (int fm = 0; fm < F_FM; ++fm)
+                for (int fm = 0; fm < AM; ++fm)
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) {
+                    for (int e = 0; e < AE; ++e) {
                         const float v = acc[fm][fn][e];
-                        const uint64_t bit = 1ull << (fm * 16 + e);
+                        const OffT bit = (OffT)1 << (fm * AE + e);
                         const bool pass = v < t && !(offered[fn] & bit);
                         if (!__ballot(pass)) continue;
                         if (!pass) continue;
                         const int slot = atomicAdd(&cand_n[ql], 1);
                         if (slot < FCB) {
                             cand_v[ql * FCB + slot] = v;
-                            cand_r[ql * FCB + slot] =
-                                (int32_t)(rt + wm * WROWS + fm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh);
+                            cand_r[ql * FCB + slot] = (int32_t)(rt + wm * WROWS + fm * TT +
+                                                                (M16 ? 4 * lg + e : (e & 3) + 8 * (e >> 2) + 4 * lh));
                             offered[fn] |= bit;
                         } else {
                             ovf[round & 1] = 1;
@@ -850,6 +919,37 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
             dma_piece(fs, fk0, fdst, j);
         };
         const unsigned char* cur = fsm + st * F_STAGE;
+        if constexpr (M16) {
+            // one K = 32 step of 16x16x32 MFMAs: B fragments of the wave's 4 query tiles,
+            // then the 8 row tiles in two halves (4 A fragments live at a time); DMA piece j
+            // follows MFMA j * 32 / PCS, as in the 32x32 form
+            h16x8 bf[AN];
+#pragma unroll
+            for (int f = 0; f < AN; ++f)
+                bf[f] = __builtin_bit_cast(h16x8, *reinterpret_cast<const u32x4*>(cur + b_rd[0] + f * 1024));
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                h16x8 af[AM / 2];
+#pragma unroll
+                for (int f = 0; f < AM / 2; ++f)
+                    af[f] = __builtin_bit_cast(h16x8,
+                                               *reinterpret_cast<const u32x4*>(cur + a_rd[0] + (half * AM / 2 + f) * 1024));
+#pragma unroll
+                for (int f = 0; f < AM / 2; ++f)
+#pragma unroll
+                    for (int fn = 0; fn < AN; ++fn) {
+                        const int fm = half * AM / 2 + f;
+                        acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[f], bf[fn], acc[fm][fn], 0, 0, 0);
+                        constexpr int PS16 = AM * AN / PCS;
+                        const int m = fm * AN + fn;
+                        if (m % PS16 == 0 && m / PS16 < PCS) {
+                            __builtin_amdgcn_sched_barrier(0);
+                            piece(m / PS16);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    }
+            }
+        } else {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             h16x8 af[F_FM], bf[2];
@@ -872,6 +972,7 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
                         __builtin_amdgcn_sched_barrier(0);
                     }
                 }
+        }
         }
     };
 
@@ -904,11 +1005,11 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
         epilogue(rt, pre);
         if (gq_own) graw = __hip_atomic_load(a.gbound + gq_idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-        for (int i = 0; i < F_FM; ++i)
+        for (int i = 0; i < AM; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+            for (int j = 0; j < AN; ++j)
 #pragma unroll
-                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+                for (int e = 0; e < AE; ++e) acc[i][j][e] = 0.0f;
         cur_src = nxt_src;
     }
     __syncthreads();
@@ -1356,12 +1457,16 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     if (metric == RVX_METRIC_POINCARE && !(curv > 0.0f)) return false;
     // tile shape: RVX_SCAN_WIDE 0/1/2 forces it (tests, A/B), else 256^2 for d >= 512
     const int wide_env = env_int("RVX_SCAN_WIDE", -1);
-    const int cfg = wide_env >= 0 && wide_env <= 2 ? wide_env : (d >= 512 ? 1 : 0);
-    const int FR = cfg == 1 ? FCfg<1>::FR : cfg == 2 ? FCfg<2>::FR : FCfg<0>::FR;
-    const int FQ = cfg == 1 ? FCfg<1>::FQ : cfg == 2 ? FCfg<2>::FQ : FCfg<0>::FQ;
-    const int F_LDS = cfg == 1 ? FCfg<1>::LDS : cfg == 2 ? FCfg<2>::LDS : FCfg<0>::LDS;
-    const int F_THREADS = cfg == 1 ? FCfg<1>::THREADS : cfg == 2 ? FCfg<2>::THREADS : FCfg<0>::THREADS;
-    const int F_BLOCKS = cfg == 1 ? FCfg<1>::BLOCKS : cfg == 2 ? FCfg<2>::BLOCKS : FCfg<0>::BLOCKS;
+    // RVX_SCAN_M16=1 runs the wide tile on 16x16x32 MFMAs (cfg 3)
+    int cfg = wide_env >= 0 && wide_env <= 3 ? wide_env : (d >= 512 ? 1 : 0);
+    if (cfg == 1 && env_int("RVX_SCAN_M16", 0)) cfg = 3;
+    const int FR = cfg == 1 ? FCfg<1>::FR : cfg == 2 ? FCfg<2>::FR : cfg == 3 ? FCfg<3>::FR : FCfg<0>::FR;
+    const int FQ = cfg == 1 ? FCfg<1>::FQ : cfg == 2 ? FCfg<2>::FQ : cfg == 3 ? FCfg<3>::FQ : FCfg<0>::FQ;
+    const int F_LDS = cfg == 1 ? FCfg<1>::LDS : cfg == 2 ? FCfg<2>::LDS : cfg == 3 ? FCfg<3>::LDS : FCfg<0>::LDS;
+    const int F_THREADS =
+        cfg == 1 ? FCfg<1>::THREADS : cfg == 2 ? FCfg<2>::THREADS : cfg == 3 ? FCfg<3>::THREADS : FCfg<0>::THREADS;
+    const int F_BLOCKS =
+        cfg == 1 ? FCfg<1>::BLOCKS : cfg == 2 ? FCfg<2>::BLOCKS : cfg == 3 ? FCfg<3>::BLOCKS : FCfg<0>::BLOCKS;
     // k > FKP: the lists stay FKP long (no single split proves a k-th value, so the
     // shared bound is off) and the rerank's completeness test decides per query
     if (d % FK != 0 || k > SCAN_MAX_K || n >= ((int64_t)1 << 31) - FR || nq <= 0 || n <= 0) return false;
@@ -1435,6 +1540,8 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
         RVX_FILTER_ATTR(RVX_METRIC_POINCARE, 0); RVX_FILTER_ATTR(METRIC_L2SQ, 0);
         RVX_FILTER_ATTR(RVX_METRIC_L2, 2); RVX_FILTER_ATTR(RVX_METRIC_COSINE, 2); RVX_FILTER_ATTR(RVX_METRIC_DOT, 2);
         RVX_FILTER_ATTR(RVX_METRIC_POINCARE, 2); RVX_FILTER_ATTR(METRIC_L2SQ, 2);
+        RVX_FILTER_ATTR(RVX_METRIC_L2, 3); RVX_FILTER_ATTR(RVX_METRIC_COSINE, 3); RVX_FILTER_ATTR(RVX_METRIC_DOT, 3);
+        RVX_FILTER_ATTR(RVX_METRIC_POINCARE, 3); RVX_FILTER_ATTR(METRIC_L2SQ, 3);
 #undef RVX_FILTER_ATTR
         attr = true;
     }
@@ -1472,6 +1579,7 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     }
         if (cfg == 1) { RVX_FILTER_LAUNCH(1) }
         else if (cfg == 2) { RVX_FILTER_LAUNCH(2) }
+        else if (cfg == 3) { RVX_FILTER_LAUNCH(3) }
         else { RVX_FILTER_LAUNCH(0) }
 #undef RVX_FILTER_LAUNCH
     }

@@ -46,7 +46,7 @@ def test_forced_filter_bit_exact(monkeypatch, metric, name, k):
     assert np.array_equal(dist, rd)
 
 
-@pytest.mark.parametrize("wide", ["0", "1", "2"])
+@pytest.mark.parametrize("wide", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("metric,name", METRICS)
 @pytest.mark.parametrize("d", [32, 96, 256, 768])
 def test_tile_shapes_bit_exact(monkeypatch, wide, metric, name, d):
@@ -192,7 +192,7 @@ def ball_points(n, d, seed, rmax=0.9):
     return (v * (rmax * r.random((n, 1)))).astype(np.float32)
 
 
-@pytest.mark.parametrize("d,wide", [(1024, "1"), (768, "1"), (768, "2"), (128, "0"), (64, "1")])
+@pytest.mark.parametrize("d,wide", [(1024, "1"), (1024, "3"), (768, "1"), (768, "2"), (768, "3"), (128, "0"), (64, "1")])
 @pytest.mark.parametrize("k", [10, 100])
 def test_poincare_filter_matches_valu_and_oracle(monkeypatch, d, wide, k):
     """HyperbolicHnsw exact scan through the MFMA filter with per-row bounds
