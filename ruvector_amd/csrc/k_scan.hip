@@ -1457,9 +1457,12 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     if (metric == RVX_METRIC_POINCARE && !(curv > 0.0f)) return false;
     // tile shape: RVX_SCAN_WIDE 0/1/2 forces it (tests, A/B), else 256^2 for d >= 512
     const int wide_env = env_int("RVX_SCAN_WIDE", -1);
-    // RVX_SCAN_M16=1 runs the wide tile on 16x16x32 MFMAs (cfg 3)
-    int cfg = wide_env >= 0 && wide_env <= 3 ? wide_env : (d >= 512 ? 1 : 0);
-    if (cfg == 1 && env_int("RVX_SCAN_M16", 0)) cfg = 3;
+    // the wide tile runs on 16x16x32 MFMAs (cfg 3) unless RVX_SCAN_M16=0: same cycles per
+    // flop, the chip holds a higher clock (10M x 768 / 10k: filter 156-161 vs 175-177 ms,
+    // identical results; profiles/r04_scan_m16_ab.log); RVX_SCAN_WIDE forces any form
+    const int cfg = wide_env >= 0 && wide_env <= 3 ? wide_env
+                    : d >= 512                     ? (env_int("RVX_SCAN_M16", 1) ? 3 : 1)
+                                                   : 0;
     const int FR = cfg == 1 ? FCfg<1>::FR : cfg == 2 ? FCfg<2>::FR : cfg == 3 ? FCfg<3>::FR : FCfg<0>::FR;
     const int FQ = cfg == 1 ? FCfg<1>::FQ : cfg == 2 ? FCfg<2>::FQ : cfg == 3 ? FCfg<3>::FQ : FCfg<0>::FQ;
     const int F_LDS = cfg == 1 ? FCfg<1>::LDS : cfg == 2 ? FCfg<2>::LDS : cfg == 3 ? FCfg<3>::LDS : FCfg<0>::LDS;
