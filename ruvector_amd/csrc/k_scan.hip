@@ -568,6 +568,10 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
         return ts;
     };
     // DMA piece j of a k-step: rows and queries alternate while both last, then rows
+#ifndef RVX_SCAN_ROW_CPOL
+#define RVX_SCAN_ROW_CPOL 0
+#define RVX_SCAN_QRY_CPOL 0
+#endif
     auto dma_piece = [&](const TileSrc& ts, int k0, unsigned char* dst, int j) {
         const bool qry = j < 2 * QP && (j & 1);
         const int h = j < 2 * QP ? j >> 1 : j - QP;
@@ -575,11 +579,11 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
             __builtin_amdgcn_global_load_lds((const void*)(qbase + k0 * 2 + qoff[h]),
                                              (__attribute__((address_space(3))) void*)(dst + FR * 64 +
                                                                                       (QP * wave + h) * 1024),
-                                             16, 0, 0);
+                                             16, 0, RVX_SCAN_QRY_CPOL);
         else
             __builtin_amdgcn_global_load_lds((const void*)(ts.base + k0 * 2 + ts.off[h]),
                                              (__attribute__((address_space(3))) void*)(dst + (RP * wave + h) * 1024),
-                                             16, 0, 0);
+                                             16, 0, RVX_SCAN_ROW_CPOL);
     };
     auto fill = [&](const TileSrc& ts, int k0, unsigned char* dst) {
 #pragma unroll
