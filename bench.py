@@ -124,6 +124,12 @@ def main():
     # runs every layer with its own pass.
     defer = layers > 1 and os.environ.get("RVX_SAGE_DEFER", "1") != "0"
     invs = [rv.Buffer(n_tot * 4) for _ in range(2)] if defer else None
+    # Layer l (< last) also writes a ReLU-sparse image of its output rows (rvx_row_image_pack:
+    # a 3 KiB slot of the values other than +0.0 per row), from which layer l+1's overlapped
+    # gather reads its neighbour rows — same terms, same order, same bits, ~half the bytes.
+    # RVX_SAGE_IMAGE=0 gathers from the dense table.
+    use_img = layers > 1 and 512 < d <= 768 and d % 4 == 0 and os.environ.get("RVX_SAGE_IMAGE", "1") != "0"
+    imgs = [rv.row_image(n_tot, d) for _ in range(min(layers - 1, 2))] if use_img else None
     g = rv.Graph.random_shard(n_tot, r0, n_loc, deg, 4)
     sage = [rv.GraphSAGELayer(d, d, num_samples=deg) for _ in range(layers)]
     rv.synchronize()
@@ -134,8 +140,10 @@ def main():
             dst = tables[li % 2]
             xm = invs[(li - 1) % 2].handle if defer and li > 0 else None
             yi = invs[li % 2].handle if defer and li < layers - 1 else None
-            rv._lib.call("rvx_sage_forward_exchange2", layer._h, g.handle, src.handle, xm, dst.handle, yi, off_ptr,
-                         comm._h if comm else None, int(li < layers - 1))
+            xi = imgs[(li - 1) % 2].handle if use_img and li > 0 else None
+            yimg = imgs[li % 2].handle if use_img and li < layers - 1 else None
+            rv._lib.call("rvx_sage_forward_exchange3", layer._h, g.handle, src.handle, xm, xi, dst.handle, yi, yimg,
+                         off_ptr, comm._h if comm else None, int(li < layers - 1))
             src = dst
 
     def barrier():
@@ -177,23 +185,43 @@ def main():
                 "traffic": None, "avg_ms": round(avg_s * 1e3, 4), "launches": kern[name]["launches"],
                 "work_per_launch": work_per_launch}
 
-    agg_bytes = n_loc * deg * (4 * d + 4) + n_loc * (8 + 4 * d)   # per layer
+    agg_bytes = n_loc * deg * (4 * d + 4) + n_loc * (8 + 4 * d)   # per layer, dense neighbour rows
     gemm_flops = 2.0 * n_loc * d * (2 * d)
     norm_bytes = 2 * n_loc * d * 4
     norm_layers = 1 if defer else layers  # carried normalisation: only the last layer runs the pass
-    rls = {"sage_aggregate": rl("sage_aggregate", "GB/s", agg_bytes * layers, HBM_PEAK_GBS, "hbm"),
+    agg_total, img_info, pack_bytes = agg_bytes * layers, None, 0
+    if use_img:
+        # layers >= 2 read imaged neighbour rows: per edge the record the gather loads (16-B
+        # granules of header + values; the dense row where the slot holds none) + column id +
+        # count; the image's mean over every row of the table (the graph is uniform random)
+        nnz = imgs[0].download(np.uint16, (n_tot,), offset=n_tot * 3072).astype(np.int64)
+        rec = np.where(nnz <= 736, (128 + 4 * nnz + 15) // 16 * 16, 4 * d)
+        rec_mean = float(rec.mean())
+        agg_img = n_loc * deg * (rec_mean + 4 + 2) + n_loc * (8 + 4 * d)
+        agg_total = agg_bytes + agg_img * (layers - 1)
+        pack_bytes = n_tot * (4 * d + rec_mean + 2) * (layers - 1)  # every row imaged where it lands
+        img_info = {"mean_nnz": round(float(nnz.mean()), 1), "rows_in_slots": round(float((nnz <= 736).mean()), 4),
+                    "mean_record_bytes": round(rec_mean, 1), "dense_row_bytes": 4 * d,
+                    "gather_bytes_per_layer": {"dense": agg_bytes, "imaged": round(agg_img)}}
+    rls = {"sage_aggregate": rl("sage_aggregate", "GB/s", agg_bytes * (1 if use_img else layers), HBM_PEAK_GBS, "hbm"),
            "sage_gemm": rl("sage_gemm", "TFLOP/s", gemm_flops * layers, GEMM_PEAK_TFS, "mfma"),
            "sage_normalize": rl("sage_normalize", "GB/s", norm_bytes * norm_layers, HBM_PEAK_GBS, "hbm")}
+    if use_img:  # layers >= 2 gather from the image (their own tag)
+        rls["sage_aggregate_img"] = rl("sage_aggregate_img", "GB/s", agg_img * (layers - 1), HBM_PEAK_GBS, "hbm")
+        rls["rows_image_pack"] = rl("rows_image_pack", "GB/s", pack_bytes, HBM_PEAK_GBS, "hbm")
     if comm is not None:
         rls["halo_exchange"] = rl("halo_exchange", "GB/s", (n_tot - n_loc) * d * 4 * (layers - 1), XGMI_PEAK_GBS,
                                   "xgmi")
     dom = max((k for k in rls if rls[k] and k != "halo_exchange"), key=lambda k: kern[k]["total_ms"])
-    attach_pmc_traffic(rls, {"nodes_total": n_tot, "dim": d, "degree": deg, "layers": layers,
-                             "parallelism": f"node-range x{world}", "pipeline": PIPELINE})
+    pmc_cfg = {"nodes_total": n_tot, "dim": d, "degree": deg, "layers": layers,
+               "parallelism": f"node-range x{world}", "pipeline": PIPELINE}
+    if use_img:
+        pmc_cfg["row_image"] = True  # profiles of the dense-gather pipeline do not apply
+    attach_pmc_traffic(rls, pmc_cfg)
     # whole-layer floor: HBM and MFMA work overlap, so a layer cannot beat the
     # larger of the two floors
     layer_ms = elapsed / a.steps / layers * 1e3
-    hbm_floor = (agg_bytes + norm_bytes * norm_layers / layers) / (HBM_PEAK_GBS * 1e9) * 1e3
+    hbm_floor = (agg_total / layers + norm_bytes * norm_layers / layers) / (HBM_PEAK_GBS * 1e9) * 1e3
     mfma_floor = gemm_flops / (GEMM_PEAK_TFS * 1e12) * 1e3
     layer_rl = {"layer_ms": round(layer_ms, 3), "hbm_floor_ms": round(hbm_floor, 3),
                 "mfma_floor_ms": round(mfma_floor, 3), "frac": round(max(hbm_floor, mfma_floor) / layer_ms, 4)}
@@ -213,7 +241,10 @@ def main():
                    "pipeline": PIPELINE,
                    "normalisation": ("layer l's L2 normalisation carried into layer l+1 as 1/|y| per row "
                                      "(rvx_sage_forward_exchange2); the last layer normalises in place")
-                   if defer else "every layer normalises in place"},
+                   if defer else "every layer normalises in place",
+                   "row_image": (dict(img_info, note="layer l+1 gathers layer l's ReLU-sparse rows from a packed "
+                                      "image (rvx_sage_forward_exchange3; same bits as the dense gather)")
+                                 if use_img else "off")},
         "roofline": dict(rls[dom], kernel=dom),
         "roofline_kernels": {k: v for k, v in rls.items() if v},
         "roofline_layer": layer_rl,

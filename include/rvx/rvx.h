@@ -201,6 +201,27 @@ rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g
 rvx_status rvx_sage_forward_exchange2(const rvx_sage_layer* l, const rvx_graph* g, rvx_buffer* x_full,
                                       const rvx_buffer* x_rowmul, rvx_buffer* y_full, rvx_buffer* y_rowinv,
                                       const int64_t* offsets, rvx_comm* comm, int32_t exchange);
+/* ReLU-sparse row images (an rvx extension, no reference counterpart; values unchanged).
+ * A GraphSAGE layer's output rows are (n + s).max(0.0) (graphsage.rs:172-176): about half of
+ * every entry is +0.0. An image of an [n][dim] f32 table keeps, per row, a 3 KiB slot with the
+ * row's entries other than +0.0 (bit patterns preserved) and a bitmap, when there are at most
+ * 736 of them (beyond that the dense row is fewer bytes), plus a u16 count per row; a gather over the image adds exactly the terms, in
+ * exactly the order, of a gather over the table (mean / sum aggregators), reading about half
+ * the bytes. Needs 512 < dim <= 768, dim % 4 == 0.
+ * rvx_row_image_bytes: the image buffer size for n rows.
+ * rvx_row_image_pack: rows [r0, r0 + rows) of x (n_total x dim) into the image.
+ * rvx_sage_forward_exchange3 = rvx_sage_forward_exchange2 plus: x_image (NULL = none), an image
+ * of x_full's current contents (every row; the caller keeps it current — e.g. the previous
+ * layer's y_image), read by the overlapped gather for neighbour rows; y_image (NULL = none)
+ * receives the image of every row of y_full the call writes or receives. Same output bits
+ * with or without images. */
+rvx_status rvx_row_image_bytes(int64_t n, int32_t dim, int64_t* bytes);
+rvx_status rvx_row_image_pack(const rvx_buffer* x, int64_t n_total, int64_t r0, int64_t rows, int32_t dim,
+                              rvx_buffer* image);
+rvx_status rvx_sage_forward_exchange3(const rvx_sage_layer* l, const rvx_graph* g, rvx_buffer* x_full,
+                                      const rvx_buffer* x_rowmul, rvx_buffer* x_image, rvx_buffer* y_full,
+                                      rvx_buffer* y_rowinv, rvx_buffer* y_image, const int64_t* offsets,
+                                      rvx_comm* comm, int32_t exchange);
 
 
 /* ------------------------------------------------------------------ */

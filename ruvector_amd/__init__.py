@@ -16,7 +16,7 @@ from .core import (DistanceMetric, FlatIndex, HnswConfig, HnswIndex, RuvectorErr
 from .gnn import (GCNLayer, GnnError, GraphSAGELayer, RuvectorLayer, aggregate, differentiable_search,
                   differentiable_search_device,  # noqa: E402
                   differentiable_search_batch, hierarchical_forward, hierarchical_forward_batch,
-                  hierarchical_forward_device)
+                  hierarchical_forward_device, pack_row_image, row_image, row_image_bytes)
 from .attention import DualSpaceAttention, DualSpaceConfig, EdgeFeaturedAttention, EdgeFeaturedConfig  # noqa: E402
 from .hyperbolic import (DualSpaceIndex, HyperbolicError, HyperbolicHnsw, HyperbolicHnswConfig,  # noqa: E402
                          ShardedHyperbolicHnsw, ShardedHyperbolicSearch)
@@ -33,5 +33,6 @@ __all__ = [
     "EdgeFeaturedConfig", "HyperbolicError", "HyperbolicHnsw", "HyperbolicHnswConfig", "ShardedHyperbolicHnsw", "ShardedHyperbolicSearch",
     "DualSpaceIndex",
     "NeuralSearch", "QueryMode", "RuvectorQuery", "DbOptions", "SearchQuery", "VectorDB", "VectorEntry", "differentiable_search_device", "hnsw_last_search_stats", "scan_last_stats",
+    "pack_row_image", "row_image", "row_image_bytes",
 ]
 __version__ = "0.1.0"

@@ -122,6 +122,9 @@ SIGNATURES = {
     "rvx_sage_forward_shard_device": (None, [P, P, P, I64, P]),
     "rvx_sage_forward_exchange": (None, [P, P, P, P, PI64, P, I32]),
     "rvx_sage_forward_exchange2": (None, [P, P, P, P, P, P, PI64, P, I32]),
+    "rvx_sage_forward_exchange3": (None, [P, P, P, P, P, P, P, P, PI64, P, I32]),
+    "rvx_row_image_bytes": (None, [I64, I32, PI64]),
+    "rvx_row_image_pack": (None, [P, I64, I64, I64, I32, P]),
     "rvx_gcn_layer_create": (None, [I32, I32, I32, PF32, PF32, PP]),
     "rvx_gcn_layer_destroy": (None, [P]),
     "rvx_gcn_forward": (None, [P, P, I32, PF32, I64, PF32]),

@@ -44,6 +44,14 @@ __device__ __forceinline__ float4 ld_row4(const float* p) {
     return *reinterpret_cast<const float4*>(p);
 }
 
+template <int NV, int AGG>
+__device__ __forceinline__ void agg_row_finish(float4 (&acc)[NV], const bool (&active)[NV], int cnt_total,
+                                               const float* __restrict__ x, int dim, int empty_fill, int post_scale,
+                                               float* __restrict__ out, const float* __restrict__ self_x,
+                                               float* __restrict__ row_scale, _Float16* __restrict__ planes,
+                                               int64_t pstride, const float* __restrict__ self_mul, int64_t row,
+                                               int lane);
+
 // One wave computes destination row `row` (see k_aggregate_vec for the arguments).
 template <int NV, int AGG, bool W, int U, bool NT>
 __device__ __forceinline__ void agg_vec_row(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
@@ -109,6 +117,19 @@ __device__ __forceinline__ void agg_vec_row(const int64_t* __restrict__ rp, cons
         }
     }
 
+    agg_row_finish<NV, AGG>(acc, active, cnt_total, x, dim, empty_fill, post_scale, out, self_x, row_scale, planes,
+                            pstride, self_mul, row, lane);
+}
+
+// The end of a destination row: mean / GCN scale, the split-f16 operand scale (and planes) over
+// [aggregate | self], the store (or the empty-row fill). Shared by the dense and image gathers.
+template <int NV, int AGG>
+__device__ __forceinline__ void agg_row_finish(float4 (&acc)[NV], const bool (&active)[NV], int cnt_total,
+                                               const float* __restrict__ x, int dim, int empty_fill, int post_scale,
+                                               float* __restrict__ out, const float* __restrict__ self_x,
+                                               float* __restrict__ row_scale, _Float16* __restrict__ planes,
+                                               int64_t pstride, const float* __restrict__ self_mul, int64_t row,
+                                               int lane) {
     float* dst = out + row * dim + 4 * lane;
     if (cnt_total > 0) {
         if (AGG == AGG_MEAN) {
@@ -173,31 +194,197 @@ __device__ __forceinline__ void agg_vec_row(const int64_t* __restrict__ rp, cons
         if (active[j]) *reinterpret_cast<float4*>(dst + 256 * j) = acc[j];
 }
 
+// ---- ReLU-sparse row image (RowImage, kernels.hpp) ----
+// inclusive wave64 prefix sum in VALU: DPP row shifts 1/2/4/8, then row broadcasts 15 / 31
+__device__ __forceinline__ unsigned img_wave_scan(unsigned x) {
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+// header bits of this lane (12: block j's 4 columns at bits 4j..4j+3) -> the packed position of
+// the lane's first value in each block (values are stored block by block, lane by lane); also
+// the row's total count
+__device__ __forceinline__ void img_positions(unsigned h, int (&p)[3], unsigned& total) {
+    const unsigned c = __popc(h & 15u) | (__popc((h >> 4) & 15u) << 10) | (__popc((h >> 8) & 15u) << 20);
+    const unsigned s = img_wave_scan(c);
+    const unsigned tot = (unsigned)__builtin_amdgcn_readlane((int)s, 63);
+    const unsigned ex = s - c;
+    const int b1 = (int)(tot & 1023u), b2 = b1 + (int)((tot >> 10) & 1023u);
+    p[0] = (int)(ex & 1023u);
+    p[1] = b1 + (int)((ex >> 10) & 1023u);
+    p[2] = b2 + (int)(ex >> 20);
+    total = (unsigned)b2 + (tot >> 20);
+}
+// a value is kept unless its bits are those of +0.0 (so -0.0 and NaN travel as they are)
+__device__ __forceinline__ unsigned img_nz(float v) { return __float_as_uint(v) != 0u; }
+
+// Image gather of one destination row (mean / sum, no edge weights, NV == 3): the same terms,
+// order and arithmetic as agg_vec_row<3, AGG, false, 8, true>, so the same bits. Per group of 8
+// neighbour rows, three 16-B loads per lane and row — from the row's slot (lanes past the
+// record re-read its last 16 B: only the record's bytes are fetched) when nnz <= IMG_CAP, else
+// from the dense row — then, two rows at a time, each imaged record passes through one of the
+// wave's two 3 KiB LDS windows (ds_write_b128 per KiB it spans) and each lane reads its header
+// bits and its values (12 ds_read_b32 at the packed positions).
+template <int AGG>
+__device__ __forceinline__ void agg_img_row(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                            const float* __restrict__ x, int dim,
+                                            const unsigned char* __restrict__ slots,
+                                            const uint16_t* __restrict__ nnz, float* __restrict__ out,
+                                            const float* __restrict__ self_x, float* __restrict__ row_scale,
+                                            const float* __restrict__ row_mul, const float* __restrict__ self_mul,
+                                            int64_t row, int lane, unsigned char* win) {
+#ifndef RVX_IMG_U
+#define RVX_IMG_U 8
+#endif
+    constexpr int NV = 3, U = RVX_IMG_U;
+    const int64_t beg = rp[row], end = rp[row + 1];
+    const int cnt_total = (int)(end - beg);
+    float4 acc[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    bool active[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) active[j] = (4 * lane + 256 * j) < dim;
+    const int dlast = (dim - 4) * 4;  // byte offset of the row's last float4 (inactive lanes re-read it)
+    int doff[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) doff[j] = active[j] ? (4 * lane + 256 * j) * 4 : dlast;
+
+    for (int64_t e0 = beg; e0 < end; e0 += 64) {
+        const int cnt = (int)min<int64_t>(64, end - e0);
+        const int my_c = lane < cnt ? col[e0 + lane] : 0;
+        const float my_m = (row_mul && lane < cnt) ? row_mul[my_c] : 1.0f;
+        const int my_n = lane < cnt ? (int)nnz[my_c] : 0;
+        for (int t = 0; t < cnt; t += U) {
+            float4 v[U][NV];
+            bool img[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int tu = min(t + u, cnt - 1);  // a short group re-reads its last row (not accumulated)
+                const int c = __builtin_amdgcn_readlane(my_c, tu);
+                const int nz = __builtin_amdgcn_readlane(my_n, tu);
+                img[u] = nz <= IMG_CAP;
+                const char* base;
+                int o[NV];
+                if (img[u]) {
+                    base = reinterpret_cast<const char*>(slots + (int64_t)c * IMG_SLOT);
+                    const int last = ((128 + 4 * nz - 1) & ~15);
+                    o[0] = min(16 * lane, last);
+                    o[1] = min(1024 + 16 * lane, last);
+                    o[2] = min(2048 + 16 * lane, last);
+                } else {
+                    base = reinterpret_cast<const char*>(x + (int64_t)c * dim);
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) o[j] = doff[j];
+                }
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    const f32x4 w = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(base + o[j]));
+                    v[u][j] = make_float4(w.x, w.y, w.z, w.w);
+                }
+            }
+            // rows in pairs through the wave's two windows: both records in, both expanded, then
+            // accumulated in edge order (the LDS round trips of the pair overlap)
+#pragma unroll
+            for (int u = 0; u < U; u += 2) {
+                if (t + u >= cnt) break;
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+#ifdef RVX_IMG_NOEXP  // timing-only ablation: imaged rows accumulated unexpanded (wrong values)
+                    continue;
+#endif
+                    if (t + u + b >= cnt || !img[u + b]) continue;
+                    const int rec = 128 + 4 * __builtin_amdgcn_readlane(my_n, t + u + b);
+                    f32x4* wv = reinterpret_cast<f32x4*>(win + b * IMG_SLOT);
+                    wv[lane] = f32x4{v[u + b][0].x, v[u + b][0].y, v[u + b][0].z, v[u + b][0].w};
+                    if (rec > 1024) wv[64 + lane] = f32x4{v[u + b][1].x, v[u + b][1].y, v[u + b][1].z, v[u + b][1].w};
+                    if (rec > 2048) wv[128 + lane] = f32x4{v[u + b][2].x, v[u + b][2].y, v[u + b][2].z, v[u + b][2].w};
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+#ifdef RVX_IMG_NOEXP
+                    continue;
+#endif
+                    if (t + u + b >= cnt || !img[u + b]) continue;
+                    const unsigned char* wb = win + b * IMG_SLOT;
+                    const unsigned h = reinterpret_cast<const uint16_t*>(wb)[lane];
+                    const float* wf = reinterpret_cast<const float*>(wb + 128);
+                    int p[3];
+                    unsigned tot;
+                    img_positions(h, p, tot);
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) {
+                        const unsigned nib = (h >> (4 * j)) & 15u;
+                        float e[4];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const int q = min(p[j] + (int)__popc(nib & ((1u << k) - 1u)), IMG_CAP - 1);
+                            const float val = wf[q];
+                            e[k] = ((nib >> k) & 1u) ? val : 0.0f;
+                        }
+                        v[u + b][j] = make_float4(e[0], e[1], e[2], e[3]);
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // reads done before the next pair's writes
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    if (t + u + b >= cnt) break;
+                    if (row_mul) {
+                        const float mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_m), t + u + b));
+#pragma unroll
+                        for (int j = 0; j < NV; ++j) v[u + b][j] = scale4(v[u + b][j], mu);
+                    }
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) acc[j] = agg_op<AGG>(acc[j], v[u + b][j]);
+                }
+            }
+        }
+    }
+    agg_row_finish<NV, AGG>(acc, active, cnt_total, x, dim, 0, 0, out, self_x, row_scale, nullptr, 0, self_mul, row,
+                            lane);
+}
+
 // Dynamic form of the overlapped GraphSAGE gather (AggHelp): every wave takes destination
 // rows from the chunk's counter until it passes n. Used by the chunk's own gather kernel and
-// by the previous chunk's GEMM blocks once their tiles are done.
+// by the previous chunk's GEMM blocks once their tiles are done. `win`: this wave's two
+// IMG_SLOT LDS windows for the image path.
 template <int NV, int AGG>
-__device__ __forceinline__ void agg_help_rows(const AggHelp& h, int lane) {
+__device__ __forceinline__ void agg_help_rows(const AggHelp& h, int lane, unsigned char* win) {
+    const bool use_img = NV == 3 && AGG != AGG_MAX && h.img_slots != nullptr;
     for (;;) {
         int64_t row = 0;
         if (lane == 0) row = (int64_t)atomicAdd(h.counter, 1u);
         row = __builtin_amdgcn_readfirstlane((int)row);
         if (row >= h.n) return;
+        if constexpr (NV == 3 && AGG != AGG_MAX) {
+            if (use_img) {
+                agg_img_row<AGG>(h.rp, h.col, h.x, h.dim, h.img_slots, h.img_nnz, h.out, h.self_x, h.row_scale,
+                                 h.row_mul, h.self_mul, row, lane, win);
+                continue;
+            }
+        }
         agg_vec_row<NV, AGG, false, 8, true>(h.rp, h.col, nullptr, h.x, h.dim, 0, 0, h.out, h.self_x, h.row_scale,
                                             nullptr, 0, h.row_mul, h.self_mul, row, lane);
     }
 }
 template <int NV>
-__device__ __forceinline__ void agg_help_run_nv(const AggHelp& h, int lane) {
-    if (h.agg == AGG_MEAN) agg_help_rows<NV, AGG_MEAN>(h, lane);
-    else if (h.agg == AGG_SUM) agg_help_rows<NV, AGG_SUM>(h, lane);
-    else agg_help_rows<NV, AGG_MAX>(h, lane);
+__device__ __forceinline__ void agg_help_run_nv(const AggHelp& h, int lane, unsigned char* win) {
+    if (h.agg == AGG_MEAN) agg_help_rows<NV, AGG_MEAN>(h, lane, win);
+    else if (h.agg == AGG_SUM) agg_help_rows<NV, AGG_SUM>(h, lane, win);
+    else agg_help_rows<NV, AGG_MAX>(h, lane, win);
 }
-__device__ __forceinline__ void agg_help_run(const AggHelp& h) {
+// lds: IMG_WIN bytes per wave of the block (wave w uses lds + w * IMG_WIN)
+__device__ __forceinline__ void agg_help_run(const AggHelp& h, unsigned char* lds) {
     const int lane = threadIdx.x & 63;
-    if (h.dim > 512) agg_help_run_nv<3>(h, lane);
-    else if (h.dim > 256) agg_help_run_nv<2>(h, lane);
-    else agg_help_run_nv<1>(h, lane);
+    unsigned char* win = lds + (threadIdx.x >> 6) * IMG_WIN;
+    if (h.dim > 512) agg_help_run_nv<3>(h, lane, win);
+    else if (h.dim > 256) agg_help_run_nv<2>(h, lane, win);
+    else agg_help_run_nv<1>(h, lane, win);
 }
 
 }  // namespace aggrow

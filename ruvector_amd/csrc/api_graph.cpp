@@ -264,9 +264,12 @@ __global__ void k_scale_rows(float* __restrict__ x, int64_t rows, int dim, const
 // and in the GEMM's self-operand split); y_inv (nullable) makes the layer leave its output
 // rows unnormalised and write 1/|y| per row instead (from the GEMM epilogue's per-tile
 // sums of squares) — the pass that re-reads and re-writes y is not run.
+// Row images (RowImage, kernels.hpp; both optional): x_img, an image of every row of x (global
+// row ids), lets the overlapped gather read ReLU-sparse neighbour rows from it; y_img (indexed
+// like y, i.e. this graph's rows) receives the image of each output row chunk as it completes.
 void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* x, float* y, int64_t row_offset = 0,
                       int chunks = 0, const ChunkHook& hook = nullptr, const float* x_mul = nullptr,
-                      float* y_inv = nullptr) {
+                      float* y_inv = nullptr, RowImage x_img = RowImage(), RowImage y_img = RowImage()) {
     // rows with more than num_samples neighbours aggregate the reference's
     // sample_neighbors subset (graphsage.rs:92-102, k_sample.hip)
     g = sampled_graph(g, l->num_samples);
@@ -340,10 +343,12 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
             RVX_HIP(hipStreamWaitEvent(d.aux2, evg[cc], 0));
             StreamScope on_norm(d.aux2);
             normalize_rows(y + rr0 * l->out, rrows, l->out, true, "sage_normalize");
+            if (y_img) rows_image_pack(y, rr0, rrows, l->out, y_img);
             if (hook) hook(cc, rr0, rrows);
             return;
         }
         if (norm) normalize_rows(y + rr0 * l->out, rrows, l->out, true, "sage_normalize");
+        if (y_img) rows_image_pack(y, rr0, rrows, l->out, y_img);
         if (hook) {
             if (norm_side) {  // keep the hooks in chunk order on the normalise stream
                 RVX_HIP(hipEventRecord(evg[cc], main_s));
@@ -377,6 +382,10 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         h.out = agg + rr0 * l->in; h.self_x = x + (row_offset + rr0) * l->in; h.row_scale = scale + rr0;
         h.row_mul = x_mul; h.self_mul = x_mul ? x_mul + row_offset + rr0 : nullptr;
         h.counter = counters + (rr0 / step) * 16;
+        if (x_img && row_image_ok(l->in) && a != AGG_MAX) {
+            h.img_slots = x_img.slots;
+            h.img_nnz = x_img.nnz;
+        }
         return h;
     };
     StreamScope on_main(main_s);
@@ -388,7 +397,9 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
             StreamScope on_aux(gath_s);
             // the layer's first chunk has no GEMM beside it: a wider grid (RVX_AGG_FIRST_CAP
             // blocks per CU, read per call; same rows, same bits)
-            aggregate_rows_help(help_of(r0), "sage_aggregate", c == 0 ? env_int("RVX_AGG_FIRST_CAP", 4) : 0);
+            const AggHelp hc = help_of(r0);
+            aggregate_rows_help(hc, hc.img_slots ? "sage_aggregate_img" : "sage_aggregate",
+                                c == 0 ? env_int("RVX_AGG_FIRST_CAP", 4) : 0);
             RVX_HIP(hipEventRecord(ev[c], gath_s));
             RVX_HIP(hipStreamWaitEvent(main_s, ev[c], 0));
         } else if (chunks > 1) {
@@ -681,6 +692,51 @@ rvx_status rvx_sage_forward_exchange(const rvx_sage_layer* l, const rvx_graph* g
 rvx_status rvx_sage_forward_exchange2(const rvx_sage_layer* l, const rvx_graph* g, rvx_buffer* x_full,
                                       const rvx_buffer* x_rowmul, rvx_buffer* y_full, rvx_buffer* y_rowinv,
                                       const int64_t* offsets, rvx_comm* comm, int32_t exchange) {
+    return rvx_sage_forward_exchange3(l, g, x_full, x_rowmul, nullptr, y_full, y_rowinv, nullptr, offsets, comm,
+                                      exchange);
+}
+
+rvx_status rvx_row_image_bytes(int64_t n, int32_t dim, int64_t* bytes) {
+    return guard([&] {
+        RVX_REQUIRE(bytes && n >= 0 && n < ((int64_t)1 << 40), RVX_ERR_INVALID_PARAMETER, "bad row-image arguments");
+        RVX_REQUIRE(row_image_ok(dim), RVX_ERR_UNSUPPORTED, "row images need 512 < dim <= 768, dim % 4 == 0");
+        *bytes = n * (IMG_SLOT + 2) + 16;  // slots, then the nnz array (u16 per row)
+    });
+}
+
+namespace {
+RowImage image_of(rvx_buffer* b, int64_t n, int dim, const char* what) {
+    if (!b) return RowImage();
+    RVX_REQUIRE(row_image_ok(dim), RVX_ERR_UNSUPPORTED, std::string(what) + ": row images need 512 < dim <= 768");
+    RVX_REQUIRE(b->mem.bytes >= n * (IMG_SLOT + 2) + 16, RVX_ERR_DIMENSION_MISMATCH,
+                std::string(what) + " smaller than rvx_row_image_bytes");
+    RowImage im;
+    im.slots = b->mem.as<unsigned char>();
+    im.nnz = reinterpret_cast<uint16_t*>(im.slots + n * IMG_SLOT);
+    return im;
+}
+RowImage image_rows(RowImage im, int64_t r0) {  // the same image seen from row r0 on
+    if (im) { im.slots += r0 * IMG_SLOT; im.nnz += r0; }
+    return im;
+}
+}  // namespace
+
+rvx_status rvx_row_image_pack(const rvx_buffer* x, int64_t n_total, int64_t r0, int64_t rows, int32_t dim,
+                              rvx_buffer* image) {
+    return guard([&] {
+        RVX_REQUIRE(x && image && r0 >= 0 && rows >= 0 && r0 + rows <= n_total, RVX_ERR_INVALID_PARAMETER,
+                    "bad row-image pack arguments");
+        RVX_REQUIRE(x->mem.bytes >= n_total * dim * 4, RVX_ERR_DIMENSION_MISMATCH, "x smaller than n_total*dim");
+        const RowImage im = image_of(image, n_total, dim, "image");
+        ComputeLock cl;
+        rows_image_pack(x->mem.as<float>(), r0, rows, dim, im);
+    });
+}
+
+rvx_status rvx_sage_forward_exchange3(const rvx_sage_layer* l, const rvx_graph* g, rvx_buffer* x_full,
+                                      const rvx_buffer* x_rowmul, rvx_buffer* x_image, rvx_buffer* y_full,
+                                      rvx_buffer* y_rowinv, rvx_buffer* y_image, const int64_t* offsets,
+                                      rvx_comm* comm, int32_t exchange) {
     return guard([&] {
         check_graph(g);
         RVX_REQUIRE(l && x_full && y_full && offsets, RVX_ERR_INVALID_PARAMETER, "null argument");
@@ -696,6 +752,9 @@ rvx_status rvx_sage_forward_exchange2(const rvx_sage_layer* l, const rvx_graph* 
         RVX_REQUIRE(y_full->mem.bytes >= N * l->out * 4, RVX_ERR_DIMENSION_MISMATCH, "y_full smaller than N*out");
         RVX_REQUIRE(!x_rowmul || x_rowmul->mem.bytes >= N * 4, RVX_ERR_DIMENSION_MISMATCH, "x_rowmul smaller than N");
         RVX_REQUIRE(!y_rowinv || y_rowinv->mem.bytes >= N * 4, RVX_ERR_DIMENSION_MISMATCH, "y_rowinv smaller than N");
+        RVX_REQUIRE(!x_image || x_image != y_image, RVX_ERR_INVALID_PARAMETER, "x_image and y_image must differ");
+        const RowImage ximg = image_of(x_image, N, l->in, "x_image");
+        const RowImage yimg = image_of(y_image, N, l->out, "y_image");
         ComputeLock cl;
         float* y = y_full->mem.as<float>();
         const float* x = x_full->mem.as<float>();
@@ -721,8 +780,11 @@ rvx_status rvx_sage_forward_exchange2(const rvx_sage_layer* l, const rvx_graph* 
             yinv = nullptr;
         }
         float* yinv_rows = yinv ? yinv + offsets[me] : nullptr;
+        // (x_image describes x as the caller passed it: a rescale in place above would stale it)
+        const RowImage xi = xm || !x_rowmul ? ximg : RowImage();
         if (!exchange || world == 1) {
-            sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], 0, nullptr, xm, yinv_rows);
+            sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], 0, nullptr, xm, yinv_rows, xi,
+                             image_rows(yimg, offsets[me]));
             return;
         }
         const std::vector<ExchangeRound> plan = exchange_plan(PLAN_SAGE, offsets, world);
@@ -736,8 +798,12 @@ rvx_status rvx_sage_forward_exchange2(const rvx_sage_layer* l, const rvx_graph* 
             ProfScope ps("halo_exchange");
             comm_exchange_rows(comm, y, l->out, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
             if (yinv_xchg) comm_exchange_rows(comm, yinv_xchg, 1, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
+            if (yimg)  // the rows that arrived, imaged where they land (this rank's own: sage_forward_dev)
+                for (int p = 0; p < world; ++p)
+                    if (p != me) rows_image_pack(y, plan[c].r0[p], plan[c].rows[p], l->out, yimg);
         };
-        sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], chunks, hook, xm, yinv_rows);
+        sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], chunks, hook, xm, yinv_rows, xi,
+                         image_rows(yimg, offsets[me]));
         RVX_HIP(hipEventRecord(ev[chunks], d.xfer));
         {
             // the exchange's tail the compute stream waits for: from the last chunk's

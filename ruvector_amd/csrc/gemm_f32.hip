@@ -1663,12 +1663,17 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt
             h2w_tile<DUAL, WN, BN, NW, PIPE, AMX, GATE>(g, epi, first + t);
             __syncthreads();  // LDS stages and s_t are reused by the next tile
         }
-        if constexpr (HELP) aggrow::agg_help_run(g.help);
+        // the loop ends after a barrier: the stage memory is free for the image windows
+        if constexpr (HELP) aggrow::agg_help_run(g.help, xsm);
         return;
     }
     const int64_t nwg = g.nblocks, bid = blockIdx.x;
     h2w_tile<DUAL, WN, BN, NW, PIPE, AMX, GATE>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
-    if constexpr (HELP) aggrow::agg_help_run(g.help);
+    if constexpr (HELP) {
+        extern __shared__ __attribute__((aligned(16))) unsigned char xsm_h[];
+        __syncthreads();  // every wave is done with the tile's stages
+        aggrow::agg_help_run(g.help, xsm_h);
+    }
 }
 
 // B rows n of one or two [N][K] matrices: common scale t_n, f16 planes of each

@@ -271,8 +271,65 @@ void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, 
 }
 
 namespace {
-__global__ __launch_bounds__(256) void k_aggregate_help(AggHelp h) { aggrow::agg_help_run(h); }
+__global__ __launch_bounds__(256) void k_aggregate_help(AggHelp h) {
+    __shared__ __attribute__((aligned(16))) unsigned char win[ROWS_PER_BLOCK * IMG_WIN];  // image windows
+    aggrow::agg_help_run(h, win);
+}
+
+// One wave per row: header bits, packed positions (agg_row.hpp), the record assembled in the
+// wave's LDS window (scattered 4-B LDS stores), then written out as whole 16-B chunks
+// (coalesced); nnz for every row (rows above IMG_CAP keep no slot: readers take the dense row).
+__global__ __launch_bounds__(256) void k_rows_image_pack(const float* __restrict__ x, int64_t r0, int64_t rows,
+                                                         int dim, unsigned char* __restrict__ slots,
+                                                         uint16_t* __restrict__ nnz) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) f32x4 win[ROWS_PER_BLOCK][IMG_SLOT / 16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * ROWS_PER_BLOCK + w;
+    if (i >= rows) return;
+    const int64_t r = r0 + i;
+    const float* src = x + r * dim;
+    float4 v[3];
+    unsigned h = 0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const bool act = 4 * lane + 256 * j < dim;
+        v[j] = act ? *reinterpret_cast<const float4*>(src + 4 * lane + 256 * j) : make_float4(0, 0, 0, 0);
+        const unsigned nib = aggrow::img_nz(v[j].x) | (aggrow::img_nz(v[j].y) << 1) | (aggrow::img_nz(v[j].z) << 2) |
+                             (aggrow::img_nz(v[j].w) << 3);
+        h |= (act ? nib : 0u) << (4 * j);
+    }
+    int p[3];
+    unsigned tot;
+    aggrow::img_positions(h, p, tot);
+    if (lane == 0) nnz[r] = (uint16_t)tot;
+    if (tot > (unsigned)IMG_CAP) return;
+    unsigned char* wb = reinterpret_cast<unsigned char*>(win[w]);
+    reinterpret_cast<uint16_t*>(wb)[lane] = (uint16_t)h;
+    float* vals = reinterpret_cast<float*>(wb + 128);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+        int q = p[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if ((h >> (4 * j + k)) & 1u) vals[q++] = e[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int chunks = (128 + 4 * (int)tot + 15) / 16;
+    f32x4* dst = reinterpret_cast<f32x4*>(slots + r * IMG_SLOT);
+    for (int c = lane; c < chunks; c += 64) dst[c] = win[w][c];
+}
 }  // namespace
+
+bool row_image_ok(int dim) { return dim > 512 && dim <= 768 && dim % 4 == 0; }
+
+void rows_image_pack(const float* x, int64_t r0, int64_t rows, int dim, const RowImage& img) {
+    if (rows <= 0) return;
+    RVX_REQUIRE(img && row_image_ok(dim) && ((uintptr_t)x & 15) == 0, RVX_ERR_INVALID_SHAPE, "row image: bad arguments");
+    RVX_LAUNCH("rows_image_pack", k_rows_image_pack, dim3((unsigned)((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK)),
+               dim3(256), 0, x, r0, rows, dim, img.slots, img.nnz);
+}
 
 bool agg_help_ok(int dim, const float* x, const float* out, const float* self_x) {
     auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };

@@ -31,12 +31,32 @@ struct GemmOperand {
 // chunk's own gather kernel and by the previous chunk's persistent GEMM once its tiles are done
 // (GemmEpilogue::help). Arguments as aggregate_rows with the vector path's overlapped settings
 // (no edge weights, zero-filled empty rows, no post-scale, no planes).
+// ReLU-sparse row image of a node table (rows_image_pack): a GraphSAGE layer's output is
+// (n + s).max(0.0) (graphsage.rs:172-176), so about half of every row is +0.0. Row r keeps a
+// 3 KiB slot at slots + r * IMG_SLOT — a 128-B header (u16 per lane: bit 4j+k set <=> column
+// 4*lane + 256*j + k is not +0.0) followed by those values in column order — when it has at
+// most IMG_CAP such values; nnz[r] says which (nnz > IMG_CAP: the slot is unused and readers
+// take the dense row). A reader reproduces every value bit for bit (omitted columns are
+// exactly +0.0), so a gather over the image adds the same terms in the same order as over
+// the table. For 512 < dim <= 768 (three 256-column blocks per row).
+constexpr int IMG_SLOT = 3072, IMG_CAP = (IMG_SLOT - 128) / 4;  // 736: beyond it the dense row is fewer bytes
+constexpr int IMG_WIN = 2 * IMG_SLOT;  // LDS per gathering wave (two row windows)
+struct RowImage {
+    unsigned char* slots = nullptr; uint16_t* nnz = nullptr;
+    explicit operator bool() const { return slots && nnz; }
+};
+bool row_image_ok(int dim);
+// rows [r0, r0 + rows) of x (row stride dim) into the image
+void rows_image_pack(const float* x, int64_t r0, int64_t rows, int dim, const RowImage& img);
+
 struct AggHelp {
     const int64_t* rp; const int32_t* col; int64_t n;
     const float* x; int dim; int agg;
     float* out; const float* self_x; float* row_scale;
     const float* row_mul; const float* self_mul;
     unsigned* counter;
+    // optional image of x (mean / sum, row_image_ok(dim)): neighbour rows are read from it
+    const unsigned char* img_slots; const uint16_t* img_nnz;
 };
 // Epilogue: C = epi(alpha * acc + bias0 + bias1 + addend[row][col])
 constexpr int ROWSUMSQ_SLOTS = 8;  // per-row partial sums of squares (column tiles >= 128 wide, N <= 1024)

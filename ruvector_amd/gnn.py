@@ -164,6 +164,24 @@ class GraphSAGELayer:
             pass
 
 
+def row_image_bytes(n: int, dim: int) -> int:
+    """Size of a ReLU-sparse row image of an n x dim table (rvx_row_image_bytes; rvx.h)."""
+    b = C.c_int64()
+    _check("rvx_row_image_bytes", int(n), int(dim), C.byref(b))
+    return b.value
+
+
+def row_image(n: int, dim: int) -> Buffer:
+    """An uninitialised row-image buffer for n rows of dim (see rvx_sage_forward_exchange3)."""
+    return Buffer(row_image_bytes(n, dim))
+
+
+def pack_row_image(x: Buffer, n_total: int, dim: int, image: Buffer, r0: int = 0, rows: Optional[int] = None) -> None:
+    """Rows [r0, r0 + rows) of the n_total x dim table x into the image (rvx_row_image_pack)."""
+    rows = n_total - r0 if rows is None else rows
+    _check("rvx_row_image_pack", x.handle, int(n_total), int(r0), int(rows), int(dim), image.handle)
+
+
 class GCNLayer:
     """GCNLayer::new_with_normalize (gcn.rs:24-53)."""
 

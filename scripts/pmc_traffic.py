@@ -34,6 +34,7 @@ TAGS = {  # kernel symbol substring -> bench tag
     "k_rows_to_f16": "scan_f16",
     "k_hnsw_search": "hnsw_search",
     "k_edge_attn": "gnn_edge_attention",
+    "k_rows_image_pack": "rows_image_pack",
 }
 
 

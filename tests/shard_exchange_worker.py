@@ -132,6 +132,33 @@ def main():
         res["sage_mixed_defer_layer1_row_rel"] = row_rel(a1d, e1)
         res["sage_mixed_defer_layer2_row_rel"] = row_rel(a2d[o0:o1], e2[o0:o1])
 
+        # ---- ReLU-sparse row images across the exchange (rvx_sage_forward_exchange3): every
+        # rank images its own layer-1 rows and the rows it receives; layer 2 gathers from the
+        # image. Same bits as the image-free stack; the image counts match the table.
+        dI = 768
+        xI = rv.Buffer.from_numpy(O.fill_uniform(N * dI, 86).reshape(N, dI) - 0.5)
+        layI = [rv.GraphSAGELayer(dI, dI, num_samples=deg) for _ in range(2)]
+        ivI = rv.Buffer(N * 4)
+        outs = []
+        for use_img in (False, True):
+            img = rv.row_image(N, dI) if use_img else None
+            h = img.handle if img else None
+            t1, t2 = rv.Buffer(N * dI * 4), rv.Buffer(N * dI * 4)
+            call("rvx_sage_forward_exchange3", layI[0]._h, g_loc.handle, xI.handle, None, None, t1.handle,
+                 ivI.handle, h, off_p, comm._h, 1)
+            call("rvx_sage_forward_exchange3", layI[1]._h, g_loc.handle, t1.handle, ivI.handle, h, t2.handle,
+                 None, None, off_p, comm._h, 0)
+            outs.append((t1.download(np.float32, (N, dI)), t2.download(np.float32, (N, dI))[o0:o1]))
+            if img is not None:
+                nnz = img.download(np.uint16, (N,), offset=N * 3072).astype(np.int64)
+                res["image_nnz_all_rows_match"] = bool(np.array_equal(
+                    nnz, (outs[-1][0].view(np.uint32) != 0).sum(axis=1)))
+                res["image_rows_in_slots"] = float((nnz <= 736).mean())
+            del t1, t2, img
+        res["image_layer1_all_rows_equal"] = bool(np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32)))
+        res["image_layer2_owned_equal"] = bool(np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32)))
+        del outs, xI
+
         # ---- RuvectorLayer (M|K|V exchange) and the attention head (T exchange)
         n2 = int(offsets[-1])
         H, heads, deg2 = 64, 4, 5

@@ -1185,14 +1185,15 @@ def test_graphsage_overlapped_gather_prefetch_bits(monkeypatch, in_f, deg):
 
 
 @pytest.mark.parametrize("aggregator", ["mean", "maxpool"])
-@pytest.mark.parametrize("dims,n,deg,chunks", [((768, 768, 768), 20000, 9, 4), ((96, 200, 128), 9000, 5, 3),
-                                               ((512, 256, 512), 8000, 6, 5), ((64, 64, 64), 3000, 0, 2)])
+@pytest.mark.parametrize("dims,n,deg,chunks", [((768, 768, 768), 40000, 9, 2), ((96, 200, 128), 50000, 5, 3),
+                                               ((512, 256, 512), 33000, 6, 2), ((64, 64, 64), 33000, 0, 2)])
 def test_graphsage_gemm_helps_gather_bits(monkeypatch, aggregator, dims, n, deg, chunks):
     """The dynamic overlapped gather (RVX_SAGE_HELP=1, default): chunk c's gather takes its
     rows from a counter and the persistent GEMM of chunk c-1 computes some of them once its
     tiles are done. Same rows, same per-row code (agg_row.hpp), so the stack — deferred
     normalisation factors included — is bit-identical to the static gather (RVX_SAGE_HELP=0),
-    on d 768 / 512 / <= 256 rows, ragged chunk ends and all-empty neighbourhoods."""
+    on d 768 / 512 / <= 256 rows, ragged chunk ends and all-empty neighbourhoods. (A layer is
+    chunked only from 16384 rows per chunk, sage_chunks_for: the sizes keep every case chunked.)"""
     monkeypatch.setenv("RVX_SAGE_CHUNKS", str(chunks))
     d0, d1, d2 = dims
     x = O.fill_uniform(n * d0, 90 + n).reshape(n, d0)

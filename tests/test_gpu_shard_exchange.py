@@ -42,7 +42,7 @@ def test_exchange_entry_points_multi_rank(offsets, tmp_path):
              str(out), ",".join(map(str, offsets))], env=env, start_new_session=True)))
     try:
         for _, p in procs:
-            p.wait(timeout=110)
+            p.wait(timeout=170)
     finally:
         for _, p in procs:
             if p.poll() is None:
@@ -64,3 +64,6 @@ def test_exchange_entry_points_multi_rank(offsets, tmp_path):
         assert r["gnn_owned_equal"], r
         assert r["gnn_fold_owned_equal"] and r["gnn_fold_vs_oracle"] <= 1e-5, r
         assert r["efa_owned_equal"], r
+        # row images across the exchange: received rows imaged on arrival, same bits
+        assert r["image_nnz_all_rows_match"] and r["image_rows_in_slots"] > 0.9, r
+        assert r["image_layer1_all_rows_equal"] and r["image_layer2_owned_equal"], r
