@@ -124,11 +124,12 @@ def main():
     # runs every layer with its own pass.
     defer = layers > 1 and os.environ.get("RVX_SAGE_DEFER", "1") != "0"
     invs = [rv.Buffer(n_tot * 4) for _ in range(2)] if defer else None
-    # Layer l (< last) also writes a ReLU-sparse image of its output rows (rvx_row_image_pack:
-    # a 3 KiB slot of the values other than +0.0 per row), from which layer l+1's overlapped
-    # gather reads its neighbour rows — same terms, same order, same bits, ~half the bytes.
-    # RVX_SAGE_IMAGE=0 gathers from the dense table.
-    use_img = layers > 1 and 512 < d <= 768 and d % 4 == 0 and os.environ.get("RVX_SAGE_IMAGE", "1") != "0"
+    # RVX_SAGE_IMAGE=1 (opt-in): layer l (< last) also writes a ReLU-sparse image of its output
+    # rows (rvx_row_image_pack: a 3 KiB slot of the values other than +0.0 per row), from which
+    # layer l+1's overlapped gather reads its neighbour rows — same terms, same order, same bits,
+    # 46% fewer bytes; beside the GEMM the expansion through LDS costs what the bytes save
+    # (DESIGN.md §4.3), so the default gathers from the dense table.
+    use_img = layers > 1 and 512 < d <= 768 and d % 4 == 0 and os.environ.get("RVX_SAGE_IMAGE", "0") == "1"
     imgs = [rv.row_image(n_tot, d) for _ in range(min(layers - 1, 2))] if use_img else None
     g = rv.Graph.random_shard(n_tot, r0, n_loc, deg, 4)
     sage = [rv.GraphSAGELayer(d, d, num_samples=deg) for _ in range(layers)]

@@ -300,6 +300,9 @@ __device__ __forceinline__ void agg_img_row(const int64_t* __restrict__ rp, cons
                     if (t + u + b >= cnt || !img[u + b]) continue;
                     const int rec = 128 + 4 * __builtin_amdgcn_readlane(my_n, t + u + b);
                     f32x4* wv = reinterpret_cast<f32x4*>(win + b * IMG_SLOT);
+#ifdef RVX_IMG_NOWRITE  // timing-only ablation (wrong values)
+                    continue;
+#endif
                     wv[lane] = f32x4{v[u + b][0].x, v[u + b][0].y, v[u + b][0].z, v[u + b][0].w};
                     if (rec > 1024) wv[64 + lane] = f32x4{v[u + b][1].x, v[u + b][1].y, v[u + b][1].z, v[u + b][1].w};
                     if (rec > 2048) wv[128 + lane] = f32x4{v[u + b][2].x, v[u + b][2].y, v[u + b][2].z, v[u + b][2].w};
@@ -316,18 +319,25 @@ __device__ __forceinline__ void agg_img_row(const int64_t* __restrict__ rp, cons
                     const float* wf = reinterpret_cast<const float*>(wb + 128);
                     int p[3];
                     unsigned tot;
+#ifdef RVX_IMG_NOSCAN  // timing-only ablation (wrong values)
+                    p[0] = 4 * lane; p[1] = 256 + 4 * lane; p[2] = 480 + 4 * lane; tot = 0;
+#else
                     img_positions(h, p, tot);
+#endif
 #pragma unroll
                     for (int j = 0; j < NV; ++j) {
+                        // the lane's values of block j are consecutive from p[j]: four 4-B reads
+                        // at p[j]..p[j]+3 (two ds_read2_b32; the window has slack past its end),
+                        // then value k is the one of rank popc(bits below k), or +0.0
                         const unsigned nib = (h >> (4 * j)) & 15u;
-                        float e[4];
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            const int q = min(p[j] + (int)__popc(nib & ((1u << k) - 1u)), IMG_CAP - 1);
-                            const float val = wf[q];
-                            e[k] = ((nib >> k) & 1u) ? val : 0.0f;
-                        }
-                        v[u + b][j] = make_float4(e[0], e[1], e[2], e[3]);
+                        const float w0 = wf[p[j]], w1 = wf[p[j] + 1], w2 = wf[p[j] + 2], w3 = wf[p[j] + 3];
+                        const bool b0 = nib & 1u, b1 = nib & 2u, b2 = nib & 4u, b3 = nib & 8u;
+                        const int r2 = (int)b0 + (int)b1, r3 = r2 + (int)b2;
+                        const float e0 = b0 ? w0 : 0.0f;
+                        const float e1 = b1 ? (b0 ? w1 : w0) : 0.0f;
+                        const float e2 = b2 ? (r2 == 0 ? w0 : r2 == 1 ? w1 : w2) : 0.0f;
+                        const float e3 = b3 ? (r3 == 0 ? w0 : r3 == 1 ? w1 : r3 == 2 ? w2 : w3) : 0.0f;
+                        v[u + b][j] = make_float4(e0, e1, e2, e3);
                     }
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // reads done before the next pair's writes

@@ -40,7 +40,7 @@ struct GemmOperand {
 // exactly +0.0), so a gather over the image adds the same terms in the same order as over
 // the table. For 512 < dim <= 768 (three 256-column blocks per row).
 constexpr int IMG_SLOT = 3072, IMG_CAP = (IMG_SLOT - 128) / 4;  // 736: beyond it the dense row is fewer bytes
-constexpr int IMG_WIN = 2 * IMG_SLOT;  // LDS per gathering wave (two row windows)
+constexpr int IMG_WIN = 2 * IMG_SLOT + 16;  // LDS per gathering wave (two row windows + read slack)
 struct RowImage {
     unsigned char* slots = nullptr; uint16_t* nnz = nullptr;
     explicit operator bool() const { return slots && nnz; }

@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/imgvar; mkdir -p $O
-for v in base img_u4 img_noexp base; do
+for v in ${VARIANTS:-base img_u4 img_noexp base}; do
   lib=ruvector_amd/librvx.so; [ "$v" = base ] || lib=variants/librvx_$v.so
   RVX_LIB=$lib timeout -k 10 300 python -u bench.py --no-scan --no-hnsw --no-c4 --no-cpu > $O/$v.log 2>&1 || exit 1
   python3 - $O/$v.log $v <<'PY'
