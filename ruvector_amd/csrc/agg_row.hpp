@@ -363,15 +363,15 @@ __device__ __forceinline__ void agg_img_row(const int64_t* __restrict__ rp, cons
 // rows from the chunk's counter until it passes n. Used by the chunk's own gather kernel and
 // by the previous chunk's GEMM blocks once their tiles are done. `win`: this wave's two
 // IMG_SLOT LDS windows for the image path.
-template <int NV, int AGG>
+template <int NV, int AGG, bool IMG>
 __device__ __forceinline__ void agg_help_rows(const AggHelp& h, int lane, unsigned char* win) {
-    const bool use_img = NV == 3 && AGG != AGG_MAX && h.img_slots != nullptr;
+    const bool use_img = IMG && NV == 3 && AGG != AGG_MAX && h.img_slots != nullptr;
     for (;;) {
         int64_t row = 0;
         if (lane == 0) row = (int64_t)atomicAdd(h.counter, 1u);
         row = __builtin_amdgcn_readfirstlane((int)row);
         if (row >= h.n) return;
-        if constexpr (NV == 3 && AGG != AGG_MAX) {
+        if constexpr (IMG && NV == 3 && AGG != AGG_MAX) {
             if (use_img) {
                 agg_img_row<AGG>(h.rp, h.col, h.x, h.dim, h.img_slots, h.img_nnz, h.out, h.self_x, h.row_scale,
                                  h.row_mul, h.self_mul, row, lane, win);
@@ -382,19 +382,21 @@ __device__ __forceinline__ void agg_help_rows(const AggHelp& h, int lane, unsign
                                             nullptr, 0, h.row_mul, h.self_mul, row, lane);
     }
 }
-template <int NV>
+template <int NV, bool IMG>
 __device__ __forceinline__ void agg_help_run_nv(const AggHelp& h, int lane, unsigned char* win) {
-    if (h.agg == AGG_MEAN) agg_help_rows<NV, AGG_MEAN>(h, lane, win);
-    else if (h.agg == AGG_SUM) agg_help_rows<NV, AGG_SUM>(h, lane, win);
-    else agg_help_rows<NV, AGG_MAX>(h, lane, win);
+    if (h.agg == AGG_MEAN) agg_help_rows<NV, AGG_MEAN, IMG>(h, lane, win);
+    else if (h.agg == AGG_SUM) agg_help_rows<NV, AGG_SUM, IMG>(h, lane, win);
+    else agg_help_rows<NV, AGG_MAX, IMG>(h, lane, win);
 }
-// lds: IMG_WIN bytes per wave of the block (wave w uses lds + w * IMG_WIN)
+// IMG: the image path is compiled in (h.img_slots may then be set); lds: IMG_WIN bytes per
+// wave of the block (wave w uses lds + w * IMG_WIN), unused without IMG
+template <bool IMG>
 __device__ __forceinline__ void agg_help_run(const AggHelp& h, unsigned char* lds) {
     const int lane = threadIdx.x & 63;
     unsigned char* win = lds + (threadIdx.x >> 6) * IMG_WIN;
-    if (h.dim > 512) agg_help_run_nv<3>(h, lane, win);
-    else if (h.dim > 256) agg_help_run_nv<2>(h, lane, win);
-    else agg_help_run_nv<1>(h, lane, win);
+    if (h.dim > 512) agg_help_run_nv<3, IMG>(h, lane, win);
+    else if (h.dim > 256) agg_help_run_nv<2, IMG>(h, lane, win);
+    else agg_help_run_nv<1, IMG>(h, lane, win);
 }
 
 }  // namespace aggrow

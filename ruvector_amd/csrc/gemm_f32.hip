@@ -1664,7 +1664,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt
             __syncthreads();  // LDS stages and s_t are reused by the next tile
         }
         // the loop ends after a barrier: the stage memory is free for the image windows
-        if constexpr (HELP) aggrow::agg_help_run(g.help, xsm);
+        if constexpr (HELP) aggrow::agg_help_run<true>(g.help, xsm);
         return;
     }
     const int64_t nwg = g.nblocks, bid = blockIdx.x;
@@ -1672,7 +1672,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt
     if constexpr (HELP) {
         extern __shared__ __attribute__((aligned(16))) unsigned char xsm_h[];
         __syncthreads();  // every wave is done with the tile's stages
-        aggrow::agg_help_run(g.help, xsm_h);
+        aggrow::agg_help_run<true>(g.help, xsm_h);
     }
 }
 

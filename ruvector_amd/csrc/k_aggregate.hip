@@ -271,9 +271,12 @@ void aggregate_rows(const int64_t* row_ptr, const int32_t* col, const float* w, 
 }
 
 namespace {
+// IMG: with the row-image path (and its LDS windows, ROWS_PER_BLOCK * IMG_WIN of dynamic LDS);
+// the dense form keeps its registers and no LDS (4 waves per SIMD for the layer's first chunk)
+template <bool IMG>
 __global__ __launch_bounds__(256) void k_aggregate_help(AggHelp h) {
-    __shared__ __attribute__((aligned(16))) unsigned char win[ROWS_PER_BLOCK * IMG_WIN];  // image windows
-    aggrow::agg_help_run(h, win);
+    extern __shared__ __attribute__((aligned(16))) unsigned char win[];
+    aggrow::agg_help_run<IMG>(h, win);
 }
 
 // One wave per row: header bits, packed positions (agg_row.hpp), the record assembled in the
@@ -344,7 +347,11 @@ void aggregate_rows_help(const AggHelp& h, const char* tag, int blocks_per_cu) {
     const int cap = blocks_per_cu > 0 ? blocks_per_cu : std::max(1, g_agg_overlap_cap);
     const int64_t blocks = std::min<int64_t>((h.n + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK,
                                              (int64_t)cap * active_cus());
-    RVX_LAUNCH(tag ? tag : "aggregate", k_aggregate_help, dim3((unsigned)blocks), dim3(256), 0, h);
+    if (h.img_slots)
+        RVX_LAUNCH(tag ? tag : "aggregate", k_aggregate_help<true>, dim3((unsigned)blocks), dim3(256),
+                   ROWS_PER_BLOCK * IMG_WIN, h);
+    else
+        RVX_LAUNCH(tag ? tag : "aggregate", k_aggregate_help<false>, dim3((unsigned)blocks), dim3(256), 0, h);
 }
 
 }  // namespace rvx
