@@ -472,6 +472,9 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef RVX_SCAN_PRIO  // experiment: static priority for the second-dispatched half of the waves
+    if (wave >= Cf::NW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
     const int lr = lane & 31, lh = lane >> 5, wm = wave & 1, wn = wave >> 1;
     const int lc = lane & 15, lg = lane >> 4;  // 16x16x32 lane roles: query / row-group
     const int lq = M16 ? lc : lr;              // the lane's query column inside an accumulator tile

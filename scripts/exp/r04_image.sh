@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4: row-image tests, then the bench with and without images (interleaved)
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_row_image.py \
   "tests/test_gpu_parity.py::test_graphsage_gemm_helps_gather_bits" > gpurun_out/r04_image_pytest.log 2>&1 &&

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4: bench with / without row images (per-layer gather tags)
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 for v in 1 0; do
   RVX_SAGE_IMAGE=$v timeout -k 10 300 python -u bench.py --no-scan --no-hnsw --no-c4 > gpurun_out/r04_image2_bench_$v.log 2>&1 || exit 1

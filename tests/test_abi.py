@@ -65,3 +65,15 @@ def test_library_built_from_shipped_sources():
     lib = _lib.load()
     assert _lib.built_hash(lib) == _lib.source_hash()
     assert len(_lib.source_hash()) == 16
+
+
+def test_row_image_sizes_without_gpu():
+    """rvx_row_image_bytes (host only): a 3 KiB slot and a u16 count per row, for
+    512 < dim <= 768 with dim % 4 == 0; anything else is refused with a status."""
+    import ruvector_amd as rv
+    assert rv.row_image_bytes(0, 768) == 16
+    assert rv.row_image_bytes(10, 768) == 10 * (3072 + 2) + 16
+    assert rv.row_image_bytes(7, 516) == 7 * (3072 + 2) + 16
+    for n, d in ((10, 512), (10, 772), (10, 770), (-1, 768)):
+        with pytest.raises(rv.RvxError):
+            rv.row_image_bytes(n, d)
