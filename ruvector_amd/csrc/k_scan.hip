@@ -765,7 +765,16 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
                 const float t = thr[ql];
                 if (!__ballot(vmin[fn] < t)) continue;  // none of the wave's queries has a value below its threshold
 #pragma unroll
-                for (int fm = 0; fm < AM; ++fm)
+                for (int fm = 0; fm < AM; ++fm) {
+#ifdef RVX_SCAN_FMSKIP  // experiment: one wave vote per accumulator tile before its per-value votes
+                    {
+                        bool anyf = false;
+#pragma unroll
+                        for (int e = 0; e < AE; ++e)
+                            anyf = anyf || (acc[fm][fn][e] < t && !(offered[fn] & ((OffT)1 << (fm * AE + e))));
+                        if (!__ballot(anyf)) continue;
+                    }
+#endif
 #pragma unroll
                     for (int e = 0; e < AE; ++e) {
                         const float v = acc[fm][fn][e];
@@ -783,6 +792,7 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
                             ovf[round & 1] = 1;
                         }
                     }
+                }
             }
             __syncthreads();
             // Insertion of this round's offers into the sorted lists (a query with no
