@@ -84,6 +84,10 @@ def parse():
     p.add_argument("--transport", choices=("rccl", "host"), default="rccl",
                    help="N>1 exchange: RCCL over xGMI, or host memory + stdlib sockets (ranks may share a GPU)")
     p.add_argument("--check-rows", type=int, default=8192, help="N>1: oracle-checked rows of the last rank")
+    p.add_argument("--force-comm", action="store_true",
+                   help="N=1: build the RCCL communicator anyway and run every exchange round through it "
+                        "(RVX_COMM_SELF_P2P=1: grouped send/recv to the rank itself), so the RCCL barriers, "
+                        "clock all-reduce and p2p rounds run on a one-GPU box")
     return p.parse_args()
 
 
@@ -112,6 +116,12 @@ def main():
     # max-over-ranks clock as RCCL all-reduces (no other collective library);
     # or the host-staged socket transport
     comm = comm_from_env(a.transport)
+    forced = False
+    if comm is None and a.force_comm:
+        from ruvector_amd.shard import RcclComm, rendezvous_unique_id
+        os.environ["RVX_COMM_SELF_P2P"] = "1"
+        comm = RcclComm(1, 0, rendezvous_unique_id(0, 1, RcclComm.unique_id))
+        forced = True
 
     # ---- inputs resident in HBM: the node table (same on every GPU), this
     # rank's CSR rows (global column ids), two full tables for layer outputs
@@ -253,6 +263,8 @@ def main():
     }
 
     if comm is not None:
+        line["comm"] = {"transport": a.transport, "forced": forced,
+                        "self_p2p_rounds": kern.get("halo_exchange", {}).get("launches", 0) if forced else 0}
         line["multi_gpu"] = exchange_report(a, kern, comm, world, rank, offsets, d, layers)
         line["multi_gpu"]["transport"] = ("rccl (p2p over xGMI)" if a.transport == "rccl" else
                                           "host-staged (host memory + stdlib TCP sockets)")

@@ -29,6 +29,15 @@ namespace rvx {
 int comm_rank(const rvx_comm* c) { return c ? c->rank : 0; }
 int comm_size(const rvx_comm* c) { return c ? c->nranks : 1; }
 
+// RVX_COMM_SELF_P2P=1 (read per call; tests and `bench.py --force-comm`): an RCCL
+// communicator of one rank still runs every collective of the exchange and search paths —
+// the grouped ncclSend/ncclRecv of comm_exchange_rows to its own rank, ncclBroadcast,
+// ncclAllGather — so the RCCL code runs on a one-GPU box with the results checked
+// bit-identical to the path that skips them.
+bool comm_self_p2p(const rvx_comm* c) {
+    return c && c->comm && c->nranks == 1 && env_int("RVX_COMM_SELF_P2P", 0) != 0;
+}
+
 namespace {
 // Host-staged round: wait for the rows on `s`, copy this rank's block to host,
 // let the host transport move every block, copy the peers' blocks back.
@@ -61,6 +70,20 @@ void host_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int6
 
 void comm_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int64_t* r0, const int64_t* rows,
                         hipStream_t s) {
+    if (comm_self_p2p(c)) {
+        // one rank: its block goes out and comes back through RCCL's p2p path (a grouped
+        // send/recv pair to itself), lands in a staging buffer and is copied over the rows
+        const int64_t cnt = rows[0] * row_elems;
+        if (cnt <= 0) return;
+        DevMem stage(cnt * 4);
+        RVX_NCCL(ncclGroupStart());
+        RVX_NCCL(ncclSend(table + r0[0] * row_elems, (size_t)cnt, ncclFloat32, 0, c->comm, s));
+        RVX_NCCL(ncclRecv(stage.p, (size_t)cnt, ncclFloat32, 0, c->comm, s));
+        RVX_NCCL(ncclGroupEnd());
+        RVX_HIP(hipMemcpyAsync(table + r0[0] * row_elems, stage.p, (size_t)cnt * 4, hipMemcpyDeviceToDevice, s));
+        RVX_HIP(hipStreamSynchronize(s));  // the staging buffer is freed on return
+        return;
+    }
     if (!c || c->nranks <= 1) return;
     if (c->host_fn) {
         host_exchange_rows(c, table, row_elems, r0, rows, s);
@@ -80,6 +103,10 @@ void comm_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int6
 }
 
 void comm_broadcast_bytes(rvx_comm* c, void* buf, int64_t bytes, int root, hipStream_t s) {
+    if (bytes > 0 && comm_self_p2p(c) && root == 0) {
+        RVX_NCCL(ncclBroadcast(buf, buf, (size_t)bytes, ncclUint8, 0, c->comm, s));
+        return;
+    }
     if (!c || c->nranks <= 1 || bytes <= 0) return;
     RVX_REQUIRE(root >= 0 && root < c->nranks, RVX_ERR_INVALID_PARAMETER, "bad broadcast root");
     if (!c->host_fn) {
@@ -106,6 +133,10 @@ void comm_broadcast_bytes(rvx_comm* c, void* buf, int64_t bytes, int root, hipSt
 void comm_allgather_bytes(rvx_comm* c, const void* send, void* recv, int64_t bytes, hipStream_t s) {
     const int w = comm_size(c), me = comm_rank(c);
     if (bytes <= 0) return;
+    if (comm_self_p2p(c)) {
+        RVX_NCCL(ncclAllGather(send, recv, (size_t)bytes, ncclUint8, c->comm, s));
+        return;
+    }
     if (w <= 1) {
         if (recv != send) RVX_HIP(hipMemcpyAsync(recv, send, (size_t)bytes, hipMemcpyDeviceToDevice, s));
         return;

@@ -106,7 +106,7 @@ std::vector<ExchangeRound> exchange_plan(int kind, const int64_t* offsets, int w
 void produce_and_exchange(rvx_comm* comm, const int64_t* offsets, const std::vector<TableRef>& tables,
                           const std::function<void(int64_t r0, int64_t rows)>& produce) {
     const int world = comm_size(comm), me = comm_rank(comm);
-    if (world <= 1) {
+    if (world <= 1 && !comm_self_p2p(comm)) {
         produce(offsets[me], offsets[me + 1] - offsets[me]);
         return;
     }
@@ -782,7 +782,7 @@ rvx_status rvx_sage_forward_exchange3(const rvx_sage_layer* l, const rvx_graph* 
         float* yinv_rows = yinv ? yinv + offsets[me] : nullptr;
         // (x_image describes x as the caller passed it: a rescale in place above would stale it)
         const RowImage xi = xm || !x_rowmul ? ximg : RowImage();
-        if (!exchange || world == 1) {
+        if (!exchange || (world == 1 && !comm_self_p2p(comm))) {
             sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], 0, nullptr, xm, yinv_rows, xi,
                              image_rows(yimg, offsets[me]));
             return;

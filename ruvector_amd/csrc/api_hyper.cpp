@@ -109,8 +109,9 @@ void search_dev(const rvx_hyperbolic* h, const float* dq, int64_t nq, int k, int
         // point, keep k * prune_factor, exact Poincaré re-rank
         RVX_REQUIRE(ix->cfg.metric == RVX_METRIC_POINCARE, RVX_ERR_UNSUPPORTED,
                     "search_with_pruning is implemented for the Poincaré metric");
-        const int nc = (int)std::min<int64_t>((int64_t)k * h->cfg.prune_factor, ix->n);
-        RVX_REQUIRE(nc <= SCAN_MAX_K, RVX_ERR_UNSUPPORTED, "k * prune_factor must be <= 128");
+        const int64_t nc64 = std::min<int64_t>((int64_t)k * h->cfg.prune_factor, ix->n);
+        RVX_REQUIRE(nc64 < ((int64_t)1 << 31), RVX_ERR_INVALID_PARAMETER, "k * prune_factor too large");
+        const int nc = (int)nc64;
         float* qt = scratch_f32("hyp_qt", nq * d);
         std::vector<float> cen((size_t)d);
         ix->tan_centroid.download(cen.data(), (int64_t)d * 4);
@@ -325,9 +326,10 @@ rvx_status rvx_hyperbolic_search_device(const rvx_hyperbolic* h, const rvx_buffe
     });
 }
 
-// The shard-dependent conditions search_dev enforces (pruned: Poincaré metric and
-// k * prune_factor <= 128 on this shard's size; graph: a fresh graph and ef in range;
-// exact: k <= 128), checked locally before the sharded entry points enter any collective.
+// The shard-dependent conditions search_dev enforces (pruned: the Poincaré metric;
+// graph: a fresh graph), checked locally before the sharded entry points enter any
+// collective. k, ef and k * prune_factor are unbounded as in the reference
+// (hnsw.rs:427-489).
 static void hyp_shard_precheck(const rvx_hyperbolic* h, int64_t nq, int k, int ef, int mode) {
     RVX_REQUIRE(h && nq >= 0 && k >= 1 && mode >= 0 && mode <= 2, RVX_ERR_INVALID_PARAMETER,
                 "bad sharded search arguments");
@@ -337,14 +339,10 @@ static void hyp_shard_precheck(const rvx_hyperbolic* h, int64_t nq, int k, int e
     if (m == 2) {
         RVX_REQUIRE(ix->cfg.metric == RVX_METRIC_POINCARE, RVX_ERR_UNSUPPORTED,
                     "search_with_pruning is implemented for the Poincaré metric");
-        RVX_REQUIRE(std::min<int64_t>((int64_t)k * h->cfg.prune_factor, ix->n) <= SCAN_MAX_K, RVX_ERR_UNSUPPORTED,
-                    "k * prune_factor must be <= 128");
-    } else if (m == 1) {
-        RVX_REQUIRE(k <= SCAN_MAX_K, RVX_ERR_INVALID_PARAMETER, "k must be in [1, 128]");
-    } else {
+        RVX_REQUIRE((int64_t)k * h->cfg.prune_factor < ((int64_t)1 << 31), RVX_ERR_INVALID_PARAMETER,
+                    "k * prune_factor too large");
+    } else if (m == 0) {
         RVX_REQUIRE(ix->has_graph && ix->graph_n == ix->n, RVX_ERR_INDEX, "HNSW graph missing or stale");
-        const int e = std::max(ef > 0 ? ef : ix->cfg.ef_search, k);
-        RVX_REQUIRE(e >= 1 && e <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER, "ef out of range");
     }
 }
 

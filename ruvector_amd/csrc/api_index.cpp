@@ -122,14 +122,8 @@ void check_query_args(const rvx_index* ix, int64_t nq, int k) {
 void index_shard_precheck(const rvx_index* ix, int64_t nq, int k, int ef, bool exact) {
     check_query_args(ix, nq, k);
     if (ix->n == 0 || nq == 0) return;
-    if (exact || ix->cfg.kind == RVX_INDEX_FLAT) {
-        RVX_REQUIRE(k <= SCAN_MAX_K, RVX_ERR_INVALID_PARAMETER, "k must be in [1, " + std::to_string(SCAN_MAX_K) + "]");
-        return;
-    }
+    if (exact || ix->cfg.kind == RVX_INDEX_FLAT) return;  // any k (flat.rs:63-64)
     RVX_REQUIRE(ix->has_graph && ix->graph_n == ix->n, RVX_ERR_INDEX, "HNSW graph missing or stale");
-    const int e = std::max(ef > 0 ? ef : ix->cfg.ef_search, k);
-    RVX_REQUIRE(e >= 1 && e <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER,
-                "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
 }
 
 }  // namespace

@@ -10,15 +10,22 @@ using namespace rvx;
 
 namespace {
 
-// One hit as it travels between ranks (24 B): the reported distance and the merge key
-// (the distance with NaN — e.g. cosine against a zero row — and empty slots at +inf, so
-// every rank's list is totally ordered and each output slot is written exactly once).
+// One hit as it travels between ranks (24 B): the reported distance and the merge key.
+// The key orders real hits by distance (NaN as +inf) and every empty slot (gid -1) after
+// every real hit, +inf and NaN hits included: the high word is 1 for an empty slot, the
+// low word the order-preserving image of the distance. Every rank's list is ascending in
+// that key, so each output slot is written exactly once and the first `count` slots are
+// real hits.
 struct Hit {
     int64_t gid;
     int64_t lid;
     float d;
-    float key;
+    uint32_t key_lo;  // order-preserving bits of the distance (NaN -> +inf)
 };
+
+__device__ __forceinline__ uint64_t hit_key(const Hit& h) {
+    return ((uint64_t)(h.gid == -1 ? 1u : 0u) << 32) | h.key_lo;
+}
 
 __global__ void k_pack_hits(const int64_t* gid, const int64_t* lid, const float* d, int64_t total, Hit* out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -27,16 +34,18 @@ __global__ void k_pack_hits(const int64_t* gid, const int64_t* lid, const float*
     h.gid = gid[i];
     h.lid = lid ? lid[i] : 0;
     h.d = h.gid == -1 ? INFINITY : d[i];
-    h.key = isnan(h.d) ? INFINITY : h.d;
+    const float kv = isnan(h.d) ? INFINITY : h.d;
+    const uint32_t b = __float_as_uint(kv);
+    h.key_lo = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
     out[i] = h;
 }
 
-// count of entries of the ascending list l[0..k) with d' < v (strict) or d' <= v
-__device__ __forceinline__ int count_before(const Hit* l, int k, float v, bool inclusive) {
+// count of entries of the ascending list l[0..k) with key' < v (strict) or key' <= v
+__device__ __forceinline__ int count_before(const Hit* l, int k, uint64_t v, bool inclusive) {
     int lo = 0, hi = k;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        const float x = l[mid].key;
+        const uint64_t x = hit_key(l[mid]);
         if (inclusive ? (x <= v) : (x < v)) lo = mid + 1;
         else hi = mid;
     }
@@ -60,7 +69,7 @@ __global__ void k_merge_hits(const Hit* all, int w, int64_t nq, int k, int64_t* 
     int pos = j;
     for (int p = 0; p < w && pos < k; ++p) {
         if (p == r) continue;
-        pos += count_before(all + (int64_t)p * per_rank + q * k, k, h.key, p < r);
+        pos += count_before(all + (int64_t)p * per_rank + q * k, k, hit_key(h), p < r);
     }
     if (pos < k) {
         out_gid[q * k + pos] = h.gid;
@@ -83,13 +92,14 @@ namespace rvx {
 
 void shard_agree(rvx_comm* c, rvx_status status, const std::string& why, const int64_t (&args)[5]) {
     const int w = comm_size(c), me = comm_rank(c);
-    if (w <= 1) {
+    if (w <= 1 && !comm_self_p2p(c)) {
         if (status != RVX_OK) fail(status, why);
         return;
     }
     // fixed-size all-gather: {status, args...} per rank, so ranks that disagree on the
     // arguments (or failed before any collective) still exchange the same byte count
     constexpr int F = 8;
+    ComputeLock cl;  // the scratch slot is only valid under the device's compute lock
     int64_t mine[F] = {(int64_t)status, args[0], args[1], args[2], args[3], args[4], 0, 0};
     auto* dev = (int64_t*)scratch_bytes("shard_agree", (int64_t)(w + 1) * F * 8);
     RVX_HIP(hipMemcpyAsync(dev, mine, sizeof mine, hipMemcpyHostToDevice, stream()));

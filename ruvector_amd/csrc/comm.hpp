@@ -12,6 +12,9 @@ namespace rvx {
 
 int comm_rank(const rvx_comm* c);
 int comm_size(const rvx_comm* c);
+// An RCCL communicator of one rank with RVX_COMM_SELF_P2P=1: the exchange and search
+// drivers still run their collectives (to the rank itself) instead of skipping them.
+bool comm_self_p2p(const rvx_comm* c);
 
 // One grouped point-to-point round on stream `s`: this rank sends its rows
 // [r0[me], r0[me]+rows[me]) of `table` to every peer and receives each peer

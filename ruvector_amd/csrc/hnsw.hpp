@@ -4,7 +4,10 @@
 
 namespace rvx {
 
-constexpr int HNSW_MAX_EF = 8192;  // bounded in practice by one wave's LDS (hnsw_search_lds)
+// ef is unbounded in the reference (ef = max(ef_arg, k), hnsw.rs:1519); here R lives in
+// one wave's LDS up to ~19k entries (d 768) and in HBM beyond, so the only limit is the
+// int32 index range of the R row.
+constexpr int HNSW_MAX_EF = (1 << 30);
 constexpr int HNSW_MAX_LEVEL = 16;  // NB_LAYER_MAX (patches/hnsw_rs/src/hnsw.rs:41)
 
 // Layer 0 is a CSR over all n points; layer l>=1 is a CSR over the sorted ids

@@ -52,11 +52,16 @@ struct SearchArgs {
     float curv;        // Poincaré curvature
     int hyper;         // HyperbolicHnsw::search semantics (see below)
     int coop;          // wave-cooperative LDS-staged distances (hnsw_dev.hpp wave_dist)
+    float* rg_d;       // RG kernels: R in HBM, [nslots][ef + 1] distances ...
+    int* rg_i;         // ... and flagged ids (ef past one wave's LDS)
 };
 
 // RB: float4s per streamed row batch of the per-lane distances (hnsw_dev.hpp
-// stream_acc); NST: LDS stages of the wave-cooperative distances.
-template <int METRIC, int RB, int NST = 2>
+// stream_acc); NST: LDS stages of the wave-cooperative distances. RG: the result list R
+// lives in a per-slot HBM scratch row instead of LDS (ef beyond what one wave's 160 KB
+// hold: 19,007 entries at d 768): the same code over global memory, with a workgroup
+// fence after each write phase so the other lanes' reads see it.
+template <int METRIC, int RB, int NST = 2, bool RG = false>
 __device__ __forceinline__ void search_body(const SearchArgs& a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int lane = threadIdx.x;
@@ -66,9 +71,18 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     unsigned char* wst = lds_raw;                                // [NST * WD_STAGE] distance stages (coop)
     float* qs = reinterpret_cast<float*>(lds_raw + (coop ? wd_lds(NST) : 0));  // [d rounded to 4]
     const int dq = (a.d + 3) & ~3;
-    float* rd = qs + dq;                                        // R dist [ef+1]
-    int* ri = reinterpret_cast<int*>(rd + ef + 1);              // R id | expanded flag (bit 31)
-    float* sdb = reinterpret_cast<float*>(ri + ef + 1);         // admitted batch [64]
+    float* rd;                                                  // R dist [ef+1]
+    int* ri;                                                    // R id | expanded flag (bit 31)
+    float* sdb;                                                 // admitted batch [64]
+    if constexpr (RG) {
+        rd = a.rg_d + (int64_t)blockIdx.x * (ef + 1);
+        ri = a.rg_i + (int64_t)blockIdx.x * (ef + 1);
+        sdb = qs + dq;
+    } else {
+        rd = qs + dq;
+        ri = reinterpret_cast<int*>(rd + ef + 1);
+        sdb = reinterpret_cast<float*>(ri + ef + 1);
+    }
     int* sib = reinterpret_cast<int*>(sdb + 64);
 
     unsigned long long* vis = a.vbits ? nullptr : a.visited + (int64_t)blockIdx.x * a.vcap;
@@ -177,6 +191,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             const int c_id = ri[at];
             __builtin_amdgcn_wave_barrier();
             if (lane == 0) ri[at] = c_id | INT_MIN;
+            if constexpr (RG) __threadfence_block();
             __builtin_amdgcn_wave_barrier();
             scan = at + 1;
             const int64_t b = a.g.rp0[c_id], e = a.g.rp0[c_id + 1];
@@ -199,6 +214,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
                 const int na = sort_batch(adm, dd, nid, sdb, sib, lane);
                 if (na == 0) continue;
                 scan = min(scan, merge_into_r(rd, ri, rs, sdb, sib, na, r, lane));
+                if constexpr (RG) __threadfence_block();
                 rs = r;
             }
         }
@@ -238,6 +254,11 @@ template <int METRIC>
 __global__ __launch_bounds__(64) void k_hnsw_search_wide(SearchArgs a) {
     search_body<METRIC, ROW_BATCH, 1>(a);
 }
+// ef past one wave's LDS: R in HBM (one distance stage when coop).
+template <int METRIC>
+__global__ __launch_bounds__(64) void k_hnsw_search_rg(SearchArgs a) {
+    search_body<METRIC, ROW_BATCH, 1, true>(a);
+}
 
 }  // namespace
 
@@ -257,6 +278,11 @@ size_t hnsw_search_lds(int d, int ef, bool coop) {
     const int dq = (d + 3) & ~3;
     return (coop ? (size_t)wd_lds(hnsw_wide_ef(coop, ef) ? 1 : 2) : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 8;
 }
+// LDS of the RG kernel: distance stage + query + admitted batch (R is in HBM)
+size_t hnsw_search_lds_rg(int d, bool coop) {
+    const int dq = (d + 3) & ~3;
+    return (coop ? (size_t)wd_lds(1) : 0) + (size_t)dq * 4 + 64 * 8;
+}
 
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
                  const float* qnorm, int64_t nq, int k, int ef, float* out_d, int64_t* out_i, int32_t* out_n,
@@ -264,6 +290,9 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     if (nq <= 0) return;
     RVX_REQUIRE(ef >= 1 && ef <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER,
                 "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
+    // R in LDS when one wave's 160 KB hold it, else in HBM (RVX_HNSW_RG=1 forces, tests)
+    const bool coop0 = hnsw_coop(metric, d, g.n);
+    const bool rg = hnsw_search_lds(d, ef, coop0) > 160 * 1024 || env_int("RVX_HNSW_RG", 0) != 0;
     const unsigned vcap = visited_capacity(ef, g.max_deg);
     // visited set: a per-slot bitmap over all n nodes (cleared per query by its
     // wave: no launch-wide memset, no probing, n/8 bytes touched) when at least
@@ -287,8 +316,10 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     const int64_t fit_slots = budget / (vwords * 4);
     const bool bitmap = bm_mode == 2 || (bm_mode == 1 && fit_slots >= std::min<int64_t>(bm_slots, 1024));
     const int64_t mem_slots = std::max<int64_t>(256, ((int64_t)8 << 30) / ((int64_t)vcap * 8));
-    const int nslots = (int)(bitmap ? (bm_mode == 2 ? bm_slots : std::min(bm_slots, fit_slots))
-                                    : std::min<int64_t>(bm_slots, mem_slots));
+    int nslots = (int)(bitmap ? (bm_mode == 2 ? bm_slots : std::min(bm_slots, fit_slots))
+                              : std::min<int64_t>(bm_slots, mem_slots));
+    // RG: each slot also holds an HBM row of ef + 1 R entries (8 B each), within 4 GiB
+    if (rg) nslots = (int)std::max<int64_t>(1, std::min<int64_t>(nslots, ((int64_t)4 << 30) / ((int64_t)(ef + 1) * 8)));
     unsigned long long* vis = nullptr;
     unsigned* vbits = nullptr;
     if (bitmap) {
@@ -300,11 +331,17 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     int* status = (int*)scratch_bytes("hnsw_status", 256);
     auto* stats = reinterpret_cast<unsigned long long*>(status + 16);
     RVX_HIP(hipMemsetAsync(status, 0, 256, stream()));
-    const bool coop = hnsw_coop(metric, d, g.n);
+    const bool coop = coop0;
+    float* rg_d = nullptr;
+    int* rg_i = nullptr;
+    if (rg) {
+        rg_d = scratch_f32("hnsw_rg_d", (int64_t)nslots * (ef + 1));
+        rg_i = (int*)scratch_bytes("hnsw_rg_i", (int64_t)nslots * (ef + 1) * 4);
+    }
     SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, vbits, vwords, nslots, vcap, out_d, out_i, out_n, status, stats,
-                 curv, hyper, coop ? 1 : 0};
-    const size_t lds = hnsw_search_lds(d, ef, coop);
-    RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");
+                 curv, hyper, coop ? 1 : 0, rg_d, rg_i};
+    const size_t lds = rg ? hnsw_search_lds_rg(d, coop) : hnsw_search_lds(d, ef, coop);
+    RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension too large for one wave's LDS");
     static bool attr = false;
     if (!attr) {
         RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -321,11 +358,27 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_wide<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_wide<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_wide<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_rg<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_rg<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_rg<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_rg<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_rg<RVX_METRIC_POINCARE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_rg<RVX_METRIC_HYP_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
     const char* t = tag ? tag : "hnsw_search";
     const bool short_rows = !coop && d <= 256 && env_int("RVX_HNSW_SHORT", 1);  // read per call: tests cover both
-    if (short_rows && metric != RVX_METRIC_POINCARE && metric != RVX_METRIC_HYP_L2) {
+    if (rg) {
+        switch (metric) {
+            case RVX_METRIC_L2: RVX_LAUNCH(t, k_hnsw_search_rg<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_hnsw_search_rg<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_DOT: RVX_LAUNCH(t, k_hnsw_search_rg<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_L1: RVX_LAUNCH(t, k_hnsw_search_rg<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_POINCARE: RVX_LAUNCH(t, k_hnsw_search_rg<RVX_METRIC_POINCARE>, dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_HYP_L2: RVX_LAUNCH(t, k_hnsw_search_rg<RVX_METRIC_HYP_L2>, dim3(nslots), dim3(64), lds, a); break;
+            default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by HNSW search");
+        }
+    } else if (short_rows && metric != RVX_METRIC_POINCARE && metric != RVX_METRIC_HYP_L2) {
         switch (metric) {
             case RVX_METRIC_L2: RVX_LAUNCH(t, k_hnsw_search_short<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
             case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_hnsw_search_short<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;

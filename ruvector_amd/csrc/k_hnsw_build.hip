@@ -49,6 +49,7 @@ struct BuildArgs {
     float curv;  // Poincaré curvature
     int hyper;   // HyperbolicHnsw::insert rules
     int coop;    // wave-cooperative LDS-staged distances in the layer searches
+    float* rg_d; int* rg_i;  // RG: R in HBM, [nslots][ef_c + 1] (ef_c past one wave's LDS)
 };
 
 __device__ __forceinline__ int list_get(const BuildGraph& G, int p, int l, const int** ids, const float** ds) {
@@ -73,7 +74,7 @@ __device__ __forceinline__ int list_key(const BuildGraph& G, int p, int l) {  //
 // R-only form (hnsw_dev.hpp merge_into_r, as the query kernel k_hnsw.hip): the
 // nearest candidate is the nearest unexpanded entry of R (id bit 31 = expanded);
 // the flags are cleared before returning.
-template <int METRIC>
+template <int METRIC, bool RG = false>
 __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn, int ep, float d_ep, int ef, int l,
                                   unsigned long long* vis, unsigned vmask, unsigned long long tag, float* rd, int* ri,
                                   float* sdb, int* sib, unsigned char* wst, int lane) {
@@ -96,6 +97,7 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
         const int c_id = ri[at];
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) ri[at] = c_id | INT_MIN;
+        if constexpr (RG) __threadfence_block();
         __builtin_amdgcn_wave_barrier();
         scan = at + 1;
         const int* nbi;
@@ -131,10 +133,12 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
             const int na = sort_batch(adm, dd, nid, sdb, sib, lane);
             if (na == 0) continue;
             scan = min(scan, merge_into_r(rd, ri, rs, sdb, sib, na, r, lane));
+            if constexpr (RG) __threadfence_block();
             rs = r;
         }
     }
     for (int i = lane; i < rs; i += 64) ri[i] &= ID_MASK;
+    if constexpr (RG) __threadfence_block();
     __builtin_amdgcn_wave_barrier();
     return rs;
 }
@@ -142,7 +146,7 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
 #ifndef RVX_BUILD_WPE
 #define RVX_BUILD_WPE
 #endif
-template <int METRIC>
+template <int METRIC, bool RG = false>
 __global__ __launch_bounds__(64) RVX_BUILD_WPE void k_build_insert(BuildArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int lane = threadIdx.x;
@@ -150,9 +154,18 @@ __global__ __launch_bounds__(64) RVX_BUILD_WPE void k_build_insert(BuildArgs a) 
     const int dq = (a.d + 3) & ~3;
     unsigned char* wst = lds_raw;  // [WD_LDS] distance stages (coop)
     float* qs = reinterpret_cast<float*>(lds_raw + (a.coop ? WD_LDS : 0));
-    float* rd = qs + dq;
-    int* ri = reinterpret_cast<int*>(rd + ef + 1);
-    float* sd = reinterpret_cast<float*>(ri + ef + 1);  // selected [MAX_C0] (search: admitted batch [64])
+    float* rd;
+    int* ri;
+    float* sd;  // selected [MAX_C0] (search: admitted batch [64])
+    if constexpr (RG) {
+        rd = a.rg_d + (int64_t)blockIdx.x * (ef + 1);
+        ri = a.rg_i + (int64_t)blockIdx.x * (ef + 1);
+        sd = qs + dq;
+    } else {
+        rd = qs + dq;
+        ri = reinterpret_cast<int*>(rd + ef + 1);
+        sd = reinterpret_cast<float*>(ri + ef + 1);
+    }
     int* si = reinterpret_cast<int*>(sd + MAX_C0);
     unsigned long long* vis = a.visited + (int64_t)blockIdx.x * a.vcap;
     const unsigned vmask = a.vcap - 1;
@@ -174,7 +187,7 @@ __global__ __launch_bounds__(64) RVX_BUILD_WPE void k_build_insert(BuildArgs a) 
         // 1. greedy descent, ef = 1 (hnsw.rs:1105-1146)
         for (int l = a.entry_level; l >= lev + 1; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
-            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, 1, l, vis, vmask, tag, rd, ri, sd, si, wst,
+            const int rs = build_search_layer<METRIC, RG>(a, qs, qn, ep, d_ep, 1, l, vis, vmask, tag, rd, ri, sd, si, wst,
                                                       lane);
             if (rs > 0 && rd[0] < d_ep) { ep = ri[0]; d_ep = rd[0]; }
         }
@@ -183,7 +196,7 @@ __global__ __launch_bounds__(64) RVX_BUILD_WPE void k_build_insert(BuildArgs a) 
         const int ltop = a.hyper ? min(lev, a.entry_level) : lev;
         for (int l = ltop; l >= 0; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
-            const int rs = build_search_layer<METRIC>(a, qs, qn, ep, d_ep, ef, l, vis, vmask, tag, rd, ri, sd, si, wst,
+            const int rs = build_search_layer<METRIC, RG>(a, qs, qn, ep, d_ep, ef, l, vis, vmask, tag, rd, ri, sd, si, wst,
                                                       lane);
             if (rs == 0) continue;
             const int nb_conn = l == 0 ? a.G.C0 : a.G.M;
@@ -348,9 +361,9 @@ __global__ __launch_bounds__(256) void k_build_merge(BuildArgs a, int nrec) {
 
 }  // namespace
 
-size_t build_lds_bytes(int d, int ef, bool coop) {
+size_t build_lds_bytes(int d, int ef, bool coop, bool rg = false) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)WD_LDS : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + (size_t)MAX_C0 * 8;
+    return (coop ? (size_t)WD_LDS : 0) + (size_t)dq * 4 + (rg ? 0 : (size_t)(ef + 1) * 8) + (size_t)MAX_C0 * 8;
 }
 
 void build_insert_batch(const BuildGraph& G, int metric, const float* x, const float* xnorm, int d,
@@ -361,15 +374,23 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
                 "GPU HNSW build supports layer-0 lists of <= 256 and upper lists of <= 128 neighbours");
     RVX_REQUIRE(ef_c >= 1 && ef_c <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER, "ef_construction out of range");
     const unsigned vcap = visited_capacity(ef_c, G.C0);
-    const int nslots = (int)std::min<int64_t>(std::min(batch_n, 8192),
-                                              std::max<int64_t>(1024, ((int64_t)4 << 30) / ((int64_t)vcap * 8)));
+    const bool coop = hnsw_coop(metric, d, batch_begin + batch_n);
+    // R in LDS when one wave's 160 KB hold it, else in HBM (RVX_HNSW_RG=1 forces, tests)
+    const bool rg = build_lds_bytes(d, ef_c, coop) > 160 * 1024 || env_int("RVX_HNSW_RG", 0) != 0;
+    int nslots = (int)std::min<int64_t>(std::min(batch_n, 8192),
+                                        std::max<int64_t>(1024, ((int64_t)4 << 30) / ((int64_t)vcap * 8)));
+    if (rg) nslots = (int)std::max<int64_t>(1, std::min<int64_t>(nslots, ((int64_t)4 << 30) / ((int64_t)(ef_c + 1) * 8)));
     const int rev_cap = G.C0 + G.M * G.max_layer;
     BuildArgs a{};
     a.G = G; a.x = x; a.xnorm = xnorm; a.d = d;
     a.batch_begin = batch_begin; a.batch_n = batch_n; a.entry = entry; a.entry_level = entry_level;
     a.nonempty_mask = nonempty_mask; a.ef_c = ef_c;
     a.curv = curv; a.hyper = hyper;
-    a.coop = hnsw_coop(metric, d, batch_begin + batch_n) ? 1 : 0;
+    a.coop = coop ? 1 : 0;
+    if (rg) {
+        a.rg_d = scratch_f32("build_rg_d", (int64_t)nslots * (ef_c + 1));
+        a.rg_i = (int*)scratch_bytes("build_rg_i", (int64_t)nslots * (ef_c + 1) * 4);
+    }
     a.vcap = vcap;
     a.visited = (unsigned long long*)scratch_bytes("build_visited", (int64_t)nslots * vcap * 8);
     const int64_t nrec = (int64_t)batch_n * rev_cap;
@@ -381,10 +402,15 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     a.rev_cap = rev_cap;
     a.nslots = nslots;
     RVX_HIP(hipMemsetAsync(a.visited, 0, (size_t)nslots * vcap * 8, stream()));
-    const size_t lds = build_lds_bytes(d, ef_c, a.coop != 0);
-    RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension/ef too large for one wave's LDS");
+    const size_t lds = build_lds_bytes(d, ef_c, a.coop != 0, rg);
+    RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension too large for one wave's LDS");
     static bool attr = false;
     if (!attr) {
+        RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_COSINE, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_POINCARE, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_HYP_L2, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -392,6 +418,16 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
         RVX_HIP(hipFuncSetAttribute((const void*)k_build_insert<RVX_METRIC_HYP_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
+    if (rg) {
+        switch (metric) {
+            case RVX_METRIC_L2: RVX_LAUNCH("hnsw_build_insert", (k_build_insert<RVX_METRIC_L2, true>), dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_COSINE: RVX_LAUNCH("hnsw_build_insert", (k_build_insert<RVX_METRIC_COSINE, true>), dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_L1: RVX_LAUNCH("hnsw_build_insert", (k_build_insert<RVX_METRIC_L1, true>), dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_POINCARE: RVX_LAUNCH("hnsw_build_insert", (k_build_insert<RVX_METRIC_POINCARE, true>), dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_HYP_L2: RVX_LAUNCH("hnsw_build_insert", (k_build_insert<RVX_METRIC_HYP_L2, true>), dim3(nslots), dim3(64), lds, a); break;
+            default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by the GPU HNSW build");
+        }
+    } else
     switch (metric) {
         case RVX_METRIC_L2: RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
         case RVX_METRIC_COSINE: RVX_LAUNCH("hnsw_build_insert", k_build_insert<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;

@@ -163,6 +163,18 @@ __global__ __launch_bounds__(64) void k_rerank(const float* q, int64_t nq, const
     if (lane == 0 && out_n) out_n[qi] = take;
 }
 
+// k * prune_factor > SCAN_MAX_K: every candidate's exact distance (NaN for an empty
+// candidate slot), then select_topk by (distance, position) — the stable sort of
+// hnsw.rs:481 over the ascending tangent order.
+__global__ void k_rerank_dist(const float* q, int64_t nq, const float* x, int d, float c, const int64_t* cand, int nc,
+                              float* out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nq * nc) return;
+    const int64_t qi = t / nc;
+    const int64_t id = cand[t];
+    out[t] = (id >= 0 && id != INT64_MAX) ? pdev::hyp_dist(q + qi * d, x + id * d, d, c) : __builtin_nanf("");
+}
+
 }  // namespace
 
 void project_rows(float* x, int64_t n, int d, float c) {
@@ -200,7 +212,14 @@ void col_chain(const float* rows, int64_t n, int d, float w, float* acc) {
 void rerank(const float* q, int64_t nq, const float* x, int d, float c, const int64_t* cand, int nc, int k,
             float* out_d, int64_t* out_i, int32_t* out_n) {
     if (nq <= 0) return;
-    RVX_REQUIRE(nc >= 1 && nc <= SCAN_MAX_K, RVX_ERR_INVALID_PARAMETER, "candidate count out of range");
+    RVX_REQUIRE(nc >= 1, RVX_ERR_INVALID_PARAMETER, "candidate count out of range");
+    if (nc > SCAN_MAX_K) {
+        float* dist = scratch_f32("hyp_rerank_d", nq * (int64_t)nc);
+        RVX_LAUNCH("hyp_rerank", k_rerank_dist, dim3((unsigned)((nq * nc + 255) / 256)), dim3(256), 0, q, nq, x, d, c,
+                   cand, nc, dist);
+        select_topk(dist, nq, nc, nc, k, cand, 0, out_d, out_i, out_n);
+        return;
+    }
     RVX_LAUNCH("hyp_rerank", k_rerank, dim3((unsigned)nq), dim3(64), 0, q, nq, x, d, c, cand, nc, k, out_d, out_i,
                out_n);
 }

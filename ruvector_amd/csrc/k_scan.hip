@@ -64,9 +64,13 @@ struct ScanArgs {
     int64_t id_offset;               // added to row index
     const uint8_t* deleted;          // optional tombstones [n]
     float curv;                      // Poincaré curvature
+    float* full;                     // FULL: distances [nq][full_ld] (deleted rows NaN)
+    int64_t full_ld;
 };
 
-template <int METRIC>
+// FULL = false: the fused top-k (k <= SCAN_MAX_K). FULL = true: the same tiles write every
+// (query, row) distance to a.full for the any-k selection (k_select.hip).
+template <int METRIC, bool FULL = false>
 __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     float* qs = reinterpret_cast<float*>(lds_raw);                // [TQ][ROWF]
@@ -181,6 +185,23 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
             __syncthreads();
         }
 
+        if constexpr (FULL) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t qi = q0 + tq + 8 * i;
+                if (qi >= a.nq) continue;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t ri = rt + tr + 32 * j;
+                    if (ri >= r_end) continue;
+                    const float xn = (METRIC == RVX_METRIC_COSINE || METRIC == RVX_METRIC_POINCARE) ? a.xnorm[ri] : 0.0f;
+                    const float dist = (a.deleted && a.deleted[ri]) ? __builtin_nanf("")
+                                                                    : pair_finish<METRIC>(acc[i][j], qn[i], xn, a.curv);
+                    a.full[qi * a.full_ld + ri] = dist;
+                }
+            }
+            continue;  // uniform: FULL is a template parameter
+        }
         // candidates that beat the running k-th distance of their query
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -224,6 +245,7 @@ __global__ __launch_bounds__(256) void k_scan_topk(ScanArgs a) {
         __syncthreads();
     }
 
+    if constexpr (FULL) return;
     for (int i = tid; i < TQ * K; i += 256) {
         const int ql = i / K, s = i % K;
         const int64_t qi = q0 + ql;
@@ -1462,6 +1484,9 @@ __global__ void k_scatter_topk(const float* sd, const int64_t* si, const int32_t
 void scan_topk_valu(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
                     const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
                     const char* tag, float curv);
+void scan_topk_wide(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
+                    const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
+                    float curv);
 
 // Returns false (nothing written) when the call should take the VALU scan.
 bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
@@ -1697,8 +1722,7 @@ ScanStats& last_scan_stats() {
 void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
                const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
                const char* tag, float curv) {
-    RVX_REQUIRE(k >= 1 && k <= SCAN_MAX_K, RVX_ERR_INVALID_PARAMETER,
-                "k must be in [1, " + std::to_string(SCAN_MAX_K) + "]");
+    RVX_REQUIRE(k >= 1, RVX_ERR_INVALID_PARAMETER, "k must be >= 1");
     RVX_REQUIRE(d % 4 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)x & 15) == 0, RVX_ERR_UNSUPPORTED,
                 "scan needs dim % 4 == 0 and 16-B aligned rows");
     if (nq <= 0) return;
@@ -1708,7 +1732,9 @@ void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const
         RVX_HIP(hipMemsetAsync(out_i, 0xFF, (size_t)(nq * k * 8), stream()));
         return;
     }
-    if (scan_topk_mfma(metric, q, qnorm, nq, x, xnorm, deleted, n, d, k, id_offset, out_d, out_i, curv)) return;
+    if (k <= SCAN_MAX_K &&
+        scan_topk_mfma(metric, q, qnorm, nq, x, xnorm, deleted, n, d, k, id_offset, out_d, out_i, curv))
+        return;
     if (metric == RVX_METRIC_POINCARE && (!qnorm || !xnorm)) {  // squared norms for the VALU scan (K8)
         float* qn = scratch_f32("scan_pc_qn", nq);
         float* xn = scratch_f32("scan_pc_xn", n);
@@ -1717,10 +1743,56 @@ void scan_topk(int metric, const float* q, const float* qnorm, int64_t nq, const
         qnorm = qn;
         xnorm = xn;
     }
+    if (k > SCAN_MAX_K) {
+        scan_topk_wide(metric, q, qnorm, nq, x, xnorm, deleted, n, d, k, id_offset, out_d, out_i, curv);
+        return;
+    }
     scan_topk_valu(metric, q, qnorm, nq, x, xnorm, deleted, n, d, k, id_offset, out_d, out_i, tag, curv);
 }
 
 namespace {
+// k > SCAN_MAX_K (flat.rs:63-64 sorts every pair and truncates to any k): K1's tiles write
+// the whole distance rows of a query batch (reference scalar order, the same arithmetic as
+// the fused top-k), and select_topk takes the first k by (distance, id) from them. Batches
+// of queries so that the rows fit min(4 GiB, 1/8 of the free HBM).
+void scan_topk_wide(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
+                    const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
+                    float curv) {
+    RVX_REQUIRE(n < ((int64_t)1 << 32), RVX_ERR_INVALID_PARAMETER, "k > 128 scans take up to 2^32 rows");
+    last_scan_stats().valu_queries += nq;
+    size_t fr = 0, tot = 0;
+    RVX_HIP(hipMemGetInfo(&fr, &tot));
+    int64_t budget = std::min<int64_t>((int64_t)4 << 30, std::max<int64_t>((int64_t)256 << 20, (int64_t)(fr / 8)));
+    const int64_t cap_mb = env_int("RVX_SCAN_WIDE_BUDGET_MB", 0);  // tests force several batches
+    if (cap_mb > 0) budget = cap_mb << 20;
+    const int64_t nqb = std::max<int64_t>(1, std::min<int64_t>(nq, budget / (n * 4)));
+    float* D = scratch_f32("scan_wide_d", nqb * n);
+    for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
+        const int64_t nb = std::min(nqb, nq - q0);
+        const int64_t qtiles = (nb + TQ - 1) / TQ;
+        int64_t nchunks = std::min<int64_t>(std::max<int64_t>(1, (2048 + qtiles - 1) / qtiles),
+                                            std::min<int64_t>(std::max<int64_t>(1, (n + TR - 1) / TR), 65535));
+        int64_t rows_per_chunk = ((n + nchunks - 1) / nchunks + TR - 1) / TR * TR;
+        nchunks = std::max<int64_t>(1, (n + rows_per_chunk - 1) / rows_per_chunk);
+        const float* qn = qnorm ? qnorm + q0 : nullptr;
+        ScanArgs a{q + q0 * d, x, qn, xnorm, nb, n, d, 0, rows_per_chunk, (int)nchunks, nullptr, nullptr, id_offset,
+                   deleted, curv, D, n};
+        const dim3 grid((unsigned)qtiles, (unsigned)nchunks);
+        const size_t lds = scan_lds_bytes(0);
+        switch (metric) {
+            case RVX_METRIC_L2: RVX_LAUNCH("scan_wide", (k_scan_topk<RVX_METRIC_L2, true>), grid, dim3(256), lds, a); break;
+            case RVX_METRIC_COSINE: RVX_LAUNCH("scan_wide", (k_scan_topk<RVX_METRIC_COSINE, true>), grid, dim3(256), lds, a); break;
+            case RVX_METRIC_DOT: RVX_LAUNCH("scan_wide", (k_scan_topk<RVX_METRIC_DOT, true>), grid, dim3(256), lds, a); break;
+            case RVX_METRIC_L1: RVX_LAUNCH("scan_wide", (k_scan_topk<RVX_METRIC_L1, true>), grid, dim3(256), lds, a); break;
+            case RVX_METRIC_POINCARE: RVX_LAUNCH("scan_wide", (k_scan_topk<RVX_METRIC_POINCARE, true>), grid, dim3(256), lds, a); break;
+            case RVX_METRIC_HYP_L2: RVX_LAUNCH("scan_wide", (k_scan_topk<RVX_METRIC_HYP_L2, true>), grid, dim3(256), lds, a); break;
+            case METRIC_L2SQ: RVX_LAUNCH("scan_wide", (k_scan_topk<METRIC_L2SQ, true>), grid, dim3(256), lds, a); break;
+            default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by the flat scan");
+        }
+        select_topk(D, nb, n, n, k, nullptr, id_offset, out_d + q0 * k, out_i + q0 * k, nullptr);
+    }
+}
+
 void scan_topk_valu(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
                     const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
                     const char* tag, float curv) {
@@ -1736,7 +1808,8 @@ void scan_topk_valu(int metric, const float* q, const float* qnorm, int64_t nq, 
 
     float* part_d = (float*)scratch_bytes("scan_part_d", nq * nchunks * k * 4);
     int64_t* part_i = (int64_t*)scratch_bytes("scan_part_i", nq * nchunks * k * 8);
-    ScanArgs a{q, x, qnorm, xnorm, nq, n, d, k, rows_per_chunk, (int)nchunks, part_d, part_i, id_offset, deleted, curv};
+    ScanArgs a{q, x, qnorm, xnorm, nq, n, d, k, rows_per_chunk, (int)nchunks, part_d, part_i, id_offset, deleted, curv,
+               nullptr, 0};
     const size_t lds = scan_lds_bytes(k);
     static bool attr_done = false;
     if (!attr_done) {

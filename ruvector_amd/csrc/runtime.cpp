@@ -286,8 +286,11 @@ rvx_status rvx_buffer_zero(rvx_buffer* buf) {
 
 rvx_status rvx_buffer_checksum(const rvx_buffer* buf, int64_t offset, int64_t bytes, uint64_t* out) {
     return guard([&] {
-        RVX_REQUIRE(buf && out && offset >= 0 && bytes >= 0 && offset + bytes <= buf->mem.bytes,
+        RVX_REQUIRE(buf && out && offset >= 0 && bytes >= 0 && offset <= buf->mem.bytes &&
+                        bytes <= buf->mem.bytes - offset,
                     RVX_ERR_INVALID_PARAMETER, "checksum range outside the buffer");
+        RVX_REQUIRE(offset % 8 == 0, RVX_ERR_INVALID_PARAMETER, "checksum offset must be a multiple of 8 bytes");
+        ComputeLock cl;  // the scratch slot is only valid under the device's compute lock
         auto* d = (uint64_t*)scratch_bytes("checksum", 8);
         checksum((const uint8_t*)buf->mem.p + offset, bytes, d);
         RVX_HIP(hipMemcpyAsync(out, d, 8, hipMemcpyDeviceToHost, stream()));

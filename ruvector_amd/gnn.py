@@ -171,9 +171,17 @@ def row_image_bytes(n: int, dim: int) -> int:
     return b.value
 
 
+_IMG_SLOT = 3072  # bytes per row slot of a row image (kernels.hpp IMG_SLOT)
+
+
 def row_image(n: int, dim: int) -> Buffer:
-    """An uninitialised row-image buffer for n rows of dim (see rvx_sage_forward_exchange3)."""
-    return Buffer(row_image_bytes(n, dim))
+    """A row-image buffer for n rows of dim (see rvx_sage_forward_exchange3). Every row's
+    count starts at 0xFFFF (> IMG_CAP: "no slot, read the dense row"), so a row that is
+    never packed falls back to the dense table instead of decoding an unwritten slot."""
+    b = Buffer(row_image_bytes(n, dim))
+    if n > 0:
+        b.upload(np.full(int(n), 0xFFFF, np.uint16), offset=int(n) * _IMG_SLOT)
+    return b
 
 
 def pack_row_image(x: Buffer, n_total: int, dim: int, image: Buffer, r0: int = 0, rows: Optional[int] = None) -> None:

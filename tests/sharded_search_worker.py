@@ -120,17 +120,28 @@ def main():
         checks["pruned_sorted"] = bool(np.all(np.diff(gd, axis=1) >= 0))
         # every shard's centroid and tangent coordinates equal the oracle's bits
         checks["pruned_exact"] = bool(np.array_equal(gid, ei) and close(gd, ed))
-        # a precondition that fails on some shards only (k * prune_factor = 200 > 128 where a
-        # shard holds more than 128 points; a 7-point shard passes) fails on EVERY rank
-        # instead of leaving the passing ranks waiting in a collective, and so do
-        # arguments that differ between ranks; the group stays usable afterwards
-        def fails(*args):
+        # k * prune_factor is unbounded (hnsw.rs:469-470): 200 tangent candidates per shard
+        gid, lid, gd, cnt = grp.search_batch(qa, 20, 0, "pruned")
+        parts = [(np.where(oi >= 0, oi + offsets[s], -1), od)
+                 for s, o in enumerate(orc) for oi, od in [o.search_with_pruning(q, 20)]]
+        ei, ed = merge(parts, 20)
+        checks["pruned_k20_exact"] = bool(np.array_equal(gid, ei) and close(gd, ed))
+        # a precondition that fails on some shards only (rank 1's shard uses the Euclidean
+        # metric, which search_with_pruning does not serve) fails on EVERY rank instead of
+        # leaving the passing ranks waiting in a collective, and so do arguments that differ
+        # between ranks; the group stays usable afterwards
+        def fails(*args, group=None):
             try:
-                grp.search_batch(*args)
+                (group or grp).search_batch(*args)
                 return False
             except rv.RvxError:
                 return True
-        checks["one_shard_failure_fails_all"] = fails(qa, 20, 0, "pruned")
+        hx = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=9, metric="euclidean" if rank == 1 else "poincare"),
+                               dim=d)
+        hx.insert_batch(x[o0:o0 + min(50, o1 - o0)])
+        hx.build_tangent_cache()
+        checks["one_shard_failure_fails_all"] = fails(qa, 10, 0, "pruned",
+                                                      group=rv.ShardedHyperbolicSearch(hx, comm, o0))
         checks["arg_mismatch_fails_all"] = fails(qa, 10 if rank == 0 else 9, 0, "exact")
         checks["rank0_without_queries_fails_all"] = fails(nq, 10, 0, "exact")
         gid2, _, gd2, _ = grp.search_batch(qa, 10, 0, "exact")
@@ -147,6 +158,17 @@ def main():
         ids, dd, cnt = fl.sharded_search_array(comm, qa, 10)
         ri, rd = O.flat_search(x, q, 10)
         checks["flat_exact"] = bool(np.array_equal(ids.astype(np.int64), ri) and np.array_equal(dd, rd))
+        # a real hit at +inf (the 3e19 rows of ranks > 0 overflow the squared
+        # distance) orders before every rank's empty slots (gid -1), so the first `count`
+        # merged slots are real hits in rank order
+        fz = rv.FlatIndex(d, rv.DistanceMetric.Euclidean)
+        fz.add_array(np.full((1, d), 3e19 if rank > 0 else 0.0, np.float32), np.array([1000 + rank], np.uint64))
+        kz = 4
+        zi, zd, zc = fz.sharded_search_array(comm, qa, kz)
+        m = min(kz, world)
+        checks["inf_hits_before_empty_slots"] = bool(
+            np.all(zc == m) and np.array_equal(zi[:, :m].astype(np.int64), np.tile(1000 + np.arange(m), (nq, 1))) and
+            np.all(np.isfinite(zd[:, 0])) and np.all(np.isinf(zd[:, 1:m])))
         horc = []
         for s in range(world):
             o = O.Hnsw(d, "l2", m=8, ef_construction=64, seed=3 + s)

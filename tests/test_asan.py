@@ -6,6 +6,7 @@ truncated / corrupt hnsw_rs dumps, feature files and layer JSON (test_parsers_fu
 the formats and golden fixtures, the oracle's known-answer and libm checks — in a child
 Python with that runtime preloaded; any sanitizer report fails the child (exit 66)."""
 import glob
+import importlib.util
 import os
 import subprocess
 import sys
@@ -26,8 +27,10 @@ def test_host_parsers_and_oracle_under_asan_ubsan():
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1:exitcode=66", PYTHONDONTWRITEBYTECODE="1")
     tests = ["tests/test_parsers_fuzz.py", "tests/test_formats.py", "tests/test_golden.py",
              "tests/test_oracle_known_answers.py", "tests/test_libm.py::test_check_counts_wrong_device_outputs"]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "not gpu", "-p", "no:cacheprovider",
-                        "--timeout", "600"] + tests, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    # pytest-timeout is optional: the subprocess timeout below bounds the run either way
+    extra = ["--timeout", "600"] if importlib.util.find_spec("pytest_timeout") else []
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "not gpu", "-p", "no:cacheprovider"]
+                       + extra + tests, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     out = r.stdout[-6000:] + r.stderr[-6000:]
     assert "ERROR: AddressSanitizer" not in out and "runtime error:" not in out, out
     assert r.returncode == 0, out
