@@ -80,6 +80,8 @@ def parse():
     p.add_argument("--no-hnsw", action="store_true", help="skip the HNSW queries/s@recall95 leg")
     p.add_argument("--no-scan", action="store_true", help="skip the 10M x 768 exact-scan queries/s leg")
     p.add_argument("--no-c4", action="store_true", help="skip the C4 leg (3 x RuvectorLayer + graph-attention head)")
+    p.add_argument("--no-c3", action="store_true", help="skip the C3 leg (HNSW build + search + GNN re-rank on the table)")
+    p.add_argument("--c3-ef", default="100,400,1600", help="C3 leg: ef sweep")
     p.add_argument("--c4-nodes", type=int, default=0, help="C4 leg nodes (default: --nodes)")
     p.add_argument("--transport", choices=("rccl", "host"), default="rccl",
                    help="N>1 exchange: RCCL over xGMI, or host memory + stdlib sockets (ranks may share a GPU)")
@@ -276,6 +278,9 @@ def main():
     del tables, g, invs
     if not a.no_scan:
         line["exact_scan"] = scan_leg(a, x, n_tot, d, rank, world, comm)
+        rv.release_scratch()
+    if not a.no_c3:
+        line["c3"] = c3_leg(a, x, n_tot, d, rank, world, comm)
     del x
     rv.release_scratch()  # the C4 leg needs ~235 GB of the 288 GB at 10M x 768
     if not a.no_c4:
@@ -390,6 +395,29 @@ def c4_leg(a, comm, rank, world):
     n = a.c4_nodes or a.nodes
     return bench_gnn.run(n, a.dim, a.degree, 8, 3, steps=2, warmup=1, comm=comm, rank=rank, world=world,
                          graph="random", cpu=(rank == 0 and world == 1 and not a.no_cpu), cpu_seconds=8.0)
+
+
+def c3_leg(a, x, n, d, rank, world, comm):
+    """configs[2] on the bench's resident table: GPU HNSW build (M 32, ef_c 200), k=10 ef sweep
+    with recall against the exact scan, NeuralSearch re-rank (RuvectorQuery defaults,
+    query.rs:44-58) QPS with an oracle check, and the oracle's search_filter on the same graph
+    as the CPU baseline (rank 0, N = 1). Replicas at N > 1: each rank builds and searches its
+    own copy; the job rates are summed."""
+    import bench_c3
+    import ruvector_amd as rv
+    nq = 10_000
+    qb = rv.Buffer(nq * d * 4)
+    qb.fill_normal(nq * d, 6)
+    res = bench_c3.leg(x, n, d, qb, nq, 32, 200, [int(e) for e in a.c3_ef.split(",")], 10,
+                       cpu=(rank == 0 and world == 1 and not a.no_cpu), cpu_seconds=8.0, log=lambda s: None,
+                       check=8 if rank == 0 else 0, seed=5)
+    qps = res["neural_search"]["qps"]
+    if comm is not None:
+        qps = comm.allreduce([qps])[0]
+    res["value"] = round(qps, 1)
+    res["unit"] = "queries/s (NeuralSearch re-rank: HNSW ef 50 candidates + 2 GNN layers + differentiable_search; " \
+                  "replicas summed over GPUs)"
+    return res
 
 
 def hnsw_leg(a, rank, world, comm):

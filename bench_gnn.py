@@ -137,6 +137,7 @@ def run(n, d=768, deg=32, heads=8, nlayers=3, steps=2, warmup=1, comm=None, rank
             "ms_per_layer": round(edge_ms, 3), "work_per_layer": edge_bytes, "traffic": None,
             "bytes": "per edge 3*4*H (k, v, m rows of the neighbour) + 8; per node 8 + 4H (q) + 2*4H (out, h)"},
     }
+    attach_c4_traffic(roof, {"nodes": n, "edges": E, "layers": nlayers, "parallelism": f"node-range x{world}"})
     line = {
         "metric": "GNN-layer edges/sec (RuvectorLayer stack + graph-attention head)",
         "value": round(E * (nlayers + 1) / dt, 1), "unit": "edges/s", "n_gpus": world, "steps": steps,
@@ -167,6 +168,31 @@ def run(n, d=768, deg=32, heads=8, nlayers=3, steps=2, warmup=1, comm=None, rank
     return line
 
 
+def attach_c4_traffic(roof, cfg):
+    """HBM bytes per layer of the layer GEMMs and the edge kernel from the committed rocprofv3
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this leg (scripts/c4_traffic.sh ->
+    profiles/pmc_traffic_c4.json, gfx950 FETCH correction), when the configuration matches:
+    the profiled run's total bytes per tag over its forwards x layers."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic_c4.json")
+    if not os.path.exists(path):
+        return
+    try:
+        pmc = json.load(open(path))
+    except ValueError:
+        return
+    pc = pmc.get("config") or {}
+    if any(pc.get(k) != v for k, v in cfg.items()) or not pc.get("forwards"):
+        return
+    per = pc["forwards"] * cfg["layers"]
+    for key, tag in (("gnn_gemm (all dense layers of one RuvectorLayer)", "gnn_gemm"),
+                     ("gnn_edge_attention", "gnn_edge_attention")):
+        ent = (pmc.get("kernels") or {}).get(tag)
+        if ent and key in roof:
+            roof[key]["traffic"] = round(ent["hbm_bytes_total"] / per, 0)
+            roof[key]["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE(x2, gfx950) + WRITE_SIZE per layer, "
+                                           "profiles/pmc_traffic_c4.json")
+
+
 def cpu_baseline(cpu_seconds, x_buf, g, layer, n, d, deg, offsets, host_csr=None, y1=None):
     """Oracle RuvectorLayer::forward on a bounded sample of layer-1 rows (the CPU
     baseline) and the per-row parity of the GPU's layer 1 on the same rows."""
@@ -186,22 +212,29 @@ def cpu_baseline(cpu_seconds, x_buf, g, layer, n, d, deg, offsets, host_csr=None
     y1 = y1 if y1 is not None else rv.Buffer(n * layer.hidden_dim * 4)
     layer.forward_exchange(g, x_buf, y1, offsets)
 
-    def ref_rows(r):
-        # only the sample's rows and their neighbours leave HBM
+    def inputs(r):
+        # only the sample's rows and their neighbours leave HBM (before any timed region)
         nb = col[:rp[r]].astype(np.int64)
         need = np.concatenate([np.arange(r, dtype=np.int64), nb])
-        h = x_buf.gather_rows(n, d, need)
-        return O.rvl_forward_graph(W, h, rp[:r + 1], (r + np.arange(nb.size)).astype(np.int32), ew[:rp[r]],
-                                   rows=(0, r), threads=threads)
+        return x_buf.gather_rows(n, d, need), (r + np.arange(nb.size)).astype(np.int32)
 
-    rows = 64
-    t0 = time.perf_counter()
-    ref_rows(rows)
-    dt = time.perf_counter() - t0
-    rows = int(min(n, max(rows, rows * cpu_seconds / max(dt, 1e-3))))
-    t0 = time.perf_counter()
-    ref = ref_rows(rows)
-    dt = time.perf_counter() - t0
+    def timed(r):
+        h, cols = inputs(r)
+        t0 = time.perf_counter()
+        ref = O.rvl_forward_graph(W, h, rp[:r + 1], cols, ew[:rp[r]], rows=(0, r), threads=threads)
+        return ref, time.perf_counter() - t0
+
+    # calibrate on growing samples until one takes >= half the target, then time a sample
+    # sized for the whole target (host copies of the rows are made before each timed call)
+    rows, dt = 256, 0.0
+    while True:
+        _, dt = timed(rows)
+        if dt >= 0.5 * cpu_seconds or rows >= n:
+            break
+        rows = int(min(n, max(2 * rows, rows * 0.6 * cpu_seconds / max(dt, 1e-3))))
+    if dt < 0.8 * cpu_seconds and rows < n:
+        rows = int(min(n, rows * cpu_seconds / max(dt, 1e-3)))
+    ref, dt = timed(rows)
     got = y1.download(np.float32, (rows, layer.hidden_dim))
     del y1
     err, row_err = rel_errs(got, ref)

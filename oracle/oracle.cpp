@@ -606,16 +606,24 @@ void* orc_hnsw_from_graph(const float* vecs, int64_t n, int64_t d, int32_t metri
                           const int32_t* up_ids, const int64_t* up_rp, const int32_t* up_col) {
     auto* h = new OHnsw();
     h->d = d; h->metric = metric; h->M = 16; h->ef_c = 0; h->max_layer = 16;
-    h->data.assign(vecs, vecs + n * d);
+    h->data.resize((size_t)(n * d));
     h->level.assign(levels, levels + n);
     h->nb.resize(n);
     std::unique_ptr<std::mutex[]> nl(new std::mutex[std::max<int64_t>(n, 1)]);
     h->locks = std::move(nl);
-    for (int64_t i = 0; i < n; ++i) {
-        h->nb[i].resize(17);
-        h->count_at_level[levels[i]].fetch_add(1);
-        for (int64_t p = rp0[i]; p < rp0[i + 1]; ++p) h->nb[i][0].push_back({0.0f, col0[p]});
-    }
+    // rows and layer-0 lists in parallel (a 10M-node graph is the C3 CPU baseline's input)
+    const int threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const int64_t blk = 65536;
+    pfor((n + blk - 1) / blk, threads, [&](int64_t b) {
+        const int64_t i0 = b * blk, i1 = std::min(n, i0 + blk);
+        std::copy(vecs + i0 * d, vecs + i1 * d, h->data.begin() + i0 * d);
+        for (int64_t i = i0; i < i1; ++i) {
+            h->nb[i].resize(17);
+            h->count_at_level[levels[i]].fetch_add(1);
+            h->nb[i][0].reserve((size_t)(rp0[i + 1] - rp0[i]));
+            for (int64_t p = rp0[i]; p < rp0[i + 1]; ++p) h->nb[i][0].push_back({0.0f, col0[p]});
+        }
+    });
     int64_t oi = 0, orp = 0, oc = 0;
     for (int l = 1; l <= max_level; ++l) {
         const int64_t cnt = upper_count[l];

@@ -19,6 +19,22 @@
 // fast_acosh (poincare.rs:259-276), log_map (:431-451, atanh) and exp_map (:407-428,
 // tanh). Every float operation here is a single IEEE operation (the library builds with
 // -ffp-contract=off); the double FMAs in logf are explicit.
+//
+// Notices of the restated algorithms, tables and constants:
+//
+//   logf (glibc sysdeps/ieee754/flt-32/e_logf.c, e_logf_data.c) comes from Arm's
+//   optimized-routines:
+//     Copyright (c) 2017-2018, Arm Limited.
+//     (upstream licence: MIT, later Apache-2.0 WITH LLVM-exception; distributed in
+//     glibc under the GNU Lesser General Public License 2.1 or later)
+//
+//   log1pf, expm1f, tanhf (glibc sysdeps/ieee754/flt-32/s_log1pf.c, s_expm1f.c,
+//   s_tanhf.c) are fdlibm's float conversions:
+//     Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//     Developed at SunPro, a Sun Microsystems, Inc. business.
+//     Permission to use, copy, modify, and distribute this software is freely granted,
+//     provided that this notice is preserved.
+//   (float conversions by Ian Lance Taylor, Cygnus Support)
 #pragma once
 #include <cmath>
 #include <cstdint>

@@ -53,13 +53,30 @@ def load(d, counter):
     return {k: (v[0], len(v[1])) for k, v in acc.items()}
 
 
+# C4 stack (bench_gnn.py): the RuvectorLayer GEMMs are the split-f16 h2w tiles (the attention
+# head's transform runs split-bf16 x3g, its own tag), the edge kernel k_edge_attn_grouped
+TAGS_C4 = {
+    "gemm_nt_h2w": "gnn_gemm",
+    "gemm_nt_h2g": "gnn_gemm",
+    "k_edge_attn": "gnn_edge_attention",
+    "k_gru_finish": "gnn_finish",
+    "k_mul_amax": "gnn_gate",
+    "gemm_nt_x3g": "efa_gemm",
+    "k_edge_feat": "efa_edge",
+}
+
+
 def main():
+    tags = TAGS
+    if "--c4" in sys.argv:
+        sys.argv.remove("--c4")
+        tags = TAGS_C4
     fdir, wdir, out = sys.argv[1:4]
     fetch = load(fdir, "FETCH_SIZE")
     write = load(wdir, "WRITE_SIZE")
     res = {}
     for name in set(fetch) | set(write):
-        tag = next((t for s, t in TAGS.items() if s in name), None)
+        tag = next((t for s, t in tags.items() if s in name), None)
         if tag is None:
             continue
         fk, fn = fetch.get(name, (0.0, 0))
@@ -76,6 +93,7 @@ def main():
         e["read_bytes_per_launch_corrected"] = rd
         e["write_bytes_per_launch"] = wr
         e["hbm_bytes_per_launch"] = rd + wr
+        e["hbm_bytes_total"] = 2.0 * e["fetch_kib"] * 1024 + e["write_kib"] * 1024
     if "sage_aggregate" in res and "sage_gemm" in res:
         a, g = res["sage_aggregate"], res["sage_gemm"]
         res["sage_chunk_gather_gemm"] = {
@@ -88,7 +106,10 @@ def main():
     if len(sys.argv) > 4:
         for line in open(sys.argv[4], errors="replace"):
             if line.startswith("{") and '"metric"' in line:
-                cfg = json.loads(line).get("config")
+                j = json.loads(line)
+                cfg = j.get("config")
+                if tags is TAGS_C4 and cfg is not None:  # forwards in the profiled run: warm-up + timed
+                    cfg = dict(cfg, forwards=int(j.get("warmup", 0)) + int(j.get("steps", 0)))
     json.dump({"config": cfg, "kernels": res}, open(out, "w"), indent=1)
     print(json.dumps({k: round(v["hbm_bytes_per_launch"] / 1e9, 3) for k, v in res.items()}))
 
