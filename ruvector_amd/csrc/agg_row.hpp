@@ -359,6 +359,125 @@ __device__ __forceinline__ void agg_img_row(const int64_t* __restrict__ rp, cons
                             lane);
 }
 
+// Image gather of one destination row with the expansion in registers (AggHelp::img_reg):
+// the same terms, order and arithmetic as agg_vec_row<3, AGG, false, 8, true>, so the same
+// bits, without the LDS round trip of agg_img_row. Per group of U neighbour rows: each
+// lane loads its u16 header word of every imaged row (128 B per row), the DPP scan turns
+// it into the packed positions of the lane's three blocks, and the lane loads its values
+// of block j straight from the record as one 16-B load at 128 + 4 p[j] (4-B aligned;
+// bytes past the lane's own values belong to the next lane or the next slot and are not
+// used), then expands them with the header bits. Two dependent round trips per group, so
+// the next group's headers are issued before this group's values are consumed.
+template <int AGG>
+__device__ __forceinline__ void agg_img_row_reg(const int64_t* __restrict__ rp, const int32_t* __restrict__ col,
+                                                const float* __restrict__ x, int dim,
+                                                const unsigned char* __restrict__ slots,
+                                                const uint16_t* __restrict__ nnz, float* __restrict__ out,
+                                                const float* __restrict__ self_x, float* __restrict__ row_scale,
+                                                const float* __restrict__ row_mul, const float* __restrict__ self_mul,
+                                                int64_t row, int lane) {
+#ifndef RVX_IMGR_U
+#define RVX_IMGR_U 8
+#endif
+    constexpr int NV = 3, U = RVX_IMGR_U;
+    const int64_t beg = rp[row], end = rp[row + 1];
+    const int cnt_total = (int)(end - beg);
+    float4 acc[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    bool active[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) active[j] = (4 * lane + 256 * j) < dim;
+    const int dlast = (dim - 4) * 4;  // byte offset of the row's last float4 (inactive lanes re-read it)
+    int doff[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) doff[j] = active[j] ? (4 * lane + 256 * j) * 4 : dlast;
+
+    for (int64_t e0 = beg; e0 < end; e0 += 64) {
+        const int cnt = (int)min<int64_t>(64, end - e0);
+        const int my_c = lane < cnt ? col[e0 + lane] : 0;
+        const float my_m = (row_mul && lane < cnt) ? row_mul[my_c] : 1.0f;
+        const int my_n = lane < cnt ? (int)nnz[my_c] : 0;
+        unsigned hh[U];
+        auto load_hdr = [&](int t, unsigned (&h)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int tu = min(t + u, cnt - 1);
+                const int c = __builtin_amdgcn_readlane(my_c, tu);
+                const int nz = __builtin_amdgcn_readlane(my_n, tu);
+                h[u] = nz <= IMG_CAP
+                           ? (unsigned)__builtin_nontemporal_load(
+                                 reinterpret_cast<const uint16_t*>(slots + (int64_t)c * IMG_SLOT) + lane)
+                           : 0u;
+            }
+        };
+        load_hdr(0, hh);
+        for (int t = 0; t < cnt; t += U) {
+            float4 v[U][NV];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int tu = min(t + u, cnt - 1);  // a short group re-reads its last row (not accumulated)
+                const int c = __builtin_amdgcn_readlane(my_c, tu);
+                const int nz = __builtin_amdgcn_readlane(my_n, tu);
+                const char* base;
+                int o[NV];
+                if (nz <= IMG_CAP) {
+                    int p[3];
+                    unsigned tot;
+                    img_positions(hh[u], p, tot);
+                    base = reinterpret_cast<const char*>(slots + (int64_t)c * IMG_SLOT + 128);
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) o[j] = 4 * p[j];
+                } else {
+                    base = reinterpret_cast<const char*>(x + (int64_t)c * dim);
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) o[j] = doff[j];
+                }
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    f32x4 w;
+                    __builtin_memcpy(&w, base + o[j], 16);  // 4-B aligned: unaligned-access mode
+                    v[u][j] = make_float4(w.x, w.y, w.z, w.w);
+                }
+            }
+            unsigned hn[U];
+            if (t + U < cnt) load_hdr(t + U, hn);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (t + u >= cnt) break;
+                const int nz = __builtin_amdgcn_readlane(my_n, t + u);
+                if (nz <= IMG_CAP) {
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) {
+                        const unsigned nib = (hh[u] >> (4 * j)) & 15u;
+                        const float w0 = v[u][j].x, w1 = v[u][j].y, w2 = v[u][j].z, w3 = v[u][j].w;
+                        const bool b0 = nib & 1u, b1 = nib & 2u, b2 = nib & 4u, b3 = nib & 8u;
+                        const int r2 = (int)b0 + (int)b1, r3 = r2 + (int)b2;
+                        const float x0 = b0 ? w0 : 0.0f;
+                        const float x1 = b1 ? (b0 ? w1 : w0) : 0.0f;
+                        const float x2 = b2 ? (r2 == 0 ? w0 : r2 == 1 ? w1 : w2) : 0.0f;
+                        const float x3 = b3 ? (r3 == 0 ? w0 : r3 == 1 ? w1 : r3 == 2 ? w2 : w3) : 0.0f;
+                        v[u][j] = make_float4(x0, x1, x2, x3);
+                    }
+                }
+                if (row_mul) {
+                    const float mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_m), t + u));
+#pragma unroll
+                    for (int j = 0; j < NV; ++j) v[u][j] = scale4(v[u][j], mu);
+                }
+#pragma unroll
+                for (int j = 0; j < NV; ++j) acc[j] = agg_op<AGG>(acc[j], v[u][j]);
+            }
+            if (t + U < cnt) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) hh[u] = hn[u];
+            }
+        }
+    }
+    agg_row_finish<NV, AGG>(acc, active, cnt_total, x, dim, 0, 0, out, self_x, row_scale, nullptr, 0, self_mul, row,
+                            lane);
+}
+
 // Dynamic form of the overlapped GraphSAGE gather (AggHelp): every wave takes destination
 // rows from the chunk's counter until it passes n. Used by the chunk's own gather kernel and
 // by the previous chunk's GEMM blocks once their tiles are done. `win`: this wave's two
@@ -373,8 +492,12 @@ __device__ __forceinline__ void agg_help_rows(const AggHelp& h, int lane, unsign
         if (row >= h.n) return;
         if constexpr (IMG && NV == 3 && AGG != AGG_MAX) {
             if (use_img) {
-                agg_img_row<AGG>(h.rp, h.col, h.x, h.dim, h.img_slots, h.img_nnz, h.out, h.self_x, h.row_scale,
-                                 h.row_mul, h.self_mul, row, lane, win);
+                if (h.img_reg)
+                    agg_img_row_reg<AGG>(h.rp, h.col, h.x, h.dim, h.img_slots, h.img_nnz, h.out, h.self_x,
+                                         h.row_scale, h.row_mul, h.self_mul, row, lane);
+                else
+                    agg_img_row<AGG>(h.rp, h.col, h.x, h.dim, h.img_slots, h.img_nnz, h.out, h.self_x, h.row_scale,
+                                     h.row_mul, h.self_mul, row, lane, win);
                 continue;
             }
         }

@@ -335,9 +335,29 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         if (main_s != d.stream) RVX_HIP(hipStreamWaitEvent(main_s, ev[chunks], 0));
         if (norm_side) RVX_HIP(hipStreamWaitEvent(d.aux2, ev[chunks], 0));
     }
+    // RVX_SAGE_NORM_AUX (opt-in, read per call; no hooks or images): the row normalisation
+    // of chunk c runs on the gather stream after the gather of chunk c+1 (and after the GEMM
+    // of chunk c), before the gather of chunk c+2, instead of between the GEMMs of chunks c and
+    // c+1 — the GEMM of chunk c+1 no longer waits for it, and at most two kernels share the
+    // chip at any time (the third-stream form above had three). Same kernel, same bits.
+    const bool norm_aux = chunks > 1 && l->normalize && !hook && !y_img && !norm_side && split == 0 &&
+                          env_int("RVX_SAGE_NORM_AUX", 0);
+    struct PendingNorm { bool on = false; int cc = 0; int64_t rr0 = 0, rrows = 0; } pend;
+    auto flush_norm = [&]() {  // on the gather stream, behind the gather just queued there
+        if (!pend.on) return;
+        RVX_HIP(hipStreamWaitEvent(gath_s, evg[pend.cc], 0));
+        StreamScope on_gather(gath_s);
+        normalize_rows(y + pend.rr0 * l->out, pend.rrows, l->out, true, "sage_normalize");
+        pend.on = false;
+    };
     // chunk c's output finished by the GEMM: normalise it (third stream or in line), then
     // the caller's hook on the stream that completed the rows
     auto finish_chunk = [&](int cc, int64_t rr0, int64_t rrows, bool norm) {
+        if (norm && norm_aux) {
+            RVX_HIP(hipEventRecord(evg[cc], main_s));  // the GEMM of chunk cc is done
+            pend.on = true; pend.cc = cc; pend.rr0 = rr0; pend.rrows = rrows;
+            return;
+        }
         if (norm && norm_side) {
             RVX_HIP(hipEventRecord(evg[cc], main_s));
             RVX_HIP(hipStreamWaitEvent(d.aux2, evg[cc], 0));
@@ -375,6 +395,8 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         RVX_HIP(hipEventRecord(ev[chunks], d.stream));
         RVX_HIP(hipStreamWaitEvent(gath_s, ev[chunks], 0));
     }
+    // imaged rows expanded in registers (1, default) or through LDS windows (0); read per call
+    const int img_reg = env_int("RVX_IMG_REG", 1) != 0 ? 1 : 0;
     auto help_of = [&](int64_t rr0) {
         AggHelp h{};
         h.rp = g->row_ptr + rr0; h.col = g->col; h.n = std::min(step, n - rr0);
@@ -385,6 +407,7 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         if (x_img && row_image_ok(l->in) && a != AGG_MAX) {
             h.img_slots = x_img.slots;
             h.img_nnz = x_img.nnz;
+            h.img_reg = img_reg;
         }
         return h;
     };
@@ -402,6 +425,7 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
                                 c == 0 ? env_int("RVX_AGG_FIRST_CAP", 4) : 0);
             RVX_HIP(hipEventRecord(ev[c], gath_s));
             RVX_HIP(hipStreamWaitEvent(main_s, ev[c], 0));
+            flush_norm();  // chunk c-1's normalisation, behind gather c
         } else if (chunks > 1) {
             StreamScope on_aux(gath_s);
             CuScope aux_cu(gath_cus);
@@ -412,6 +436,7 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
                            x_mul ? x_mul + row_offset + r0 : nullptr);
             RVX_HIP(hipEventRecord(ev[c], gath_s));
             RVX_HIP(hipStreamWaitEvent(main_s, ev[c], 0));
+            flush_norm();
         } else {
             aggregate_rows(g->row_ptr, g->col, nullptr, n, x, l->in, a, 0, 0, agg, "sage_aggregate", false,
                            x + row_offset * l->in, scale, aplanes, a_plane, x_mul, x_mul ? x_mul + row_offset : nullptr);
@@ -466,6 +491,7 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
         finish_chunk(c, r0, rows, false);
 #endif
     }
+    flush_norm();  // the last chunk's
     for (; hook && c < chunks; ++c) finish_chunk(c, n, 0, false);
     if (main_s != d.stream) {
         RVX_HIP(hipEventRecord(ev[chunks + 1], main_s));
@@ -473,6 +499,10 @@ void sage_forward_dev(const rvx_sage_layer* l, const rvx_graph* g, const float* 
     }
     if (norm_side) {  // the normalise stream's last chunk (and hooks) before anything after the layer
         RVX_HIP(hipEventRecord(evg[chunks], d.aux2));
+        RVX_HIP(hipStreamWaitEvent(d.stream, evg[chunks], 0));
+    }
+    if (norm_aux) {  // the gather stream's last normalisation before anything after the layer
+        RVX_HIP(hipEventRecord(evg[chunks], gath_s));
         RVX_HIP(hipStreamWaitEvent(d.stream, evg[chunks], 0));
     }
 }

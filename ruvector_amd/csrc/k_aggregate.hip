@@ -349,7 +349,7 @@ void aggregate_rows_help(const AggHelp& h, const char* tag, int blocks_per_cu) {
                                              (int64_t)cap * active_cus());
     if (h.img_slots)
         RVX_LAUNCH(tag ? tag : "aggregate", k_aggregate_help<true>, dim3((unsigned)blocks), dim3(256),
-                   ROWS_PER_BLOCK * IMG_WIN, h);
+                   h.img_reg ? 0 : ROWS_PER_BLOCK * IMG_WIN, h);  // register expansion: no LDS windows
     else
         RVX_LAUNCH(tag ? tag : "aggregate", k_aggregate_help<false>, dim3((unsigned)blocks), dim3(256), 0, h);
 }

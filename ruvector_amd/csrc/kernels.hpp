@@ -57,6 +57,9 @@ struct AggHelp {
     unsigned* counter;
     // optional image of x (mean / sum, row_image_ok(dim)): neighbour rows are read from it
     const unsigned char* img_slots; const uint16_t* img_nnz;
+    // 1: imaged rows expanded in registers (header, then each lane's values straight from
+    // the record); 0: through the wave's LDS windows (RVX_IMG_REG)
+    int img_reg;
 };
 // Epilogue: C = epi(alpha * acc + bias0 + bias1 + addend[row][col])
 constexpr int ROWSUMSQ_SLOTS = 8;  // per-row partial sums of squares (column tiles >= 128 wide, N <= 1024)

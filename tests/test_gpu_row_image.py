@@ -67,11 +67,13 @@ def _graph(n, deg, seed):
     return rp, col
 
 
+@pytest.mark.parametrize("img_reg", ["1", "0"])  # expansion in registers (default) or through LDS windows
 @pytest.mark.parametrize("defer", [True, False])
 @pytest.mark.parametrize("dims,n,deg,chunks", [((768, 768, 768), 70000, 9, 4), ((256, 640, 512), 50000, 6, 3),
                                                ((768, 768, 256), 34000, 12, 2)])
-def test_sage_stack_with_row_image_is_bit_identical(monkeypatch, defer, dims, n, deg, chunks):
+def test_sage_stack_with_row_image_is_bit_identical(monkeypatch, defer, dims, n, deg, chunks, img_reg):
     monkeypatch.setenv("RVX_SAGE_CHUNKS", str(chunks))
+    monkeypatch.setenv("RVX_IMG_REG", img_reg)
     d0, d1, d2 = dims
     x = O.fill_uniform(n * d0, 400 + n).reshape(n, d0) - 0.5
     rp, col = _graph(n, deg, 401)
@@ -90,11 +92,13 @@ def test_sage_stack_with_row_image_is_bit_identical(monkeypatch, defer, dims, n,
     assert np.array_equal(dec[held].view(np.uint32), y1b[held].view(np.uint32))
 
 
-def test_row_image_dense_fallback_signed_zeros_and_nan(monkeypatch):
+@pytest.mark.parametrize("img_reg", ["1", "0"])
+def test_row_image_dense_fallback_signed_zeros_and_nan(monkeypatch, img_reg):
     """An input table packed directly (rvx_row_image_pack): rows with every value nonzero (the
     dense fallback), rows of mixed density, an all-zero row, -0.0 and NaN entries. A layer
     reading it through x_image gives the bits of the layer reading the table."""
     monkeypatch.setenv("RVX_SAGE_CHUNKS", "3")
+    monkeypatch.setenv("RVX_IMG_REG", img_reg)
     n, d, deg = 50000, 768, 10
     rng = np.random.default_rng(7)
     x = (rng.standard_normal((n, d)) * 0.1).astype(np.float32)
