@@ -93,6 +93,27 @@ def parse():
     return p.parse_args()
 
 
+_STAGE = ["start"]
+
+
+def _progress(stage):
+    """Name the leg that runs now; a daemon thread prints it to stderr every minute so a
+    supervisor watching the output sees a long leg (the C3 build, the C4 stack) alive."""
+    _STAGE[0] = stage
+    print(f"[bench] {stage}", file=sys.stderr, flush=True)
+
+
+def _start_progress_thread():
+    import threading
+    t0 = time.perf_counter()
+
+    def run():
+        while True:
+            time.sleep(60.0)
+            print(f"[bench] ... {_STAGE[0]} ({time.perf_counter() - t0:.0f} s)", file=sys.stderr, flush=True)
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -102,6 +123,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if rank == 0:
+        _start_progress_thread()
     import ruvector_amd as rv
     from ruvector_amd.shard import REDUCE_MAX, ShardPlan, comm_from_env
 
@@ -164,6 +187,7 @@ def main():
         if comm is not None:
             comm.barrier()
 
+    _progress("graphsage headline")
     for _ in range(a.warmup):
         step()
     barrier()
@@ -272,21 +296,26 @@ def main():
                                           "host-staged (host memory + stdlib TCP sockets)")
         line["parity"] = multi_rank_check(a, comm, rank, world, offsets, x, tables, invs, n_tot, d, deg, layers)
     if rank == 0 and world == 1 and not a.no_cpu:
+        _progress("graphsage cpu baseline + parity")
         line["cpu_baseline"], line["parity"] = cpu_baseline(a, x, g, tables, n_tot, d, deg, layers, invs)
     if world == 1:
         line["gemm_paths"] = gemm_alternatives(g, x, tables[0], off_ptr, d, deg)
     del tables, g, invs
     if not a.no_scan:
+        _progress("exact scan leg")
         line["exact_scan"] = scan_leg(a, x, n_tot, d, rank, world, comm)
         rv.release_scratch()
     if not a.no_c3:
+        _progress("c3 leg (HNSW build, search, re-rank)")
         line["c3"] = c3_leg(a, x, n_tot, d, rank, world, comm)
     del x
     rv.release_scratch()  # the C4 leg needs ~235 GB of the 288 GB at 10M x 768
     if not a.no_c4:
+        _progress("c4 leg")
         line["c4"] = c4_leg(a, comm, rank, world)
         rv.release_scratch()
     if not a.no_hnsw:
+        _progress("c1 hnsw leg")
         line["hnsw"] = hnsw_leg(a, rank, world, comm)
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -409,8 +438,9 @@ def c3_leg(a, x, n, d, rank, world, comm):
     qb = rv.Buffer(nq * d * 4)
     qb.fill_normal(nq * d, 6)
     res = bench_c3.leg(x, n, d, qb, nq, 32, 200, [int(e) for e in a.c3_ef.split(",")], 10,
-                       cpu=(rank == 0 and world == 1 and not a.no_cpu), cpu_seconds=8.0, log=lambda s: None,
-                       check=8 if rank == 0 else 0, seed=5)
+                       cpu=(rank == 0 and world == 1 and not a.no_cpu), cpu_seconds=8.0,
+                       log=(lambda s: print(f"[bench] {s}", file=sys.stderr, flush=True)) if rank == 0 else
+                       (lambda s: None), check=8 if rank == 0 else 0, seed=5)
     qps = res["neural_search"]["qps"]
     if comm is not None:
         qps = comm.allreduce([qps])[0]
