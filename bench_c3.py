@@ -81,6 +81,7 @@ def leg(xb, n, d, qb, nq, m=32, efc=200, efs=(100, 400, 1600), k=10, cpu=True, c
     ok = [s for s in sweep if s["recall"] >= 0.95]
     best = max(ok, key=lambda s: s["qps"]) if ok else None
     out.update(sweep=sweep, qps_at_recall95=best["qps"] if best else None, ef_at_recall95=best["ef"] if best else None)
+    out["c3_config"] = {"n": n, "d": d, "nq": nq, "m": m, "efc": efc}  # what profiles/pmc_traffic_c3.json matches
     attach_search_traffic(out, n, d, nq, m, efc)
 
     # NeuralSearch re-rank (query.rs:44-58, search.rs:56-162)

@@ -66,7 +66,45 @@ TAGS_C4 = {
 }
 
 
+def load_dispatches(d, counter, substr):
+    """Per-dispatch counter totals of the kernels whose name contains substr, in dispatch order."""
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    acc = defaultdict(float)
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter or substr not in row.get("Kernel_Name", ""):
+                    continue
+                acc[int(row.get("Dispatch_Id") or row.get("Correlation_Id"))] += float(row["Counter_Value"])
+    return [acc[k] for k in sorted(acc)]
+
+
+def main_c3():
+    """bench_c3.py under --pmc: the hnsw_search dispatches run in the order warm / timed per ef of
+    the sweep, then NeuralSearch's warm-up and timed searches; the timed launch of sweep entry i
+    is dispatch 2 i + 1. Usage: pmc_traffic.py --c3 <fetch_dir> <write_dir> <out.json> <bench.json>"""
+    fdir, wdir, out, bj = sys.argv[1:5]
+    j = json.loads([l for l in open(bj) if l.startswith("{")][-1])
+    fetch = load_dispatches(fdir, "FETCH_SIZE", "k_hnsw_search")
+    write = load_dispatches(wdir, "WRITE_SIZE", "k_hnsw_search")
+    by_ef = {}
+    for i, s in enumerate(j["sweep"]):
+        t = 2 * i + 1
+        if t < len(fetch) and t < len(write):
+            rd, wr = 2.0 * fetch[t] * 1024, write[t] * 1024
+            by_ef[str(s["ef"])] = {"read_bytes_per_launch_corrected": rd, "write_bytes_per_launch": wr,
+                                   "hbm_bytes_per_launch": rd + wr,
+                                   "alg_bytes_per_launch": s["roofline"]["alg_bytes_per_launch"]}
+    cfg = j.get("c3_config") or {}
+    json.dump({"config": cfg, "kernels": {"hnsw_search_by_ef": by_ef}, "dispatches": len(fetch)}, open(out, "w"),
+              indent=1)
+    print(json.dumps({k: round(v["hbm_bytes_per_launch"] / 1e9, 2) for k, v in by_ef.items()}))
+
+
 def main():
+    if "--c3" in sys.argv:
+        sys.argv.remove("--c3")
+        return main_c3()
     tags = TAGS
     if "--c4" in sys.argv:
         sys.argv.remove("--c4")
