@@ -1299,8 +1299,132 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_h2g(GemmArgs g, int epi) {
 #ifndef H2W_RING
 #define H2W_RING 4
 #endif
-template <bool DUAL, int WN, int BN, int NW, bool PIPE = false, bool AMX = false, bool GATE = false>
+// K loop and epilogue of h2w_tile<..., M16 = true> (WN = 1: wave wm owns tile rows
+// [32 wm, 32 wm + 32), all BN columns). Lane (lc, lg) = (lane & 15, lane >> 4): A fragment =
+// row lc of a 16-row half, k 8 lg .. 8 lg + 7 (LDS chunks 2 lg, 2 lg + 1); B fragment = column lc
+// of a 16-column subtile, k 8 lg .. 8 lg + 7 (chunk lg) of each f16 plane; accumulator element v
+// = row 4 lg + v, column lc of the (half, subtile).
+template <bool DUAL, int BN, int NW, bool AMX, class Issue>
+__device__ __forceinline__ void h2w_m16_body(const GemmArgs& g, int epi, int64_t m0, int n0, int tn, int wm, int lane,
+                                             int nk0, int nkt, const float* asc, const float* asc1, Issue& issue) {
+    constexpr int XA = 32 * NW * 128, BPL = BN * 64, STG = XA + 2 * BPL;
+    constexpr int NS = BN / 16;       // 16-column subtiles per wave
+    constexpr int NBP = BN / (8 * NW);
+    extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
+    const int lc = lane & 15, lg = lane >> 4;
+    const int arow = wm * 32 + lc;
+    const int aswz = (arow & 7) ^ ((arow >> 3) & 1);  // rows arow and arow + 16 share it
+    const int a_rd0 = arow * 128 + (((2 * lg) ^ aswz) << 4);
+    const int a_rd1 = arow * 128 + (((2 * lg + 1) ^ aswz) << 4);
+    const int b_rd = XA + lc * 64 + ((lg ^ ((4 - ((lc >> 2) & 3)) & 3)) << 4);  // + 1024 per subtile
+
+    f32x4 acc[2][NS];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int ns = 0; ns < NS; ++ns) acc[h][ns] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+#pragma unroll
+    for (int j = 0; j < 4 + NBP; ++j) issue(0, xsm, j);
+    auto ktile = [&](const unsigned char* __restrict__ cur, unsigned char* __restrict__ nxt, int t) {
+        if (t + 1 < nkt) {
+#pragma unroll
+            for (int j = 0; j < 4 + NBP; ++j) issue(t + 1, nxt, j);
+        }
+        const float sc = DUAL && t >= nk0 ? asc1[0] : asc[0];
+        f16x8 af[2][2];  // [half][hi, lo]
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float4 alo = *reinterpret_cast<const float4*>(cur + a_rd0 + h * 2048);
+            const float4 ahi = *reinterpret_cast<const float4*>(cur + a_rd1 + h * 2048);
+            unsigned w[2][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                split_h2_pair(f4_at(alo, ahi, 2 * j), f4_at(alo, ahi, 2 * j + 1), sc, w[0][j], w[1][j]);
+#pragma unroll
+            for (int p = 0; p < 2; ++p) af[h][p] = __builtin_bit_cast(f16x8, u32x4{w[p][0], w[p][1], w[p][2], w[p][3]});
+        }
+#pragma unroll
+        for (int ns = 0; ns < NS; ++ns) {
+            const f16x8 b0 = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(cur + b_rd + ns * 1024));
+            const f16x8 b1 = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4*>(cur + b_rd + ns * 1024 + BPL));
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                acc[h][ns] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[h][1], b0, acc[h][ns], 0, 0, 0);
+                acc[h][ns] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[h][0], b1, acc[h][ns], 0, 0, 0);
+                acc[h][ns] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[h][0], b0, acc[h][ns], 0, 0, 0);
+            }
+        }
+    };
+    for (int t = 0; t < nkt; ++t) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();  // stage t landed for every wave; stage t-1 fully read
+        asm volatile("" ::: "memory");
+        ktile(xsm + (t & 1) * STG, xsm + ((t + 1) & 1) * STG, t);
+    }
+
+    // epilogue: undo the row and column scales (powers of two: exact), then alpha / bias /
+    // addend / activation; per row the tile's sum of squares (16-lane reduction)
+    float cinv[NS], cb[NS];
+#pragma unroll
+    for (int ns = 0; ns < NS; ++ns) {
+        const int col = std::min(n0 + ns * 16 + lc, g.N - 1);
+        cinv[ns] = g.b_inv[col];
+        float b = 0.0f;
+        if (g.bias0) b = g.bias0[col];
+        if (g.bias1) b += g.bias1[col];
+        cb[ns] = b;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int64_t row = m0 + wm * 32 + h * 16 + 4 * lg + v;
+            const float rinv = 1.0f / g.a_scale[std::min<int64_t>(row, g.M - 1)];
+            float ssq = 0.0f, amx = 0.0f;
+            float addv[NS];
+            if (AMX && g.addend) {
+                const int64_t arow2 = std::min<int64_t>(row, g.M - 1);
+#pragma unroll
+                for (int ns = 0; ns < NS; ++ns) addv[ns] = g.addend[arow2 * g.ld_add + std::min(n0 + ns * 16 + lc, g.N - 1)];
+            }
+#pragma unroll
+            for (int ns = 0; ns < NS; ++ns) {
+                const int col = n0 + ns * 16 + lc;
+                if (col < g.N && row < g.M) {
+                    float x = (acc[h][ns][v] * rinv) * cinv[ns];
+                    if (g.alpha != 1.0f) x *= g.alpha;
+                    if (g.bias0 || g.bias1) x += cb[ns];
+                    if (g.addend) x += AMX ? addv[ns] : g.addend[row * g.ld_add + col];
+                    x = epi_apply(epi, x);
+                    g.C[row * g.ldc + col] = x;
+                    ssq = __fadd_rn(ssq, __fmul_rn(x, x));
+                    if constexpr (AMX) amx = fmaxf(amx, fabsf(x));
+                }
+            }
+            if constexpr (AMX) {
+#pragma unroll
+                for (int off = 8; off > 0; off >>= 1) amx = fmaxf(amx, __shfl_xor(amx, off));
+                if (lc == 0 && row < g.M) g.row_absmax[row * ROWSUMSQ_SLOTS + tn] = amx;
+            }
+            if (g.row_sumsq) {
+#pragma unroll
+                for (int off = 8; off > 0; off >>= 1) ssq += __shfl_xor(ssq, off);
+                if (lc == 0 && row < g.M) g.row_sumsq[row * ROWSUMSQ_SLOTS + tn] = ssq;
+            }
+        }
+}
+// M16 (WN == 1, K loop without PIPE): the same tile on v_mfma_f32_16x16x32_f16 — a wave's 32
+// rows as two 16-row halves, its columns as 16-column subtiles, one K = 32 MFMA step per
+// (half, subtile) and product (a_lo b_hi, a_hi b_lo, a_hi b_hi); the chip holds a higher clock
+// under the smaller shape (MI355X_MICROARCH.md DVFS, K10's +11%). The swizzles change so the
+// 16x16x32 fragment reads stay bank-conflict free (enumerated for ds_read_b128's lane groups):
+// A chunk c of row r at c ^ ((r & 7) ^ ((r >> 3) & 1)), B chunk c at c ^ ((4 - ((r >> 2) & 3)) & 3).
+// One MFMA sums 32 products instead of two sums of 16, so the bits differ from h2g's (within
+// the same error bound; tests hold M16 to the oracle, and M16 tilings to each other).
+template <bool DUAL, int WN, int BN, int NW, bool PIPE = false, bool AMX = false, bool GATE = false, bool M16 = false>
 __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgid) {
+    static_assert(!M16 || (WN == 1 && !PIPE && !GATE), "16x16x32 form: waves own whole tile rows, plain K loop");
     constexpr int BM = 32 * NW;        // 256 rows with 8 waves, 128 with 4
     constexpr int WMW = NW / WN;                // waves along M
     constexpr int RB = BM / WMW / 32, NB = BN / WN / 32;  // 32-row / 32-column blocks per wave
@@ -1323,8 +1447,8 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
     const int nk0 = g.K0 / 32;
     const int nkt = nk0 + (DUAL ? g.K1 / 32 : 0);
 
-    auto sw_a = [](int row) { return (row >> 1) & 7; };
-    auto sw_b = [](int row) { return (row >> 2) & 3; };
+    auto sw_a = [](int row) { return M16 ? ((row & 7) ^ ((row >> 3) & 1)) : ((row >> 1) & 7); };
+    auto sw_b = [](int row) { return M16 ? ((4 - ((row >> 2) & 3)) & 3) : ((row >> 2) & 3); };
 
     // 64 DMA pieces of 1 KB per stage, 8 per wave: A pieces 4 wave + j (8 rows x 128 B),
     // B pieces 4 wave + j of 32 (plane piece / 16, 16 rows x 64 B each)
@@ -1391,6 +1515,10 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
         asc1[rb] = g.a1_rowmul ? asc[rb] * g.a1_rowmul[r] : asc[rb];
     }
 
+    if constexpr (M16) {
+        h2w_m16_body<DUAL, BN, NW, AMX>(g, epi, m0, n0, tn, wm, lane, nk0, nkt, asc, asc1, issue);
+        return;
+    } else {
     f32x16 acc[RB][NB];
 #pragma unroll
     for (int i = 0; i < RB; ++i)
@@ -1636,6 +1764,7 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
             }
         }
     }
+    }  // !M16
 }
 
 // One tile per block (XCD-mapped tile order), or a persistent grid of one block per CU
@@ -1647,7 +1776,7 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
 // (g.help, aggrow::agg_help_run) — the GEMM's CU slots would otherwise idle beside the gather's
 // one block per CU until the chunk's gather ends.
 template <bool DUAL, int WN, int BN, int NW = 8, bool PIPE = false, bool HELP = false, bool AMX = false,
-          bool GATE = false>
+          bool GATE = false, bool M16 = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt_h2w(GemmArgs g, int epi) {
     if (g.queue) {
         extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
@@ -1660,7 +1789,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt
             const int64_t t = *s_t;
             __syncthreads();  // every wave holds t before the tile's DMA overwrites the word
             if (t >= cnt) break;
-            h2w_tile<DUAL, WN, BN, NW, PIPE, AMX, GATE>(g, epi, first + t);
+            h2w_tile<DUAL, WN, BN, NW, PIPE, AMX, GATE, M16>(g, epi, first + t);
             __syncthreads();  // LDS stages and s_t are reused by the next tile
         }
         // the loop ends after a barrier: the stage memory is free for the image windows
@@ -1668,7 +1797,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt
         return;
     }
     const int64_t nwg = g.nblocks, bid = blockIdx.x;
-    h2w_tile<DUAL, WN, BN, NW, PIPE, AMX, GATE>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
+    h2w_tile<DUAL, WN, BN, NW, PIPE, AMX, GATE, M16>(g, epi, xcd_first(nwg, bid % 8) + bid / 8);
     if constexpr (HELP) {
         extern __shared__ __attribute__((aligned(16))) unsigned char xsm_h[];
         __syncthreads();  // every wave is done with the tile's stages
@@ -1899,6 +2028,10 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 256, 8, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 8, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 8, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 8, false, true, false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 8, false, true, false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 8, false, false, false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
+            RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 192, 8, false, false, false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 256, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<false, 1, 256, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l256));
             RVX_HIP(hipFuncSetAttribute((const void*)gemm_nt_h2w<true, 1, 192, 8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, l192));
@@ -1938,6 +2071,8 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
             g.ld_gate_out = ep.ld_gate_out; g.gate_col0 = ep.gate_col0;
         }
         const dim3 wg((unsigned)wgrid), wb(wide_mode == 4 || wide_mode == 7 ? 256 : 512);
+        // the 256 x 192 tile on 16x16x32 MFMAs (RVX_GEMM_M16, read per call; tests cover both)
+        const bool m16 = env_int("RVX_GEMM_M16", 0) != 0;
         // RVX_GEMM_WIDE=1: waves 2 (M) x 4 (N), 128 x 64 each; 2: waves 8 x 1, 32 x 256 each
         // (A converted once per row instead of by four waves)
         if (gate) {
@@ -1961,6 +2096,13 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
         } else if (wide_mode == 4) {
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 4>), wg, wb, wlds, g, ep.epi);
             else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 4>), wg, wb, wlds, g, ep.epi);
+        } else if (wide_mode == 3 && m16 && ep.help && ep.help->n > 0) {
+            g.help = *ep.help;
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 8, false, true, false, false, true>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 8, false, true, false, false, true>), wg, wb, wlds, g, ep.epi);
+        } else if (wide_mode == 3 && m16) {
+            if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 8, false, false, false, false, true>), wg, wb, wlds, g, ep.epi);
+            else RVX_LAUNCH(t, (gemm_nt_h2w<false, 1, 192, 8, false, false, false, false, true>), wg, wb, wlds, g, ep.epi);
         } else if (wide_mode == 3 && ep.help && ep.help->n > 0) {
             g.help = *ep.help;
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 1, 192, 8, false, true>), wg, wb, wlds, g, ep.epi);

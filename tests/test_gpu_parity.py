@@ -987,6 +987,7 @@ def test_graphsage_wide_gemm_bits(monkeypatch, in_f, out_f, n, deg, chunks, wide
     layer = rv.GraphSAGELayer(in_f, out_f, num_samples=max(deg, 1))
     if chunks:
         monkeypatch.setenv("RVX_SAGE_CHUNKS", str(chunks))
+    monkeypatch.setenv("RVX_GEMM_M16", "0")  # the 32x32x16 forms share h2g's summation order
     monkeypatch.setenv("RVX_GEMM_WIDE", "0")
     y0 = layer.forward_graph(x, g)
     monkeypatch.setenv("RVX_GEMM_WIDE", wide)
@@ -994,6 +995,34 @@ def test_graphsage_wide_gemm_bits(monkeypatch, in_f, out_f, n, deg, chunks, wide
     assert np.array_equal(y0, y1)
     if n <= 1000:
         assert_close(y1, O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0))
+
+
+@pytest.mark.parametrize("in_f,out_f,n,deg,chunks", [(768, 768, 600, 9, 0), (96, 232, 1000, 5, 0),
+                                                     (64, 130, 257, 0, 0), (32, 32, 129, 3, 0),
+                                                     (768, 768, 40000, 7, 2), (128, 512, 40000, 4, 2)])
+def test_graphsage_m16_gemm(monkeypatch, in_f, out_f, n, deg, chunks):
+    """The 256 x 192 tile on 16x16x32 MFMAs (RVX_GEMM_M16=1; one MFMA sums 32 products, so
+    its bits are its own): within 1e-5 of the oracle on ragged M and N, all-empty
+    neighbourhoods and the chunked pipeline, and the helped dynamic gather gives the same
+    bits as the static one on it (same GEMM, same arithmetic)."""
+    x = O.fill_uniform(n * in_f, 90 + n).reshape(n, in_f)
+    rp, col = O.random_csr(n, deg, 91)
+    g = rv.Graph.from_csr(rp, col)
+    layer = rv.GraphSAGELayer(in_f, out_f, num_samples=max(deg, 1))
+    if chunks:
+        monkeypatch.setenv("RVX_SAGE_CHUNKS", str(chunks))
+    else:
+        monkeypatch.setenv("RVX_GEMM_WIDE", "3")  # the one-launch layer takes the standalone tile otherwise
+    monkeypatch.setenv("RVX_GEMM_M16", "1")
+    y1 = layer.forward_graph(x, g)
+    rows = min(n, 1000)
+    ref = O.sage_forward(x, rp, col, O.sage_init(in_f, out_f, 0), O.sage_init(in_f, out_f, 1000), 0,
+                         rows=(0, rows))
+    assert_close(y1[:rows], ref)
+    if chunks:
+        monkeypatch.setenv("RVX_SAGE_HELP", "0")
+        y2 = layer.forward_graph(x, g)
+        assert np.array_equal(y1, y2)
 
 
 @pytest.mark.parametrize("wide", ["1", "2", "3", "4", "5", "6", "7"])
