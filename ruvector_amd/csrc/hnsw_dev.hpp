@@ -159,11 +159,54 @@ __device__ __forceinline__ float wd_chunk(float acc, const float* qs, int c, int
 // in flight, everything older (this chunk) has landed — and before refilling a
 // stage it waits lgkmcnt(0) so the stage's reads have returned. The asm
 // statements clobber memory, which also keeps the DMA groups in issue order.
+// vmcnt(8 * G): at most G chunk groups (8 DMAs each) still in flight
+template <int G>
+__device__ __forceinline__ void wd_wait_groups() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * G) : "memory");
+}
+// the ring's tail: `left` (< NST - 1, wave-uniform) younger groups may stay in flight
+template <int NST>
+__device__ __forceinline__ void wd_wait_left(int left) {
+    static_assert(NST <= 8, "vmcnt holds at most 63 outstanding loads");
+    switch (left) {
+        case 0: wd_wait_groups<0>(); break;
+        case 1: wd_wait_groups<1>(); break;
+        case 2: wd_wait_groups<2>(); break;
+        case 3: wd_wait_groups<3>(); break;
+        case 4: wd_wait_groups<4>(); break;
+        case 5: wd_wait_groups<5>(); break;
+        default: wd_wait_groups<6>(); break;
+    }
+}
+
 template <int METRIC, int NST = 2>
 __device__ __forceinline__ float wd_run(const float* __restrict__ x, int d, const float* qs, const int (&rid)[8], int lane,
                                         unsigned char* s0, unsigned char* s1) {
     const int nch = d / WD_CH;
     float acc = 0.0f;
+    if constexpr (NST >= 3) {
+        // a ring of NST stages (s0 .. s0 + (NST-1) * WD_STAGE): NST - 1 chunks in flight
+        // while one accumulates — for waves alone on their CU (large ef: R holds most
+        // of the LDS), where no other wave hides a chunk's memory round trip
+        int fill = 0;  // stage the next fill lands in
+        for (; fill < NST - 1 && fill < nch; ++fill) wd_fill<METRIC>(x, d, rid, fill, lane, s0 + fill * WD_STAGE);
+        int cur = 0;  // stage chunk c is in
+        for (int c = 0; c < nch; ++c) {
+            const int nx = c + NST - 1;
+            if (nx < nch) {
+                // stage `fill` held chunk c - 1, whose reads returned (lgkmcnt(0) below)
+                wd_fill<METRIC>(x, d, rid, nx, lane, s0 + fill * WD_STAGE);
+                fill = fill + 1 == NST ? 0 : fill + 1;
+                wd_wait_groups<NST - 1>();
+            } else {
+                wd_wait_left<NST>(nch - 1 - c);
+            }
+            acc = wd_chunk<METRIC>(acc, qs, c, lane, s0 + cur * WD_STAGE);
+            cur = cur + 1 == NST ? 0 : cur + 1;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        return acc;
+    }
     if constexpr (NST == 1) {
         for (int c = 0; c < nch; ++c) {
             wd_fill<METRIC>(x, d, rid, c, lane, s0);
@@ -477,27 +520,45 @@ __device__ __forceinline__ int rank_in_r(const float* rd, const int* ri, int n, 
 // R entry j moves right by #{batch entries ranked <= j}, a constant over every
 // 64-entry chunk that holds no batch rank, so only chunks at or after the
 // first rank move and each costs one ballot. Returns the first batch rank
-// (entries before it did not move).
+// (entries before it did not move). Chunks move in groups of MG walking back:
+// a group is read whole, then written (entries only move right, so a group's
+// writes land at or above its own lowest entry and never on the next group's),
+// which keeps MG reads in flight instead of one memory round trip per chunk —
+// at ef 12288 a merge walks up to 192 chunks.
+constexpr int MERGE_GROUP = 8;
 __device__ __forceinline__ int merge_into_r(float* rd, int* ri, int n, const float* sd, const int* si, int na, int nkeep,
                                             int lane) {
     float bd = 0.f; int bi = 0, rk = INT_MAX;
     if (lane < na) { bd = sd[lane]; bi = si[lane]; rk = rank_in_r(rd, ri, n, bd, bi); }
     const int first = __shfl(rk, 0);
     __builtin_amdgcn_wave_barrier();
-    for (int base = ((n - 1) / 64) * 64; base >= 0 && base + 63 >= first; base -= 64) {
-        const int j = base + lane;
-        // batch entries ranked at or before the chunk, and those inside it
-        int shift = __popcll(__ballot(lane < na && rk <= base));
-        unsigned long long in = __ballot(lane < na && rk > base && rk <= base + 63);
-        while (in) {
-            const int b = __ffsll((long long)in) - 1;
-            in &= in - 1;
-            shift += (j >= __shfl(rk, b)) ? 1 : 0;
+    for (int top = ((n - 1) / 64) * 64; top >= 0 && top + 63 >= first; top -= 64 * MERGE_GROUP) {
+        float vd[MERGE_GROUP];
+        int vi[MERGE_GROUP], sh[MERGE_GROUP];
+#pragma unroll
+        for (int g = 0; g < MERGE_GROUP; ++g) {
+            const int base = top - 64 * g;
+            const int j = base + lane;
+            sh[g] = -1;
+            vd[g] = 0.f; vi[g] = 0;
+            if (base >= 0 && base + 63 >= first) {  // wave-uniform
+                // batch entries ranked at or before the chunk, and those inside it
+                int shift = __popcll(__ballot(lane < na && rk <= base));
+                unsigned long long in = __ballot(lane < na && rk > base && rk <= base + 63);
+                while (in) {
+                    const int b = __ffsll((long long)in) - 1;
+                    in &= in - 1;
+                    shift += (j >= __shfl(rk, b)) ? 1 : 0;
+                }
+                if (j < n) { vd[g] = rd[j]; vi[g] = ri[j]; sh[g] = shift; }
+            }
         }
-        float vd = 0.f; int vi = 0;
-        if (j < n) { vd = rd[j]; vi = ri[j]; }
         __builtin_amdgcn_wave_barrier();
-        if (j < n && j + shift < nkeep) { rd[j + shift] = vd; ri[j + shift] = vi; }
+#pragma unroll
+        for (int g = 0; g < MERGE_GROUP; ++g) {
+            const int j = top - 64 * g + lane;
+            if (sh[g] >= 0 && j + sh[g] < nkeep) { rd[j + sh[g]] = vd[g]; ri[j + sh[g]] = vi[g]; }
+        }
         __builtin_amdgcn_wave_barrier();
     }
     if (lane < na && lane + rk < nkeep) { rd[lane + rk] = bd; ri[lane + rk] = bi; }

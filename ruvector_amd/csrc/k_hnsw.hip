@@ -249,20 +249,41 @@ template <int METRIC>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_hnsw_search_short(SearchArgs a) {
     search_body<METRIC, 4>(a);
 }
-// Wide searches over LDS-staged rows (coop, ef >= 1024): one distance stage.
-template <int METRIC>
-__global__ __launch_bounds__(64) void k_hnsw_search_wide(SearchArgs a) {
-    search_body<METRIC, ROW_BATCH, 1>(a);
+// LDS-staged rows (coop) with NST distance stages other than the default two:
+// 1 past ef 1024 (R costs most of the LDS, more waves fit a CU), a deeper ring
+// where one wave is alone on its CU (hnsw_nst).
+template <int METRIC, int NST>
+__global__ __launch_bounds__(64) void k_hnsw_search_st(SearchArgs a) {
+    search_body<METRIC, ROW_BATCH, NST>(a);
 }
 // ef past one wave's LDS: R in HBM (one distance stage when coop).
-template <int METRIC>
+template <int METRIC, int NST = 1>
 __global__ __launch_bounds__(64) void k_hnsw_search_rg(SearchArgs a) {
-    search_body<METRIC, ROW_BATCH, 1, true>(a);
+    search_body<METRIC, ROW_BATCH, NST, true>(a);
 }
 
 }  // namespace
 
 SearchStats g_search_stats;
+
+namespace {
+template <int NST>
+void set_st_attr() {
+    RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_st<RVX_METRIC_L2, NST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_st<RVX_METRIC_COSINE, NST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_st<RVX_METRIC_DOT, NST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_st<RVX_METRIC_L1, NST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+}
+template <int NST>
+void launch_st(const char* t, int metric, int nslots, size_t lds, const SearchArgs& a) {
+    switch (metric) {
+        case RVX_METRIC_L2: RVX_LAUNCH(t, (k_hnsw_search_st<RVX_METRIC_L2, NST>), dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_COSINE: RVX_LAUNCH(t, (k_hnsw_search_st<RVX_METRIC_COSINE, NST>), dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_DOT: RVX_LAUNCH(t, (k_hnsw_search_st<RVX_METRIC_DOT, NST>), dim3(nslots), dim3(64), lds, a); break;
+        default: RVX_LAUNCH(t, (k_hnsw_search_st<RVX_METRIC_L1, NST>), dim3(nslots), dim3(64), lds, a); break;
+    }
+}
+}  // namespace
 
 bool hnsw_coop(int metric, int d, int64_t rows) {
     // 0 off, 1 auto (tables past the per-CU translation reach), 2 always
@@ -272,16 +293,34 @@ bool hnsw_coop(int metric, int d, int64_t rows) {
     return mode == 2 || rows * (int64_t)d * 4 >= min_bytes;
 }
 
-bool hnsw_wide_ef(bool coop, int ef) { return coop && ef >= 1024 && env_int("RVX_HNSW_WIDE", 1); }  // read per call
+namespace {
+size_t search_lds_nst(int d, int ef, int nst) {
+    const int dq = (d + 3) & ~3;
+    return (size_t)wd_lds(nst) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 8;
+}
+}  // namespace
+
+// Distance stages per wave of the LDS-staged (coop) search. RVX_HNSW_NST forces
+// 1, 2, 3, 4 or 6 (read per call: tests and A/Bs); by default 2, and 1 from ef
+// 1024 (RVX_HNSW_WIDE=0 keeps 2) where one stage more would cost a wave per CU.
+int hnsw_nst(bool coop, int d, int ef) {
+    if (!coop) return 0;
+    const int f = env_int("RVX_HNSW_NST", 0);
+    if ((f == 1 || f == 2 || f == 3 || f == 4 || f == 6) && search_lds_nst(d, ef, f) <= 160 * 1024) return f;
+    return ef >= 1024 && env_int("RVX_HNSW_WIDE", 1) ? 1 : 2;
+}
 
 size_t hnsw_search_lds(int d, int ef, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)wd_lds(hnsw_wide_ef(coop, ef) ? 1 : 2) : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 8;
+    return (coop ? (size_t)wd_lds(hnsw_nst(coop, d, ef)) : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 8;
 }
 // LDS of the RG kernel: distance stage + query + admitted batch (R is in HBM)
+// distance stages of the RG kernel, 2 unless RVX_HNSW_RG_NST=1 (read per call): with R out
+// of LDS the second stage costs no wave (ef 12288 above: 1134 -> 1266 QPS)
+int hnsw_rg_nst() { return env_int("RVX_HNSW_RG_NST", 2) == 1 ? 1 : 2; }
 size_t hnsw_search_lds_rg(int d, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)wd_lds(1) : 0) + (size_t)dq * 4 + 64 * 8;
+    return (coop ? (size_t)wd_lds(hnsw_rg_nst()) : 0) + (size_t)dq * 4 + 64 * 8;
 }
 
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
@@ -290,9 +329,16 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     if (nq <= 0) return;
     RVX_REQUIRE(ef >= 1 && ef <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER,
                 "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
-    // R in LDS when one wave's 160 KB hold it, else in HBM (RVX_HNSW_RG=1 forces, tests)
+    // R in LDS when one wave's 160 KB hold it, else in HBM. The LDS-staged (coop) search also
+    // takes the HBM R once an LDS R would leave fewer than 3 waves per CU: each expansion is a
+    // chain of dependent memory round trips, so waves in flight, not bytes, bound it (10M x 768
+    // M 32, 1024 queries: ef 8192 1573 -> 2232 QPS, 12288 495 -> 1266, 16384 339 -> 827; ef 3200,
+    // 4 waves per CU with R in LDS, stays: 8486 vs 7331; scripts/exp/exp_hnsw_nst.py).
+    // RVX_HNSW_RG: 1 always, 0 only past the LDS, unset auto (read per call: tests force both)
     const bool coop0 = hnsw_coop(metric, d, g.n);
-    const bool rg = hnsw_search_lds(d, ef, coop0) > 160 * 1024 || env_int("RVX_HNSW_RG", 0) != 0;
+    const int rg_mode = env_int("RVX_HNSW_RG", -1);
+    const size_t lds_r = hnsw_search_lds(d, ef, coop0);
+    const bool rg = lds_r > 160 * 1024 || rg_mode == 1 || (rg_mode < 0 && coop0 && lds_r * 3 > 160 * 1024);
     const unsigned vcap = visited_capacity(ef, g.max_deg);
     // visited set: a per-slot bitmap over all n nodes (cleared per query by its
     // wave: no launch-wide memset, no probing, n/8 bytes touched) when at least
@@ -354,10 +400,10 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_short<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_short<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_short<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_wide<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_wide<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_wide<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_wide<RVX_METRIC_L1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        set_st_attr<1>();
+        set_st_attr<3>();
+        set_st_attr<4>();
+        set_st_attr<6>();
         RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_rg<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_rg<RVX_METRIC_COSINE>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_rg<RVX_METRIC_DOT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -368,7 +414,14 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     }
     const char* t = tag ? tag : "hnsw_search";
     const bool short_rows = !coop && d <= 256 && env_int("RVX_HNSW_SHORT", 1);  // read per call: tests cover both
-    if (rg) {
+    if (rg && coop && hnsw_rg_nst() == 2) {
+        switch (metric) {
+            case RVX_METRIC_L2: RVX_LAUNCH(t, (k_hnsw_search_rg<RVX_METRIC_L2, 2>), dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_COSINE: RVX_LAUNCH(t, (k_hnsw_search_rg<RVX_METRIC_COSINE, 2>), dim3(nslots), dim3(64), lds, a); break;
+            case RVX_METRIC_DOT: RVX_LAUNCH(t, (k_hnsw_search_rg<RVX_METRIC_DOT, 2>), dim3(nslots), dim3(64), lds, a); break;
+            default: RVX_LAUNCH(t, (k_hnsw_search_rg<RVX_METRIC_L1, 2>), dim3(nslots), dim3(64), lds, a); break;
+        }
+    } else if (rg) {
         switch (metric) {
             case RVX_METRIC_L2: RVX_LAUNCH(t, k_hnsw_search_rg<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
             case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_hnsw_search_rg<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
@@ -385,12 +438,12 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
             case RVX_METRIC_DOT: RVX_LAUNCH(t, k_hnsw_search_short<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, a); break;
             default: RVX_LAUNCH(t, k_hnsw_search_short<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
         }
-    } else if (hnsw_wide_ef(coop, ef)) {  // coop is never set for the Poincaré metrics
-        switch (metric) {
-            case RVX_METRIC_L2: RVX_LAUNCH(t, k_hnsw_search_wide<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
-            case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_hnsw_search_wide<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
-            case RVX_METRIC_DOT: RVX_LAUNCH(t, k_hnsw_search_wide<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, a); break;
-            default: RVX_LAUNCH(t, k_hnsw_search_wide<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
+    } else if (coop && hnsw_nst(coop, d, ef) != 2) {  // coop is never set for the Poincaré metrics
+        switch (hnsw_nst(coop, d, ef)) {
+            case 1: launch_st<1>(t, metric, nslots, lds, a); break;
+            case 3: launch_st<3>(t, metric, nslots, lds, a); break;
+            case 4: launch_st<4>(t, metric, nslots, lds, a); break;
+            default: launch_st<6>(t, metric, nslots, lds, a); break;
         }
     } else
     switch (metric) {

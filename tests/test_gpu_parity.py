@@ -187,6 +187,50 @@ def test_hnsw_search_large_ef_bit_exact(monkeypatch, coop, wide):
         assert np.array_equal(dist, rd)
 
 
+_RING_PAIRS = {}
+
+
+@pytest.mark.parametrize("nst", ["1", "2", "3", "4", "6"])
+@pytest.mark.parametrize("d,metric", [(32, "l2"), (96, "cosine"), (224, "l2")])
+def test_hnsw_search_stage_ring_bit_exact(monkeypatch, nst, d, metric):
+    # LDS-staged distances with 1..6 stages per wave (RVX_HNSW_NST; 3+ is the ring of
+    # hnsw_dev.hpp wd_run): 1, 3 and 7 chunks of 32 dims, fewer chunks than stages included
+    monkeypatch.setenv("RVX_HNSW_COOP", "2")
+    monkeypatch.setenv("RVX_HNSW_NST", nst)
+    monkeypatch.setenv("RVX_HNSW_RG", "0")  # R in LDS (the auto rule moves it to HBM at 3+ stages here)
+    if (d, metric) not in _RING_PAIRS:
+        _RING_PAIRS[(d, metric)] = _hnsw_pair(3000, d, metric, 8, 60, 13)
+    x, h, g, idx = _RING_PAIRS[(d, metric)]
+    q = O.fill_uniform(48 * d, 14).reshape(48, d)
+    for k, ef in ((10, 64), (20, 1200)):
+        ids, dist, cnt = idx.search_array(q, k, ef)
+        rids, rd, rc = h.search(q, k, ef)
+        assert np.array_equal(cnt, rc)
+        assert np.array_equal(ids.astype(np.int64)[:, :k], rids)
+        assert np.array_equal(dist, rd)
+
+
+@pytest.mark.parametrize("rg_nst", ["1", "2"])
+@pytest.mark.parametrize("d,metric", [(32, "l2"), (224, "l2"), (96, "cosine")])
+def test_hnsw_search_auto_hbm_r_coop_bit_exact(monkeypatch, rg_nst, d, metric):
+    # LDS-staged distances at an ef whose LDS R would leave < 3 waves per CU: the search
+    # takes the HBM-resident R by itself (k_hnsw.hip hnsw_search), with 1 or 2 stages
+    monkeypatch.setenv("RVX_HNSW_COOP", "2")
+    monkeypatch.delenv("RVX_HNSW_RG", raising=False)
+    monkeypatch.setenv("RVX_HNSW_RG_NST", rg_nst)
+    if (d, metric) not in _RING_PAIRS:
+        _RING_PAIRS[(d, metric)] = _hnsw_pair(3000, d, metric, 8, 60, 13)
+    x, h, g, idx = _RING_PAIRS[(d, metric)]
+    q = O.fill_uniform(48 * d, 15).reshape(48, d)
+    for k, ef in ((10, 6000), (300, 2900)):
+        ids, dist, cnt = idx.search_array(q, k, ef)
+        assert rv.hnsw_last_search_stats()["slots"] >= 1
+        rids, rd, rc = h.search(q, k, ef)
+        assert np.array_equal(cnt, rc)
+        assert np.array_equal(ids.astype(np.int64)[:, :k], rids)
+        assert np.array_equal(dist, rd)
+
+
 def test_hnsw_search_tie_heavy_bit_exact():
     # 3000 points on 12 distinct vectors: hundreds of exact distance ties at R's
     # farthest (the round-1 candidate list overflowed here and raised RVX_ERR_INDEX);
