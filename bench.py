@@ -126,7 +126,7 @@ def main():
     if rank == 0:
         _start_progress_thread()
     import ruvector_amd as rv
-    from ruvector_amd.shard import REDUCE_MAX, ShardPlan, comm_from_env
+    from ruvector_amd.shard import REDUCE_MAX, ShardPlan, comm_from_env, comm_traffic
 
     # host transport: ranks may outnumber the GPUs and share them
     rv.set_device(local % max(rv.device_count(), 1) if a.transport == "host" else local)
@@ -192,6 +192,7 @@ def main():
         step()
     barrier()
     prof = rv.Profiler()
+    traffic0 = comm_traffic(comm) if comm is not None else (0, 0)
     with prof:
         barrier()
         t0 = time.perf_counter()
@@ -202,6 +203,7 @@ def main():
         barrier()
     elapsed = t1 - t0
     kern = prof.summary()
+    traffic = tuple(v - v0 for v, v0 in zip(comm_traffic(comm), traffic0)) if comm is not None else (0, 0)
     if comm is not None:
         elapsed = comm.allreduce([elapsed], REDUCE_MAX)[0]
 
@@ -291,7 +293,7 @@ def main():
     if comm is not None:
         line["comm"] = {"transport": a.transport, "forced": forced,
                         "self_p2p_rounds": kern.get("halo_exchange", {}).get("launches", 0) if forced else 0}
-        line["multi_gpu"] = exchange_report(a, kern, comm, world, rank, offsets, d, layers)
+        line["multi_gpu"] = exchange_report(a, kern, comm, world, rank, offsets, d, layers, traffic)
         line["multi_gpu"]["transport"] = ("rccl (p2p over xGMI)" if a.transport == "rccl" else
                                           "host-staged (host memory + stdlib TCP sockets)")
         line["parity"] = multi_rank_check(a, comm, rank, world, offsets, x, tables, invs, n_tot, d, deg, layers)
@@ -384,11 +386,14 @@ def multi_rank_check(a, comm, rank, world, offsets, x, tables, invs, n_tot, d, d
                        "exchanged layer-1 table (and 1/|y|) has the same checksum"}
 
 
-def exchange_report(a, kern, comm, world, rank, offsets, d, layers):
-    """Per-rank view of the halo exchange (the 8-GPU bottleneck candidate): bytes this rank
-    sends / receives per exchanged layer, the transfer stream's exchange time and the
-    exposed tail the compute stream waits for (rvx profiler tag exchange_wait: from the
-    last chunk's compute to the last round's arrival), per layer, for every rank."""
+def exchange_report(a, kern, comm, world, rank, offsets, d, layers, traffic):
+    """Per-rank view of the halo exchange (the 8-GPU bottleneck candidate): bytes each rank
+    handed to / took from the transport per exchanged layer over the timed steps, as the
+    library counted them (rvx_comm_traffic: the compact row records, their counts, 1/|y| and
+    the dense rows of records past the slot), beside the dense-row bytes; the transfer
+    stream's exchange time and the exposed tail the compute stream waits for (rvx profiler
+    tag exchange_wait: from the last chunk's compute to the last round's arrival), per layer,
+    for every rank."""
     exchanged = max(layers - 1, 0)
     n_loc = int(offsets[rank + 1] - offsets[rank])
     n_tot = int(offsets[-1])
@@ -404,9 +409,20 @@ def exchange_report(a, kern, comm, world, rank, offsets, d, layers):
 
     wait = per_rank(ms_per_layer("exchange_wait"))
     xfer = per_rank(ms_per_layer("halo_exchange"))
+    per_layer = max(a.steps * exchanged, 1)
+    sent = per_rank(traffic[0] / per_layer)
+    recv = per_rank(traffic[1] / per_layer)
+    dense_sent = [int(offsets[p + 1] - offsets[p]) * (d * 4 + 4) * (world - 1) for p in range(world)]
     return {"exchanged_layers_per_step": exchanged,
-            "bytes_sent_per_layer": [int(offsets[p + 1] - offsets[p]) * d * 4 * (world - 1) for p in range(world)],
-            "bytes_recv_per_layer": [(n_tot - int(offsets[p + 1] - offsets[p])) * d * 4 for p in range(world)],
+            "bytes_sent_per_layer": [int(v) for v in sent],
+            "bytes_recv_per_layer": [int(v) for v in recv],
+            "dense_bytes_sent_per_layer": dense_sent,
+            "sent_vs_dense": [round(s_ / max(d_, 1), 4) for s_, d_ in zip(sent, dense_sent)],
+            "format": ("compact ReLU-sparse row records (bitmap + values other than +0.0, back to back within a "
+                       "per-round byte budget agreed from chunk 0, expanded bit for bit on arrival; rows past the "
+                       "budget sent dense after the rounds)"
+                       if os.environ.get("RVX_XCHG_IMAGE", "1") != "0" and 512 < d <= 768 and d % 4 == 0
+                       else "dense rows"),
             "exchange_ms_per_layer": [round(v, 3) for v in xfer],
             "exchange_wait_ms_per_layer": [round(v, 3) for v in wait],
             "note": "exchange_ms: transfer-stream time of the chunked RCCL p2p rounds (overlapped with compute); "

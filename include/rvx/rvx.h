@@ -634,6 +634,10 @@ rvx_status rvx_comm_allreduce_f64(rvx_comm* c, double* values, int32_t count, in
 typedef int32_t (*rvx_host_exchange_fn)(void* user, const void* send, int64_t send_bytes, void* const* recv,
                                         const int64_t* recv_bytes);
 rvx_status rvx_comm_init_host(int32_t nranks, int32_t rank, rvx_host_exchange_fn fn, void* user, rvx_comm** out);
+/* Payload bytes this rank has handed to the transport (sent: a row block shipped to k peers
+ * counts k times) and taken from it, over every exchange, broadcast and all-gather since the
+ * communicator was made (an rvx extension: the exchange's measured bytes for bench reports). */
+rvx_status rvx_comm_traffic(const rvx_comm* c, int64_t* sent, int64_t* recv);
 
 /* The p2p round plan of the node-range exchange that the
  * *_forward_exchange entry points run: kind 0 = GraphSAGE (rvx_sage_forward_exchange:

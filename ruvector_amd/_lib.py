@@ -210,6 +210,7 @@ SIGNATURES = {
     "rvx_comm_allgather_f32": (None, [P, P, I64, P]),
     "rvx_comm_allreduce_max_f64": (None, [P, C.POINTER(C.c_double)]),
     "rvx_comm_allreduce_f64": (None, [P, C.POINTER(C.c_double), I32, I32]),
+    "rvx_comm_traffic": (None, [P, PI64, PI64]),
 }
 
 _lib = None

@@ -14,6 +14,7 @@ struct rvx_comm {
     int nranks = 0, rank = 0;
     rvx_host_exchange_fn host_fn = nullptr;  // host-staged transport (rvx_comm_init_host)
     void* host_user = nullptr;
+    int64_t sent = 0, recv = 0;  // payload bytes this rank handed to / took from the transport (rvx_comm_traffic)
 };
 
 #define RVX_NCCL(expr)                                                                         \
@@ -75,6 +76,8 @@ void comm_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int6
         // send/recv pair to itself), lands in a staging buffer and is copied over the rows
         const int64_t cnt = rows[0] * row_elems;
         if (cnt <= 0) return;
+        c->sent += cnt * 4;
+        c->recv += cnt * 4;
         DevMem stage(cnt * 4);
         RVX_NCCL(ncclGroupStart());
         RVX_NCCL(ncclSend(table + r0[0] * row_elems, (size_t)cnt, ncclFloat32, 0, c->comm, s));
@@ -85,6 +88,10 @@ void comm_exchange_rows(rvx_comm* c, float* table, int64_t row_elems, const int6
         return;
     }
     if (!c || c->nranks <= 1) return;
+    for (int p = 0; p < c->nranks; ++p) {
+        if (p == c->rank) c->sent += rows[p] * row_elems * 4 * (c->nranks - 1);
+        else c->recv += rows[p] * row_elems * 4;
+    }
     if (c->host_fn) {
         host_exchange_rows(c, table, row_elems, r0, rows, s);
         return;
@@ -109,6 +116,8 @@ void comm_broadcast_bytes(rvx_comm* c, void* buf, int64_t bytes, int root, hipSt
     }
     if (!c || c->nranks <= 1 || bytes <= 0) return;
     RVX_REQUIRE(root >= 0 && root < c->nranks, RVX_ERR_INVALID_PARAMETER, "bad broadcast root");
+    if (c->rank == root) c->sent += bytes * (c->nranks - 1);
+    else c->recv += bytes;
     if (!c->host_fn) {
         RVX_NCCL(ncclBroadcast(buf, buf, (size_t)bytes, ncclUint8, root, c->comm, s));
         return;
@@ -141,6 +150,8 @@ void comm_allgather_bytes(rvx_comm* c, const void* send, void* recv, int64_t byt
         if (recv != send) RVX_HIP(hipMemcpyAsync(recv, send, (size_t)bytes, hipMemcpyDeviceToDevice, s));
         return;
     }
+    c->sent += bytes * (w - 1);
+    c->recv += bytes * (w - 1);
     if (!c->host_fn) {
         RVX_NCCL(ncclAllGather(send, recv, (size_t)bytes, ncclUint8, c->comm, s));
         return;
@@ -168,6 +179,14 @@ void comm_allgather_bytes(rvx_comm* c, const void* send, void* recv, int64_t byt
 }  // namespace rvx
 
 extern "C" {
+
+rvx_status rvx_comm_traffic(const rvx_comm* c, int64_t* sent, int64_t* recv) {
+    return guard([&] {
+        RVX_REQUIRE(c && sent && recv, RVX_ERR_INVALID_PARAMETER, "null argument");
+        *sent = c->sent;
+        *recv = c->recv;
+    });
+}
 
 rvx_status rvx_comm_unique_id(uint8_t id[RVX_COMM_ID_BYTES]) {
     return guard([&] {

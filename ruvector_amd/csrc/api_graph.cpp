@@ -763,6 +763,11 @@ rvx_status rvx_row_image_pack(const rvx_buffer* x, int64_t n_total, int64_t r0, 
     });
 }
 
+namespace {
+// the broadcast buffer of the dense-row pass: cnt ids (int64), then their rows
+float* ids_rows(int64_t* ids, int64_t cnt) { return reinterpret_cast<float*>(ids + cnt); }
+}  // namespace
+
 rvx_status rvx_sage_forward_exchange3(const rvx_sage_layer* l, const rvx_graph* g, rvx_buffer* x_full,
                                       const rvx_buffer* x_rowmul, rvx_buffer* x_image, rvx_buffer* y_full,
                                       rvx_buffer* y_rowinv, rvx_buffer* y_image, const int64_t* offsets,
@@ -821,19 +826,136 @@ rvx_status rvx_sage_forward_exchange3(const rvx_sage_layer* l, const rvx_graph* 
         const int chunks = (int)plan.size();
         Device& d = device();
         hipEvent_t* ev = pipeline_events(SAGE_PIPE_EVENTS(chunks) + chunks + 1) + SAGE_PIPE_EVENTS(chunks);  // after sage_forward_dev's
+        // Compact records (kernels.hpp rows_xchg_pack): a layer's output rows are ReLU-sparse
+        // (graphsage.rs:172-176), so a round's rows travel as their image records — bitmap + the
+        // values other than +0.0 — back to back, with a u32 count per row, and are expanded
+        // back into the dense rows bit for bit on arrival. RCCL p2p needs both sides to know a
+        // message's size, with no host wait per round: each rank's round block gets a byte
+        // budget of rows x (bytes per row), the rate agreed once per call from chunk 0 (every
+        // rank's mean record bytes over its chunk-0 rows, all-gathered, the largest + 2% +
+        // 16 B; one host wait, at the first round). Records sit at the prefix sums of their
+        // sizes, which the receiver recomputes from the counts; rows whose record ends past
+        // the budget (or holds more than IMG_CAP values) travel dense after the rounds (counts
+        // all-gathered, then each owner's broadcast). Where records would save less than 15%
+        // of a dense row the call exchanges dense rows. At 768 dims with about half the values
+        // +0.0: ~1,700 + 4 B per 3,072-B row. RVX_XCHG_IMAGE=0 exchanges dense rows;
+        // RVX_XCHG_ROW_BYTES fixes the rate (tests force overflows). Every rank decides alike.
+        const bool xallow = row_image_ok(l->out) && env_int("RVX_XCHG_IMAGE", 1) != 0 && ((uintptr_t)y & 15) == 0;
+        const int rate_env = env_int("RVX_XCHG_ROW_BYTES", 0);
+        double rate = 0.0;  // budget bytes per row, decided in round 0
+        bool xrec = false;
+        int64_t round_rows = 0;  // staging rows per rank and round (the largest block of any round)
+        for (const ExchangeRound& r : plan)
+            for (int p = 0; p < world; ++p) round_rows = std::max(round_rows, r.rows[p]);
+        unsigned char* xs = nullptr;
+        uint32_t* xcnt = nullptr;
+        uint64_t* xoff = nullptr;
+        int64_t* ovf_ids = nullptr;
+        // [0] own overflow rows, [1 .. world] all-gathered; [world + 1], [world + 2] own chunk-0
+        // record bytes and rows, [world + 3 ..] all-gathered pairs
+        unsigned long long* ctr = nullptr;
+        void* scan_tmp = nullptr;
+        size_t scan_bytes = 0;
+        std::vector<int64_t> st(world), st16(world), blk16(world);  // staging: rank p's block at p * round_rows
+        for (int p = 0; p < world; ++p) {
+            st[p] = p * round_rows;
+            st16[p] = p * round_rows * (IMG_SLOT / 16);
+        }
+        if (xallow) {  // (every scratch slot taken before the pipeline queues work that could use it)
+            xs = (unsigned char*)scratch_bytes("sage_xchg_rec", (int64_t)world * round_rows * IMG_SLOT);
+            xcnt = (uint32_t*)scratch_bytes("sage_xchg_cnt", (int64_t)world * round_rows * 4);
+            xoff = (uint64_t*)scratch_bytes("sage_xchg_off", (int64_t)world * round_rows * 8);
+            ovf_ids = (int64_t*)scratch_bytes("sage_xchg_ovf_ids", std::max<int64_t>(g->n, 1) * 8);
+            ctr = (unsigned long long*)scratch_bytes("sage_xchg_ctr", 8 * (3 * world + 3));
+            scan_bytes = rec_offsets_temp_bytes(round_rows);
+            scan_tmp = scratch_bytes("sage_xchg_scan", (int64_t)std::max<size_t>(scan_bytes, 16));
+            RVX_HIP(hipMemsetAsync(ctr, 0, 8 * (size_t)(3 * world + 3), d.xfer));
+        }
+        auto budget = [&](int64_t rows) { return ((uint64_t)std::ceil((double)rows * rate) + 15) / 16 * 16; };
         auto hook = [&](int c, int64_t, int64_t) {
             RVX_HIP(hipEventRecord(ev[c], stream()));  // chunk c's rows are complete on the pipeline's main stream
             RVX_HIP(hipStreamWaitEvent(d.xfer, ev[c], 0));
             StreamScope on_xfer(d.xfer);
             ProfScope ps("halo_exchange");
-            comm_exchange_rows(comm, y, l->out, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
-            if (yinv_xchg) comm_exchange_rows(comm, yinv_xchg, 1, plan[c].r0.data(), plan[c].rows.data(), d.xfer);
-            if (yimg)  // the rows that arrived, imaged where they land (this rank's own: sage_forward_dev)
-                for (int p = 0; p < world; ++p)
-                    if (p != me) rows_image_pack(y, plan[c].r0[p], plan[c].rows[p], l->out, yimg);
+            const std::vector<int64_t>& rows = plan[c].rows;
+            bool counted = false;
+            if (c == 0 && xallow) {
+                if (rate_env > 0) {
+                    rate = rate_env;
+                } else {
+                    unsigned long long* acc = ctr + world + 1;
+                    rows_rec_count(y, plan[0].r0[me], rows[me], l->out, xcnt + st[me], acc);
+                    counted = true;
+                    comm_allgather_bytes(comm, acc, acc + 2, 16, d.xfer);
+                    std::vector<unsigned long long> all(2 * (size_t)world);
+                    RVX_HIP(hipMemcpyAsync(all.data(), acc + 2, all.size() * 8, hipMemcpyDeviceToHost, d.xfer));
+                    RVX_HIP(hipStreamSynchronize(d.xfer));
+                    for (int p = 0; p < world; ++p)
+                        if (all[2 * p + 1] > 0) rate = std::max(rate, (double)all[2 * p] / (double)all[2 * p + 1]);
+                    rate = rate * 1.02 + 16.0;
+                }
+                xrec = rate + 4.0 <= 0.85 * 4.0 * l->out;
+            }
+            if (xrec) {
+                if (!counted) rows_rec_count(y, plan[c].r0[me], rows[me], l->out, xcnt + st[me], nullptr);
+                rec_offsets(xcnt + st[me], rows[me], xoff + st[me], scan_tmp, scan_bytes);
+                rows_xchg_pack(y, plan[c].r0[me], rows[me], l->out, xs + st16[me] * 16, budget(rows[me]), xcnt + st[me],
+                               xoff + st[me], ovf_ids, ctr);
+                for (int p = 0; p < world; ++p) blk16[p] = (int64_t)(budget(rows[p]) / 16);
+                comm_exchange_rows(comm, reinterpret_cast<float*>(xcnt), 1, st.data(), rows.data(), d.xfer);
+                comm_exchange_rows(comm, reinterpret_cast<float*>(xs), 4, st16.data(), blk16.data(), d.xfer);
+            } else {
+                comm_exchange_rows(comm, y, l->out, plan[c].r0.data(), rows.data(), d.xfer);
+            }
+            if (yinv_xchg) comm_exchange_rows(comm, yinv_xchg, 1, plan[c].r0.data(), rows.data(), d.xfer);
+            for (int p = 0; p < world; ++p) {
+                if (p == me) continue;
+                if (xrec) {  // records back into dense rows (and the image, when asked for)
+                    rec_offsets(xcnt + st[p], rows[p], xoff + st[p], scan_tmp, scan_bytes);
+                    rows_xchg_unpack(y, plan[c].r0[p], rows[p], l->out, xs + st16[p] * 16, budget(rows[p]),
+                                     xcnt + st[p], xoff + st[p], yimg);
+                } else if (yimg) {  // the rows that arrived, imaged where they land (this rank's own: sage_forward_dev)
+                    rows_image_pack(y, plan[c].r0[p], rows[p], l->out, yimg);
+                }
+            }
         };
         sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], chunks, hook, xm, yinv_rows, xi,
                          image_rows(yimg, offsets[me]));
+        if (xrec) {
+            // rows past the slot: counts all-gathered, then each owner broadcasts its rows (ids
+            // + dense values) and the others scatter them. A host wait per layer, at its end.
+            StreamScope on_xfer(d.xfer);
+            ProfScope ps("halo_exchange_dense_rows");
+            auto* cnt_d = reinterpret_cast<int64_t*>(ctr) + 1;
+            comm_allgather_bytes(comm, ctr, cnt_d, 8, d.xfer);
+            std::vector<int64_t> cnt(world, 0);
+            RVX_HIP(hipMemcpyAsync(cnt.data(), cnt_d, (size_t)world * 8, hipMemcpyDeviceToHost, d.xfer));
+            RVX_HIP(hipStreamSynchronize(d.xfer));
+            int64_t tot = 0, most = 0;
+            for (int p = 0; p < world; ++p) {
+                tot += cnt[p];
+                most = std::max(most, cnt[p]);
+            }
+            if (tot > 0) {
+                RVX_HIP(hipStreamSynchronize(d.stream));  // nothing of this layer may still use scratch
+                DevMem buf(most * (8 + (int64_t)l->out * 4));
+                auto* ids = buf.as<int64_t>();
+                for (int p = 0; p < world; ++p) {
+                    if (cnt[p] == 0) continue;
+                    const int64_t bytes = cnt[p] * (8 + (int64_t)l->out * 4);
+                    if (p == me) {  // ids first, then their rows, contiguous for the broadcast
+                        RVX_HIP(hipMemcpyAsync(ids, ovf_ids, (size_t)cnt[p] * 8, hipMemcpyDeviceToDevice, d.xfer));
+                        rows_by_id(y, l->out, ids, cnt[p], ids_rows(ids, cnt[p]), false);
+                    }
+                    comm_broadcast_bytes(comm, buf.p, bytes, p, d.xfer);
+                    if (p != me) {
+                        rows_by_id(y, l->out, ids, cnt[p], ids_rows(ids, cnt[p]), true);
+                        if (yimg) rows_image_pack_ids(y, ids, cnt[p], l->out, yimg);
+                    }
+                }
+                RVX_HIP(hipStreamSynchronize(d.xfer));  // buf is freed on return
+            }
+        }
         RVX_HIP(hipEventRecord(ev[chunks], d.xfer));
         {
             // the exchange's tail the compute stream waits for: from the last chunk's

@@ -20,6 +20,9 @@
 #include "kernels.hpp"
 #include "agg_row.hpp"
 
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
+
 namespace rvx {
 namespace {
 
@@ -282,15 +285,16 @@ __global__ __launch_bounds__(256) void k_aggregate_help(AggHelp h) {
 // One wave per row: header bits, packed positions (agg_row.hpp), the record assembled in the
 // wave's LDS window (scattered 4-B LDS stores), then written out as whole 16-B chunks
 // (coalesced); nnz for every row (rows above IMG_CAP keep no slot: readers take the dense row).
+// ids (nullable): row i is ids[i] instead of r0 + i.
 __global__ __launch_bounds__(256) void k_rows_image_pack(const float* __restrict__ x, int64_t r0, int64_t rows,
                                                          int dim, unsigned char* __restrict__ slots,
-                                                         uint16_t* __restrict__ nnz) {
+                                                         uint16_t* __restrict__ nnz, const int64_t* __restrict__ ids) {
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) f32x4 win[ROWS_PER_BLOCK][IMG_SLOT / 16];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t i = (int64_t)blockIdx.x * ROWS_PER_BLOCK + w;
     if (i >= rows) return;
-    const int64_t r = r0 + i;
+    const int64_t r = ids ? ids[i] : r0 + i;
     const float* src = x + r * dim;
     float4 v[3];
     unsigned h = 0;
@@ -323,7 +327,204 @@ __global__ __launch_bounds__(256) void k_rows_image_pack(const float* __restrict
     f32x4* dst = reinterpret_cast<f32x4*>(slots + r * IMG_SLOT);
     for (int c = lane; c < chunks; c += 64) dst[c] = win[w][c];
 }
+
+// ---- compact exchange records (rvx_sage_forward_exchange3 at world > 1) ----
+// A round's block of rows travels as the rows' image records (header + kept values, as
+// k_rows_image_pack, 16-B rounded) back to back within a byte budget agreed in advance, and
+// their counts. Record i sits at the exclusive prefix sum of the record sizes before it
+// (rec_bytes of the counts), which sender and receiver compute alike from the counts; a
+// row whose record ends past the budget, or has more than IMG_CAP kept values (its dense
+// row is smaller), is an overflow row and travels dense after the rounds.
+__device__ __forceinline__ uint64_t rec_bytes(unsigned t) {
+    return t > (unsigned)IMG_CAP ? 0ull : (uint64_t)((128 + 4 * t + 15) / 16 * 16);
+}
+struct RecBytes {
+    __device__ uint64_t operator()(uint32_t t) const { return rec_bytes(t); }
+};
+
+// counts (values other than +0.0) of rows r0 + i into cnt[i]; with acc: acc[0] += record
+// bytes (dense bytes for a row past IMG_CAP), acc[1] += rows (the budget estimate of chunk 0)
+__global__ __launch_bounds__(256) void k_rows_rec_count(const float* __restrict__ x, int64_t r0, int64_t rows, int dim,
+                                                        uint32_t* __restrict__ cnt, unsigned long long* __restrict__ acc) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * ROWS_PER_BLOCK + w;
+    if (i >= rows) return;
+    const float* src = x + (r0 + i) * dim;
+    int t = 0;
+    for (int c = lane; c < dim; c += 64) t += aggrow::img_nz(src[c]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if (lane == 0) {
+        cnt[i] = (uint32_t)t;
+        if (acc) {
+            const unsigned long long rb = rec_bytes((unsigned)t);
+            atomicAdd(&acc[0], rb ? rb : (unsigned long long)(4 * dim));
+            atomicAdd(&acc[1], 1ull);
+        }
+    }
+}
+
+// Row r0 + i's record at xs + off[i] when it fits the budget, else its global id appended to
+// ovf_ids.
+__global__ __launch_bounds__(256) void k_rows_xchg_pack(const float* __restrict__ x, int64_t r0, int64_t rows, int dim,
+                                                        unsigned char* __restrict__ xs, uint64_t budget,
+                                                        const uint32_t* __restrict__ cnt, const uint64_t* __restrict__ off,
+                                                        int64_t* __restrict__ ovf_ids,
+                                                        unsigned long long* __restrict__ ovf_n) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) f32x4 win[ROWS_PER_BLOCK][IMG_SLOT / 16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * ROWS_PER_BLOCK + w;
+    if (i >= rows) return;
+    const int64_t r = r0 + i;
+    const uint64_t rb = rec_bytes(cnt[i]);
+    if (rb == 0 || off[i] + rb > budget) {
+        if (lane == 0) ovf_ids[atomicAdd(ovf_n, 1ull)] = r;
+        return;
+    }
+    const float* src = x + r * dim;
+    float4 v[3];
+    unsigned h = 0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const bool act = 4 * lane + 256 * j < dim;
+        v[j] = act ? *reinterpret_cast<const float4*>(src + 4 * lane + 256 * j) : make_float4(0, 0, 0, 0);
+        const unsigned nib = aggrow::img_nz(v[j].x) | (aggrow::img_nz(v[j].y) << 1) | (aggrow::img_nz(v[j].z) << 2) |
+                             (aggrow::img_nz(v[j].w) << 3);
+        h |= (act ? nib : 0u) << (4 * j);
+    }
+    int p[3];
+    unsigned tot;
+    aggrow::img_positions(h, p, tot);
+    unsigned char* wb = reinterpret_cast<unsigned char*>(win[w]);
+    reinterpret_cast<uint16_t*>(wb)[lane] = (uint16_t)h;
+    float* vals = reinterpret_cast<float*>(wb + 128);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+        int q = p[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if ((h >> (4 * j + k)) & 1u) vals[q++] = e[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int chunks = (int)(rb / 16);
+    f32x4* dst = reinterpret_cast<f32x4*>(xs + off[i]);
+    for (int c = lane; c < chunks; c += 64) dst[c] = win[w][c];
+}
+
+// The receiving side: record i back into the dense row r0 + i of x — every kept value's bits,
+// +0.0 elsewhere, so the row equals the sender's — and, with an image, into that row's image
+// slot. Overflow rows are left to the dense pass, which images them again (their image
+// count is set past IMG_CAP meanwhile).
+__global__ __launch_bounds__(256) void k_rows_xchg_unpack(float* __restrict__ x, int64_t r0, int64_t rows, int dim,
+                                                          const unsigned char* __restrict__ xs, uint64_t budget,
+                                                          const uint32_t* __restrict__ cnt,
+                                                          const uint64_t* __restrict__ off,
+                                                          unsigned char* __restrict__ slots,
+                                                          uint16_t* __restrict__ nnz) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) f32x4 win[ROWS_PER_BLOCK][IMG_SLOT / 16 + 1];  // + slack for wf[p + 3]
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * ROWS_PER_BLOCK + w;
+    if (i >= rows) return;
+    const int64_t r = r0 + i;
+    const unsigned tot = cnt[i];
+    const uint64_t rb = rec_bytes(tot);
+    if (rb == 0 || off[i] + rb > budget) {
+        if (nnz && lane == 0) nnz[r] = (uint16_t)(IMG_CAP + 1);
+        return;
+    }
+    const int chunks = (int)(rb / 16);
+    const f32x4* src = reinterpret_cast<const f32x4*>(xs + off[i]);
+    for (int c = lane; c < chunks; c += 64) win[w][c] = src[c];
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const unsigned char* wb = reinterpret_cast<const unsigned char*>(win[w]);
+    const unsigned h = reinterpret_cast<const uint16_t*>(wb)[lane];
+    int p[3];
+    unsigned t2;
+    aggrow::img_positions(h, p, t2);
+    const float* wf = reinterpret_cast<const float*>(wb + 128);
+    float* dst = x + r * dim;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        if (4 * lane + 256 * j >= dim) continue;
+        const unsigned nib = (h >> (4 * j)) & 15u;
+        const float w0 = wf[p[j]], w1 = wf[p[j] + 1], w2 = wf[p[j] + 2], w3 = wf[p[j] + 3];
+        const bool b0 = nib & 1u, b1 = nib & 2u, b2 = nib & 4u, b3 = nib & 8u;
+        const int q2 = (int)b0 + (int)b1, q3 = q2 + (int)b2;
+        float4 e;
+        e.x = b0 ? w0 : 0.0f;
+        e.y = b1 ? (b0 ? w1 : w0) : 0.0f;
+        e.z = b2 ? (q2 == 0 ? w0 : q2 == 1 ? w1 : w2) : 0.0f;
+        e.w = b3 ? (q3 == 0 ? w0 : q3 == 1 ? w1 : q3 == 2 ? w2 : w3) : 0.0f;
+        *reinterpret_cast<float4*>(dst + 4 * lane + 256 * j) = e;
+    }
+    if (slots) {
+        f32x4* sd = reinterpret_cast<f32x4*>(slots + r * IMG_SLOT);
+        for (int c = lane; c < chunks; c += 64) sd[c] = win[w][c];
+        if (lane == 0) nnz[r] = (uint16_t)tot;
+    }
+}
+
+// Dense rows by global id: gather (ids -> rows[cnt][dim]) or scatter (rows -> x[ids]); one
+// block per row.
+__global__ __launch_bounds__(192) void k_rows_by_id(float* __restrict__ x, int dim, const int64_t* __restrict__ ids,
+                                                    float* __restrict__ rows, int scatter) {
+    const int64_t i = blockIdx.x;
+    const int64_t r = ids[i];
+    for (int c = threadIdx.x; c < dim; c += blockDim.x) {
+        if (scatter) x[r * dim + c] = rows[i * dim + c];
+        else rows[i * dim + c] = x[r * dim + c];
+    }
+}
 }  // namespace
+
+void rows_rec_count(const float* x, int64_t r0, int64_t rows, int dim, uint32_t* cnt, unsigned long long* acc) {
+    if (rows <= 0) return;
+    RVX_LAUNCH("rows_rec_count", k_rows_rec_count, dim3((unsigned)((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK)),
+               dim3(256), 0, x, r0, rows, dim, cnt, acc);
+}
+
+size_t rec_offsets_temp_bytes(int64_t rows) {
+    size_t bytes = 0;
+    rocprim::transform_iterator<const uint32_t*, RecBytes, uint64_t> in(nullptr, RecBytes());
+    RVX_HIP(rocprim::exclusive_scan(nullptr, bytes, in, (uint64_t*)nullptr, (uint64_t)0,
+                                    (size_t)std::max<int64_t>(rows, 1), rocprim::plus<uint64_t>(), stream()));
+    return bytes;
+}
+
+void rec_offsets(const uint32_t* cnt, int64_t rows, uint64_t* off, void* temp, size_t temp_bytes) {
+    if (rows <= 0) return;
+    rocprim::transform_iterator<const uint32_t*, RecBytes, uint64_t> in(cnt, RecBytes());
+    size_t bytes = temp_bytes;
+    RVX_HIP(rocprim::exclusive_scan(temp, bytes, in, off, (uint64_t)0, (size_t)rows, rocprim::plus<uint64_t>(),
+                                    stream()));
+}
+
+void rows_xchg_pack(const float* x, int64_t r0, int64_t rows, int dim, unsigned char* xs, uint64_t budget,
+                    const uint32_t* cnt, const uint64_t* off, int64_t* ovf_ids, unsigned long long* ovf_n) {
+    if (rows <= 0) return;
+    RVX_REQUIRE(row_image_ok(dim) && ((uintptr_t)x & 15) == 0 && ((uintptr_t)xs & 15) == 0, RVX_ERR_INVALID_SHAPE,
+                "exchange records: bad arguments");
+    RVX_LAUNCH("rows_xchg_pack", k_rows_xchg_pack, dim3((unsigned)((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK)),
+               dim3(256), 0, x, r0, rows, dim, xs, budget, cnt, off, ovf_ids, ovf_n);
+}
+
+void rows_xchg_unpack(float* x, int64_t r0, int64_t rows, int dim, const unsigned char* xs, uint64_t budget,
+                      const uint32_t* cnt, const uint64_t* off, const RowImage& img) {
+    if (rows <= 0) return;
+    RVX_REQUIRE(row_image_ok(dim) && ((uintptr_t)x & 15) == 0 && ((uintptr_t)xs & 15) == 0, RVX_ERR_INVALID_SHAPE,
+                "exchange records: bad arguments");
+    RVX_LAUNCH("rows_xchg_unpack", k_rows_xchg_unpack, dim3((unsigned)((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK)),
+               dim3(256), 0, x, r0, rows, dim, xs, budget, cnt, off, img.slots, img.nnz);
+}
+
+void rows_by_id(float* x, int dim, const int64_t* ids, int64_t cnt, float* rows, bool scatter) {
+    if (cnt <= 0) return;
+    RVX_LAUNCH("rows_by_id", k_rows_by_id, dim3((unsigned)cnt), dim3(192), 0, x, dim, ids, rows, scatter ? 1 : 0);
+}
 
 bool row_image_ok(int dim) { return dim > 512 && dim <= 768 && dim % 4 == 0; }
 
@@ -331,7 +532,14 @@ void rows_image_pack(const float* x, int64_t r0, int64_t rows, int dim, const Ro
     if (rows <= 0) return;
     RVX_REQUIRE(img && row_image_ok(dim) && ((uintptr_t)x & 15) == 0, RVX_ERR_INVALID_SHAPE, "row image: bad arguments");
     RVX_LAUNCH("rows_image_pack", k_rows_image_pack, dim3((unsigned)((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK)),
-               dim3(256), 0, x, r0, rows, dim, img.slots, img.nnz);
+               dim3(256), 0, x, r0, rows, dim, img.slots, img.nnz, (const int64_t*)nullptr);
+}
+
+void rows_image_pack_ids(const float* x, const int64_t* ids, int64_t cnt, int dim, const RowImage& img) {
+    if (cnt <= 0) return;
+    RVX_REQUIRE(img && row_image_ok(dim) && ((uintptr_t)x & 15) == 0, RVX_ERR_INVALID_SHAPE, "row image: bad arguments");
+    RVX_LAUNCH("rows_image_pack", k_rows_image_pack, dim3((unsigned)((cnt + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK)),
+               dim3(256), 0, x, (int64_t)0, cnt, dim, img.slots, img.nnz, ids);
 }
 
 bool agg_help_ok(int dim, const float* x, const float* out, const float* self_x) {

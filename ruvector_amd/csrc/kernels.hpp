@@ -48,6 +48,28 @@ struct RowImage {
 bool row_image_ok(int dim);
 // rows [r0, r0 + rows) of x (row stride dim) into the image
 void rows_image_pack(const float* x, int64_t r0, int64_t rows, int dim, const RowImage& img);
+// Compact exchange records of the node-range exchange (rvx_sage_forward_exchange3 at world > 1):
+// a block of rows travels as the rows' image records back to back within a byte budget, and
+// their counts; record i sits at off[i] = exclusive prefix sum of the record bytes (16-B
+// rounded 128 + 4 * count; none past IMG_CAP) before it. Rows whose record ends past the budget
+// (or have none) are overflow rows, sent dense after the rounds.
+// counts of rows r0 + i into cnt[i]; acc (nullable) += {record bytes (dense bytes for rows past
+// IMG_CAP), rows}
+void rows_rec_count(const float* x, int64_t r0, int64_t rows, int dim, uint32_t* cnt, unsigned long long* acc);
+// off[0 .. rows) from cnt (rocPRIM scan; temp of rec_offsets_temp_bytes(>= rows))
+size_t rec_offsets_temp_bytes(int64_t rows);
+void rec_offsets(const uint32_t* cnt, int64_t rows, uint64_t* off, void* temp, size_t temp_bytes);
+// the sender: records of rows r0 + i at xs + off[i]; overflow rows' global ids appended to ovf_ids
+void rows_xchg_pack(const float* x, int64_t r0, int64_t rows, int dim, unsigned char* xs, uint64_t budget,
+                    const uint32_t* cnt, const uint64_t* off, int64_t* ovf_ids, unsigned long long* ovf_n);
+// the receiver: records back into the dense rows r0 + i of x, bit for bit (and into img when
+// given); overflow rows are left for rows_by_id
+void rows_xchg_unpack(float* x, int64_t r0, int64_t rows, int dim, const unsigned char* xs, uint64_t budget,
+                      const uint32_t* cnt, const uint64_t* off, const RowImage& img);
+// Dense rows by global id: rows[i] = x[ids[i]] (gather) or x[ids[i]] = rows[i] (scatter).
+void rows_by_id(float* x, int dim, const int64_t* ids, int64_t cnt, float* rows, bool scatter);
+// rows ids[0 .. cnt) of x into the image (as rows_image_pack)
+void rows_image_pack_ids(const float* x, const int64_t* ids, int64_t cnt, int dim, const RowImage& img);
 
 struct AggHelp {
     const int64_t* rp; const int32_t* col; int64_t n;

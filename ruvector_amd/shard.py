@@ -109,6 +109,14 @@ def rendezvous_unique_id(rank: int, world: int, make_id: Callable[[], bytes], ad
 REDUCE_SUM, REDUCE_MAX, REDUCE_MIN = 0, 1, 2
 
 
+def comm_traffic(comm) -> tuple:
+    """(sent, received) payload bytes of a librvx communicator (RcclComm / SocketComm) since it
+    was made: every exchange round, broadcast and all-gather (rvx_comm_traffic)."""
+    sent, recv = C.c_int64(), C.c_int64()
+    L.call("rvx_comm_traffic", comm._h, C.byref(sent), C.byref(recv))
+    return sent.value, recv.value
+
+
 class RcclComm:
     """RCCL communicator of librvx (one per process/GPU)."""
 

@@ -157,7 +157,54 @@ def main():
             del t1, t2, img
         res["image_layer1_all_rows_equal"] = bool(np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32)))
         res["image_layer2_owned_equal"] = bool(np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32)))
-        del outs, xI
+        del outs
+
+        # ---- compact exchange records (kernels.hpp rows_xchg_pack/unpack): rows travel as
+        # bitmap + values other than +0.0 in a fixed slot and are expanded on arrival; rows
+        # past the slot travel dense after the rounds. Every row of layer 1 (owned and
+        # received) and layer 2's owned rows bit-identical to one process, for the dense
+        # exchange (RVX_XCHG_IMAGE=0), the default (slot sized from chunk 0), a slot about half
+        # the rows overflow and one every row overflows.
+        from ruvector_amd.shard import comm_traffic
+        q1, q2 = rv.Buffer(N * dI * 4), rv.Buffer(N * dI * 4)
+        refI = [rv.GraphSAGELayer(dI, dI, num_samples=deg) for _ in range(2)]
+        call("rvx_sage_forward_exchange3", refI[0]._h, g_full.handle, xI.handle, None, None, q1.handle, ivI.handle,
+             None, one_p, None, 0)
+        call("rvx_sage_forward_exchange3", refI[1]._h, g_full.handle, q1.handle, ivI.handle, None, q2.handle, None,
+             None, one_p, None, 0)
+        e1, e2 = q1.download(np.float32, (N, dI)).view(np.uint32), q2.download(np.float32, (N, dI)).view(np.uint32)
+        nz = (e1 != 0).sum(axis=1)
+        res["xchg_row_nnz_mean"] = float(nz.mean())
+        rec = {}
+        rec_mean = float(np.where(nz <= 736, (128 + 4 * nz + 15) // 16 * 16, 4 * dI).mean())
+        res["xchg_record_bytes_mean"] = rec_mean
+        for name, env in (("dense", {"RVX_XCHG_IMAGE": "0"}), ("default", {}),
+                          ("half", {"RVX_XCHG_ROW_BYTES": str(int(rec_mean / 2))}), ("all", {"RVX_XCHG_ROW_BYTES": "16"})):
+            os.environ.update(env)
+            ls = [rv.GraphSAGELayer(dI, dI, num_samples=deg) for _ in range(2)]
+            img = rv.row_image(N, dI) if name == "half" else None
+            t1, t2 = rv.Buffer(N * dI * 4), rv.Buffer(N * dI * 4)
+            t1.upload(np.full((N, dI), np.nan, np.float32))
+            s0 = comm_traffic(comm)[0]
+            call("rvx_sage_forward_exchange3", ls[0]._h, g_loc.handle, xI.handle, None, None, t1.handle, ivI.handle,
+                 img.handle if img else None, off_p, comm._h, 1)
+            rv.synchronize()
+            sent = comm_traffic(comm)[0] - s0
+            call("rvx_sage_forward_exchange3", ls[1]._h, g_loc.handle, t1.handle, ivI.handle,
+                 img.handle if img else None, t2.handle, None, None, off_p, comm._h, 0)
+            a1 = t1.download(np.float32, (N, dI)).view(np.uint32)
+            a2 = t2.download(np.float32, (N, dI)).view(np.uint32)
+            r = {"sent": int(sent), "layer1_all_rows_equal": bool(np.array_equal(a1, e1)),
+                 "layer2_owned_equal": bool(np.array_equal(a2[o0:o1], e2[o0:o1]))}
+            if img is not None:  # rows past the budget are imaged again after their dense pass
+                inz = img.download(np.uint16, (N,), offset=N * 3072).astype(np.int64)
+                r["image_counts_ok"] = bool(np.array_equal(inz, nz))
+            rec[name] = r
+            for k in env:
+                os.environ.pop(k)
+            del t1, t2, img, ls
+        res["xchg"] = rec
+        del xI, q1, q2
 
         # ---- RuvectorLayer (M|K|V exchange) and the attention head (T exchange)
         n2 = int(offsets[-1])

@@ -31,6 +31,9 @@ def test_bench_self_launches_ranks_and_checks_itself(gpus, nodes):
     mg = line["multi_gpu"]
     assert len(mg["bytes_recv_per_layer"]) == gpus and len(mg["exchange_ms_per_layer"]) == gpus
     assert mg["transport"].startswith("host")
+    # compact row records on the bench's half-zero rows: <= 0.6x the dense exchange bytes, as
+    # the library counted them (rvx_comm_traffic)
+    assert mg["format"].startswith("compact") and max(mg["sent_vs_dense"]) <= 0.6, mg
     par = line["parity"]
     assert par["tables_agree"], par
     assert par["ok"], par

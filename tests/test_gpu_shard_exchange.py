@@ -67,3 +67,12 @@ def test_exchange_entry_points_multi_rank(offsets, tmp_path):
         # row images across the exchange: received rows imaged on arrival, same bits
         assert r["image_nnz_all_rows_match"] and r["image_rows_in_slots"] > 0.9, r
         assert r["image_layer1_all_rows_equal"] and r["image_layer2_owned_equal"], r
+        # compact exchange records: same bits as one process in every mode, overflow rows sent
+        # dense after the rounds; the default sends the mean record (+2%, + counts) per row
+        x = r["xchg"]
+        for name in ("dense", "default", "half", "all"):
+            assert x[name]["layer1_all_rows_equal"] and x[name]["layer2_owned_equal"], (name, x)
+        per_row = (r["xchg_record_bytes_mean"] * 1.02 + 16 + 8 + 16) / (4 * 768 + 4)
+        assert x["default"]["sent"] <= per_row * x["dense"]["sent"], (per_row, x)
+        assert x["half"]["image_counts_ok"], x
+        assert x["all"]["sent"] > x["dense"]["sent"] * 0.9, x  # nearly every row went dense
