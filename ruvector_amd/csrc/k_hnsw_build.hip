@@ -74,7 +74,7 @@ __device__ __forceinline__ int list_key(const BuildGraph& G, int p, int l) {  //
 // R-only form (hnsw_dev.hpp merge_into_r, as the query kernel k_hnsw.hip): the
 // nearest candidate is the nearest unexpanded entry of R (id bit 31 = expanded);
 // the flags are cleared before returning.
-template <int METRIC, bool RG = false>
+template <int METRIC, bool RG = false, int NST = 2>
 __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn, int ep, float d_ep, int ef, int l,
                                   unsigned long long* vis, unsigned vmask, unsigned long long tag, float* rd, int* ri,
                                   float* sdb, int* sib, unsigned char* wst, int lane) {
@@ -119,7 +119,7 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
             if (coop) {
                 if constexpr (METRIC != RVX_METRIC_POINCARE && METRIC != RVX_METRIC_HYP_L2) {
                     const int row = fresh ? nid : -1;
-                    const float dv = wave_dist<METRIC>(qs, a.x, a.d, row, qn,
+                    const float dv = wave_dist<METRIC, NST>(qs, a.x, a.d, row, qn,
                                                        (METRIC == RVX_METRIC_COSINE && fresh) ? a.xnorm[nid] : 0.0f,
                                                        wst, lane);
                     if (fresh) dd = dv;
@@ -146,14 +146,14 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
 #ifndef RVX_BUILD_WPE
 #define RVX_BUILD_WPE
 #endif
-template <int METRIC, bool RG = false>
-__global__ __launch_bounds__(64) RVX_BUILD_WPE void k_build_insert(BuildArgs a) {
+template <int METRIC, bool RG, int NST>
+__device__ __forceinline__ void build_insert_body(const BuildArgs& a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int lane = threadIdx.x;
     const int ef = a.ef_c;
     const int dq = (a.d + 3) & ~3;
-    unsigned char* wst = lds_raw;  // [WD_LDS] distance stages (coop)
-    float* qs = reinterpret_cast<float*>(lds_raw + (a.coop ? WD_LDS : 0));
+    unsigned char* wst = lds_raw;  // [NST * WD_STAGE] distance stages (coop)
+    float* qs = reinterpret_cast<float*>(lds_raw + (a.coop ? wd_lds(NST) : 0));
     float* rd;
     int* ri;
     float* sd;  // selected [MAX_C0] (search: admitted batch [64])
@@ -187,8 +187,8 @@ __global__ __launch_bounds__(64) RVX_BUILD_WPE void k_build_insert(BuildArgs a) 
         // 1. greedy descent, ef = 1 (hnsw.rs:1105-1146)
         for (int l = a.entry_level; l >= lev + 1; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
-            const int rs = build_search_layer<METRIC, RG>(a, qs, qn, ep, d_ep, 1, l, vis, vmask, tag, rd, ri, sd, si, wst,
-                                                      lane);
+            const int rs = build_search_layer<METRIC, RG, NST>(a, qs, qn, ep, d_ep, 1, l, vis, vmask, tag, rd, ri, sd,
+                                                               si, wst, lane);
             if (rs > 0 && rd[0] < d_ep) { ep = ri[0]; d_ep = rd[0]; }
         }
         // 2. layers lev .. 0 (hnsw.rs:1149-1196); HyperbolicHnsw inserts at
@@ -196,8 +196,8 @@ __global__ __launch_bounds__(64) RVX_BUILD_WPE void k_build_insert(BuildArgs a) 
         const int ltop = a.hyper ? min(lev, a.entry_level) : lev;
         for (int l = ltop; l >= 0; --l) {
             const unsigned long long tag = (unsigned long long)(++epoch) << 32;
-            const int rs = build_search_layer<METRIC, RG>(a, qs, qn, ep, d_ep, ef, l, vis, vmask, tag, rd, ri, sd, si, wst,
-                                                      lane);
+            const int rs = build_search_layer<METRIC, RG, NST>(a, qs, qn, ep, d_ep, ef, l, vis, vmask, tag, rd, ri, sd,
+                                                               si, wst, lane);
             if (rs == 0) continue;
             const int nb_conn = l == 0 ? a.G.C0 : a.G.M;
             int ss = 0;
@@ -262,6 +262,11 @@ __global__ __launch_bounds__(64) RVX_BUILD_WPE void k_build_insert(BuildArgs a) 
         }
         for (int i = rec + lane; i < a.rev_cap; i += 64) a.rev_key[rbase + i] = -1;
     }
+}
+
+template <int METRIC, bool RG = false>
+__global__ __launch_bounds__(64) RVX_BUILD_WPE void k_build_insert(BuildArgs a) {
+    build_insert_body<METRIC, RG, 2>(a);
 }
 
 // One wave per list that received reverse edges (the record that found the
@@ -361,9 +366,9 @@ __global__ __launch_bounds__(256) void k_build_merge(BuildArgs a, int nrec) {
 
 }  // namespace
 
-size_t build_lds_bytes(int d, int ef, bool coop, bool rg = false) {
+size_t build_lds_bytes(int d, int ef, bool coop, bool rg = false, int nst = 2) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)WD_LDS : 0) + (size_t)dq * 4 + (rg ? 0 : (size_t)(ef + 1) * 8) + (size_t)MAX_C0 * 8;
+    return (coop ? (size_t)wd_lds(nst) : 0) + (size_t)dq * 4 + (rg ? 0 : (size_t)(ef + 1) * 8) + (size_t)MAX_C0 * 8;
 }
 
 void build_insert_batch(const BuildGraph& G, int metric, const float* x, const float* xnorm, int d,
@@ -375,7 +380,10 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     RVX_REQUIRE(ef_c >= 1 && ef_c <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER, "ef_construction out of range");
     const unsigned vcap = visited_capacity(ef_c, G.C0);
     const bool coop = hnsw_coop(metric, d, batch_begin + batch_n);
-    // R in LDS when one wave's 160 KB hold it, else in HBM (RVX_HNSW_RG=1 forces, tests)
+    // R in LDS when one wave's 160 KB hold it, else in HBM (RVX_HNSW_RG=1 forces, tests). Unlike
+    // the high-ef search, more waves do not speed the build: R in HBM with one distance stage at
+    // 3 waves per SIMD built the same graph slower (4M x 768 M 32: 41.7 vs 36.4 s; 2M M 128 ef_c
+    // 500: > 180 vs 129 s; profiles/r05_build_wide_ab.txt, round 5).
     const bool rg = build_lds_bytes(d, ef_c, coop) > 160 * 1024 || env_int("RVX_HNSW_RG", 0) != 0;
     int nslots = (int)std::min<int64_t>(std::min(batch_n, 8192),
                                         std::max<int64_t>(1024, ((int64_t)4 << 30) / ((int64_t)vcap * 8)));

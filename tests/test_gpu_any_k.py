@@ -123,10 +123,13 @@ def test_hnsw_ef_past_8192_bit_exact(monkeypatch, wide_graph, k, ef, rg):
     assert np.array_equal(dist, rd)
 
 
-def test_hnsw_build_with_hbm_r_same_graph(monkeypatch):
+@pytest.mark.parametrize("coop", ["0", "2"])
+def test_hnsw_build_with_hbm_r_same_graph(monkeypatch, coop):
     # the builder's layer searches with R in HBM build the same graph as with R in LDS
-    n, d = 6000, 24
+    # (per-lane and LDS-staged distances)
+    n, d = 6000, 64
     x = O.fill_uniform(n * d, 210).reshape(n, d)
+    monkeypatch.setenv("RVX_HNSW_COOP", coop)
     graphs = []
     for rg in ("0", "1"):
         monkeypatch.setenv("RVX_HNSW_RG", rg)
