@@ -872,30 +872,23 @@ rvx_status rvx_sage_forward_exchange3(const rvx_sage_layer* l, const rvx_graph* 
             RVX_HIP(hipMemsetAsync(ctr, 0, 8 * (size_t)(3 * world + 3), d.xfer));
         }
         auto budget = [&](int64_t rows) { return ((uint64_t)std::ceil((double)rows * rate) + 15) / 16 * 16; };
-        auto hook = [&](int c, int64_t, int64_t) {
-            RVX_HIP(hipEventRecord(ev[c], stream()));  // chunk c's rows are complete on the pipeline's main stream
-            RVX_HIP(hipStreamWaitEvent(d.xfer, ev[c], 0));
-            StreamScope on_xfer(d.xfer);
-            ProfScope ps("halo_exchange");
+        // the all-gathered chunk-0 record bytes land in pinned host memory; with more than one
+        // round the host reads them at round 1 (chunk 1 already queued), so the GPU never idles
+        // on this wait, and round 0's exchange goes out then
+        static unsigned long long* pinned = nullptr;
+        if (xallow && rate_env <= 0 && !pinned) RVX_HIP(hipHostMalloc((void**)&pinned, 2 * 8 * 1024, 0));
+        RVX_REQUIRE(!xallow || world <= 1024, RVX_ERR_INVALID_PARAMETER, "compact exchange: at most 1024 ranks");
+        bool rate_pending = false;
+        auto settle_rate = [&]() {  // xfer holds the chunk-0 count, its all-gather and the copy
+            RVX_HIP(hipStreamSynchronize(d.xfer));
+            for (int p = 0; p < world; ++p)
+                if (pinned[2 * p + 1] > 0) rate = std::max(rate, (double)pinned[2 * p] / (double)pinned[2 * p + 1]);
+            rate = rate * 1.02 + 16.0;
+            xrec = rate + 4.0 <= 0.85 * 4.0 * l->out;
+            rate_pending = false;
+        };
+        auto round = [&](int c, bool counted) {  // round c's exchange on the transfer stream (ev[c] waited)
             const std::vector<int64_t>& rows = plan[c].rows;
-            bool counted = false;
-            if (c == 0 && xallow) {
-                if (rate_env > 0) {
-                    rate = rate_env;
-                } else {
-                    unsigned long long* acc = ctr + world + 1;
-                    rows_rec_count(y, plan[0].r0[me], rows[me], l->out, xcnt + st[me], acc);
-                    counted = true;
-                    comm_allgather_bytes(comm, acc, acc + 2, 16, d.xfer);
-                    std::vector<unsigned long long> all(2 * (size_t)world);
-                    RVX_HIP(hipMemcpyAsync(all.data(), acc + 2, all.size() * 8, hipMemcpyDeviceToHost, d.xfer));
-                    RVX_HIP(hipStreamSynchronize(d.xfer));
-                    for (int p = 0; p < world; ++p)
-                        if (all[2 * p + 1] > 0) rate = std::max(rate, (double)all[2 * p] / (double)all[2 * p + 1]);
-                    rate = rate * 1.02 + 16.0;
-                }
-                xrec = rate + 4.0 <= 0.85 * 4.0 * l->out;
-            }
             if (xrec) {
                 if (!counted) rows_rec_count(y, plan[c].r0[me], rows[me], l->out, xcnt + st[me], nullptr);
                 rec_offsets(xcnt + st[me], rows[me], xoff + st[me], scan_tmp, scan_bytes);
@@ -918,6 +911,33 @@ rvx_status rvx_sage_forward_exchange3(const rvx_sage_layer* l, const rvx_graph* 
                     rows_image_pack(y, plan[c].r0[p], rows[p], l->out, yimg);
                 }
             }
+        };
+        auto hook = [&](int c, int64_t, int64_t) {
+            RVX_HIP(hipEventRecord(ev[c], stream()));  // chunk c's rows are complete on the pipeline's main stream
+            StreamScope on_xfer(d.xfer);
+            ProfScope ps("halo_exchange");
+            if (rate_pending) {  // round 1: chunk 0's rate is on its way; round 0 goes out first
+                settle_rate();
+                round(0, true);
+            }
+            RVX_HIP(hipStreamWaitEvent(d.xfer, ev[c], 0));
+            if (c == 0 && xallow) {
+                if (rate_env > 0) {
+                    rate = rate_env;
+                    xrec = rate + 4.0 <= 0.85 * 4.0 * l->out;
+                } else {
+                    unsigned long long* acc = ctr + world + 1;
+                    rows_rec_count(y, plan[0].r0[me], plan[0].rows[me], l->out, xcnt + st[me], acc);
+                    comm_allgather_bytes(comm, acc, acc + 2, 16, d.xfer);
+                    RVX_HIP(hipMemcpyAsync(pinned, acc + 2, 2 * 8 * (size_t)world, hipMemcpyDeviceToHost, d.xfer));
+                    rate_pending = true;
+                    if (chunks > 1) return;  // round 0 leaves with round 1
+                    settle_rate();
+                    round(0, true);
+                    return;
+                }
+            }
+            round(c, false);
         };
         sage_forward_dev(l, g, x, y + offsets[me] * l->out, offsets[me], chunks, hook, xm, yinv_rows, xi,
                          image_rows(yimg, offsets[me]));

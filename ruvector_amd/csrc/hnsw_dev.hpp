@@ -524,8 +524,10 @@ __device__ __forceinline__ int rank_in_r(const float* rd, const int* ri, int n, 
 // a group is read whole, then written (entries only move right, so a group's
 // writes land at or above its own lowest entry and never on the next group's),
 // which keeps MG reads in flight instead of one memory round trip per chunk —
-// at ef 12288 a merge walks up to 192 chunks.
-constexpr int MERGE_GROUP = 8;
+// at ef 12288 a merge walks up to 192 chunks. MG costs 3 VGPRs per chunk: 8 for R
+// in HBM, 2 for R in LDS (short round trips; the LDS kernels' occupancy is
+// register-bound).
+template <int MERGE_GROUP = 2>
 __device__ __forceinline__ int merge_into_r(float* rd, int* ri, int n, const float* sd, const int* si, int na, int nkeep,
                                             int lane) {
     float bd = 0.f; int bi = 0, rk = INT_MAX;
