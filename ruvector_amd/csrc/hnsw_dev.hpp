@@ -527,7 +527,10 @@ __device__ __forceinline__ int rank_in_r(const float* rd, const int* ri, int n, 
 // at ef 12288 a merge walks up to 192 chunks. MG costs 3 VGPRs per chunk: 8 for R
 // in HBM, 2 for R in LDS (short round trips; the LDS kernels' occupancy is
 // register-bound).
-template <int MERGE_GROUP = 2>
+#ifndef RVX_MERGE_LDS_G
+#define RVX_MERGE_LDS_G 2
+#endif
+template <int MERGE_GROUP = RVX_MERGE_LDS_G>
 __device__ __forceinline__ int merge_into_r(float* rd, int* ri, int n, const float* sd, const int* si, int na, int nkeep,
                                             int lane) {
     float bd = 0.f; int bi = 0, rk = INT_MAX;

@@ -213,7 +213,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
                 const unsigned long long adm = decide_batch(fmask, dd, nid, ef, rd, ri, rs, r, lane);
                 const int na = sort_batch(adm, dd, nid, sdb, sib, lane);
                 if (na == 0) continue;
-                scan = min(scan, merge_into_r<RG ? 8 : 2>(rd, ri, rs, sdb, sib, na, r, lane));
+                scan = min(scan, merge_into_r<RG ? 8 : RVX_MERGE_LDS_G>(rd, ri, rs, sdb, sib, na, r, lane));
                 if constexpr (RG) __threadfence_block();
                 rs = r;
             }
@@ -251,10 +251,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
 }
 // LDS-staged rows (coop) with NST distance stages other than the default two:
 // 1 past ef 1024 (R costs most of the LDS, more waves fit a CU), a deeper ring
-// where one wave is alone on its CU (hnsw_nst). At most 168 VGPRs (3 waves per
-// SIMD; 151 without spilling, 171 unbounded).
+// where one wave is alone on its CU (hnsw_nst). Capping it at 3 waves per SIMD
+// (151 VGPRs instead of 171) made it slower although LDS sets the waves per CU
+// there (4M x 768: ef 1600 22.8k -> 19.5k QPS, ef 3200 8.8k -> 7.4k;
+// scripts/exp/exp_hnsw_variants.sh, profiles/r05_hnsw_variants_ab.txt).
+#ifndef RVX_ST_WPE
+#define RVX_ST_WPE
+#endif
 template <int METRIC, int NST>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_hnsw_search_st(SearchArgs a) {
+__global__ __launch_bounds__(64) RVX_ST_WPE void k_hnsw_search_st(SearchArgs a) {
     search_body<METRIC, ROW_BATCH, NST>(a);
 }
 // ef past one wave's LDS: R in HBM (one distance stage when coop).
