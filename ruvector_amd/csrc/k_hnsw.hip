@@ -267,13 +267,6 @@ template <int METRIC, int NST = 1>
 __global__ __launch_bounds__(64) void k_hnsw_search_rg(SearchArgs a) {
     search_body<METRIC, ROW_BATCH, NST, true>(a);
 }
-// RG over LDS-staged rows at 4 waves per SIMD (R out of LDS leaves 19.5 KB per wave, so
-// registers set the waves per CU: 161 VGPRs -> 3 per SIMD; the per-lane row batches only
-// serve the upper layers' few distances and shrink to 4 float4s)
-template <int METRIC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_hnsw_search_rg4(SearchArgs a) {
-    search_body<METRIC, 4, 2, true>(a);
-}
 
 }  // namespace
 
@@ -427,14 +420,7 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     }
     const char* t = tag ? tag : "hnsw_search";
     const bool short_rows = !coop && d <= 256 && env_int("RVX_HNSW_SHORT", 1);  // read per call: tests cover both
-    if (rg && coop && hnsw_rg_nst() == 2 && env_int("RVX_HNSW_RG4", 0)) {
-        switch (metric) {
-            case RVX_METRIC_L2: RVX_LAUNCH(t, k_hnsw_search_rg4<RVX_METRIC_L2>, dim3(nslots), dim3(64), lds, a); break;
-            case RVX_METRIC_COSINE: RVX_LAUNCH(t, k_hnsw_search_rg4<RVX_METRIC_COSINE>, dim3(nslots), dim3(64), lds, a); break;
-            case RVX_METRIC_DOT: RVX_LAUNCH(t, k_hnsw_search_rg4<RVX_METRIC_DOT>, dim3(nslots), dim3(64), lds, a); break;
-            default: RVX_LAUNCH(t, k_hnsw_search_rg4<RVX_METRIC_L1>, dim3(nslots), dim3(64), lds, a); break;
-        }
-    } else if (rg && coop && hnsw_rg_nst() == 2) {
+    if (rg && coop && hnsw_rg_nst() == 2) {
         switch (metric) {
             case RVX_METRIC_L2: RVX_LAUNCH(t, (k_hnsw_search_rg<RVX_METRIC_L2, 2>), dim3(nslots), dim3(64), lds, a); break;
             case RVX_METRIC_COSINE: RVX_LAUNCH(t, (k_hnsw_search_rg<RVX_METRIC_COSINE, 2>), dim3(nslots), dim3(64), lds, a); break;
