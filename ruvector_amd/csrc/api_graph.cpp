@@ -764,6 +764,20 @@ rvx_status rvx_row_image_pack(const rvx_buffer* x, int64_t n_total, int64_t r0, 
 }
 
 namespace {
+// Page-locked host words per device (the exchange's small device-to-host reads that the host
+// picks up later without stalling the stream); callers hold the device's ComputeLock.
+unsigned long long* pinned_words(int64_t n) {
+    static std::mutex mu;
+    static std::map<int, std::pair<unsigned long long*, int64_t>> held;
+    std::lock_guard<std::mutex> lk(mu);
+    auto& h = held[device().id];
+    if (h.second < n) {
+        if (h.first) RVX_HIP(hipHostFree(h.first));
+        RVX_HIP(hipHostMalloc((void**)&h.first, (size_t)n * 8, 0));
+        h.second = n;
+    }
+    return h.first;
+}
 // the broadcast buffer of the dense-row pass: cnt ids (int64), then their rows
 float* ids_rows(int64_t* ids, int64_t cnt) { return reinterpret_cast<float*>(ids + cnt); }
 }  // namespace
@@ -875,9 +889,8 @@ rvx_status rvx_sage_forward_exchange3(const rvx_sage_layer* l, const rvx_graph* 
         // the all-gathered chunk-0 record bytes land in pinned host memory; with more than one
         // round the host reads them at round 1 (chunk 1 already queued), so the GPU never idles
         // on this wait, and round 0's exchange goes out then
-        static unsigned long long* pinned = nullptr;
-        if (xallow && rate_env <= 0 && !pinned) RVX_HIP(hipHostMalloc((void**)&pinned, 2 * 8 * 1024, 0));
         RVX_REQUIRE(!xallow || world <= 1024, RVX_ERR_INVALID_PARAMETER, "compact exchange: at most 1024 ranks");
+        unsigned long long* pinned = xallow && rate_env <= 0 ? pinned_words(2 * 1024) : nullptr;
         bool rate_pending = false;
         auto settle_rate = [&]() {  // xfer holds the chunk-0 count, its all-gather and the copy
             RVX_HIP(hipStreamSynchronize(d.xfer));
