@@ -527,10 +527,18 @@ def test_gcn_matches_oracle(weighted):
 
 
 # ------------------------------------------------------------------ RuvectorLayer
-def _layer_and_weights(in_dim, hidden, heads, dropout, seed=1):
+_RVL_WEIGHTS = {}  # the oracle's copy of a seeded layer's weights (a 768-wide layer's JSON takes seconds)
+
+
+def _layer_and_weights(in_dim, hidden, heads, dropout, seed=1, fresh_json=False):
     layer = rv.RuvectorLayer(in_dim, hidden, heads, dropout, seed=seed)
-    js = json.loads(layer.to_json())
-    return layer, O.RvlWeights(js), js
+    if fresh_json:  # the caller edits the JSON
+        js = json.loads(layer.to_json())
+        return layer, O.RvlWeights(js), js
+    key = (in_dim, hidden, heads, dropout, seed)
+    if key not in _RVL_WEIGHTS:
+        _RVL_WEIGHTS[key] = O.RvlWeights(json.loads(layer.to_json()))
+    return layer, _RVL_WEIGHTS[key], None
 
 
 def test_ruvector_layer_errors():
@@ -563,7 +571,7 @@ def test_ruvector_forward_one_weight_edge_cases():
 
 
 def test_ruvector_json_roundtrip_is_exact():
-    layer, W, js = _layer_and_weights(8, 16, 2, 0.25, seed=3)
+    layer, W, js = _layer_and_weights(8, 16, 2, 0.25, seed=3, fresh_json=True)
     again = rv.RuvectorLayer.from_json(layer.to_json())
     node = O.fill_uniform(8, 1)
     nbrs = list(O.fill_uniform(3 * 8, 2).reshape(3, 8))
@@ -600,7 +608,7 @@ def test_ruvector_forward_graph_folded_attention(monkeypatch, hidden, heads, deg
     (incl. isolated rows and nonzero biases) within 1e-5 of the oracle's
     per-pair K/V evaluation, and of the unfolded GPU path."""
     n = 300
-    layer, W, js = _layer_and_weights(hidden, hidden, heads, 0.1, seed=11)
+    layer, W, js = _layer_and_weights(hidden, hidden, heads, 0.1, seed=11, fresh_json=True)
     # nonzero attention biases so the folded b_k / b_v terms are exercised
     for name in ("q_linear", "k_linear", "v_linear"):
         b = js["attention"][name]["bias"]
