@@ -530,6 +530,9 @@ __device__ __forceinline__ int rank_in_r(const float* rd, const int* ri, int n, 
 #ifndef RVX_MERGE_LDS_G
 #define RVX_MERGE_LDS_G 2
 #endif
+#ifndef RVX_MERGE_RG_G
+#define RVX_MERGE_RG_G 8
+#endif
 template <int MERGE_GROUP = RVX_MERGE_LDS_G>
 __device__ __forceinline__ int merge_into_r(float* rd, int* ri, int n, const float* sd, const int* si, int na, int nkeep,
                                             int lane) {

@@ -132,7 +132,7 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
             const unsigned long long adm = decide_batch(fmask, dd, nid, ef, rd, ri, rs, r, lane);
             const int na = sort_batch(adm, dd, nid, sdb, sib, lane);
             if (na == 0) continue;
-            scan = min(scan, merge_into_r<RG ? 8 : RVX_MERGE_LDS_G>(rd, ri, rs, sdb, sib, na, r, lane));
+            scan = min(scan, merge_into_r<RG ? RVX_MERGE_RG_G : RVX_MERGE_LDS_G>(rd, ri, rs, sdb, sib, na, r, lane));
             if constexpr (RG) __threadfence_block();
             rs = r;
         }

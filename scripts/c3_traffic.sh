@@ -2,6 +2,7 @@
 # C3 leg (bench_c3.py: 10M x 768 HNSW M 32 / ef_c 200, ef sweep 100/400/1600, NeuralSearch) under
 # rocprofv3: kernel trace + stats, then one --pmc pass for FETCH_SIZE and one for WRITE_SIZE
 # (separate runs), reduced per ef by scripts/pmc_traffic.py --c3. A failure stops the script.
+# C3_EFS overrides the ef list (the bench leg's 100,400,1600; 8192 and 12288 run R in HBM).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOTDIR=$(pwd)
@@ -11,7 +12,7 @@ run() {  # $1 tag, rest: rocprofv3 options
   local tag=$1; shift
   rm -rf "gpurun_out/c3_$tag"
   timeout -k 10 540 rocprofv3 "$@" -d "$ROOTDIR/gpurun_out/c3_$tag" -o run --output-format csv -- \
-      python3 -u bench_c3.py --ef 100,400,1600 --no-cpu --check 0 > "gpurun_out/c3_${tag}.json" 2> "gpurun_out/c3_${tag}.log"
+      python3 -u bench_c3.py --ef "${C3_EFS:-100,400,1600}" --no-cpu --check 0 > "gpurun_out/c3_${tag}.json" 2> "gpurun_out/c3_${tag}.log"
   local rc=$?
   if [ $rc -ne 0 ]; then echo "c3 $tag failed rc=$rc"; tail -5 "gpurun_out/c3_${tag}.log"; exit 1; fi
   echo "c3 $tag ok"
