@@ -56,6 +56,20 @@ struct SearchArgs {
     int* rg_i;         // ... and flagged ids (ef past one wave's LDS)
 };
 
+// Diagnostic build only (-DRVX_HNSW_PHASES, scripts/exp/build_variant.sh): shader-clock cycles
+// of each layer-0 phase summed over waves into stats[2..7] — 0 find the next unexpanded entry,
+// 1 claim neighbours, 2 distances, 3 admission decisions + batch sort, 4 merge into R.
+#ifdef RVX_HNSW_PHASES
+#define PH_MARK(k)                                              \
+    do {                                                        \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        ph[k] += t_ - ph_t;                                     \
+        ph_t = t_;                                              \
+    } while (0)
+#else
+#define PH_MARK(k) do {} while (0)
+#endif
+
 // RB: float4s per streamed row batch of the per-lane distances (hnsw_dev.hpp
 // stream_acc); NST: LDS stages of the wave-cooperative distances. RG: the result list R
 // lives in a per-slot HBM scratch row instead of LDS (ef beyond what one wave's 160 KB
@@ -90,6 +104,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     unsigned* vb = a.vbits ? a.vbits + (int64_t)blockIdx.x * a.vwords : nullptr;
 
     unsigned long long n_dist = 0, n_expand = 0;  // lane 0's tallies for this wave
+#ifdef RVX_HNSW_PHASES
+    unsigned long long ph[5] = {0, 0, 0, 0, 0}, ph_t = __builtin_amdgcn_s_memtime();
+#endif
     for (int64_t qi = blockIdx.x; qi < a.nq; qi += a.nslots) {
         const unsigned long long qtag = (unsigned long long)(qi + 1) << 32;
         for (int i = lane; i < dq; i += 64) qs[i] = (i < a.d) ? a.q[qi * a.d + i] : 0.0f;
@@ -181,6 +198,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             __builtin_amdgcn_wave_barrier();
         }
         int scan = 0;  // every entry of R before `scan` is expanded
+#ifdef RVX_HNSW_PHASES
+        ph_t = __builtin_amdgcn_s_memtime();
+#endif
         for (;;) {
             int at = -1;
             for (int b0 = scan; b0 < rs; b0 += 64) {
@@ -196,6 +216,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             scan = at + 1;
             const int64_t b = a.g.rp0[c_id], e = a.g.rp0[c_id + 1];
             n_expand += 1;
+            PH_MARK(0);
             for (int64_t c0 = b; c0 < e; c0 += 64) {
                 const int64_t p = c0 + lane;
                 int nid = -1;
@@ -205,17 +226,21 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
                     fresh = claim(nid);
                 }
                 const unsigned long long fmask = __ballot(fresh);
+                PH_MARK(1);
                 if (!fmask) continue;
                 const float dd = dist_lane(fresh ? nid : -1);
+                PH_MARK(2);
                 n_dist += (unsigned long long)__popcll(fmask);
                 // admission in neighbour order (hnsw.rs:1004-1046), batched exactly
                 int r = rs;
                 const unsigned long long adm = decide_batch(fmask, dd, nid, ef, rd, ri, rs, r, lane);
                 const int na = sort_batch(adm, dd, nid, sdb, sib, lane);
+                PH_MARK(3);
                 if (na == 0) continue;
                 scan = min(scan, merge_into_r<RG ? RVX_MERGE_RG_G : RVX_MERGE_LDS_G>(rd, ri, rs, sdb, sib, na, r, lane));
                 if constexpr (RG) __threadfence_block();
                 rs = r;
+                PH_MARK(4);
             }
         }
 
@@ -231,6 +256,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     if (lane == 0 && a.stats) {
         atomicAdd(&a.stats[0], n_dist + 2);  // + the entry point's distance and layer 0's start
         atomicAdd(&a.stats[1], n_expand);
+#ifdef RVX_HNSW_PHASES
+        for (int k = 0; k < 5; ++k) atomicAdd(&a.stats[2 + k], ph[k]);
+#endif
     }
 }
 
@@ -464,8 +492,16 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     int st[32] = {0};
     RVX_HIP(hipMemcpyAsync(st, status, sizeof(st), hipMemcpyDeviceToHost, stream()));
     sync();
-    unsigned long long tally[2];
+    unsigned long long tally[7];
     std::memcpy(tally, st + 16, sizeof(tally));
+#ifdef RVX_HNSW_PHASES
+    {
+        const double tot = (double)(tally[2] + tally[3] + tally[4] + tally[5] + tally[6]);
+        std::fprintf(stderr, "[hnsw phases] ef %d rg %d: next %.3f claim %.3f dist %.3f decide %.3f merge %.3f "
+                     "(cycles per expansion %.0f)\n", ef, rg ? 1 : 0, tally[2] / tot, tally[3] / tot, tally[4] / tot,
+                     tally[5] / tot, tally[6] / tot, tot / (double)std::max<unsigned long long>(tally[1], 1));
+    }
+#endif
     g_search_stats.n_dist = (int64_t)tally[0];
     g_search_stats.n_expand = (int64_t)tally[1];
     g_search_stats.nq = nq;
