@@ -423,19 +423,50 @@ __device__ __forceinline__ unsigned long long decide_batch(unsigned long long fm
     return adm;
 }
 
+// The same admissions decided in parallel (R in LDS). Sequentially (hnsw.rs:1004-1046) fresh
+// neighbour i enters R iff |R| < ef or it precedes R's farthest. While R is full its farthest
+// never grows, and a refused neighbour is at or beyond it, so the refused ones never precede a
+// later admitted one: neighbour i enters iff fewer than ef entries of R_0 ∪ {fresh j < i}
+// precede it — its rank in R_0 (a binary search in LDS, every lane at once) plus the earlier
+// fresh neighbours before it (one pass of wave-uniform lane reads). Same admissions as
+// decide_batch for distinct (d, id) pairs (R never holds a fresh node); callers keep
+// decide_batch when a distance is NaN. rk: the lane's rank in R_0 (merge_into_r reuses it).
+__device__ __forceinline__ int rank_in_r(const float* rd, const int* ri, int n, float d, int id);
+__device__ __forceinline__ unsigned long long decide_par(unsigned long long fmask, float dd, int nid, int ef,
+                                                         const float* rd, const int* ri, int rs, int& r, int& rk,
+                                                         int lane) {
+    const bool mine = (fmask >> lane) & 1ull;
+    rk = mine ? rank_in_r(rd, ri, rs, dd, nid) : 0;
+    int before = 0;
+    for (unsigned long long t = fmask; t; t &= t - 1) {
+        const int o = __ffsll((long long)t) - 1;
+        const float od = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dd), o));
+        const int oi = __builtin_amdgcn_readlane(nid, o);
+        before += (o < lane && lt_de(od, oi, dd, nid)) ? 1 : 0;
+    }
+    const unsigned long long adm = __ballot(mine && rk + before < ef);
+    r = min(ef, rs + __popcll(adm));
+    return adm;
+}
+
 // The admitted lanes' (d, id) sorted ascending into the scratch (sd, si)[0..na).
-__device__ __forceinline__ int sort_batch(unsigned long long adm, float dd, int nid, float* sd, int* si, int lane) {
+// srk (nullable): also each entry's rank in R (decide_par's rk) at its sorted position.
+__device__ __forceinline__ int sort_batch(unsigned long long adm, float dd, int nid, float* sd, int* si, int lane,
+                                          int* srk = nullptr, int rk = 0) {
     const int na = __popcll(adm);
     if (na == 0) return 0;
     const bool mine = (adm >> lane) & 1ull;
     int rank = 0;
     for (unsigned long long t = adm; t; t &= t - 1) {
         const int o = __ffsll((long long)t) - 1;
-        const float od = __shfl(dd, o);
-        const int oi = __shfl(nid, o);
+        const float od = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dd), o));
+        const int oi = __builtin_amdgcn_readlane(nid, o);
         rank += lt_de(od, oi, dd, nid) ? 1 : 0;
     }
-    if (mine) { sd[rank] = dd; si[rank] = nid; }
+    if (mine) {
+        sd[rank] = dd; si[rank] = nid;
+        if (srk) srk[rank] = rk;
+    }
     __builtin_amdgcn_wave_barrier();
     return na;
 }
@@ -535,9 +566,9 @@ __device__ __forceinline__ int rank_in_r(const float* rd, const int* ri, int n, 
 #endif
 template <int MERGE_GROUP = RVX_MERGE_LDS_G>
 __device__ __forceinline__ int merge_into_r(float* rd, int* ri, int n, const float* sd, const int* si, int na, int nkeep,
-                                            int lane) {
+                                            int lane, const int* srk = nullptr) {
     float bd = 0.f; int bi = 0, rk = INT_MAX;
-    if (lane < na) { bd = sd[lane]; bi = si[lane]; rk = rank_in_r(rd, ri, n, bd, bi); }
+    if (lane < na) { bd = sd[lane]; bi = si[lane]; rk = srk ? srk[lane] : rank_in_r(rd, ri, n, bd, bi); }
     const int first = __shfl(rk, 0);
     __builtin_amdgcn_wave_barrier();
     for (int top = ((n - 1) / 64) * 64; top >= 0 && top + 63 >= first; top -= 64 * MERGE_GROUP) {

@@ -54,6 +54,7 @@ struct SearchArgs {
     int coop;          // wave-cooperative LDS-staged distances (hnsw_dev.hpp wave_dist)
     float* rg_d;       // RG kernels: R in HBM, [nslots][ef + 1] distances ...
     int* rg_i;         // ... and flagged ids (ef past one wave's LDS)
+    int par_decide;    // hnsw_dev.hpp decide_par where R is in LDS
 };
 
 // Diagnostic build only (-DRVX_HNSW_PHASES, scripts/exp/build_variant.sh): shader-clock cycles
@@ -98,6 +99,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         sdb = reinterpret_cast<float*>(ri + ef + 1);
     }
     int* sib = reinterpret_cast<int*>(sdb + 64);
+    int* srk = sib + 64;  // the admitted batch's ranks in R (decide_par; R in LDS)
 
     unsigned long long* vis = a.vbits ? nullptr : a.visited + (int64_t)blockIdx.x * a.vcap;
     const unsigned vmask = a.vcap - 1;
@@ -232,12 +234,18 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
                 PH_MARK(2);
                 n_dist += (unsigned long long)__popcll(fmask);
                 // admission in neighbour order (hnsw.rs:1004-1046), batched exactly
-                int r = rs;
-                const unsigned long long adm = decide_batch(fmask, dd, nid, ef, rd, ri, rs, r, lane);
-                const int na = sort_batch(adm, dd, nid, sdb, sib, lane);
+                int r = rs, rk = 0;
+                // R in LDS: admissions decided in parallel (decide_par), the ranks reused by the
+                // merge; R in HBM (binary searches there cost round trips) or a NaN distance: the
+                // sequential window (RVX_HNSW_PAR_DECIDE=0 keeps it everywhere)
+                const bool par = !RG && a.par_decide && !__ballot(((fmask >> lane) & 1ull) && dd != dd);
+                const unsigned long long adm = par ? decide_par(fmask, dd, nid, ef, rd, ri, rs, r, rk, lane)
+                                                   : decide_batch(fmask, dd, nid, ef, rd, ri, rs, r, lane);
+                const int na = sort_batch(adm, dd, nid, sdb, sib, lane, par ? srk : nullptr, rk);
                 PH_MARK(3);
                 if (na == 0) continue;
-                scan = min(scan, merge_into_r<RG ? RVX_MERGE_RG_G : RVX_MERGE_LDS_G>(rd, ri, rs, sdb, sib, na, r, lane));
+                scan = min(scan, merge_into_r<RG ? RVX_MERGE_RG_G : RVX_MERGE_LDS_G>(rd, ri, rs, sdb, sib, na, r, lane,
+                                                                                  par ? srk : nullptr));
                 if constexpr (RG) __threadfence_block();
                 rs = r;
                 PH_MARK(4);
@@ -330,7 +338,7 @@ bool hnsw_coop(int metric, int d, int64_t rows) {
 namespace {
 size_t search_lds_nst(int d, int ef, int nst) {
     const int dq = (d + 3) & ~3;
-    return (size_t)wd_lds(nst) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 8;
+    return (size_t)wd_lds(nst) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 12;
 }
 }  // namespace
 
@@ -346,7 +354,7 @@ int hnsw_nst(bool coop, int d, int ef) {
 
 size_t hnsw_search_lds(int d, int ef, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)wd_lds(hnsw_nst(coop, d, ef)) : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 8;
+    return (coop ? (size_t)wd_lds(hnsw_nst(coop, d, ef)) : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 12;
 }
 // LDS of the RG kernel: distance stage + query + admitted batch (R is in HBM)
 // distance stages of the RG kernel, 2 unless RVX_HNSW_RG_NST=1 (read per call): with R out
@@ -354,7 +362,7 @@ size_t hnsw_search_lds(int d, int ef, bool coop) {
 int hnsw_rg_nst() { return env_int("RVX_HNSW_RG_NST", 2) == 1 ? 1 : 2; }
 size_t hnsw_search_lds_rg(int d, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)wd_lds(hnsw_rg_nst()) : 0) + (size_t)dq * 4 + 64 * 8;
+    return (coop ? (size_t)wd_lds(hnsw_rg_nst()) : 0) + (size_t)dq * 4 + 64 * 12;
 }
 
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
@@ -419,7 +427,7 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         rg_i = (int*)scratch_bytes("hnsw_rg_i", (int64_t)nslots * (ef + 1) * 4);
     }
     SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, vbits, vwords, nslots, vcap, out_d, out_i, out_n, status, stats,
-                 curv, hyper, coop ? 1 : 0, rg_d, rg_i};
+                 curv, hyper, coop ? 1 : 0, rg_d, rg_i, env_int("RVX_HNSW_PAR_DECIDE", 1) != 0 ? 1 : 0};
     const size_t lds = rg ? hnsw_search_lds_rg(d, coop) : hnsw_search_lds(d, ef, coop);
     RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension too large for one wave's LDS");
     static bool attr = false;

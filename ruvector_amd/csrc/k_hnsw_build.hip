@@ -128,11 +128,16 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
                 dd = row_dist<METRIC>(qs, a.x + (int64_t)nid * a.d, a.d, qn,
                                       METRIC == RVX_METRIC_COSINE ? a.xnorm[nid] : 0.0f, a.curv);
             }
-            int r = rs;
-            const unsigned long long adm = decide_batch(fmask, dd, nid, ef, rd, ri, rs, r, lane);
-            const int na = sort_batch(adm, dd, nid, sdb, sib, lane);
+            int r = rs, rk = 0;
+            // parallel admissions where R is in LDS (hnsw_dev.hpp decide_par, as the search)
+            int* srk = sib + MAX_C0;
+            const bool par = !RG && !__ballot(((fmask >> lane) & 1ull) && dd != dd);
+            const unsigned long long adm = par ? decide_par(fmask, dd, nid, ef, rd, ri, rs, r, rk, lane)
+                                               : decide_batch(fmask, dd, nid, ef, rd, ri, rs, r, lane);
+            const int na = sort_batch(adm, dd, nid, sdb, sib, lane, par ? srk : nullptr, rk);
             if (na == 0) continue;
-            scan = min(scan, merge_into_r<RG ? RVX_MERGE_RG_G : RVX_MERGE_LDS_G>(rd, ri, rs, sdb, sib, na, r, lane));
+            scan = min(scan, merge_into_r<RG ? RVX_MERGE_RG_G : RVX_MERGE_LDS_G>(rd, ri, rs, sdb, sib, na, r, lane,
+                                                                              par ? srk : nullptr));
             if constexpr (RG) __threadfence_block();
             rs = r;
         }
@@ -368,7 +373,8 @@ __global__ __launch_bounds__(256) void k_build_merge(BuildArgs a, int nrec) {
 
 size_t build_lds_bytes(int d, int ef, bool coop, bool rg = false, int nst = 2) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)wd_lds(nst) : 0) + (size_t)dq * 4 + (rg ? 0 : (size_t)(ef + 1) * 8) + (size_t)MAX_C0 * 8;
+    return (coop ? (size_t)wd_lds(nst) : 0) + (size_t)dq * 4 + (rg ? 0 : (size_t)(ef + 1) * 8) + (size_t)MAX_C0 * 8 +
+           64 * 4;  // + the admitted batch's ranks in R
 }
 
 void build_insert_batch(const BuildGraph& G, int metric, const float* x, const float* xnorm, int d,
