@@ -362,7 +362,7 @@ size_t hnsw_search_lds(int d, int ef, bool coop) {
 int hnsw_rg_nst() { return env_int("RVX_HNSW_RG_NST", 2) == 1 ? 1 : 2; }
 size_t hnsw_search_lds_rg(int d, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)wd_lds(hnsw_rg_nst()) : 0) + (size_t)dq * 4 + 64 * 12;
+    return (coop ? (size_t)wd_lds(hnsw_rg_nst()) : 0) + (size_t)dq * 4 + 64 * 8;  // (no srk: decide_batch)
 }
 
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
