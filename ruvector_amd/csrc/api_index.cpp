@@ -557,6 +557,8 @@ rvx_status rvx_scan_last_stats(int64_t* mfma_queries, int64_t* valu_queries, int
 
 rvx_status rvx_hnsw_last_search_stats(int64_t* n_dist, int64_t* n_expand, int64_t* nq) {
     return guard([&] {
+        ComputeLock cl;
+        hnsw_search_stats_settle();
         if (n_dist) *n_dist = g_search_stats.n_dist;
         if (n_expand) *n_expand = g_search_stats.n_expand;
         if (nq) *nq = g_search_stats.nq;

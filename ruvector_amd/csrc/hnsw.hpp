@@ -46,5 +46,7 @@ struct SearchStats {
     int32_t visited_bitmap = 0, slots = 0;  // visited-set form and search slots of the launch
 };
 extern SearchStats g_search_stats;
+// The last search's device tallies (n_dist, n_expand) into g_search_stats (waits for the search).
+void hnsw_search_stats_settle();
 
 }  // namespace rvx

@@ -26,6 +26,7 @@
 // The visited set is an open-addressing hash in a per-wave global scratch slot
 // (CAS-claimed by all lanes at once); neighbour distances are one row per lane.
 #include <cstring>
+#include <map>
 
 #include "common.hpp"
 #include "graph.hpp"
@@ -309,6 +310,21 @@ __global__ __launch_bounds__(64) void k_hnsw_search_rg(SearchArgs a) {
 SearchStats g_search_stats;
 
 namespace {
+struct SearchTally {
+    unsigned long long* host = nullptr;  // [7]: distance evaluations, expansions, (phase cycles)
+    bool pending = false;
+};
+SearchTally& search_tally() {  // per device (callers hold its ComputeLock)
+    static std::mutex mu;
+    static std::map<int, SearchTally> t;
+    std::lock_guard<std::mutex> lk(mu);
+    SearchTally& s = t[device().id];
+    if (!s.host) RVX_HIP(hipHostMalloc((void**)&s.host, 8 * 8, 0));
+    return s;
+}
+}  // namespace
+
+namespace {
 template <int NST>
 void set_st_attr() {
     RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_st<RVX_METRIC_L2, NST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -497,24 +513,33 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         case RVX_METRIC_HYP_L2: RVX_LAUNCH(t, k_hnsw_search<RVX_METRIC_HYP_L2>, dim3(nslots), dim3(64), lds, a); break;
         default: fail(RVX_ERR_UNSUPPORTED, "metric not supported by HNSW search");
     }
-    int st[32] = {0};
-    RVX_HIP(hipMemcpyAsync(st, status, sizeof(st), hipMemcpyDeviceToHost, stream()));
-    sync();
-    unsigned long long tally[7];
-    std::memcpy(tally, st + 16, sizeof(tally));
+    // the work tallies reach page-locked host memory behind the search; the search itself returns
+    // with its work queued (no host wait) and rvx_hnsw_last_search_stats settles them on demand
+    SearchTally& tl = search_tally();
+    RVX_HIP(hipMemcpyAsync(tl.host, stats, 7 * 8, hipMemcpyDeviceToHost, stream()));
+    tl.pending = true;
+    g_search_stats.nq = nq;
+    g_search_stats.visited_bitmap = bitmap ? 1 : 0;
+    g_search_stats.slots = nslots;
 #ifdef RVX_HNSW_PHASES
     {
+        sync();
+        const unsigned long long* tally = tl.host;
         const double tot = (double)(tally[2] + tally[3] + tally[4] + tally[5] + tally[6]);
         std::fprintf(stderr, "[hnsw phases] ef %d rg %d: next %.3f claim %.3f dist %.3f decide %.3f merge %.3f "
                      "(cycles per expansion %.0f)\n", ef, rg ? 1 : 0, tally[2] / tot, tally[3] / tot, tally[4] / tot,
                      tally[5] / tot, tally[6] / tot, tot / (double)std::max<unsigned long long>(tally[1], 1));
     }
 #endif
-    g_search_stats.n_dist = (int64_t)tally[0];
-    g_search_stats.n_expand = (int64_t)tally[1];
-    g_search_stats.nq = nq;
-    g_search_stats.visited_bitmap = bitmap ? 1 : 0;
-    g_search_stats.slots = nslots;
+}
+
+void hnsw_search_stats_settle() {
+    SearchTally& tl = search_tally();
+    if (!tl.pending) return;
+    sync();
+    g_search_stats.n_dist = (int64_t)tl.host[0];
+    g_search_stats.n_expand = (int64_t)tl.host[1];
+    tl.pending = false;
 }
 
 }  // namespace rvx
