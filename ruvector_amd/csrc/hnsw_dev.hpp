@@ -141,10 +141,26 @@ __device__ __forceinline__ void wd_fill(const float* __restrict__ x, int d, cons
     }
 }
 
-template <int METRIC>
+// QC: qs is the query row in global memory, read through the constant address space, so
+// the wave-uniform reads are scalar loads (lgkmcnt, not vmcnt: the DMA accounting below stays
+// exact) and the query needs no LDS; else qs is the query staged in LDS.
+template <int METRIC, bool QC = false>
 __device__ __forceinline__ float wd_chunk(float acc, const float* qs, int c, int lane, const unsigned char* st) {
-    const float4* qq = reinterpret_cast<const float4*>(qs + c * WD_CH);
     const int sw = (lane >> 1) & 7;
+    if constexpr (QC) {
+        typedef const __attribute__((address_space(4))) float cf;
+        cf* qq = (cf*)(qs + c * WD_CH);
+        float4 qv[WD_CH / 4];
+#pragma unroll
+        for (int p = 0; p < WD_CH / 4; ++p) qv[p] = make_float4(qq[4 * p], qq[4 * p + 1], qq[4 * p + 2], qq[4 * p + 3]);
+#pragma unroll
+        for (int p = 0; p < WD_CH / 4; ++p) {
+            const float4 v = *reinterpret_cast<const float4*>(st + lane * (WD_CH * 4) + ((p ^ sw) << 4));
+            acc = acc4<METRIC>(acc, qv[p], v);
+        }
+        return acc;
+    }
+    const float4* qq = reinterpret_cast<const float4*>(qs + c * WD_CH);
 #pragma unroll
     for (int p = 0; p < WD_CH / 4; ++p) {
         const float4 v = *reinterpret_cast<const float4*>(st + lane * (WD_CH * 4) + ((p ^ sw) << 4));
@@ -179,7 +195,7 @@ __device__ __forceinline__ void wd_wait_left(int left) {
     }
 }
 
-template <int METRIC, int NST = 2>
+template <int METRIC, int NST = 2, bool QC = false>
 __device__ __forceinline__ float wd_run(const float* __restrict__ x, int d, const float* qs, const int (&rid)[8], int lane,
                                         unsigned char* s0, unsigned char* s1) {
     const int nch = d / WD_CH;
@@ -201,7 +217,7 @@ __device__ __forceinline__ float wd_run(const float* __restrict__ x, int d, cons
             } else {
                 wd_wait_left<NST>(nch - 1 - c);
             }
-            acc = wd_chunk<METRIC>(acc, qs, c, lane, s0 + cur * WD_STAGE);
+            acc = wd_chunk<METRIC, QC>(acc, qs, c, lane, s0 + cur * WD_STAGE);
             cur = cur + 1 == NST ? 0 : cur + 1;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
@@ -211,7 +227,7 @@ __device__ __forceinline__ float wd_run(const float* __restrict__ x, int d, cons
         for (int c = 0; c < nch; ++c) {
             wd_fill<METRIC>(x, d, rid, c, lane, s0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            acc = wd_chunk<METRIC>(acc, qs, c, lane, s0);
+            acc = wd_chunk<METRIC, QC>(acc, qs, c, lane, s0);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
         return acc;
@@ -224,7 +240,7 @@ __device__ __forceinline__ float wd_run(const float* __restrict__ x, int d, cons
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        acc = wd_chunk<METRIC>(acc, qs, c, lane, s0);
+        acc = wd_chunk<METRIC, QC>(acc, qs, c, lane, s0);
         if (c + 1 >= nch) break;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (c + 2 < nch) {
@@ -233,21 +249,21 @@ __device__ __forceinline__ float wd_run(const float* __restrict__ x, int d, cons
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        acc = wd_chunk<METRIC>(acc, qs, c + 1, lane, s1);
+        acc = wd_chunk<METRIC, QC>(acc, qs, c + 1, lane, s1);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     return acc;
 }
 
 // All 64 lanes call together. row < 0: no row (the lane's result is garbage).
-template <int METRIC, int NST = 2>
+template <int METRIC, int NST = 2, bool QC = false>
 __device__ __forceinline__ float wave_dist(const float* qs, const float* __restrict__ x, int d, int row, float qn,
                                            float xn, unsigned char* stage, int lane) {
     int rid[8];
     const int mine = row < 0 ? 0 : row;
 #pragma unroll
     for (int i = 0; i < 8; ++i) rid[i] = __shfl(mine, 8 * i + (lane >> 3));
-    const float acc = wd_run<METRIC, NST>(x, d, qs, rid, lane, stage, stage + WD_STAGE);
+    const float acc = wd_run<METRIC, NST, QC>(x, d, qs, rid, lane, stage, stage + WD_STAGE);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stages are refilled by the next call
     return finish_dist<METRIC>(acc, qn, xn);
 }

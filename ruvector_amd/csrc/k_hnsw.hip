@@ -77,25 +77,28 @@ struct SearchArgs {
 // lives in a per-slot HBM scratch row instead of LDS (ef beyond what one wave's 160 KB
 // hold: 19,007 entries at d 768): the same code over global memory, with a workgroup
 // fence after each write phase so the other lanes' reads see it.
-template <int METRIC, int RB, int NST = 2, bool RG = false>
+// QG (LDS-staged distances only): the query is read from global memory through the constant
+// address space (hnsw_dev.hpp wd_chunk QC) instead of being staged in LDS.
+template <int METRIC, int RB, int NST = 2, bool RG = false, bool QG = false>
 __device__ __forceinline__ void search_body(const SearchArgs& a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     const int lane = threadIdx.x;
     const int ef = a.ef;
     constexpr bool COOP_OK = METRIC != RVX_METRIC_POINCARE && METRIC != RVX_METRIC_HYP_L2;
-    const bool coop = COOP_OK && a.coop;
+    const bool coop = COOP_OK && (QG || a.coop);
     unsigned char* wst = lds_raw;                                // [NST * WD_STAGE] distance stages (coop)
-    float* qs = reinterpret_cast<float*>(lds_raw + (coop ? wd_lds(NST) : 0));  // [d rounded to 4]
-    const int dq = (a.d + 3) & ~3;
+    float* qs_l = reinterpret_cast<float*>(lds_raw + (coop ? wd_lds(NST) : 0));  // [d rounded to 4]
+    const int dq = QG ? 0 : (a.d + 3) & ~3;
+    float* qs = qs_l;
     float* rd;                                                  // R dist [ef+1]
     int* ri;                                                    // R id | expanded flag (bit 31)
     float* sdb;                                                 // admitted batch [64]
     if constexpr (RG) {
         rd = a.rg_d + (int64_t)blockIdx.x * (ef + 1);
         ri = a.rg_i + (int64_t)blockIdx.x * (ef + 1);
-        sdb = qs + dq;
+        sdb = qs_l + dq;
     } else {
-        rd = qs + dq;
+        rd = qs_l + dq;
         ri = reinterpret_cast<int*>(rd + ef + 1);
         sdb = reinterpret_cast<float*>(ri + ef + 1);
     }
@@ -112,6 +115,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
 #endif
     for (int64_t qi = blockIdx.x; qi < a.nq; qi += a.nslots) {
         const unsigned long long qtag = (unsigned long long)(qi + 1) << 32;
+        if constexpr (QG) qs = const_cast<float*>(a.q) + qi * a.d;  // (read only)
         for (int i = lane; i < dq; i += 64) qs[i] = (i < a.d) ? a.q[qi * a.d + i] : 0.0f;
         if (vb)  // this query's bitmap starts empty
             for (int64_t w = 4 * lane; w < a.vwords; w += 256) *reinterpret_cast<uint4*>(vb + w) = make_uint4(0, 0, 0, 0);
@@ -135,7 +139,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             float dv;
             if constexpr (COOP_OK) {
                 if (coop) {
-                    dv = wave_dist<METRIC, NST>(qs, a.x, a.d, node, qn,
+                    dv = wave_dist<METRIC, NST, QG>(qs, a.x, a.d, node, qn,
                                            (METRIC == RVX_METRIC_COSINE && node >= 0) ? a.xnorm[node] : 0.0f, wst, lane);
                     return node >= 0 ? dv : INFINITY;
                 }
@@ -299,6 +303,11 @@ template <int METRIC, int NST>
 __global__ __launch_bounds__(64) RVX_ST_WPE void k_hnsw_search_st(SearchArgs a) {
     search_body<METRIC, ROW_BATCH, NST>(a);
 }
+// LDS-staged distances with the query read from global memory (QG): NST 1 / 2, R in LDS or HBM
+template <int METRIC, int NST, bool RG>
+__global__ __launch_bounds__(64) void k_hnsw_search_qg(SearchArgs a) {
+    search_body<METRIC, ROW_BATCH, NST, RG, true>(a);
+}
 // ef past one wave's LDS: R in HBM (one distance stage when coop).
 template <int METRIC, int NST = 1>
 __global__ __launch_bounds__(64) void k_hnsw_search_rg(SearchArgs a) {
@@ -331,6 +340,22 @@ void set_st_attr() {
     RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_st<RVX_METRIC_COSINE, NST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_st<RVX_METRIC_DOT, NST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_st<RVX_METRIC_L1, NST>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+}
+template <int NST, bool RG>
+void set_qg_attr() {
+    RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_qg<RVX_METRIC_L2, NST, RG>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_qg<RVX_METRIC_COSINE, NST, RG>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_qg<RVX_METRIC_DOT, NST, RG>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search_qg<RVX_METRIC_L1, NST, RG>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+}
+template <int NST, bool RG>
+void launch_qg(const char* t, int metric, int nslots, size_t lds, const SearchArgs& a) {
+    switch (metric) {
+        case RVX_METRIC_L2: RVX_LAUNCH(t, (k_hnsw_search_qg<RVX_METRIC_L2, NST, RG>), dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_COSINE: RVX_LAUNCH(t, (k_hnsw_search_qg<RVX_METRIC_COSINE, NST, RG>), dim3(nslots), dim3(64), lds, a); break;
+        case RVX_METRIC_DOT: RVX_LAUNCH(t, (k_hnsw_search_qg<RVX_METRIC_DOT, NST, RG>), dim3(nslots), dim3(64), lds, a); break;
+        default: RVX_LAUNCH(t, (k_hnsw_search_qg<RVX_METRIC_L1, NST, RG>), dim3(nslots), dim3(64), lds, a); break;
+    }
 }
 template <int NST>
 void launch_st(const char* t, int metric, int nslots, size_t lds, const SearchArgs& a) {
@@ -444,8 +469,20 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     }
     SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, vbits, vwords, nslots, vcap, out_d, out_i, out_n, status, stats,
                  curv, hyper, coop ? 1 : 0, rg_d, rg_i, env_int("RVX_HNSW_PAR_DECIDE", 1) != 0 ? 1 : 0};
-    const size_t lds = rg ? hnsw_search_lds_rg(d, coop) : hnsw_search_lds(d, ef, coop);
+    // RVX_HNSW_QG=1 (read per call): LDS-staged distances read the query from global memory (no LDS copy)
+    const int nst_sel = rg ? hnsw_rg_nst() : hnsw_nst(coop, d, ef);
+    const bool qg = coop && (rg ? nst_sel == 2 : (nst_sel == 1 || nst_sel == 2)) && env_int("RVX_HNSW_QG", 0) != 0 &&
+                    ((uintptr_t)q & 15) == 0;
+    const size_t lds = (rg ? hnsw_search_lds_rg(d, coop) : hnsw_search_lds(d, ef, coop)) -
+                       (qg ? (size_t)((d + 3) & ~3) * 4 : 0);
     RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension too large for one wave's LDS");
+    static bool attr_qg = false;
+    if (!attr_qg) {
+        set_qg_attr<1, false>();
+        set_qg_attr<2, false>();
+        set_qg_attr<2, true>();
+        attr_qg = true;
+    }
     static bool attr = false;
     if (!attr) {
         RVX_HIP(hipFuncSetAttribute((const void*)k_hnsw_search<RVX_METRIC_L2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -472,7 +509,11 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     }
     const char* t = tag ? tag : "hnsw_search";
     const bool short_rows = !coop && d <= 256 && env_int("RVX_HNSW_SHORT", 1);  // read per call: tests cover both
-    if (rg && coop && hnsw_rg_nst() == 2) {
+    if (qg) {
+        if (rg) launch_qg<2, true>(t, metric, nslots, lds, a);
+        else if (nst_sel == 1) launch_qg<1, false>(t, metric, nslots, lds, a);
+        else launch_qg<2, false>(t, metric, nslots, lds, a);
+    } else if (rg && coop && hnsw_rg_nst() == 2) {
         switch (metric) {
             case RVX_METRIC_L2: RVX_LAUNCH(t, (k_hnsw_search_rg<RVX_METRIC_L2, 2>), dim3(nslots), dim3(64), lds, a); break;
             case RVX_METRIC_COSINE: RVX_LAUNCH(t, (k_hnsw_search_rg<RVX_METRIC_COSINE, 2>), dim3(nslots), dim3(64), lds, a); break;

@@ -18,7 +18,7 @@ n, d = int(os.environ.get("N", 10_000_000)), 768
 efs = [int(e) for e in os.environ.get("EFS", "100,800,3200,8192,12288,16384").split(",")]
 # ";"-separated environment settings, each "VAR=VAL,VAR=VAL" (empty: the defaults)
 configs = os.environ.get("CONFIGS", ";RVX_HNSW_NST=2;RVX_HNSW_RG=1;RVX_HNSW_RG=1,RVX_HNSW_RG_NST=2").split(";")
-KNOBS = ("RVX_HNSW_NST", "RVX_HNSW_RG", "RVX_HNSW_RG_NST")
+KNOBS = ("RVX_HNSW_NST", "RVX_HNSW_RG", "RVX_HNSW_RG_NST", "RVX_HNSW_QG")
 log = lambda s: print(s, file=sys.stderr, flush=True)  # noqa: E731
 xb = rv.Buffer(n * d * 4)
 xb.fill_normal(n * d, 5)

@@ -231,6 +231,28 @@ def test_hnsw_search_auto_hbm_r_coop_bit_exact(monkeypatch, rg_nst, d, metric):
         assert np.array_equal(dist, rd)
 
 
+@pytest.mark.parametrize("mode", ["nst1", "nst2", "rg"])
+@pytest.mark.parametrize("d,metric", [(32, "l2"), (224, "l2"), (96, "cosine")])
+def test_hnsw_search_query_global_bit_exact(monkeypatch, mode, d, metric):
+    # RVX_HNSW_QG=1: the LDS-staged distances read the query through scalar loads from
+    # global memory instead of an LDS copy (k_hnsw.hip k_hnsw_search_qg), R in LDS or HBM
+    monkeypatch.setenv("RVX_HNSW_COOP", "2")
+    monkeypatch.setenv("RVX_HNSW_QG", "1")
+    monkeypatch.setenv("RVX_HNSW_NST", "1" if mode == "nst1" else "2")
+    monkeypatch.setenv("RVX_HNSW_RG", "1" if mode == "rg" else "0")
+    monkeypatch.setenv("RVX_HNSW_RG_NST", "2")
+    if (d, metric) not in _RING_PAIRS:
+        _RING_PAIRS[(d, metric)] = _hnsw_pair(3000, d, metric, 8, 60, 13)
+    x, h, g, idx = _RING_PAIRS[(d, metric)]
+    q = O.fill_uniform(48 * d, 16).reshape(48, d)
+    for k, ef in ((10, 64), (20, 1200), (300, 2900)):
+        ids, dist, cnt = idx.search_array(q, k, ef)
+        rids, rd, rc = h.search(q, k, ef)
+        assert np.array_equal(cnt, rc)
+        assert np.array_equal(ids.astype(np.int64)[:, :k], rids)
+        assert np.array_equal(dist, rd)
+
+
 def test_hnsw_search_tie_heavy_bit_exact():
     # 3000 points on 12 distinct vectors: hundreds of exact distance ties at R's
     # farthest (the round-1 candidate list overflowed here and raised RVX_ERR_INDEX);
