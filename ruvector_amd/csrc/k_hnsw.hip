@@ -413,15 +413,23 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     RVX_REQUIRE(ef >= 1 && ef <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER,
                 "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
     // R in LDS when one wave's 160 KB hold it, else in HBM. The LDS-staged (coop) search also
-    // takes the HBM R once an LDS R would leave fewer than 3 waves per CU: each expansion is a
-    // chain of dependent memory round trips, so waves in flight, not bytes, bound it (10M x 768
-    // M 32, 1024 queries: ef 8192 1573 -> 2232 QPS, 12288 495 -> 1266, 16384 339 -> 827; ef 3200,
-    // 4 waves per CU with R in LDS, stays: 8486 vs 7331; scripts/exp/exp_hnsw_nst.py).
+    // takes the HBM R once an LDS R would leave fewer than 4 + d / 256 waves per CU: each
+    // expansion is a chain of dependent memory round trips, so waves in flight, not bytes, bound
+    // it (10M x 768 M 32, 1024 queries: ef 8192 1573 -> 2232 QPS, 12288 495 -> 1266, 16384 339 ->
+    // 827; 10k queries: ef 2400 14.0k -> 15.2k, 3200 8.7k -> 11.0k, 4096 5.0k -> 8.2k, ef 1600
+    // equal; 20M x 128: LDS to ef 2400, 4096 11.5k -> 14.2k; scripts/exp/exp_hnsw_nst.py,
+    // profiles/r05_hnsw_rg_rule_{10m,d128}.txt).
     // RVX_HNSW_RG: 1 always, 0 only past the LDS, unset auto (read per call: tests force both)
     const bool coop0 = hnsw_coop(metric, d, g.n);
     const int rg_mode = env_int("RVX_HNSW_RG", -1);
     const size_t lds_r = hnsw_search_lds(d, ef, coop0);
-    const bool rg = lds_r > 160 * 1024 || rg_mode == 1 || (rg_mode < 0 && coop0 && lds_r * 3 > 160 * 1024);
+    // waves per CU below which R moves to HBM: 4 + d / 256 (7 at d 768, 4.5 at d 128), the
+    // wider the rows the more an expansion's distances gain from waves in flight against the
+    // HBM R's slower merges; RVX_HNSW_RG_WAVES=W (read per call) fixes it for A/Bs
+    const int rg_waves = env_int("RVX_HNSW_RG_WAVES", 0);
+    const bool rg_auto = rg_waves > 0 ? lds_r * (size_t)rg_waves > 160 * 1024
+                                      : lds_r * (size_t)(1024 + d) > (size_t)160 * 1024 * 256;
+    const bool rg = lds_r > 160 * 1024 || rg_mode == 1 || (rg_mode < 0 && coop0 && rg_auto);
     const unsigned vcap = visited_capacity(ef, g.max_deg);
     // visited set: a per-slot bitmap over all n nodes (cleared per query by its
     // wave: no launch-wide memset, no probing, n/8 bytes touched) when at least

@@ -14,11 +14,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 import ruvector_amd as rv  # noqa: E402
 
-n, d = int(os.environ.get("N", 10_000_000)), 768
+n, d = int(os.environ.get("N", 10_000_000)), int(os.environ.get("D", 768))
 efs = [int(e) for e in os.environ.get("EFS", "100,800,3200,8192,12288,16384").split(",")]
 # ";"-separated environment settings, each "VAR=VAL,VAR=VAL" (empty: the defaults)
 configs = os.environ.get("CONFIGS", ";RVX_HNSW_NST=2;RVX_HNSW_RG=1;RVX_HNSW_RG=1,RVX_HNSW_RG_NST=2").split(";")
-KNOBS = ("RVX_HNSW_NST", "RVX_HNSW_RG", "RVX_HNSW_RG_NST", "RVX_HNSW_QG")
+KNOBS = ("RVX_HNSW_NST", "RVX_HNSW_RG", "RVX_HNSW_RG_NST", "RVX_HNSW_QG", "RVX_HNSW_RG_WAVES")
 log = lambda s: print(s, file=sys.stderr, flush=True)  # noqa: E731
 xb = rv.Buffer(n * d * 4)
 xb.fill_normal(n * d, 5)
