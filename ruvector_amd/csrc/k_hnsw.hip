@@ -384,13 +384,18 @@ size_t search_lds_nst(int d, int ef, int nst) {
 }  // namespace
 
 // Distance stages per wave of the LDS-staged (coop) search. RVX_HNSW_NST forces
-// 1, 2, 3, 4 or 6 (read per call: tests and A/Bs); by default 2, and 1 from ef
-// 1024 (RVX_HNSW_WIDE=0 keeps 2) where one stage more would cost a wave per CU.
+// 1, 2, 3, 4 or 6 (read per call: tests and A/Bs); by default 2, and 1 from ef 1024
+// (RVX_HNSW_WIDE=0 keeps 2) where one stage more would cost 2-3 waves per CU — for rows of
+// at most 8 chunks (d <= 256) throughout, for longer rows only up to ef 1151: there the
+// second stage's overlap within a row outweighs the waves (10k queries, NST 1 vs 2: d 128 ef
+// 1024-3200 +10-21% for 1; d 384 ef 1024 +9% for 1, ef 1600 +10% for 2; d 768 ef 1024 +2% for
+// 1, 1280 / 1408 +5% / +15% for 2; profiles/r05_hnsw_nst_by_d.txt).
 int hnsw_nst(bool coop, int d, int ef) {
     if (!coop) return 0;
     const int f = env_int("RVX_HNSW_NST", 0);
     if ((f == 1 || f == 2 || f == 3 || f == 4 || f == 6) && search_lds_nst(d, ef, f) <= 160 * 1024) return f;
-    return ef >= 1024 && env_int("RVX_HNSW_WIDE", 1) ? 1 : 2;
+    if (ef < 1024 || !env_int("RVX_HNSW_WIDE", 1)) return 2;
+    return d <= 256 || ef < 1152 ? 1 : 2;
 }
 
 size_t hnsw_search_lds(int d, int ef, bool coop) {
@@ -426,9 +431,11 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     // waves per CU below which R moves to HBM: 4 + d / 256 (7 at d 768, 4.5 at d 128), the
     // wider the rows the more an expansion's distances gain from waves in flight against the
     // HBM R's slower merges; RVX_HNSW_RG_WAVES=W (read per call) fixes it for A/Bs
+    // (measured on the one-stage footprint, whatever the stage count the LDS R would run)
     const int rg_waves = env_int("RVX_HNSW_RG_WAVES", 0);
-    const bool rg_auto = rg_waves > 0 ? lds_r * (size_t)rg_waves > 160 * 1024
-                                      : lds_r * (size_t)(1024 + d) > (size_t)160 * 1024 * 256;
+    const size_t lds_1 = search_lds_nst(d, ef, 1);
+    const bool rg_auto = rg_waves > 0 ? lds_1 * (size_t)rg_waves > 160 * 1024
+                                      : lds_1 * (size_t)(1024 + d) > (size_t)160 * 1024 * 256;
     const bool rg = lds_r > 160 * 1024 || rg_mode == 1 || (rg_mode < 0 && coop0 && rg_auto);
     const unsigned vcap = visited_capacity(ef, g.max_deg);
     // visited set: a per-slot bitmap over all n nodes (cleared per query by its
