@@ -384,18 +384,19 @@ size_t search_lds_nst(int d, int ef, int nst) {
 }  // namespace
 
 // Distance stages per wave of the LDS-staged (coop) search. RVX_HNSW_NST forces
-// 1, 2, 3, 4 or 6 (read per call: tests and A/Bs); by default 2, and 1 from ef 1024
-// (RVX_HNSW_WIDE=0 keeps 2) where one stage more would cost 2-3 waves per CU — for rows of
-// at most 8 chunks (d <= 256) throughout, for longer rows only up to ef 1151: there the
-// second stage's overlap within a row outweighs the waves (10k queries, NST 1 vs 2: d 128 ef
-// 1024-3200 +10-21% for 1; d 384 ef 1024 +9% for 1, ef 1600 +10% for 2; d 768 ef 1024 +2% for
-// 1, 1280 / 1408 +5% / +15% for 2; profiles/r05_hnsw_nst_by_d.txt).
+// 1, 2, 3, 4 or 6 (read per call: tests and A/Bs); by default (RVX_HNSW_WIDE=0: always 2)
+// 1 for rows of at most 8 chunks (d <= 256), where a second stage overlaps little within a
+// row and costs waves, 1 at ef 1024-1151 up to d 768, else 2 (10k queries, NST 1 vs 2: d 128
+// ef 400-3200 +2-21% for 1, ef 100 equal; d 384 ef 1024 +9% for 1, ef 1600 +10% for 2; d 768
+// ef 1024 +2% for 1, 1280 / 1408 +5% / +15% for 2; d 1024 ef 1024-2400 +5-38% for 2;
+// profiles/r05_hnsw_nst_by_d.txt, r05_hnsw_nst_d128_small_d1024.txt).
 int hnsw_nst(bool coop, int d, int ef) {
     if (!coop) return 0;
     const int f = env_int("RVX_HNSW_NST", 0);
     if ((f == 1 || f == 2 || f == 3 || f == 4 || f == 6) && search_lds_nst(d, ef, f) <= 160 * 1024) return f;
-    if (ef < 1024 || !env_int("RVX_HNSW_WIDE", 1)) return 2;
-    return d <= 256 || ef < 1152 ? 1 : 2;
+    if (!env_int("RVX_HNSW_WIDE", 1)) return 2;
+    if (d <= 256) return 1;
+    return d <= 768 && ef >= 1024 && ef < 1152 ? 1 : 2;
 }
 
 size_t hnsw_search_lds(int d, int ef, bool coop) {
@@ -418,24 +419,19 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     RVX_REQUIRE(ef >= 1 && ef <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER,
                 "ef must be in [1, " + std::to_string(HNSW_MAX_EF) + "]");
     // R in LDS when one wave's 160 KB hold it, else in HBM. The LDS-staged (coop) search also
-    // takes the HBM R once an LDS R would leave fewer than 4 + d / 256 waves per CU: each
-    // expansion is a chain of dependent memory round trips, so waves in flight, not bytes, bound
-    // it (10M x 768 M 32, 1024 queries: ef 8192 1573 -> 2232 QPS, 12288 495 -> 1266, 16384 339 ->
-    // 827; 10k queries: ef 2400 14.0k -> 15.2k, 3200 8.7k -> 11.0k, 4096 5.0k -> 8.2k, ef 1600
-    // equal; 20M x 128: LDS to ef 2400, 4096 11.5k -> 14.2k; scripts/exp/exp_hnsw_nst.py,
-    // profiles/r05_hnsw_rg_rule_{10m,d128}.txt).
+    // takes the HBM R once an LDS R would leave fewer than 4 waves per CU: each expansion is a
+    // chain of dependent memory round trips, so waves in flight, not bytes, bound it (10M x 768
+    // M 32, 1024 queries: ef 8192 1573 -> 2232 QPS, 12288 495 -> 1266, 16384 339 -> 827; 10k
+    // queries: ef 3200 8.7k -> 11.0k, 4096 5.0k -> 8.2k; 20M x 128 ef 4096 11.5k -> 14.2k;
+    // scripts/exp/exp_hnsw_nst.py, profiles/r05_hnsw_rg_rule_*.txt).
     // RVX_HNSW_RG: 1 always, 0 only past the LDS, unset auto (read per call: tests force both)
     const bool coop0 = hnsw_coop(metric, d, g.n);
     const int rg_mode = env_int("RVX_HNSW_RG", -1);
     const size_t lds_r = hnsw_search_lds(d, ef, coop0);
-    // waves per CU below which R moves to HBM: 4 + d / 256 (7 at d 768, 4.5 at d 128), the
-    // wider the rows the more an expansion's distances gain from waves in flight against the
-    // HBM R's slower merges; RVX_HNSW_RG_WAVES=W (read per call) fixes it for A/Bs
-    // (measured on the one-stage footprint, whatever the stage count the LDS R would run)
-    const int rg_waves = env_int("RVX_HNSW_RG_WAVES", 0);
-    const size_t lds_1 = search_lds_nst(d, ef, 1);
-    const bool rg_auto = rg_waves > 0 ? lds_1 * (size_t)rg_waves > 160 * 1024
-                                      : lds_1 * (size_t)(1024 + d) > (size_t)160 * 1024 * 256;
+    // waves per CU below which R moves to HBM: 4 (RVX_HNSW_RG_WAVES=W, read per call, for A/Bs),
+    // on the footprint of the stage count hnsw_nst picks
+    const int rg_waves = std::max(1, env_int("RVX_HNSW_RG_WAVES", 4));
+    const bool rg_auto = lds_r * (size_t)rg_waves > 160 * 1024;
     const bool rg = lds_r > 160 * 1024 || rg_mode == 1 || (rg_mode < 0 && coop0 && rg_auto);
     const unsigned vcap = visited_capacity(ef, g.max_deg);
     // visited set: a per-slot bitmap over all n nodes (cleared per query by its
