@@ -83,6 +83,9 @@ def parse():
     p.add_argument("--no-c3", action="store_true", help="skip the C3 leg (HNSW build + search + GNN re-rank on the table)")
     p.add_argument("--c3-ef", default="100,400,1600", help="C3 leg: ef sweep")
     p.add_argument("--c4-nodes", type=int, default=0, help="C4 leg nodes (default: --nodes)")
+    p.add_argument("--no-c5", action="store_true", help="skip the C5 leg (hyperbolic HNSW, node-range sharded)")
+    p.add_argument("--c5-per-gpu", type=int, default=6_250_000,
+                   help="C5 leg points per GPU shard (6.25M = the 50M x 1024 corpus over 8 GPUs; weak scaling)")
     p.add_argument("--transport", choices=("rccl", "host"), default="rccl",
                    help="N>1 exchange: RCCL over xGMI, or host memory + stdlib sockets (ranks may share a GPU)")
     p.add_argument("--check-rows", type=int, default=8192, help="N>1: oracle-checked rows of the last rank")
@@ -293,6 +296,10 @@ def main():
     if comm is not None:
         line["comm"] = {"transport": a.transport, "forced": forced,
                         "self_p2p_rounds": kern.get("halo_exchange", {}).get("launches", 0) if forced else 0}
+        if forced:  # the compact records' RCCL round trip + unpack, checked word for word (rvx_comm_selfcheck)
+            from ruvector_amd.shard import comm_selfcheck
+            rows_chk, bad = comm_selfcheck(comm)
+            line["comm"]["record_selfcheck"] = {"rows": rows_chk, "mismatched_words": bad}
         line["multi_gpu"] = exchange_report(a, kern, comm, world, rank, offsets, d, layers, traffic)
         line["multi_gpu"]["transport"] = ("rccl (p2p over xGMI)" if a.transport == "rccl" else
                                           "host-staged (host memory + stdlib TCP sockets)")
@@ -315,6 +322,10 @@ def main():
     if not a.no_c4:
         _progress("c4 leg")
         line["c4"] = c4_leg(a, comm, rank, world)
+        rv.release_scratch()
+    if not a.no_c5:
+        _progress("c5 leg (hyperbolic HNSW shards: build, exact + pruned search)")
+        line["c5"] = c5_leg(a, comm, rank, world)
         rv.release_scratch()
     if not a.no_hnsw:
         _progress("c1 hnsw leg")
@@ -440,6 +451,32 @@ def c4_leg(a, comm, rank, world):
     n = a.c4_nodes or a.nodes
     return bench_gnn.run(n, a.dim, a.degree, 8, 3, steps=2, warmup=1, comm=comm, rank=rank, world=world,
                          graph="random", cpu=(rank == 0 and world == 1 and not a.no_cpu), cpu_seconds=8.0)
+
+
+def c5_leg(a, comm, rank, world):
+    """configs[4] (C5): the 50M x 1024 hyperbolic-HNSW corpus as node-range shards of
+    --c5-per-gpu points per GPU (6.25M = 50M / 8, so N = 8 is the full configuration and N = 1
+    its per-GPU unit; weak scaling). Per shard the GPU builds HyperbolicHnsw (defaults,
+    hnsw.rs:127-258) and its tangent cache; every query batch runs ShardedHyperbolicHnsw::search
+    (shard.rs:354-373: rank 0's 10k queries broadcast, each shard searched, per-rank top-10
+    all-gathered and merged on the GPU) in the exact mode (K10 Poincaré scan, the ground truth)
+    and the tangent-pruned mode (search_with_pruning, hnsw.rs:450-490). The graph-search mode is
+    left out: on this data the reference's graph rules give a non-navigable graph (recall@10
+    0.002 at 6.25M, DESIGN.md §6 C5 note), so pruned search is C5's fast path. value = exact
+    queries/s (recall 1.0) over the whole corpus; the exact mode's ids and distances are checked
+    bit for bit against the oracle's scan of a query sample over every shard, whose rate on rank 0
+    at N = 1 is the CPU baseline."""
+    import bench_hyperbolic
+    res = bench_hyperbolic.run_sharded(
+        a.c5_per_gpu, 1024, 10_000, [], comm, rank, world, cpu_queries=4,
+        cpu_seconds=(6.0 if rank == 0 and world == 1 and not a.no_cpu else 0.0),
+        log=(lambda s: print(f"[bench] c5: {s}", file=sys.stderr, flush=True)) if rank == 0 else None)
+    res["value"] = res["modes"]["exact"]["qps"]
+    res["unit"] = "queries/s (exact Poincaré top-10 over every shard, recall 1.0; pruned mode beside it)"
+    ex = res["roofline"].get("exact_scan_filter")
+    if ex:
+        res["roofline_dominant"] = dict(ex, kernel="scan_filter (exact mode)")
+    return res
 
 
 def c3_leg(a, x, n, d, rank, world, comm):

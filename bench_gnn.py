@@ -158,6 +158,8 @@ def run(n, d=768, deg=32, heads=8, nlayers=3, steps=2, warmup=1, comm=None, rank
     }
     if hnsw_s is not None:
         line["hnsw_build_s"] = round(hnsw_s, 2)
+    if world > 1 and comm is not None:
+        line["parity"] = multi_rank_check(x, g, layers[0], n, d, deg, offsets, comm, rank, world, bufs[1])
     if rank == 0 and world == 1 and cpu:
         # layer 1 is recomputed into bufs[1] (it holds layer 2 of the last step): at 10M x 768
         # the HBM has no room for another table beside the stack's scratch
@@ -191,6 +193,43 @@ def attach_c4_traffic(roof, cfg):
             roof[key]["traffic"] = round(ent["hbm_bytes_total"] / per, 0)
             roof[key]["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE(x2, gfx950) + WRITE_SIZE per layer, "
                                            "profiles/pmc_traffic_c4.json")
+
+
+def multi_rank_check(x_buf, g, layer, n, d, deg, offsets, comm, rank, world, y1, rows=128):
+    """Self-check of a multi-rank C4 run (after the timed steps): layer 1 runs once more across
+    the M|K|V exchange into y1, and the LAST rank compares its first `rows` owned rows with the
+    oracle's RuvectorLayer::forward (layer.rs:379-451) over the same graph; their neighbour
+    rows' projections came from every other rank over the exchange. The errors reach every
+    rank through one max all-reduce."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as O
+    from bench import rel_errs
+    from benchutil import host_threads
+    from ruvector_amd.shard import REDUCE_MAX
+
+    layer.forward_exchange(g, x_buf, y1, offsets, comm)
+    last = world - 1
+    a0 = int(offsets[last])
+    rows = int(min(rows, int(offsets[last + 1]) - a0))
+    errs = [0.0, 0.0]
+    if rank == last and rows > 0:
+        threads, _ = host_threads()
+        W = O.RvlWeights(json.loads(layer.to_json()))
+        rp, col = O.random_csr(n, deg, 6)
+        ew = O.fill_uniform(n * deg, 7, 0.0, 1.0)
+        nb = col[rp[a0]:rp[a0 + rows]].astype(np.int64)
+        need = np.concatenate([np.arange(a0, a0 + rows, dtype=np.int64), nb])
+        rp_sub = (rp[a0:a0 + rows + 1] - rp[a0]).astype(np.int64)
+        col_sub = (rows + np.arange(nb.size)).astype(np.int32)
+        ref = O.rvl_forward_graph(W, x_buf.gather_rows(n, d, need), rp_sub, col_sub, ew[rp[a0]:rp[a0 + rows]],
+                                  rows=(0, rows), threads=threads)
+        got = y1.gather_rows(n, layer.hidden_dim, np.arange(a0, a0 + rows))
+        errs = list(rel_errs(got, ref))
+    errs = comm.allreduce(errs, REDUCE_MAX)
+    return {"ok": bool(errs[0] <= 1e-5 and errs[1] <= 1e-5), "tol": 1e-5, "max_rel_err": errs[0],
+            "row_rel_l2_max": errs[1], "checked_rows": {"owner_rank": last, "rows": [a0, a0 + rows]},
+            "input": "layer 1 across the M|K|V exchange (neighbour projections from every rank)",
+            "metrics": "normwise max|gpu-ref|/max|ref| and per-row ||gpu_r-ref_r||/||ref_r|| (tests/parity.py)"}
 
 
 def cpu_baseline(cpu_seconds, x_buf, g, layer, n, d, deg, offsets, host_csr=None, y1=None):

@@ -55,19 +55,48 @@ def recall(gt, got):
     return float(np.mean([len(set(a.tolist()) & set(b.tolist())) / k for a, b in zip(gt, got)]))
 
 
+F16_MFMA_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: dense f16/bf16 MFMA ~2.5 PF (spec)
+
+
 def main_sharded(a):
     """C5 across GPUs: node-range shards + broadcast / all-gather / merge per query batch."""
     import ruvector_amd as rv
-    from ruvector_amd.shard import REDUCE_MAX, comm_from_env
-
-    import benchutil
+    from ruvector_amd.shard import comm_from_env
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     rv.set_device(local % max(rv.device_count(), 1) if a.transport == "host" else local)
     comm = comm_from_env(a.transport)
     log = (lambda s: print(f"[rank {rank}] {s}", file=sys.stderr, flush=True))  # noqa: E731
-    n, d, nq, k = a.per_gpu, a.dim, a.queries, 10
+    out = run_sharded(a.per_gpu, a.dim, a.queries, [int(e) for e in a.ef.split(",") if e], comm, rank, world,
+                      cpu_queries=a.cpu_queries, cpu_seconds=0.0, log=log)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def run_sharded(n, d, nq, efs, comm, rank, world, cpu_queries=4, cpu_seconds=0.0, log=None, k=10):
+    """One C5 measurement over `world` node-range shards of n points (weak scaling: world x n
+    points in all; world 1 with comm None is the one-GPU shard). Every rank calls it; the
+    returned dict is the same on every rank except for rank-0-only fields.
+
+    * build: rvx_hyperbolic_insert_batch_device of this rank's rows (HyperbolicHnswConfig
+      defaults, hnsw.rs:127-258), max over ranks; tangent cache (tangent.rs), max over ranks;
+    * modes (ShardedHyperbolicHnsw::search, shard.rs:354-373): "exact" (K10 MFMA-filtered
+      Poincaré scan + reference-order re-rank, the ground truth), "pruned"
+      (search_with_pruning, hnsw.rs:450-490: tangent scan through K10, k x prune_factor
+      candidates re-ranked by Poincaré distance) and the graph search at each ef in `efs`;
+      QPS = nq / max-over-ranks wall time, recall@10 against the exact mode;
+    * roofline of the exact mode's filter (MFMA: 2 nq n d f16 flops per rank) and of the
+      pruned mode's candidate re-rank (HBM: 4 d B per evaluated candidate, §8d);
+    * oracle check: the exact mode's ids and distances of the first `cpu_queries` queries equal
+      the oracle's Poincaré scan over every shard, merged in shard.rs order (bit for bit);
+      with cpu_seconds > 0 the number of checked queries grows until the oracle's scan takes
+      about that long, and its rate is the CPU baseline (rank 0 of a one-rank run)."""
+    import ruvector_amd as rv
+    from ruvector_amd.shard import REDUCE_MAX
+
+    import benchutil
+    log = log or (lambda s: None)
     r0 = rank * n
 
     def barrier():
@@ -91,7 +120,8 @@ def main_sharded(a):
         h.insert_device(xb, n, d)
         rv.synchronize()
     build_s = vmax(time.perf_counter() - t0)
-    cpu_check = oracle_scan_shard(a, xb, n, d, r0, rank, world, comm, log) if a.cpu_queries > 0 else None
+    cpu_check = (oracle_scan_shard(cpu_queries, cpu_seconds, xb, n, d, r0, rank, world, comm, log)
+                 if cpu_queries > 0 else None)
     del xb
     t0 = time.perf_counter()
     h.build_tangent_cache()
@@ -99,18 +129,20 @@ def main_sharded(a):
     cache_s = vmax(time.perf_counter() - t0)
     grp = rv.ShardedHyperbolicSearch(h, comm, r0)
     gid, dist = rv.Buffer(nq * k * 8), rv.Buffer(nq * k * 4)
-    modes = [("exact", 0), ("pruned", 0)] + [("search", int(e)) for e in a.ef.split(",")]
+    modes = [("exact", 0), ("pruned", 0)] + [("search", int(e)) for e in efs]
     out_modes, gt = {}, None
-    prof = rv.Profiler()
+    roof = {}
     for mode, ef in modes:
         grp.search_device(qb, min(nq, 256), k, gid, dist, ef=ef, mode=mode)  # warm-up (scratch, code objects)
         barrier()
+        prof = rv.Profiler()
         with prof:
             t0 = time.perf_counter()
             with benchutil.heartbeat(f"{mode} ef={ef}", log=log):
                 grp.search_device(qb, nq, k, gid, dist, ef=ef, mode=mode)
                 barrier()
             dt = vmax(time.perf_counter() - t0)
+        kern = prof.summary()
         ids = gid.download(np.int64, (nq, k))
         if mode == "exact":
             gt = ids
@@ -119,46 +151,90 @@ def main_sharded(a):
                 cpu_check["ids_equal"] = bool(np.array_equal(ids[:m], cpu_check["ids"]))
                 cpu_check["distances_equal"] = bool(np.array_equal(dist.download(np.float32, (nq, k))[:m],
                                                                    cpu_check["dist"]))
-        phases = {t: round(prof.query(t)[0], 2) for t in ("shard_bcast", "shard_allgather", "shard_merge")}
+        phases = {t: round(kern[t]["total_ms"], 2) for t in ("shard_bcast", "shard_allgather", "shard_merge")
+                  if t in kern}
         key = mode if mode != "search" else f"search_ef{ef}"
-        out_modes[key] = {"qps": round(nq / dt, 1), "recall_at_10": round(recall(gt, ids), 4), "wall_ms": round(dt * 1e3, 1),
-                          "phase_ms_rank0": phases}
-        log(f"{key}: {out_modes[key]}")
-    if rank == 0:
-        total = world * n
-        print(json.dumps({
-            "metric": "C5 hyperbolic HNSW queries/s@recall, node-range sharded", "n_gpus": world,
-            "scaling": "weak", "config": {"workload": f"C5: {total} x {d} Poincaré ball (c=1), {world} node-range "
-                                                      f"shards of {n}, {nq} queries, k={k}, M=16 M0=32 ef_c=200"},
-            "build_s": round(build_s, 2), "tangent_cache_s": round(cache_s, 2), "modes": out_modes,
-            "ground_truth": "exact mode: global exact Poincaré top-10 over every shard",
-            "exact_vs_oracle": None if cpu_check is None else
-            {k2: v for k2, v in cpu_check.items() if k2 not in ("ids", "dist")},
-            "data": "synthetic (rvx_fill_ball_rows, seed 7 points / 8 queries)"}), flush=True)
+        out_modes[key] = {"qps": round(nq / dt, 1), "recall_at_10": round(recall(gt, ids), 4),
+                          "wall_ms": round(dt * 1e3, 1), "phase_ms_rank0": phases,
+                          "kernel_ms_rank0": {t: round(v["total_ms"], 3) for t, v in kern.items()}}
+        filt = kern.get("scan_filter")
+        if mode in ("exact", "pruned") and filt and filt["total_ms"] > 0:
+            # K10 ranks every (query, row) pair with f16 MFMA over the d Poincaré (exact) or
+            # tangent (pruned) coordinates: 2 nq n d flops on this rank's shard
+            flops = 2.0 * nq * n * d
+            tf = flops / (filt["total_ms"] * 1e-3) / 1e12
+            roof[f"{mode}_scan_filter"] = {
+                "bound": "mfma", "achieved": round(tf, 1), "peak": F16_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": round(tf / F16_MFMA_PEAK_TFS, 4), "avg_ms": round(filt["total_ms"] / filt["launches"], 3),
+                "launches": filt["launches"], "work_per_launch": flops / filt["launches"], "traffic": None}
+        rr = kern.get("hyp_rerank")
+        if mode == "pruned" and rr and rr["total_ms"] > 0:
+            cand = k * h.config.prune_factor
+            byts = float(nq) * cand * 4 * d  # §8d: 4 d B per evaluated point
+            gbs = byts / (rr["total_ms"] * 1e-3) / 1e9
+            roof["pruned_candidate_rerank"] = {
+                "bound": "hbm", "achieved": round(gbs, 1), "peak": 8000.0, "unit": "GB/s",
+                "frac": round(gbs / 8000.0, 4), "avg_ms": round(rr["total_ms"] / rr["launches"], 3),
+                "launches": rr["launches"], "work_per_launch": byts / rr["launches"], "traffic": None,
+                "bytes": f"{cand} candidates x 4 d B per query"}
+        log(f"{key}: {out_modes[key]['qps']} QPS, recall {out_modes[key]['recall_at_10']}")
+    total = world * n
+    res = {
+        "metric": "C5 hyperbolic HNSW queries/s@recall, node-range sharded", "n_gpus": world,
+        "scaling": "weak",
+        "config": {"workload": f"configs[4] C5: {total} x {d} Poincaré ball (c=1), {world} node-range shard(s) of {n} "
+                               f"(the 50M x 1024 corpus's per-GPU unit), {nq} queries, k={k}, "
+                               "HyperbolicHnswConfig defaults (M=16, M0=32, ef_c=200, prune_factor 10)",
+                   "points_total": total, "points_per_gpu": n, "dim": d, "queries": nq, "k": k},
+        "build_s": round(build_s, 2), "build_points_per_s_per_gpu": round(n / build_s, 1),
+        "tangent_cache_s": round(cache_s, 2), "modes": out_modes,
+        "ground_truth": "exact mode: global exact Poincaré top-10 over every shard",
+        "roofline": roof,
+        "data": "synthetic (rvx_fill_ball_rows: direction N(0,1) normalised, radius 0.9 U[0,1); seed 7 points, 8 queries)"}
+    if cpu_check is not None:
+        res["exact_vs_oracle"] = {k2: v for k2, v in cpu_check.items() if k2 not in ("ids", "dist", "cpu_s_rank0")}
+        if world == 1 and rank == 0:
+            res["cpu_baseline"] = {
+                "value": round(cpu_check["queries"] / cpu_check["cpu_s_rank0"], 3), "unit": "queries/s",
+                "cores": cpu_check["threads"], "kind": "port",
+                "sample": f"oracle exact Poincaré scan (poincare.rs:135-301 arithmetic, orc_hyp_scan_rows) of "
+                          f"{cpu_check['queries']} queries over all {n} rows, {cpu_check['cpu_s_rank0']:.1f} s "
+                          "(rows streamed from HBM in chunks; the copies are not timed)"}
+    return res
 
 
-def oracle_scan_shard(a, xb, n, d, r0, rank, world, comm, log):
-    """Exact Poincaré top-10 of the first `cpu_queries` queries over this rank's shard on
-    the CPU (oracle/hyperbolic.cpp orc_hyp_scan_rows, rows streamed from HBM in chunks),
-    then every rank's lists merged on rank 0 in ShardedHyperbolicHnsw::search order
-    (ascending distance, lower global id first on ties)."""
+def oracle_scan_shard(m, cpu_seconds, xb, n, d, r0, rank, world, comm, log, k=10):
+    """Exact Poincaré top-10 of the first `m` queries over this rank's shard on the CPU
+    (oracle/hyperbolic.cpp orc_hyp_scan_rows, rows streamed from HBM in chunks; only the
+    oracle calls are timed), then every rank's lists merged on rank 0 in
+    ShardedHyperbolicHnsw::search order (ascending distance, lower global id first on ties).
+    cpu_seconds > 0 (one rank): m grows (up to 64 queries) until the scan takes about that
+    long."""
     import ruvector_amd as rv
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O
     from benchutil import host_threads
-    m, k = a.cpu_queries, 10
-    q = rv.Buffer(m * d * 4)
-    q.fill_ball(m, d, 8, 0)  # the first m rows of the query batch
-    qh = q.download(np.float32, (m, d))
     threads, _ = host_threads()
-    ids = dist = None
-    t0 = time.perf_counter()
-    chunk = 1 << 18
-    for s0 in range(0, n, chunk):
-        rows = min(chunk, n - s0)
-        xs = xb.download(np.float32, (rows, d), offset=s0 * d * 4)
-        ids, dist = O.hyp_scan_rows(xs, qh, k, id_base=r0 + s0, ids=ids, dist=dist, threads=threads)
-    cpu_s = time.perf_counter() - t0
+
+    def scan(m):
+        q = rv.Buffer(m * d * 4)
+        q.fill_ball(m, d, 8, 0)  # the first m rows of the query batch
+        qh = q.download(np.float32, (m, d))
+        ids = dist = None
+        cpu_s = 0.0
+        chunk = 1 << 18
+        for s0 in range(0, n, chunk):
+            rows = min(chunk, n - s0)
+            xs = xb.download(np.float32, (rows, d), offset=s0 * d * 4)
+            t0 = time.perf_counter()
+            ids, dist = O.hyp_scan_rows(xs, qh, k, id_base=r0 + s0, ids=ids, dist=dist, threads=threads)
+            cpu_s += time.perf_counter() - t0
+        return ids, dist, cpu_s
+
+    ids, dist, cpu_s = scan(m)
+    if cpu_seconds > 0 and world == 1 and cpu_s < 0.8 * cpu_seconds:
+        m = int(min(64, max(m + 1, m * cpu_seconds / max(cpu_s, 1e-3))))
+        ids, dist, cpu_s = scan(m)
     log(f"oracle exact scan of {m} queries over {n} rows: {cpu_s:.1f} s")
     if comm is not None:  # one-hot all-reduce sums move every rank's lists to every rank
         flat = np.zeros((world, m, k, 2))

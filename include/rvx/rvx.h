@@ -426,6 +426,11 @@ rvx_status rvx_hnsw_last_search_stats(int64_t* n_dist, int64_t* n_expand, int64_
  * min(nq, 1024) slots fit min(16 GiB, 1/4 of free HBM)), 0 = the tagged hash; slots =
  * concurrent search slots. */
 rvx_status rvx_hnsw_last_search_visited(int32_t* bitmap, int32_t* slots);
+/* Kernel form of that launch (an rvx extension for tests and benchmarks; results are the same
+ * in every form): r_in_hbm 1 = the result list R in an HBM row per search slot (past one wave's
+ * LDS, or where an LDS R would leave < 4 waves per CU), 0 = in LDS; stages = LDS-staged distance
+ * stages per wave (0: per-lane distances), visited_overflow 1 = a query's visited hash filled. */
+rvx_status rvx_hnsw_last_search_form(int32_t* r_in_hbm, int32_t* stages, int32_t* visited_overflow);
 /* Path taken by the most recent exact scan in this process (rvx_index_brute_force*, FlatIndex
  * search): queries ranked by the MFMA filter + exact re-rank, queries scanned by the exact VALU
  * kernel, and queries the filter handed back to the VALU kernel (completeness not provable).
@@ -638,6 +643,13 @@ rvx_status rvx_comm_init_host(int32_t nranks, int32_t rank, rvx_host_exchange_fn
  * counts k times) and taken from it, over every exchange, broadcast and all-gather since the
  * communicator was made (an rvx extension: the exchange's measured bytes for bench reports). */
 rvx_status rvx_comm_traffic(const rvx_comm* c, int64_t* sent, int64_t* recv);
+/* RVX_COMM_SELF_P2P=1 on a one-rank RCCL communicator (an rvx extension for one-GPU boxes): the
+ * GraphSAGE exchange's compact row records go out and come back through RCCL's p2p path and are
+ * expanded by the receivers' unpack kernel into a shadow of the rows they came from; `rows` is
+ * the number of rows so checked since the communicator was made, `mismatched_words` the 32-bit
+ * words that differed (0: the record path is bit-exact behind a real RCCL transfer). Waits for
+ * the device. */
+rvx_status rvx_comm_selfcheck(rvx_comm* c, int64_t* rows, int64_t* mismatched_words);
 
 /* The p2p round plan of the node-range exchange that the
  * *_forward_exchange entry points run: kind 0 = GraphSAGE (rvx_sage_forward_exchange:

@@ -164,6 +164,7 @@ SIGNATURES = {
     "rvx_index_brute_force": (None, [P, PF32, I64, I32, PU64, PF32]),
     "rvx_index_brute_force_device": (None, [P, P, I64, I32, P, P]),
     "rvx_hnsw_last_search_visited": (None, [PI32, PI32]),
+    "rvx_hnsw_last_search_form": (None, [PI32, PI32, PI32]),
     "rvx_index_sharded_search": (None, [P, P, PF32, I64, I32, I32, I32, PU64, PF32, PI32]),
     "rvx_index_sharded_search_device": (None, [P, P, P, I64, I32, I32, I32, P, P]),
     "rvx_index_load_graph": (None, [P, C.POINTER(HnswGraph)]),
@@ -211,6 +212,7 @@ SIGNATURES = {
     "rvx_comm_allreduce_max_f64": (None, [P, C.POINTER(C.c_double)]),
     "rvx_comm_allreduce_f64": (None, [P, C.POINTER(C.c_double), I32, I32]),
     "rvx_comm_traffic": (None, [P, PI64, PI64]),
+    "rvx_comm_selfcheck": (None, [P, PI64, PI64]),
 }
 
 _lib = None

@@ -240,8 +240,10 @@ def hnsw_last_search_stats() -> dict:
     _check("rvx_hnsw_last_search_stats", C.byref(a), C.byref(b), C.byref(c))
     v, sl = C.c_int32(), C.c_int32()
     _check("rvx_hnsw_last_search_visited", C.byref(v), C.byref(sl))
+    rg, st, ov = C.c_int32(), C.c_int32(), C.c_int32()
+    _check("rvx_hnsw_last_search_form", C.byref(rg), C.byref(st), C.byref(ov))
     return {"n_dist": a.value, "n_expand": b.value, "nq": c.value, "visited_bitmap": bool(v.value),
-            "slots": sl.value}
+            "slots": sl.value, "r_in_hbm": bool(rg.value), "stages": st.value, "visited_overflow": bool(ov.value)}
 
 
 def scan_last_stats() -> dict:

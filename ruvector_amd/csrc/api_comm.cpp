@@ -15,6 +15,8 @@ struct rvx_comm {
     rvx_host_exchange_fn host_fn = nullptr;  // host-staged transport (rvx_comm_init_host)
     void* host_user = nullptr;
     int64_t sent = 0, recv = 0;  // payload bytes this rank handed to / took from the transport (rvx_comm_traffic)
+    int64_t check_rows = 0;      // RVX_COMM_SELF_P2P record check: rows compared (host count) ...
+    rvx::DevMem check_words;     // ... and mismatched 32-bit words (device counter)
 };
 
 #define RVX_NCCL(expr)                                                                         \
@@ -37,6 +39,31 @@ int comm_size(const rvx_comm* c) { return c ? c->nranks : 1; }
 // bit-identical to the path that skips them.
 bool comm_self_p2p(const rvx_comm* c) {
     return c && c->comm && c->nranks == 1 && env_int("RVX_COMM_SELF_P2P", 0) != 0;
+}
+
+namespace {
+__global__ void k_count_mismatch(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, int64_t words,
+                                 unsigned long long* __restrict__ bad) {
+    unsigned long long c = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x)
+        c += a[i] != b[i] ? 1ull : 0ull;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, c);
+}
+}  // namespace
+
+void comm_selfcheck_rows(rvx_comm* c, const float* shadow, const float* rows, int64_t nrows, int dim, hipStream_t s) {
+    if (!c || nrows <= 0) return;
+    if (!c->check_words.p) {
+        c->check_words.reset(8);
+        RVX_HIP(hipMemsetAsync(c->check_words.p, 0, 8, s));
+    }
+    const int64_t words = nrows * dim;
+    const unsigned blocks = (unsigned)std::min<int64_t>(2048, (words + 255) / 256);
+    hipLaunchKernelGGL(k_count_mismatch, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const uint32_t*>(shadow),
+                       reinterpret_cast<const uint32_t*>(rows), words, c->check_words.as<unsigned long long>());
+    RVX_HIP(hipGetLastError());
+    c->check_rows += nrows;
 }
 
 namespace {
@@ -185,6 +212,20 @@ rvx_status rvx_comm_traffic(const rvx_comm* c, int64_t* sent, int64_t* recv) {
         RVX_REQUIRE(c && sent && recv, RVX_ERR_INVALID_PARAMETER, "null argument");
         *sent = c->sent;
         *recv = c->recv;
+    });
+}
+
+rvx_status rvx_comm_selfcheck(rvx_comm* c, int64_t* rows, int64_t* mismatched_words) {
+    return guard([&] {
+        RVX_REQUIRE(c && rows && mismatched_words, RVX_ERR_INVALID_PARAMETER, "null argument");
+        unsigned long long bad = 0;
+        if (c->check_words.p) {
+            ComputeLock cl;
+            RVX_HIP(hipDeviceSynchronize());  // the checks run on the transfer stream
+            RVX_HIP(hipMemcpy(&bad, c->check_words.p, 8, hipMemcpyDeviceToHost));
+        }
+        *rows = c->check_rows;
+        *mismatched_words = (int64_t)bad;
     });
 }
 

@@ -885,6 +885,11 @@ rvx_status rvx_sage_forward_exchange3(const rvx_sage_layer* l, const rvx_graph* 
             scan_tmp = scratch_bytes("sage_xchg_scan", (int64_t)std::max<size_t>(scan_bytes, 16));
             RVX_HIP(hipMemsetAsync(ctr, 0, 8 * (size_t)(3 * world + 3), d.xfer));
         }
+        // one-rank RCCL (RVX_COMM_SELF_P2P): the rank's own records come back through RCCL and
+        // are expanded into this shadow by the receivers' unpack kernel, then compared with the
+        // rows they encode (comm_selfcheck_rows) — the record path's receive side runs behind a
+        // real RCCL transfer on a one-GPU box
+        float* shadow = xallow && comm_self_p2p(comm) ? scratch_f32("sage_xchg_shadow", round_rows * l->out) : nullptr;
         auto budget = [&](int64_t rows) { return ((uint64_t)std::ceil((double)rows * rate) + 15) / 16 * 16; };
         // the all-gathered chunk-0 record bytes land in pinned host memory; with more than one
         // round the host reads them at round 1 (chunk 1 already queued), so the GPU never idles
@@ -915,7 +920,18 @@ rvx_status rvx_sage_forward_exchange3(const rvx_sage_layer* l, const rvx_graph* 
             }
             if (yinv_xchg) comm_exchange_rows(comm, yinv_xchg, 1, plan[c].r0.data(), rows.data(), d.xfer);
             for (int p = 0; p < world; ++p) {
-                if (p == me) continue;
+                if (p == me) {
+                    if (xrec && shadow && rows[p] > 0) {
+                        const float* own = y + plan[c].r0[p] * l->out;
+                        RVX_HIP(hipMemcpyAsync(shadow, own, (size_t)(rows[p] * l->out * 4), hipMemcpyDeviceToDevice,
+                                               d.xfer));  // rows past the budget stay as they are
+                        rec_offsets(xcnt + st[p], rows[p], xoff + st[p], scan_tmp, scan_bytes);
+                        rows_xchg_unpack(shadow, 0, rows[p], l->out, xs + st16[p] * 16, budget(rows[p]), xcnt + st[p],
+                                         xoff + st[p], RowImage());
+                        comm_selfcheck_rows(comm, shadow, own, rows[p], l->out, d.xfer);
+                    }
+                    continue;
+                }
                 if (xrec) {  // records back into dense rows (and the image, when asked for)
                     rec_offsets(xcnt + st[p], rows[p], xoff + st[p], scan_tmp, scan_bytes);
                     rows_xchg_unpack(y, plan[c].r0[p], rows[p], l->out, xs + st16[p] * 16, budget(rows[p]),

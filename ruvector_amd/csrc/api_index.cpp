@@ -306,6 +306,7 @@ rvx_status rvx_index_search(const rvx_index* ix, const float* q, int64_t nq, int
         RVX_HIP(hipMemcpyAsync(out_dist, od, (size_t)(nq * k * 4), hipMemcpyDeviceToHost, stream()));
         if (out_count) RVX_HIP(hipMemcpyAsync(out_count, on, (size_t)(nq * 4), hipMemcpyDeviceToHost, stream()));
         sync();
+        if (ix->cfg.kind == RVX_INDEX_HNSW) hnsw_search_check();  // (after the wait above: no extra sync)
     });
 }
 
@@ -569,6 +570,17 @@ rvx_status rvx_hnsw_last_search_visited(int32_t* bitmap, int32_t* slots) {
     return guard([&] {
         if (bitmap) *bitmap = g_search_stats.visited_bitmap;
         if (slots) *slots = g_search_stats.slots;
+    });
+}
+
+rvx_status rvx_hnsw_last_search_form(int32_t* r_in_hbm, int32_t* stages, int32_t* visited_overflow) {
+    return guard([&] {
+        if (visited_overflow) {
+            hnsw_search_stats_settle();
+            *visited_overflow = g_search_stats.visited_overflow;
+        }
+        if (r_in_hbm) *r_in_hbm = g_search_stats.r_in_hbm;
+        if (stages) *stages = g_search_stats.stages;
     });
 }
 

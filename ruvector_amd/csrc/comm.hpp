@@ -16,6 +16,12 @@ int comm_size(const rvx_comm* c);
 // drivers still run their collectives (to the rank itself) instead of skipping them.
 bool comm_self_p2p(const rvx_comm* c);
 
+// RVX_COMM_SELF_P2P record check: the rank's own compact records, after their round trip
+// through RCCL, expanded into `shadow` (rows_xchg_unpack, the receivers' kernel), compared word
+// for word with the rows they came from (`rows` rows of `dim` floats) on stream `s`; mismatches
+// accumulate in the communicator (rvx_comm_selfcheck).
+void comm_selfcheck_rows(rvx_comm* c, const float* shadow, const float* rows, int64_t nrows, int dim, hipStream_t s);
+
 // One grouped point-to-point round on stream `s`: this rank sends its rows
 // [r0[me], r0[me]+rows[me]) of `table` to every peer and receives each peer
 // p's rows [r0[p], r0[p]+rows[p]) into the same rows of its own `table`

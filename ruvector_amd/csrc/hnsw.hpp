@@ -44,9 +44,14 @@ bool hnsw_coop(int metric, int d, int64_t rows);
 struct SearchStats {
     int64_t n_dist = 0, n_expand = 0, nq = 0;
     int32_t visited_bitmap = 0, slots = 0;  // visited-set form and search slots of the launch
+    int32_t visited_overflow = 0;           // a query's visited hash table filled (nodes were skipped)
+    int32_t r_in_hbm = 0, stages = 0;       // kernel form: R in HBM, LDS distance stages (0 per-lane)
 };
 extern SearchStats g_search_stats;
 // The last search's device tallies (n_dist, n_expand) into g_search_stats (waits for the search).
 void hnsw_search_stats_settle();
+// settle, then fail (RVX_ERR_INDEX) if the last search's visited hash overflowed; host-returning
+// entry points call it after their own wait, so it costs no extra synchronisation
+void hnsw_search_check();
 
 }  // namespace rvx

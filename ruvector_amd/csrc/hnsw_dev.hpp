@@ -270,7 +270,11 @@ __device__ __forceinline__ float wave_dist(const float* qs, const float* __restr
 
 // Claim `node` in a query's visited set: true if it was not visited yet.
 // Slots whose tag is another query's are free (the table is zeroed per launch).
-__device__ __forceinline__ bool visit_claim(unsigned long long* vis, unsigned vmask, unsigned long long qtag, int node) {
+// A table that has no free slot left sets *full (the host turns it into an error: the
+// node would otherwise be skipped without a trace); visited_capacity sizes tables so this
+// cannot happen below 8 ef expansions of full lists, and never for tables of >= 2n slots.
+__device__ __forceinline__ bool visit_claim(unsigned long long* vis, unsigned vmask, unsigned long long qtag, int node,
+                                            int* full) {
     const unsigned long long key = qtag | (unsigned)(node + 1);
     unsigned h = ((unsigned)node * 2654435761u) & vmask;
     unsigned long long cur = __hip_atomic_load(&vis[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -285,16 +289,21 @@ __device__ __forceinline__ bool visit_claim(unsigned long long* vis, unsigned vm
         if (prev == cur) return true;
         cur = prev;
     }
-    return false;  // table full: cannot happen below vmask+1 visited nodes
+    atomicOr(full, 1);  // table full (every slot probed): reported, never silent
+    return false;
 }
 
-// visited-table size for a search of width ef over lists of <= max_deg neighbours
-// (load factor well below 1/2)
-inline unsigned visited_capacity(int ef, int max_deg = 64) {
+// visited-table size (a power of two) for a search of width ef over lists of <= max_deg
+// neighbours in a graph of n nodes: a search of width ef expands ~ef..2ef nodes of <= max_deg
+// neighbours each, so 4 ef max_deg slots keep the load well below 1/2; up to 2^30 slots (8 GiB),
+// and never more than the first power of two >= 2n — a query claims each node at most once, so
+// such a table is never more than half full. Callers size their slot count by bytes.
+inline unsigned visited_capacity(int ef, int max_deg, int64_t n) {
     unsigned v = VCAP_MIN;
-    // a search of width ef expands ~ef..2ef nodes of <= max_deg neighbours each
     const uint64_t want = (uint64_t)ef * 4u * (uint64_t)std::max(max_deg, 64);
-    while (v < want && v < (1u << 24)) v <<= 1;
+    while (v < want && v < (1u << 30)) v <<= 1;
+    const uint64_t all = 2 * (uint64_t)std::max<int64_t>(n, 1);
+    while (v > 64 && (uint64_t)(v >> 1) >= all) v >>= 1;
     return v;
 }
 

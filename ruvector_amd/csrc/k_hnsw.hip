@@ -128,7 +128,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
                 const unsigned bit = 1u << (node & 31);
                 return !(atomicOr(vb + (node >> 5), bit) & bit);
             }
-            return visit_claim(vis, vmask, qtag, node);
+            return visit_claim(vis, vmask, qtag, node, reinterpret_cast<int*>(a.stats + 7));
         };
         auto dist_of = [&](int node) {
             return row_dist<METRIC, false, RB>(qs, a.x + (int64_t)node * a.d, a.d,
@@ -320,7 +320,7 @@ SearchStats g_search_stats;
 
 namespace {
 struct SearchTally {
-    unsigned long long* host = nullptr;  // [7]: distance evaluations, expansions, (phase cycles)
+    unsigned long long* host = nullptr;  // [8]: distance evaluations, expansions, (phase cycles), visited overflow
     bool pending = false;
 };
 SearchTally& search_tally() {  // per device (callers hold its ComputeLock)
@@ -433,7 +433,7 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     const int rg_waves = std::max(1, env_int("RVX_HNSW_RG_WAVES", 4));
     const bool rg_auto = lds_r * (size_t)rg_waves > 160 * 1024;
     const bool rg = lds_r > 160 * 1024 || rg_mode == 1 || (rg_mode < 0 && coop0 && rg_auto);
-    const unsigned vcap = visited_capacity(ef, g.max_deg);
+    const unsigned vcap = visited_capacity(ef, g.max_deg, g.n);
     // visited set: a per-slot bitmap over all n nodes (cleared per query by its
     // wave: no launch-wide memset, no probing, n/8 bytes touched) when at least
     // min(nq, 1024) slots' bitmaps fit the budget — what the scratch slot already
@@ -455,7 +455,8 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     }
     const int64_t fit_slots = budget / (vwords * 4);
     const bool bitmap = bm_mode == 2 || (bm_mode == 1 && fit_slots >= std::min<int64_t>(bm_slots, 1024));
-    const int64_t mem_slots = std::max<int64_t>(256, ((int64_t)8 << 30) / ((int64_t)vcap * 8));
+    // hash slots by bytes: 8 GiB of tables (one slot at the 2^30-entry maximum)
+    const int64_t mem_slots = std::max<int64_t>(1, ((int64_t)8 << 30) / ((int64_t)vcap * 8));
     int nslots = (int)(bitmap ? (bm_mode == 2 ? bm_slots : std::min(bm_slots, fit_slots))
                               : std::min<int64_t>(bm_slots, mem_slots));
     // RG: each slot also holds an HBM row of ef + 1 R entries (8 B each), within 4 GiB
@@ -568,8 +569,11 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     // the work tallies reach page-locked host memory behind the search; the search itself returns
     // with its work queued (no host wait) and rvx_hnsw_last_search_stats settles them on demand
     SearchTally& tl = search_tally();
-    RVX_HIP(hipMemcpyAsync(tl.host, stats, 7 * 8, hipMemcpyDeviceToHost, stream()));
+    RVX_HIP(hipMemcpyAsync(tl.host, stats, 8 * 8, hipMemcpyDeviceToHost, stream()));
     tl.pending = true;
+    g_search_stats.visited_overflow = 0;
+    g_search_stats.r_in_hbm = rg ? 1 : 0;
+    g_search_stats.stages = coop ? nst_sel : 0;
     g_search_stats.nq = nq;
     g_search_stats.visited_bitmap = bitmap ? 1 : 0;
     g_search_stats.slots = nslots;
@@ -591,7 +595,15 @@ void hnsw_search_stats_settle() {
     sync();
     g_search_stats.n_dist = (int64_t)tl.host[0];
     g_search_stats.n_expand = (int64_t)tl.host[1];
+    g_search_stats.visited_overflow = (int32_t)(tl.host[7] != 0);
     tl.pending = false;
+}
+
+void hnsw_search_check() {
+    hnsw_search_stats_settle();
+    RVX_REQUIRE(!g_search_stats.visited_overflow, RVX_ERR_INDEX,
+                "HNSW search: a query's visited set filled its table (more than 8 ef expansions of full lists); "
+                "results would skip nodes");
 }
 
 }  // namespace rvx

@@ -50,6 +50,7 @@ struct BuildArgs {
     int hyper;   // HyperbolicHnsw::insert rules
     int coop;    // wave-cooperative LDS-staged distances in the layer searches
     float* rg_d; int* rg_i;  // RG: R in HBM, [nslots][ef_c + 1] (ef_c past one wave's LDS)
+    int* vis_full;           // set when a visited table fills (hnsw_dev.hpp visit_claim): the batch fails
 };
 
 __device__ __forceinline__ int list_get(const BuildGraph& G, int p, int l, const int** ids, const float** ds) {
@@ -82,7 +83,7 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
     int rs = 1;
     if (lane == 0) {
         rd[0] = d_ep; ri[0] = ep;
-        visit_claim(vis, vmask, tag, ep);
+        visit_claim(vis, vmask, tag, ep, a.vis_full);
     }
     __threadfence_block();
     __builtin_amdgcn_wave_barrier();
@@ -109,7 +110,7 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
             bool fresh = false;
             if (p < cnt) {
                 nid = nbi[p];
-                fresh = visit_claim(vis, vmask, tag, nid);
+                fresh = visit_claim(vis, vmask, tag, nid, a.vis_full);
             }
             const unsigned long long fmask = __ballot(fresh);
             if (!fmask) continue;
@@ -384,15 +385,18 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     RVX_REQUIRE(G.C0 <= MAX_C0 && G.M <= MAX_C0 / 2, RVX_ERR_UNSUPPORTED,
                 "GPU HNSW build supports layer-0 lists of <= 256 and upper lists of <= 128 neighbours");
     RVX_REQUIRE(ef_c >= 1 && ef_c <= HNSW_MAX_EF, RVX_ERR_INVALID_PARAMETER, "ef_construction out of range");
-    const unsigned vcap = visited_capacity(ef_c, G.C0);
+    const unsigned vcap = visited_capacity(ef_c, G.C0, batch_begin + batch_n);
     const bool coop = hnsw_coop(metric, d, batch_begin + batch_n);
     // R in LDS when one wave's 160 KB hold it, else in HBM (RVX_HNSW_RG=1 forces, tests). Unlike
     // the high-ef search, more waves do not speed the build: R in HBM with one distance stage at
     // 3 waves per SIMD built the same graph slower (4M x 768 M 32: 41.7 vs 36.4 s; 2M M 128 ef_c
     // 500: > 180 vs 129 s; profiles/r05_build_wide_ab.txt, round 5).
     const bool rg = build_lds_bytes(d, ef_c, coop) > 160 * 1024 || env_int("RVX_HNSW_RG", 0) != 0;
+    // visited tables within 4 GiB (memset per batch): 8,192 slots of 2^16 entries at ef_c 200 / M 32,
+    // down to 4 slots of 2^27 at ef_c past 2^19 / 64 (no floor: a floor of 1,024 slots made
+    // 128 GiB of tables at ef_c >= 32,768)
     int nslots = (int)std::min<int64_t>(std::min(batch_n, 8192),
-                                        std::max<int64_t>(1024, ((int64_t)4 << 30) / ((int64_t)vcap * 8)));
+                                        std::max<int64_t>(1, ((int64_t)4 << 30) / ((int64_t)vcap * 8)));
     if (rg) nslots = (int)std::max<int64_t>(1, std::min<int64_t>(nslots, ((int64_t)4 << 30) / ((int64_t)(ef_c + 1) * 8)));
     const int rev_cap = G.C0 + G.M * G.max_layer;
     BuildArgs a{};
@@ -415,6 +419,8 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     a.rev_head = s.rev_head;
     a.rev_cap = rev_cap;
     a.nslots = nslots;
+    a.vis_full = (int*)scratch_bytes("build_vis_full", 64);
+    RVX_HIP(hipMemsetAsync(a.vis_full, 0, 4, stream()));
     RVX_HIP(hipMemsetAsync(a.visited, 0, (size_t)nslots * vcap * 8, stream()));
     const size_t lds = build_lds_bytes(d, ef_c, a.coop != 0, rg);
     RVX_REQUIRE(lds <= 160 * 1024, RVX_ERR_INVALID_PARAMETER, "dimension too large for one wave's LDS");
@@ -458,7 +464,11 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     const dim3 mgrid((unsigned)((waves + 3) / 4));
     if (G.C0 <= 128) RVX_LAUNCH("hnsw_build_merge", k_build_merge<2>, mgrid, dim3(256), 0, a, (int)nrec);
     else RVX_LAUNCH("hnsw_build_merge", k_build_merge<4>, mgrid, dim3(256), 0, a, (int)nrec);
+    int full = 0;
+    RVX_HIP(hipMemcpyAsync(&full, a.vis_full, 4, hipMemcpyDeviceToHost, stream()));
     sync();
+    RVX_REQUIRE(!full, RVX_ERR_INDEX,
+                "HNSW build: an insert's visited set filled its table (more than 8 ef_c expansions of full lists)");
 }
 
 }  // namespace rvx

@@ -214,10 +214,19 @@ void rerank(const float* q, int64_t nq, const float* x, int d, float c, const in
     if (nq <= 0) return;
     RVX_REQUIRE(nc >= 1, RVX_ERR_INVALID_PARAMETER, "candidate count out of range");
     if (nc > SCAN_MAX_K) {
-        float* dist = scratch_f32("hyp_rerank_d", nq * (int64_t)nc);
-        RVX_LAUNCH("hyp_rerank", k_rerank_dist, dim3((unsigned)((nq * nc + 255) / 256)), dim3(256), 0, q, nq, x, d, c,
-                   cand, nc, dist);
-        select_topk(dist, nq, nc, nc, k, cand, 0, out_d, out_i, out_n);
+        // query batches whose distances and selection footprint (row, histogram, min(k, nc) keys)
+        // stay within 4 GiB, as the wide scan batches its rows
+        const int64_t keys = std::min<int64_t>(k, nc);
+        const int64_t per_query = (int64_t)nc * 4 + 2048 * 4 + 64 + keys * (keys > 8192 ? 16 : 8);
+        const int64_t nqb = std::max<int64_t>(1, std::min<int64_t>(nq, ((int64_t)4 << 30) / per_query));
+        float* dist = scratch_f32("hyp_rerank_d", nqb * (int64_t)nc);
+        for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
+            const int64_t nb = std::min(nqb, nq - q0);
+            RVX_LAUNCH("hyp_rerank", k_rerank_dist, dim3((unsigned)((nb * nc + 255) / 256)), dim3(256), 0, q + q0 * d,
+                       nb, x, d, c, cand + q0 * nc, nc, dist);
+            select_topk(dist, nb, nc, nc, k, cand + q0 * nc, 0, out_d + q0 * k, out_i + q0 * k,
+                        out_n ? out_n + q0 : nullptr);
+        }
         return;
     }
     RVX_LAUNCH("hyp_rerank", k_rerank, dim3((unsigned)nq), dim3(64), 0, q, nq, x, d, c, cand, nc, k, out_d, out_i,

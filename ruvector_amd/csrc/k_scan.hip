@@ -1754,7 +1754,9 @@ namespace {
 // k > SCAN_MAX_K (flat.rs:63-64 sorts every pair and truncates to any k): K1's tiles write
 // the whole distance rows of a query batch (reference scalar order, the same arithmetic as
 // the fused top-k), and select_topk takes the first k by (distance, id) from them. Batches
-// of queries so that the rows fit min(4 GiB, 1/8 of the free HBM).
+// of queries so that a query's whole footprint — its distance row, the selection's histogram
+// and state, and its min(k, n) keys (twice past the LDS sort) — fits min(4 GiB, 1/8 of the free
+// HBM) per batch (the histograms and keys were outside the budget).
 void scan_topk_wide(int metric, const float* q, const float* qnorm, int64_t nq, const float* x, const float* xnorm,
                     const uint8_t* deleted, int64_t n, int d, int k, int64_t id_offset, float* out_d, int64_t* out_i,
                     float curv) {
@@ -1765,7 +1767,9 @@ void scan_topk_wide(int metric, const float* q, const float* qnorm, int64_t nq, 
     int64_t budget = std::min<int64_t>((int64_t)4 << 30, std::max<int64_t>((int64_t)256 << 20, (int64_t)(fr / 8)));
     const int64_t cap_mb = env_int("RVX_SCAN_WIDE_BUDGET_MB", 0);  // tests force several batches
     if (cap_mb > 0) budget = cap_mb << 20;
-    const int64_t nqb = std::max<int64_t>(1, std::min<int64_t>(nq, budget / (n * 4)));
+    const int64_t keys = std::min<int64_t>(k, n);
+    const int64_t per_query = n * 4 + 2048 * 4 + 64 + keys * (keys > 8192 ? 16 : 8);
+    const int64_t nqb = std::max<int64_t>(1, std::min<int64_t>(nq, budget / per_query));
     float* D = scratch_f32("scan_wide_d", nqb * n);
     for (int64_t q0 = 0; q0 < nq; q0 += nqb) {
         const int64_t nb = std::min(nqb, nq - q0);

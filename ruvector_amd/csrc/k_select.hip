@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void k_sel_compact(const float* __restrict__ D
         const unsigned long long key = row_key(d, i);
         if (s.all || (key >> (64 - s.bits)) <= s.prefix) {
             const int slot = atomicAdd(&cnt[seg], 1);
-            if (slot < k) sel[seg * (int64_t)k + slot] = key;
+            if (slot < k) sel[seg * (int64_t)k + slot] = key;  // (k here: the key stride min(k, len))
         }
     }
 }
@@ -177,17 +177,18 @@ __device__ __forceinline__ void sel_emit(const float* D, int64_t len, int64_t ld
     }
 }
 
-// One block per query: bitonic sort of its selected keys in LDS (P = power of two >= k).
+// One block per query: bitonic sort of its selected keys in LDS (P = power of two >= ks, the
+// key stride min(k, len); k output slots, those past the selected count padded).
 __global__ __launch_bounds__(1024) void k_sel_sort(const float* __restrict__ D, int64_t len, int64_t ld,
                                                    const int* __restrict__ cnt, const unsigned long long* __restrict__ sel,
-                                                   int k, int P, const int64_t* __restrict__ idmap, int64_t id_offset,
-                                                   float* __restrict__ out_d, int64_t* __restrict__ out_i,
-                                                   int32_t* __restrict__ out_n) {
+                                                   int k, int ks, int P, const int64_t* __restrict__ idmap,
+                                                   int64_t id_offset, float* __restrict__ out_d,
+                                                   int64_t* __restrict__ out_i, int32_t* __restrict__ out_n) {
     extern __shared__ unsigned long long sk[];
     const int64_t seg = blockIdx.x;
     const int tid = threadIdx.x;
-    const int n = min(cnt[seg], k);
-    for (int i = tid; i < P; i += 1024) sk[i] = i < n ? sel[seg * (int64_t)k + i] : ~0ull;
+    const int n = min(cnt[seg], ks);
+    for (int i = tid; i < P; i += 1024) sk[i] = i < n ? sel[seg * (int64_t)ks + i] : ~0ull;
     __syncthreads();
     for (int size = 2; size <= P; size <<= 1)
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -203,17 +204,18 @@ __global__ __launch_bounds__(1024) void k_sel_sort(const float* __restrict__ D, 
     if (tid == 0 && out_n) out_n[seg] = n;
 }
 
-// Large k: keys sorted by rocPRIM; unused slots were filled with ~0 (sorted last).
+// Large k: keys sorted by rocPRIM (stride ks = min(k, len)); unused slots were filled with ~0
+// (sorted last); k output slots per query.
 __global__ void k_sel_emit(const float* __restrict__ D, int64_t len, int64_t ld, const int* __restrict__ cnt,
-                           const unsigned long long* __restrict__ sorted, int64_t nseg, int k,
+                           const unsigned long long* __restrict__ sorted, int64_t nseg, int k, int ks,
                            const int64_t* __restrict__ idmap, int64_t id_offset, float* __restrict__ out_d,
                            int64_t* __restrict__ out_i, int32_t* __restrict__ out_n) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nseg * k) return;
     const int64_t seg = t / k;
     const int s = (int)(t - seg * k);
-    const int n = min(cnt[seg], k);
-    sel_emit(D, len, ld, idmap, id_offset, seg, s, n, sorted[t], k, out_d, out_i);
+    const int n = min(cnt[seg], ks);
+    sel_emit(D, len, ld, idmap, id_offset, seg, s, n, s < n ? sorted[seg * (int64_t)ks + s] : 0ull, k, out_d, out_i);
     if (s == 0 && out_n) out_n[seg] = n;
 }
 
@@ -236,11 +238,14 @@ void select_topk(const float* D, int64_t nseg, int64_t len, int64_t ld, int k, c
     if (nseg <= 0 || k <= 0) return;
     RVX_REQUIRE(len >= 0 && len < ((int64_t)1 << 32) && ld >= len, RVX_ERR_INVALID_PARAMETER,
                 "select_topk: rows of up to 2^32 entries");
-    RVX_REQUIRE(nseg * (int64_t)k < ((int64_t)1 << 31), RVX_ERR_INVALID_PARAMETER, "select_topk: batch too large");
+    // keys per query: at most min(k, len) rows can be selected (k > len sized the key
+    // buffers by k); the outputs keep k slots per query, padded
+    const int ks = (int)std::max<int64_t>(1, std::min<int64_t>(k, len));
+    RVX_REQUIRE(nseg * (int64_t)ks < ((int64_t)1 << 31), RVX_ERR_INVALID_PARAMETER, "select_topk: batch too large");
     auto* st = (SelState*)scratch_bytes("sel_state", nseg * (int64_t)sizeof(SelState));
     auto* hist = (unsigned*)scratch_bytes("sel_hist", nseg * SEL_BINS * 4);
     auto* cnt = (int*)scratch_bytes("sel_cnt", nseg * 4);
-    auto* sel = (unsigned long long*)scratch_bytes("sel_keys", nseg * (int64_t)k * 8);
+    auto* sel = (unsigned long long*)scratch_bytes("sel_keys", nseg * (int64_t)ks * 8);
     RVX_HIP(hipMemsetAsync(hist, 0, (size_t)nseg * SEL_BINS * 4, stream()));
     RVX_HIP(hipMemsetAsync(cnt, 0, (size_t)nseg * 4, stream()));
     RVX_LAUNCH("select_topk", k_sel_init, dim3((unsigned)((nseg + 255) / 256)), dim3(256), 0, st, nseg, k);
@@ -257,11 +262,11 @@ void select_topk(const float* D, int64_t nseg, int64_t len, int64_t ld, int k, c
                        SEL_WIDTH[p], p == 0 ? 1 : 0);
         }
         RVX_LAUNCH("select_topk", k_sel_compact, dim3((unsigned)bx, (unsigned)ns), dim3(256), 0, D + s0 * ld, len, ld,
-                   st + s0, cnt + s0, sel + s0 * k, k, chunk);
+                   st + s0, cnt + s0, sel + s0 * ks, ks, chunk);
     }
-    if (k <= SEL_LDS_SORT_MAX) {
+    if (ks <= SEL_LDS_SORT_MAX) {
         int P = 2;
-        while (P < k) P <<= 1;
+        while (P < ks) P <<= 1;
         static bool attr = false;
         if (!attr) {
             RVX_HIP(hipFuncSetAttribute((const void*)k_sel_sort, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -271,18 +276,18 @@ void select_topk(const float* D, int64_t nseg, int64_t len, int64_t ld, int k, c
         for (int64_t s0 = 0; s0 < nseg; s0 += 65535) {
             const int64_t ns = std::min<int64_t>(65535, nseg - s0);
             RVX_LAUNCH("select_topk", k_sel_sort, dim3((unsigned)ns), dim3(1024), (size_t)P * 8, D + s0 * ld, len, ld,
-                       cnt + s0, sel + s0 * k, k, P, idmap ? idmap + s0 * len : nullptr, id_offset, out_d + s0 * k,
-                       out_i + s0 * k, out_n ? out_n + s0 : nullptr);
+                       cnt + s0, sel + s0 * ks, k, ks, P, idmap ? idmap + s0 * len : nullptr, id_offset,
+                       out_d + s0 * k, out_i + s0 * k, out_n ? out_n + s0 : nullptr);
         }
         return;
     }
     // k > 8192: slots past each query's count to ~0 (sorted last), rocPRIM's segmented
     // radix sort, then decode
-    const int64_t tot = nseg * (int64_t)k;
+    const int64_t tot = nseg * (int64_t)ks;
     auto* sorted = (unsigned long long*)scratch_bytes("sel_sorted", tot * 8);
     auto* off = (unsigned*)scratch_bytes("sel_offsets", (nseg + 1) * 4);
-    RVX_LAUNCH("select_topk", k_seg_offsets, dim3((unsigned)((nseg + 1 + 255) / 256)), dim3(256), 0, off, nseg, k);
-    RVX_LAUNCH("select_topk", k_fill_tail, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, sel, cnt, nseg, k);
+    RVX_LAUNCH("select_topk", k_seg_offsets, dim3((unsigned)((nseg + 1 + 255) / 256)), dim3(256), 0, off, nseg, ks);
+    RVX_LAUNCH("select_topk", k_fill_tail, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, sel, cnt, nseg, ks);
     size_t tmp_bytes = 0;
     RVX_HIP(rocprim::segmented_radix_sort_keys(nullptr, tmp_bytes, sel, sorted, (unsigned)tot, (unsigned)nseg, off,
                                                off + 1, 0, 64, stream()));
@@ -292,8 +297,9 @@ void select_topk(const float* D, int64_t nseg, int64_t len, int64_t ld, int k, c
         RVX_HIP(rocprim::segmented_radix_sort_keys(tmp, tmp_bytes, sel, sorted, (unsigned)tot, (unsigned)nseg, off,
                                                    off + 1, 0, 64, stream()));
     }
-    RVX_LAUNCH("select_topk", k_sel_emit, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, D, len, ld, cnt, sorted,
-               nseg, k, idmap, id_offset, out_d, out_i, out_n);
+    const int64_t outs = nseg * (int64_t)k;
+    RVX_LAUNCH("select_topk", k_sel_emit, dim3((unsigned)((outs + 255) / 256)), dim3(256), 0, D, len, ld, cnt, sorted,
+               nseg, k, ks, idmap, id_offset, out_d, out_i, out_n);
 }
 
 }  // namespace rvx

@@ -117,6 +117,15 @@ def comm_traffic(comm) -> tuple:
     return sent.value, recv.value
 
 
+def comm_selfcheck(comm) -> tuple:
+    """(rows, mismatched 32-bit words) of the RVX_COMM_SELF_P2P record check: the GraphSAGE
+    exchange's compact records after an RCCL round trip to the rank itself, expanded by the
+    receivers' unpack kernel and compared with their source rows (rvx_comm_selfcheck)."""
+    rows, bad = C.c_int64(), C.c_int64()
+    L.call("rvx_comm_selfcheck", comm._h, C.byref(rows), C.byref(bad))
+    return rows.value, bad.value
+
+
 class RcclComm:
     """RCCL communicator of librvx (one per process/GPU)."""
 

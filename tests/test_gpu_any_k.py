@@ -109,18 +109,41 @@ def wide_graph():
     return _hnsw_pair(30_000, 32, 8, 40, 208)
 
 
-@pytest.mark.parametrize("k,ef,rg", [(10, 16384, "0"), (300, 16384, "0"), (10, 25000, "0"), (50, 2000, "1")])
-def test_hnsw_ef_past_8192_bit_exact(monkeypatch, wide_graph, k, ef, rg):
+@pytest.mark.parametrize("k,ef,rg,bitmap", [(10, 16384, "0", "1"), (300, 16384, "0", "1"), (10, 25000, "0", "1"),
+                                            (50, 2000, "1", "1"), (10, 70000, "0", "0")])
+def test_hnsw_ef_past_8192_bit_exact(monkeypatch, wide_graph, k, ef, rg, bitmap):
     # ef 16384: R in one wave's LDS (one wave per CU); ef 25000: past the LDS, R in HBM;
-    # rg 1 forces the HBM-resident R at an ef the LDS would hold
+    # rg 1 forces the HBM-resident R at an ef the LDS would hold; ef 70000 on the visited HASH
+    # (bitmap 0): past the old 2^24-entry table cap (ef x 4 x 64 > 2^24), the table is
+    # sized by the graph (2n slots: never more than half full) and its slots by bytes
     monkeypatch.setenv("RVX_HNSW_RG", rg)
+    monkeypatch.setenv("RVX_HNSW_BITMAP", bitmap)
     x, h, idx = wide_graph
     q = O.fill_uniform(12 * 32, 209).reshape(12, 32)
+    if ef > 30000:
+        q = q[:4]
     ids, dist, cnt = idx.search_array(q, k, ef)
     rids, rd, rc = h.search(q, k, ef)
     assert np.array_equal(cnt, rc)
     assert np.array_equal(ids.astype(np.int64)[:, :k], rids)
     assert np.array_equal(dist, rd)
+
+
+def test_flat_k_past_n_many_queries_small_budget(monkeypatch):
+    # k > n over many queries — the wide scan's batches budget the whole per-query
+    # footprint (row, selection histogram, min(k, n) keys) and select_topk sizes its keys by
+    # min(k, n); a small budget forces many batches. Equal to the oracle, padding included.
+    monkeypatch.setenv("RVX_SCAN_WIDE_BUDGET_MB", "8")
+    n, d, nq, k = 200, 16, 20_000, 300
+    x = O.fill_uniform(n * d, 213).reshape(n, d)
+    q = O.fill_uniform(nq * d, 214).reshape(nq, d)
+    idx = rv.FlatIndex(d, rv.DistanceMetric.Euclidean)
+    idx.add_array(x, np.arange(n, dtype=np.uint64))
+    ids, dist, cnt = idx.search_array(q, k)
+    rids, rd = O.flat_search(x, q, k, "l2")
+    assert np.all(cnt == n)
+    got = np.where(np.arange(k)[None, :] < cnt[:, None], ids.astype(np.int64), -1)
+    assert np.array_equal(got, rids) and np.array_equal(dist.view(np.uint32), rd.view(np.uint32))
 
 
 @pytest.mark.parametrize("coop", ["0", "2"])

@@ -253,6 +253,36 @@ def test_hnsw_search_query_global_bit_exact(monkeypatch, mode, d, metric):
         assert np.array_equal(dist, rd)
 
 
+# (ef, LDS distance stages, R in HBM) the round-5 rules pick on the LDS-staged path (k_hnsw.hip
+# hnsw_nst / hnsw_search): d <= 768 one stage at ef 1,024..1,151, else two; R moves to HBM once an
+# LDS R leaves < 4 waves per CU (LDS bytes 8,192 * stages + 4d + 8 (ef + 1) + 768 > 40,960):
+# ef >= 2,592 at d 768, >= 2,464 at d 1,024 — each boundary straddled
+_WIDTH_RULES = {768: [(1023, 2, False), (1024, 1, False), (1151, 1, False), (1152, 2, False), (2591, 2, False),
+                      (2592, 2, True)],
+                1024: [(1023, 2, False), (1024, 2, False), (2463, 2, False), (2464, 2, True)]}
+
+
+@pytest.mark.parametrize("d", [768, 1024])
+def test_hnsw_rules_at_tuned_widths_bit_exact(monkeypatch, d):
+    """the width-dependent kernel-form rules were tuned at d 768 / 1,024; at
+    those widths, on both sides of every rule boundary, with k 10 and 300, the search takes the
+    form the rule names and its ids and distances equal the oracle's on the same graph."""
+    monkeypatch.setenv("RVX_HNSW_COOP", "2")  # the LDS-staged path (tables past 4 GB take it by default)
+    for v in ("RVX_HNSW_RG", "RVX_HNSW_NST", "RVX_HNSW_RG_WAVES", "RVX_HNSW_QG", "RVX_HNSW_RG_NST"):
+        monkeypatch.delenv(v, raising=False)
+    x, h, g, idx = _hnsw_pair(3000, d, "l2", 8, 60, 17)
+    q = O.fill_uniform(32 * d, 18).reshape(32, d)
+    for ef, stages, hbm in _WIDTH_RULES[d]:
+        for k in (10, 300):
+            ids, dist, cnt = idx.search_array(q, k, ef)
+            st = rv.hnsw_last_search_stats()
+            assert (st["stages"], st["r_in_hbm"]) == (stages, hbm), (d, ef, st)
+            rids, rd, rc = h.search(q, k, ef)
+            assert np.array_equal(cnt, rc), (d, ef, k)
+            assert np.array_equal(ids.astype(np.int64)[:, :k], rids), (d, ef, k)
+            assert np.array_equal(dist, rd), (d, ef, k)
+
+
 def test_hnsw_search_tie_heavy_bit_exact():
     # 3000 points on 12 distinct vectors: hundreds of exact distance ties at R's
     # farthest (the round-1 candidate list overflowed here and raised RVX_ERR_INDEX);

@@ -108,6 +108,42 @@ def test_neural_search_pipeline_matches_oracle_composition():
     assert mism <= nq // 20
 
 
+def test_neural_search_768_h8_matches_oracle_composition():
+    """C3's re-rank at its own width — d 768, 8 heads, ef 50, gnn_depth 2
+    (RuvectorQuery NeuralSearch defaults, query.rs:44-58; search.rs:56-162, layer.rs:379-423) —
+    weights within 1e-5 of the oracle composition on the same graph and candidates; ids equal
+    except where the oracle's own adjacent weights are closer than 1e-6 (a tie the f32 rounding
+    of the GNN layers may order either way)."""
+    n, d, nq = 3000, 768, 40
+    x = O.fill_uniform(n * d, 121).reshape(n, d)
+    q = O.fill_uniform(nq * d, 122).reshape(nq, d)
+    idx = rv.HnswIndex(d, rv.DistanceMetric.Euclidean, rv.HnswConfig(m=16, ef_construction=100, ef_search=50))
+    xb = rv.Buffer.from_numpy(x)
+    idx.add_device(xb, n, 0)
+    layers = [_layer(d, d, 8, 131 + i) for i in range(2)]
+    ns = rv.NeuralSearch(idx, xb, n, d, [l for l, _ in layers])
+    query = rv.RuvectorQuery(mode=rv.QueryMode.NeuralSearch)
+    assert (query.k, query.ef, query.gnn_depth) == (10, 50, 2)
+    ids, wts = ns.search(q, query)
+    h_ref = O.Hnsw.from_graph(x, idx.export_graph())
+    cand, _, _ = h_ref.search(q, query.ef, query.ef)
+    for i in range(nq):
+        cv = x[cand[i]]
+        fi, fw = O.differentiable_search(q[i], cv, len(cv), query.temperature)
+        soft = np.empty(len(cv), np.float32)
+        soft[fi] = fw
+        h = q[i]
+        for _, W in layers[:query.gnn_depth]:
+            h = O.rvl_forward_one(W, h, cv, soft)
+        pi, pw = O.differentiable_search(h, cv, query.k, query.temperature)
+        ref_ids = cand[i][pi].astype(np.uint64)
+        assert rel_err(wts[i], pw) <= TOL, (i, rel_err(wts[i], pw))
+        for j in np.flatnonzero(ids[i] != ref_ids):
+            # a reordered slot: the oracle's weight there ties (< 1e-6) with a neighbouring slot
+            near = [abs(float(pw[j]) - float(pw[t])) for t in (j - 1, j + 1) if 0 <= t < len(pw)]
+            assert min(near) < 1e-6, (i, j, ids[i], ref_ids, pw)
+
+
 def test_ruvector_query_defaults():
     qd = rv.RuvectorQuery()
     assert (qd.k, qd.ef, qd.gnn_depth, qd.temperature, qd.mode) == (10, 50, 2, 1.0, rv.QueryMode.VectorSearch)

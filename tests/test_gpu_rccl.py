@@ -100,6 +100,35 @@ def test_sage_exchange_self_p2p_bits(comm, self_p2p, monkeypatch):
     assert float(np.max(np.abs(a[:400] - ref)) / np.max(np.abs(ref))) <= 1e-5
 
 
+@pytest.mark.parametrize("row_bytes", [None, "900"])
+def test_sage_records_unpacked_behind_rccl(comm, self_p2p, monkeypatch, row_bytes):
+    """at world 1 the receive side of the compact records (rows_xchg_unpack)
+    never ran behind RCCL. With RVX_COMM_SELF_P2P the rank's own records go out and come back
+    through RCCL's p2p path and are expanded by the receivers' unpack kernel into a shadow that
+    is compared word for word with the rows they encode (rvx_comm_selfcheck): every row checked,
+    no word different — by default and with a budget most rows overflow (those stay dense)."""
+    from ruvector_amd.shard import comm_selfcheck
+    monkeypatch.setenv("RVX_SAGE_CHUNKS", "3")
+    if row_bytes:
+        monkeypatch.setenv("RVX_XCHG_ROW_BYTES", row_bytes)
+    N, d, deg = 3 * 16384 + 77, 768, 6
+    x = O.fill_uniform(N * d, 191).reshape(N, d) - 0.5
+    rp, col = O.random_csr(N, deg, 192)
+    g = rv.Graph.from_csr(rp, col)
+    layer = rv.GraphSAGELayer(d, d, num_samples=deg)
+    xb = rv.Buffer.from_numpy(x)
+    off = np.array([0, N], np.int64)
+    off_p = off.ctypes.data_as(C.POINTER(C.c_int64))
+    iv = rv.Buffer(N * 4)
+    rows0, bad0 = comm_selfcheck(comm)
+    a, b = _sage_pair(comm, layer, g, xb, N, d, off_p, off_p, "rvx_sage_forward_exchange3", (None, None),
+                      (iv.handle, None))
+    rows1, bad1 = comm_selfcheck(comm)
+    assert rows1 - rows0 == N and bad1 == bad0 == 0, (rows0, rows1, bad0, bad1)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert 0.3 < float((a == 0).mean()) < 0.7  # ReLU-sparse rows: the records are the compact form
+
+
 def test_gnn_and_attention_exchange_self_p2p_bits(comm, self_p2p, monkeypatch):
     from ruvector_amd.attention import EdgeFeaturedAttention, EdgeFeaturedConfig
     monkeypatch.setenv("RVX_SAGE_CHUNKS", "3")
@@ -153,10 +182,13 @@ def test_bench_force_comm_rccl(tmp_path):
     max-over-ranks clock are RCCL all-reduces around a real timed step."""
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "2", "--warmup", "1",
-                        "--nodes", "200000", "--no-cpu", "--no-scan", "--no-c4", "--no-hnsw",
+                        "--nodes", "200000", "--no-cpu", "--no-scan", "--no-c4", "--no-hnsw", "--no-c5",
                         "--transport", "rccl", "--force-comm", "--check-rows", "512"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 1 and line["value"] > 0
     assert line["comm"]["transport"] == "rccl" and line["comm"]["forced"] is True
     assert line["comm"]["self_p2p_rounds"] > 0
+    # the compact records of every round came back through RCCL and unpacked bit for bit
+    chk = line["comm"]["record_selfcheck"]
+    assert chk["rows"] > 0 and chk["mismatched_words"] == 0, chk

@@ -15,6 +15,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -29,8 +30,16 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("offsets", [[0, 75001, 150001], [0, 60000, 100000, 150001]])
-def test_exchange_entry_points_multi_rank(offsets, tmp_path):
+# world 8: the driver's 8-GPU run is the first time 8-way round plans,
+# rotated peer order, record budgets and overflow passes meet RCCL, so they run here first
+# with 8 ranks on one GPU: ragged shards, one empty shard (it sends empty blocks every round,
+# contributes no chunk-0 rate and owns no overflow rows), 2 rounds (largest shard 36,000 rows
+# >= 2 x 16,384)
+W8 = [0, 9000, 30000, 30000, 66000, 80000, 101000, 120000, 150001]
+
+
+@pytest.mark.parametrize("offsets,chunks", [([0, 75001, 150001], 3), ([0, 60000, 100000, 150001], 3), (W8, 2)])
+def test_exchange_entry_points_multi_rank(offsets, chunks, tmp_path):
     world = len(offsets) - 1
     port = _free_port()
     env = dict(os.environ, PYTHONUNBUFFERED="1")
@@ -39,20 +48,21 @@ def test_exchange_entry_points_multi_rank(offsets, tmp_path):
         out = tmp_path / f"rank{r}.json"
         procs.append((out, subprocess.Popen(
             [sys.executable, os.path.join(ROOT, "tests", "shard_exchange_worker.py"), str(world), str(r), str(port),
-             str(out), ",".join(map(str, offsets))], env=env, start_new_session=True)))
+             str(out), ",".join(map(str, offsets)), str(chunks)], env=env, start_new_session=True)))
     try:
         for _, p in procs:
-            p.wait(timeout=170)
+            p.wait(timeout=170 if world <= 3 else 400)
     finally:
         for _, p in procs:
             if p.poll() is None:
                 os.killpg(p.pid, 9)
     res = [json.loads(o.read_text()) for o, _ in procs]
+    errs = {r["rank"]: r["error"] for r in res if "error" in r}
+    assert not errs, errs  # every failing rank's own traceback (the first one names the cause)
     for r in res:
-        assert "error" not in r, r.get("error")
-        assert r["rounds"] == 3
+        assert r["rounds"] == chunks
         # bench.py's multi-GPU report reads these tags: one transfer per round, one exposed wait per layer
-        assert r["prof_tags"] == {"halo_exchange": 3, "exchange_wait": 1}, r["prof_tags"]
+        assert r["prof_tags"] == {"halo_exchange": chunks, "exchange_wait": 1}, r["prof_tags"]
         assert r["sage_layer1_all_rows_equal"] and r["sage_layer1_halo_rows"] > 0, r
         assert r["sage_layer2_owned_equal"], r
         assert r["sage_layer1_vs_oracle"] <= 1e-5, r
@@ -73,6 +83,12 @@ def test_exchange_entry_points_multi_rank(offsets, tmp_path):
         for name in ("dense", "default", "half", "all"):
             assert x[name]["layer1_all_rows_equal"] and x[name]["layer2_owned_equal"], (name, x)
         per_row = (r["xchg_record_bytes_mean"] * 1.02 + 16 + 8 + 16) / (4 * 768 + 4)
-        assert x["default"]["sent"] <= per_row * x["dense"]["sent"], (per_row, x)
+        # (+ the call's fixed words: the chunk-0 rate and overflow-count all-gathers, 24 B per peer)
+        fixed = 24 * (world - 1)
+        assert x["default"]["sent"] <= per_row * x["dense"]["sent"] + fixed, (per_row, x)
         assert x["half"]["image_counts_ok"], x
-        assert x["all"]["sent"] > x["dense"]["sent"] * 0.9, x  # nearly every row went dense
+        assert x["all"]["sent"] >= x["dense"]["sent"] * 0.9, x  # nearly every row went dense
+    # the empty shard received every row of the table and sent none
+    if 0 in np.diff(offsets):
+        empty = res[int(np.flatnonzero(np.diff(offsets) == 0)[0])]
+        assert empty["sage_layer1_halo_rows"] == offsets[-1] and empty["xchg"]["dense"]["sent"] == 0, empty

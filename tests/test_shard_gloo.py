@@ -82,18 +82,19 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_node_range_shards_match_single_process():
+@pytest.mark.parametrize("world", [2, 8])
+def test_node_range_shards_match_single_process(world):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(180)
-    res = sorted(q.get(timeout=5) for _ in range(2))
-    assert res == [(0, True, True), (1, True, True)]
+    res = sorted(q.get(timeout=5) for _ in range(world))
+    assert res == [(r, True, True) for r in range(world)]
 
 
 def _exchange_worker(rank, world, port, q):
@@ -107,7 +108,10 @@ def _exchange_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         # ragged shards, one far below the pipelining threshold
-        sizes = [900_000, 150_001, 5_000][:world]  # the largest shard above PIPE_CHUNKS * PIPE_MIN_ROWS
+        # the largest shard above PIPE_CHUNKS * PIPE_MIN_ROWS; at world 8 also an empty shard and a
+        # one-row shard (they send empty blocks in most rounds)
+        sizes = ([900_000, 150_001, 5_000] if world <= 3 else
+                 [900_000, 150_001, 5_000, 0, 70_000, 1, 300_000, 20_000])[:world]
         offsets = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
         n, d = int(offsets[-1]), 3
         full = np.arange(n * d, dtype=np.float32).reshape(n, d)
@@ -141,7 +145,7 @@ def _exchange_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_chunked_halo_exchange_protocol(world):
     """rvx_sage_forward_exchange's round plan (mirrored by shard.exchange_rounds)
     reconstructs the full table on every rank with ragged shards."""
@@ -174,7 +178,9 @@ def test_shard_plan_rows_cover_and_owner():
 
 # ---- the C++ round plan and the host-staged transport (no GPU needed) --------
 @pytest.mark.parametrize("offsets", [[0, 1000], [0, 500, 1001], [0, 60000, 100000, 150001],
-                                     [0, 400000, 800000], [0, 393216 * 2, 393216 * 2 + 5, 393216 * 3]])
+                                     [0, 400000, 800000], [0, 393216 * 2, 393216 * 2 + 5, 393216 * 3],
+                                     [0, 9000, 30000, 30000, 66000, 80000, 101000, 120000, 150001],
+                                     [1250000 * p for p in range(9)]])
 def test_exchange_plan_matches_mirror(offsets):
     """rvx_exchange_plan (the plan rvx_sage_forward_exchange runs, api_graph.cpp
     exchange_plan) equals the Python mirror shard.exchange_rounds; the whole-shard
@@ -223,7 +229,7 @@ def _host_comm_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_host_transport_moves_every_block(world):
     """HostComm's exchange callback (the host-staged transport behind rvx_comm_init_host)
     delivers each rank's block to every peer, ragged and empty blocks included."""
@@ -253,7 +259,7 @@ def _rdv_worker(rank, world, port, q):
     q.put((rank, uid, len(made)))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_tcp_rendezvous_hands_rank0_id_to_every_rank(world):
     """bench.py's multi-GPU bootstrap without torch.distributed: rank 0's RCCL id
     (here a stand-in byte string) reaches every rank over the stdlib TCP

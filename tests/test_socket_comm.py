@@ -1,4 +1,4 @@
-"""The stdlib-socket host transport (ruvector_amd.shard.SocketComm) on CPU, world 3:
+"""The stdlib-socket host transport (ruvector_amd.shard.SocketComm) on CPU, world 3 and 8:
 scalar all-reduces (sum / max / min, the bench's barrier and max-over-ranks clock) and
 the rvx_host_exchange_fn frames the C++ exchange / broadcast / all-gather paths send
 (ragged blocks, an empty block, a root-only broadcast). The GPU side of the same
@@ -8,6 +8,8 @@ import socket
 import subprocess
 import sys
 import textwrap
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -57,12 +59,14 @@ def _port():
         return s.getsockname()[1]
 
 
-def test_socket_comm_world3(tmp_path):
+@pytest.mark.parametrize("world", [3, 8])
+def test_socket_comm_world(world, tmp_path):
+    """world 3 and 8 (the driver's 8-GPU size: the full mesh, scalar all-reduces through rank 0)."""
     w = tmp_path / "worker.py"
     w.write_text(WORKER)
     port = _port()
-    procs = [subprocess.Popen([sys.executable, str(w), "3", str(r), str(port), ROOT], stdout=subprocess.PIPE,
-                              stderr=subprocess.STDOUT, text=True, start_new_session=True) for r in range(3)]
+    procs = [subprocess.Popen([sys.executable, str(w), str(world), str(r), str(port), ROOT], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True, start_new_session=True) for r in range(world)]
     outs = []
     try:
         for p in procs:
