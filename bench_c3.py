@@ -75,6 +75,9 @@ def leg(xb, n, d, qb, nq, m=32, efc=200, efs=(100, 400, 1600), k=10, cpu=True, c
                       "dist_per_query": round(st["n_dist"] / nq, 1), "expand_per_query": round(st["n_expand"] / nq, 1),
                       "roofline": {"bound": "hbm", "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS,
                                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+                                   "rate_kind": RATE_KIND, "practical_ceiling_GBps": RANDOM_ROW_GBPS,
+                                   "frac_of_practical": round(ach / RANDOM_ROW_GBPS, 4) if ach else None,
+                                   "caveat": RATE_CAVEAT if ach and ach > 0.72 * HBM_PEAK_GBS else None,
                                    "traffic": None, "alg_bytes_per_launch": alg_bytes, "launches": launches}})
         log(f"c3 ef={ef}: recall@{k}={rec:.4f} qps={nq / dt:.0f} (kernel {ker_ms:.2f} ms, "
             f"{st['n_dist'] / nq:.0f} dist/query, {ach and round(ach)} GB/s algorithmic)")
@@ -170,6 +173,18 @@ def cpu_leg(idx, xb, qb, n, d, nq, k, ef, cpu_seconds, log):
             bool(np.array_equal(cids, gpu)))
 
 
+# The search reads random rows; MI355X_MICROARCH.md:357 measures 5.7-5.8 TB/s for random 2,304-B
+# rows of a table far past the Infinity Cache (6.29 TB/s for a float4 copy, :36). Rows that many
+# in-flight queries share (the entry neighbourhood, hub rows) are served from the Infinity Cache,
+# and FETCH_SIZE counts L2 misses including Infinity-Cache hits (:297), so neither the
+# algorithmic rate nor the PMC bytes are pure HBM throughput.
+RANDOM_ROW_GBPS = 5750.0
+RATE_KIND = ("fabric: algorithmic row bytes (SURVEY.md §8d) / kernel time; rows shared by concurrent queries come "
+             "from the Infinity Cache, so this bounds HBM bytes/s from above")
+RATE_CAVEAT = ("above 0.72 of HBM peak = the guide's random-row gather ceiling (5.75 TB/s): part of these bytes are "
+               "Infinity-Cache hits, so 'frac' is an upper bound on the HBM fraction, not HBM throughput")
+
+
 def attach_search_traffic(out, n, d, nq, m, efc):
     """HBM bytes per search launch from the committed rocprofv3 --pmc passes of this leg
     (scripts/c3_traffic.sh -> profiles/pmc_traffic_c3.json), when the configuration matches."""
@@ -189,7 +204,8 @@ def attach_search_traffic(out, n, d, nq, m, efc):
         if ent:
             s["roofline"]["traffic"] = round(ent["hbm_bytes_per_launch"], 0)
             s["roofline"]["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE(x2, gfx950) + WRITE_SIZE, "
-                                               "profiles/pmc_traffic_c3.json")
+                                               "profiles/pmc_traffic_c3.json: L2-miss bytes, Infinity-Cache hits "
+                                               "included (an upper bound on HBM bytes)")
 
 
 def main():

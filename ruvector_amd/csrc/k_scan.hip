@@ -21,6 +21,11 @@
 // merged by one lane per query after each row tile.
 #include <cfloat>
 #include <type_traits>
+#ifdef RVX_SCAN_CLOCK
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+#endif
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -417,6 +422,9 @@ struct FilterArgs {
     unsigned* gbound; int k; const unsigned* xsq_max_bits;
     // per-row-bound metrics (Poincaré, squared L2): row factors {R, C, S, N} and beta
     const float4* xc4; float beta;
+    // diagnostic build only (-DRVX_SCAN_CLOCK): per block {delta s_memtime, delta s_memrealtime}
+    // over the block's life; null and unused in the real kernel
+    unsigned long long* clk;
 };
 
 // Order-preserving float <-> uint (atomicMin over possibly negative values).
@@ -494,6 +502,9 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef RVX_SCAN_CLOCK  // MI355X_MICROARCH.md DVFS item 6: clock = d(s_memtime) / d(s_memrealtime) x 100 MHz
+    const unsigned long long clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef RVX_SCAN_PRIO  // experiment: static priority for the second-dispatched half of the waves
     if (wave >= Cf::NW / 2) __builtin_amdgcn_s_setprio(1);
 #endif
@@ -1060,6 +1071,13 @@ __global__ __launch_bounds__(FCfg<CFG>::THREADS, FCfg<CFG>::BLOCKS) void k_scan_
         a.part_v[o] = best_v[i];
         a.part_r[o] = best_r[i];
     }
+#ifdef RVX_SCAN_CLOCK
+    if (tid == 0) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        a.clk[2 * blockIdx.x] = t1 - clk_t0;
+        a.clk[2 * blockIdx.x + 1] = r1 - clk_r0;
+    }
+#endif
 }
 
 struct RerankArgs {
@@ -1622,11 +1640,35 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
         case METRIC_L2SQ: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, C, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<METRIC_L2SQ, C, false>), grid, blk, F_LDS, fa); break; \
         default: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, C, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_DOT, C, false>), grid, blk, F_LDS, fa); break; \
     }
+#ifdef RVX_SCAN_CLOCK
+        fa.clk = (unsigned long long*)scratch_bytes("scan_clk", (int64_t)grid.x * 16);
+#endif
         if (cfg == 1) { RVX_FILTER_LAUNCH(1) }
         else if (cfg == 2) { RVX_FILTER_LAUNCH(2) }
         else if (cfg == 3) { RVX_FILTER_LAUNCH(3) }
         else { RVX_FILTER_LAUNCH(0) }
 #undef RVX_FILTER_LAUNCH
+#ifdef RVX_SCAN_CLOCK
+        {  // median over blocks of each block's own clock; printed per launch (diagnostic build)
+            std::vector<unsigned long long> h((size_t)grid.x * 2);
+            RVX_HIP(hipMemcpyAsync(h.data(), fa.clk, h.size() * 8, hipMemcpyDeviceToHost, stream()));
+            sync();
+            std::vector<double> ghz;
+            double life = 0.0;
+            for (unsigned b = 0; b < grid.x; ++b)
+                if (h[2 * b + 1] > 0) {
+                    ghz.push_back((double)h[2 * b] / (double)h[2 * b + 1] * 0.1);
+                    life += (double)h[2 * b + 1] * 10e-9;
+                }
+            std::sort(ghz.begin(), ghz.end());
+            static int launch = 0;
+            if (!ghz.empty())
+                std::fprintf(stderr, "[scan clock] launch %d cfg %d: median %.3f GHz (p10 %.3f, p90 %.3f) over %zu blocks, "
+                             "mean block life %.2f ms\n", launch, cfg, ghz[ghz.size() / 2], ghz[ghz.size() / 10],
+                             ghz[ghz.size() * 9 / 10], ghz.size(), life / (double)ghz.size() * 1e3);
+            ++launch;
+        }
+#endif
     }
     RerankArgs ra{q, qnorm, qc, x, xnorm, nq, d, k, nsplit_total, part_v, part_r, max_bits, id_offset, out_d, out_i,
                   unsure};
@@ -1709,9 +1751,43 @@ __global__ void k_row_norm_sq(const float* x, int64_t n, int d, float* out) {
     if (r < n) out[r] = pdev::norm_sq(x + r * d, d);
 }
 
+// The same per-row chain (norm_squared's order: one running sum over groups of four) with the
+// rows staged through LDS 32 floats at a time: a thread per row reading its own 4 KB row walks
+// addresses 4 KB apart across the wave (1 TB/s at 6.25M x 1024, 25 ms); here each 128-B row
+// segment is one coalesced load and the chain reads LDS (odd row stride: no bank conflicts).
+constexpr int RNS_CH = 32;
+__global__ __launch_bounds__(256) void k_row_norm_sq_lds(const float* __restrict__ x, int64_t n, int d,
+                                                          float* __restrict__ out) {
+    __shared__ float tile[256 * (RNS_CH + 1)];
+    const int tid = threadIdx.x;
+    const int64_t r0 = (int64_t)blockIdx.x * 256;
+    const int rows = (int)min<int64_t>(256, n - r0);
+    float s = 0.0f;
+    for (int c0 = 0; c0 < d; c0 += RNS_CH) {
+#pragma unroll
+        for (int k = 0; k < RNS_CH / 4; ++k) {  // 256 rows x 8 float4: 8 lanes per 128-B row segment
+            const int f = k * 256 + tid, r = f / (RNS_CH / 4), c4 = f % (RNS_CH / 4);
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r < rows) v = *reinterpret_cast<const float4*>(x + (r0 + r) * d + c0 + 4 * c4);
+            float* t = tile + r * (RNS_CH + 1) + 4 * c4;
+            t[0] = v.x; t[1] = v.y; t[2] = v.z; t[3] = v.w;
+        }
+        __syncthreads();
+        const float* t = tile + tid * (RNS_CH + 1);
+#pragma unroll
+        for (int i = 0; i < RNS_CH; i += 4)
+            s = s + (((t[i] * t[i] + t[i + 1] * t[i + 1]) + t[i + 2] * t[i + 2]) + t[i + 3] * t[i + 3]);
+        __syncthreads();
+    }
+    if (tid < rows) out[r0 + tid] = s;
+}
+
 void row_norm_sq(const float* x, int64_t n, int d, float* out) {
     if (n <= 0) return;
-    RVX_LAUNCH("row_norm_sq", k_row_norm_sq, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, x, n, d, out);
+    if (d % RNS_CH == 0 && ((uintptr_t)x & 15) == 0)
+        RVX_LAUNCH("row_norm_sq", k_row_norm_sq_lds, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, x, n, d, out);
+    else
+        RVX_LAUNCH("row_norm_sq", k_row_norm_sq, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, x, n, d, out);
 }
 
 ScanStats& last_scan_stats() {
