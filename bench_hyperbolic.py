@@ -144,6 +144,8 @@ def run_sharded(n, d, nq, efs, comm, rank, world, cpu_queries=4, cpu_seconds=0.0
             dt = vmax(time.perf_counter() - t0)
         kern = prof.summary()
         ids = gid.download(np.int64, (nq, k))
+        if mode in ("exact", "pruned"):
+            out_scan = rv.scan_last_stats()  # K10 filter vs exact-VALU queries of this rank's scan
         if mode == "exact":
             gt = ids
             if cpu_check is not None and rank == 0:
@@ -157,6 +159,8 @@ def run_sharded(n, d, nq, efs, comm, rank, world, cpu_queries=4, cpu_seconds=0.0
         out_modes[key] = {"qps": round(nq / dt, 1), "recall_at_10": round(recall(gt, ids), 4),
                           "wall_ms": round(dt * 1e3, 1), "phase_ms_rank0": phases,
                           "kernel_ms_rank0": {t: round(v["total_ms"], 3) for t, v in kern.items()}}
+        if mode in ("exact", "pruned"):
+            out_modes[key]["scan_stats_rank0"] = out_scan
         filt = kern.get("scan_filter")
         if mode in ("exact", "pruned") and filt and filt["total_ms"] > 0:
             # K10 ranks every (query, row) pair with f16 MFMA over the d Poincaré (exact) or

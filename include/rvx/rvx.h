@@ -436,6 +436,10 @@ rvx_status rvx_hnsw_last_search_form(int32_t* r_in_hbm, int32_t* stages, int32_t
  * kernel, and queries the filter handed back to the VALU kernel (completeness not provable).
  * Results are identical either way; this is for tests and benchmarks. */
 rvx_status rvx_scan_last_stats(int64_t* mfma_queries, int64_t* valu_queries, int64_t* fallback_queries);
+/* Queries of that scan the MFMA filter ran a second time with the most splits the re-rank holds
+ * (one conversion chunk), after their first lists could not prove completeness; those still
+ * unsure are the fallback queries above (an rvx extension for tests and benchmarks). */
+rvx_status rvx_scan_last_second_pass(int64_t* second_pass_queries);
 
 /* HNSW graph interchange (fixed-graph parity and GNN topology).
  * Layer 0: CSR over all n points in stored neighbour order (hnsw_rs keeps

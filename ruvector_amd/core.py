@@ -250,7 +250,9 @@ def scan_last_stats() -> dict:
     """Path of the most recent exact scan: MFMA-filtered queries, exact-VALU queries, filter fallbacks."""
     a, b, c = C.c_int64(), C.c_int64(), C.c_int64()
     _check("rvx_scan_last_stats", C.byref(a), C.byref(b), C.byref(c))
-    return {"mfma": a.value, "valu": b.value, "fallback": c.value}
+    s2 = C.c_int64()
+    _check("rvx_scan_last_second_pass", C.byref(s2))
+    return {"mfma": a.value, "valu": b.value, "fallback": c.value, "second_pass": s2.value}
 
 
 class FlatIndex(_Index):

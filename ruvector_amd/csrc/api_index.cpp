@@ -556,6 +556,13 @@ rvx_status rvx_scan_last_stats(int64_t* mfma_queries, int64_t* valu_queries, int
     });
 }
 
+rvx_status rvx_scan_last_second_pass(int64_t* second_pass_queries) {
+    return guard([&] {
+        RVX_REQUIRE(second_pass_queries, RVX_ERR_INVALID_PARAMETER, "null argument");
+        *second_pass_queries = last_scan_stats().second_pass_queries;
+    });
+}
+
 rvx_status rvx_hnsw_last_search_stats(int64_t* n_dist, int64_t* n_expand, int64_t* nq) {
     return guard([&] {
         ComputeLock cl;

@@ -21,6 +21,7 @@
 // product is unchanged. Double-buffered LDS, one barrier per K tile, register
 // prefetch of tile k+1 during the MFMAs of tile k, XCD-aware block swizzle so
 // the column tiles of one row block share an XCD's L2.
+#include <cstdio>
 #include "common.hpp"
 #include "graph.hpp"
 #include "kernels.hpp"
@@ -1775,9 +1776,28 @@ __device__ __forceinline__ void h2w_tile(const GemmArgs& g, int epi, int64_t wgi
 // HELP: after the last tile every wave takes destination rows of the next chunk's gather
 // (g.help, aggrow::agg_help_run) — the GEMM's CU slots would otherwise idle beside the gather's
 // one block per CU until the chunk's gather ends.
+#ifdef RVX_GEMM_CLOCK
+// Diagnostic build only (scripts/exp/gemm_clock.sh): every block of gemm_nt_h2w adds its
+// s_memtime and s_memrealtime deltas; the host prints the block-time-weighted clock per launch
+// (MI355X_MICROARCH.md DVFS item 6: clock = d(s_memtime) / d(s_memrealtime) x 100 MHz).
+__device__ unsigned long long g_gemm_clk[2];
+struct GemmClockStamp {
+    unsigned long long t0, r0;
+    __device__ GemmClockStamp() : t0(__builtin_amdgcn_s_memtime()), r0(__builtin_amdgcn_s_memrealtime()) {}
+    __device__ ~GemmClockStamp() {
+        if (threadIdx.x == 0) {
+            atomicAdd(&g_gemm_clk[0], __builtin_amdgcn_s_memtime() - t0);
+            atomicAdd(&g_gemm_clk[1], __builtin_amdgcn_s_memrealtime() - r0);
+        }
+    }
+};
+#endif
 template <bool DUAL, int WN, int BN, int NW = 8, bool PIPE = false, bool HELP = false, bool AMX = false,
           bool GATE = false, bool M16 = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? (PIPE ? 2 : 3) : 1) void gemm_nt_h2w(GemmArgs g, int epi) {
+#ifdef RVX_GEMM_CLOCK
+    GemmClockStamp clk_stamp;
+#endif
     if (g.queue) {
         extern __shared__ __attribute__((aligned(16))) unsigned char xsm[];
         int64_t* s_t = reinterpret_cast<int64_t*>(xsm);
@@ -2117,6 +2137,19 @@ int gemm_nt_h2(int64_t M, int N, const GemmOperand& s0, const _Float16* B0h, con
             if (s1) RVX_LAUNCH(t, (gemm_nt_h2w<true, 4, 256>), wg, wb, wlds, g, ep.epi);
             else RVX_LAUNCH(t, (gemm_nt_h2w<false, 4, 256>), wg, wb, wlds, g, ep.epi);
         }
+#ifdef RVX_GEMM_CLOCK
+        {
+            static unsigned long long prev[2] = {0, 0};
+            unsigned long long h[2];
+            sync();
+            RVX_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_gemm_clk), sizeof h));
+            const double dt = (double)(h[0] - prev[0]), dr = (double)(h[1] - prev[1]);
+            if (dr > 0)
+                std::fprintf(stderr, "[gemm clock] %s: %.3f GHz (block-time weighted, %.1f block-ms)\n", t,
+                             dt / dr * 0.1, dr * 1e-5);
+            prev[0] = h[0]; prev[1] = h[1];
+        }
+#endif
         if (ep.gate_out && !g.gate_out)
             mul_rows(C + ep.gate_col0, ldc, ep.gate_h, ep.gate_out, M, N - ep.gate_col0, ep.row_absmax);
         else if (ep.row_absmax && !g.row_absmax)

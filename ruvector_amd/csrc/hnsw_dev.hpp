@@ -405,13 +405,12 @@ __device__ __forceinline__ void merge_sorted(float* ad, int* ai, int n, const fl
 // exact sequence of farthest values. Returns the admitted lane mask; r = |R|
 // after the batch. R ids may carry the search's expanded flag in bit 31
 // (masked off here).
-__device__ __forceinline__ unsigned long long decide_batch(unsigned long long fmask, float dd, int nid, int ef,
-                                                           const float* rd, const int* ri, int rs, int& r, int lane) {
-    int wn = min(rs, 64);
-    int below = rs - wn;
-    float wd = INFINITY; int wi = INT_MAX;
-    if (lane < wn) { wd = rd[below + lane]; wi = ri[below + lane] & ID_MASK; }
-    r = rs;
+// decide_window: the same decisions from a window already in registers — lane l < wn holds the
+// (below + l)-th smallest entry of R (ids masked), `total` = |R| (the buffered HBM R below).
+__device__ __forceinline__ unsigned long long decide_window(unsigned long long fmask, float dd, int nid, int ef,
+                                                            float wd, int wi, int wn, int below, int total, int& r,
+                                                            int lane) {
+    r = total;
     unsigned long long adm = 0ull;
     unsigned long long todo = fmask;
     while (todo) {
@@ -446,6 +445,15 @@ __device__ __forceinline__ unsigned long long decide_batch(unsigned long long fm
         }
     }
     return adm;
+}
+
+__device__ __forceinline__ unsigned long long decide_batch(unsigned long long fmask, float dd, int nid, int ef,
+                                                           const float* rd, const int* ri, int rs, int& r, int lane) {
+    const int wn = min(rs, 64);
+    const int below = rs - wn;
+    float wd = INFINITY; int wi = INT_MAX;
+    if (lane < wn) { wd = rd[below + lane]; wi = ri[below + lane] & ID_MASK; }
+    return decide_window(fmask, dd, nid, ef, wd, wi, wn, below, rs, r, lane);
 }
 
 // The same admissions decided in parallel (R in LDS). Sequentially (hnsw.rs:1004-1046) fresh
@@ -628,6 +636,122 @@ __device__ __forceinline__ int merge_into_r(float* rd, int* ri, int n, const flo
     if (lane < na && lane + rk < nkeep) { rd[lane + rk] = bd; ri[lane + rk] = bi; }
     __builtin_amdgcn_wave_barrier();
     return first;
+}
+
+// ---- R in HBM with an LDS buffer (the HBM-resident-R search, k_hnsw.hip RG) ---------------
+// R = Rh ∪ B: Rh a sorted array in the slot's HBM row, B a sorted array of <= RB_CAP entries in
+// LDS; every (d, id) pair is in one of them. Admissions go into B (an LDS merge); B moves into
+// Rh in one walk down Rh when it would overflow (flush_into_r) — instead of one walk, with a
+// binary search per admitted entry, over Rh in HBM per admission batch (the HBM-R
+// merges were 60-66% of the cycles and doubled the bytes, one merge at ef 12,288 reading and
+// rewriting ~98 KB). The search is the same set operations on R, so the same expansions, the
+// same admissions and the same result bits.
+constexpr int RB_CAP = 256;
+
+// The union window: lane l < wn gets the (below + l)-th smallest entry of Rh ∪ B (id masked),
+// wsrc 1 when it comes from B. The union's largest 64 lie within Rh's largest 64 and B's largest
+// 64 (an entry with 63 larger ones in the union has at most 63 larger in its own array). Scratch:
+// sd / si / so [64] in LDS.
+__device__ __forceinline__ void union_window(const float* rd, const int* ri, int rs, const float* bd, const int* bi,
+                                             int nb, float* sd, int* si, int* so, float& wd, int& wi, int& wsrc,
+                                             int& wn, int& below, int lane) {
+    const int wr = min(rs, 64), wb = min(nb, 64);
+    float ed = INFINITY, fd = INFINITY;
+    int eid = INT_MAX, fid = INT_MAX;
+    if (lane < wr) { ed = rd[rs - wr + lane]; eid = ri[rs - wr + lane] & ID_MASK; }
+    if (lane < wb) { fd = bd[nb - wb + lane]; fid = bi[nb - wb + lane] & ID_MASK; }
+    int rkr = lane, rkb = lane;  // rank among the wr + wb window entries (pairs are distinct)
+    for (int o = 0; o < wb; ++o) {
+        const float od = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fd), o));
+        rkr += lt_de(od, __builtin_amdgcn_readlane(fid, o), ed, eid) ? 1 : 0;
+    }
+    for (int o = 0; o < wr; ++o) {
+        const float od = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ed), o));
+        rkb += lt_de(od, __builtin_amdgcn_readlane(eid, o), fd, fid) ? 1 : 0;
+    }
+    wn = min(rs + nb, 64);
+    below = rs + nb - wn;
+    const int cut = wr + wb - wn;
+    __builtin_amdgcn_wave_barrier();
+    if (lane < wr && rkr >= cut) { sd[rkr - cut] = ed; si[rkr - cut] = eid; so[rkr - cut] = 0; }
+    if (lane < wb && rkb >= cut) { sd[rkb - cut] = fd; si[rkb - cut] = fid; so[rkb - cut] = 1; }
+    __builtin_amdgcn_wave_barrier();
+    wd = INFINITY; wi = INT_MAX; wsrc = 0;
+    if (lane < wn) { wd = sd[lane]; wi = si[lane]; wsrc = so[lane]; }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// After decide_window over the union window (wd, wi, wsrc)[0..wn) and the sorted admitted batch
+// (sd, si)[0..na): the union holds total + na entries and keeps the first r, so the
+// npop = total + na - r largest go — all within the window and the batch. Counts how many of them
+// are Rh's, B's and the batch's (each array loses its own largest).
+__device__ __forceinline__ void split_pops(float wd, int wi, int wsrc, int wn, const float* sd, const int* si, int na,
+                                           int npop, int& pop_r, int& pop_b, int& pop_a, int lane) {
+    pop_r = pop_b = pop_a = 0;
+    if (npop <= 0) return;
+    float ad = INFINITY; int aid = INT_MAX;
+    if (lane < na) { ad = sd[lane]; aid = si[lane]; }
+    int rkw = lane, rka = lane;
+    for (int o = 0; o < na; ++o) rkw += lt_de(sd[o], si[o], wd, wi) ? 1 : 0;
+    for (int o = 0; o < wn; ++o) {
+        const float od = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wd), o));
+        rka += lt_de(od, __builtin_amdgcn_readlane(wi, o), ad, aid) ? 1 : 0;
+    }
+    const int cut = wn + na - npop;
+    pop_r = __popcll(__ballot(lane < wn && rkw >= cut && wsrc == 0));
+    pop_b = __popcll(__ballot(lane < wn && rkw >= cut && wsrc != 0));
+    pop_a = __popcll(__ballot(lane < na && rka >= cut));
+}
+
+// Move the sorted buffer (bd, bi)[0..nb) (ids may carry the expanded flag) into Rh (rd, ri)[0..rs)
+// in global memory, keeping all rs + nb entries: one walk down Rh from the top, MG chunks read
+// before any is written (entries only move right, so a group's writes never land on the next
+// group's unread entries). Rh entry j moves right by #{B entries before it}; B entry b lands at
+// b + #{Rh entries before it}, found while walking the chunk that holds it. The walk stops once
+// every B entry is placed. Returns the position of B's smallest entry (nothing below it moved).
+template <int MG>
+__device__ int flush_into_r(float* rd, int* ri, int rs, const float* bd, const int* bi, int nb, int lane) {
+    int pb = nb;  // B entries [pb, nb) are placed
+    int low = rs + nb;
+    for (int top = ((rs - 1) / 64) * 64; rs > 0 && top >= 0 && pb > 0; top -= 64 * MG) {
+        float vd[MG];
+        int vi[MG];
+#pragma unroll
+        for (int g = 0; g < MG; ++g) {
+            const int j = top - 64 * g + lane;
+            vd[g] = INFINITY; vi[g] = INT_MAX;
+            if (top - 64 * g >= 0 && j < rs) { vd[g] = rd[j]; vi[g] = ri[j]; }
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int g = 0; g < MG; ++g) {
+            const int base = top - 64 * g;
+            if (base < 0 || pb == 0) break;  // wave-uniform
+            const int j = base + lane;
+            const bool valid = j < rs;
+            const int vm = vi[g] & ID_MASK;
+            const float c0d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vd[g]), 0));
+            const int c0i = __builtin_amdgcn_readlane(vm, 0);
+            int before = 0;  // B entries placed in this chunk that precede my entry
+            while (pb > 0) {
+                const float b_d = bd[pb - 1];
+                const int b_i = bi[pb - 1], b_m = b_i & ID_MASK;
+                if (!lt_de(c0d, c0i, b_d, b_m)) break;  // it precedes the chunk's first entry: lower
+                const int pos = (pb - 1) + base + __popcll(__ballot(valid && lt_de(vd[g], vm, b_d, b_m)));
+                before += (valid && lt_de(b_d, b_m, vd[g], vm)) ? 1 : 0;
+                if (lane == 0) { rd[pos] = b_d; ri[pos] = b_i; }
+                low = pos;
+                --pb;
+            }
+            const int sh = pb + before;  // every remaining B entry precedes the chunk
+            if (valid && sh > 0) { rd[j + sh] = vd[g]; ri[j + sh] = vi[g]; }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    for (int b = lane; b < pb; b += 64) { rd[b] = bd[b]; ri[b] = bi[b]; }  // below every Rh entry
+    if (pb > 0) low = 0;
+    __builtin_amdgcn_wave_barrier();
+    return low;
 }
 
 // distance between two stored rows, reference scalar order (distance.rs)

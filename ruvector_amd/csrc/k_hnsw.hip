@@ -56,6 +56,7 @@ struct SearchArgs {
     float* rg_d;       // RG kernels: R in HBM, [nslots][ef + 1] distances ...
     int* rg_i;         // ... and flagged ids (ef past one wave's LDS)
     int par_decide;    // hnsw_dev.hpp decide_par where R is in LDS
+    int rg_buf;        // RG: R's admissions buffered in LDS (hnsw_dev.hpp RB_CAP); 0 = merge into HBM per batch
 };
 
 // Diagnostic build only (-DRVX_HNSW_PHASES, scripts/exp/build_variant.sh): shader-clock cycles
@@ -103,7 +104,9 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
         sdb = reinterpret_cast<float*>(ri + ef + 1);
     }
     int* sib = reinterpret_cast<int*>(sdb + 64);
-    int* srk = sib + 64;  // the admitted batch's ranks in R (decide_par; R in LDS)
+    int* srk = sib + 64;  // the admitted batch's ranks in R (decide_par; R in LDS); RG: window origins
+    float* bfd = reinterpret_cast<float*>(srk + 64);  // RG: R's LDS buffer (hnsw_dev.hpp RB_CAP) ...
+    int* bfi = reinterpret_cast<int*>(bfd + RB_CAP);   // ... and its flagged ids
 
     unsigned long long* vis = a.vbits ? nullptr : a.visited + (int64_t)blockIdx.x * a.vcap;
     const unsigned vmask = a.vcap - 1;
@@ -190,6 +193,105 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
                     if (lo >= cnt || ids[lo] != pivot) break;
                 }
             } while (moved && a.hyper);
+        }
+
+        // ---- layer 0, R in HBM: R = rd/ri (HBM, sorted) ∪ an LDS buffer (hnsw_dev.hpp RB_CAP):
+        // the same set operations as the branch below, with admissions merged into the buffer and
+        // the buffer moved into the HBM array when full (flush_into_r)
+        if (RG && a.rg_buf) {
+            int rs = 1, nb = 0;
+            {
+                const float d0 = dist_of(pivot);
+                if (lane == 0) {
+                    rd[0] = d0; ri[0] = pivot;
+                    claim(pivot);
+                }
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+            }
+            int scan = 0;  // every entry of the HBM array before `scan` is expanded
+            for (;;) {
+                int at = -1, atb = -1;
+                for (int b0 = scan; b0 < rs; b0 += 64) {
+                    const unsigned long long m = __ballot(b0 + lane < rs && ri[b0 + lane] >= 0);
+                    if (m) { at = b0 + __ffsll((long long)m) - 1; break; }
+                }
+                for (int b0 = 0; b0 < nb; b0 += 64) {
+                    const unsigned long long m = __ballot(b0 + lane < nb && bfi[b0 + lane] >= 0);
+                    if (m) { atb = b0 + __ffsll((long long)m) - 1; break; }
+                }
+                if (at < 0 && atb < 0) break;
+                if (at >= 0 && atb >= 0 && lt_de(bfd[atb], bfi[atb], rd[at], ri[at])) at = -1;  // the buffer's is nearer
+                int c_id;
+                if (at >= 0) {
+                    c_id = ri[at];
+                    scan = at + 1;
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane == 0) ri[at] = c_id | INT_MIN;
+                    __threadfence_block();
+                } else {
+                    c_id = bfi[atb];
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane == 0) bfi[atb] = c_id | INT_MIN;
+                }
+                __builtin_amdgcn_wave_barrier();
+                const int64_t b = a.g.rp0[c_id], e = a.g.rp0[c_id + 1];
+                n_expand += 1;
+                PH_MARK(0);
+                for (int64_t c0 = b; c0 < e; c0 += 64) {
+                    const int64_t p = c0 + lane;
+                    int nid = -1;
+                    bool fresh = false;
+                    if (p < e) {
+                        nid = a.g.col0[p];
+                        fresh = claim(nid);
+                    }
+                    const unsigned long long fmask = __ballot(fresh);
+                    PH_MARK(1);
+                    if (!fmask) continue;
+                    const float dd = dist_lane(fresh ? nid : -1);
+                    PH_MARK(2);
+                    n_dist += (unsigned long long)__popcll(fmask);
+                    float wd;
+                    int wi, wsrc, wn, below;
+                    union_window(rd, ri, rs, bfd, bfi, nb, sdb, sib, srk, wd, wi, wsrc, wn, below, lane);
+                    int r = rs + nb;
+                    const unsigned long long adm = decide_window(fmask, dd, nid, ef, wd, wi, wn, below, rs + nb, r, lane);
+                    const int na = sort_batch(adm, dd, nid, sdb, sib, lane);
+                    PH_MARK(3);
+                    if (na == 0) continue;
+                    int pop_r, pop_b, pop_a;
+                    split_pops(wd, wi, wsrc, wn, sdb, sib, na, rs + nb + na - r, pop_r, pop_b, pop_a, lane);
+                    rs -= pop_r;  // each array loses its own largest entries
+                    nb -= pop_b;
+                    const int keep = na - pop_a;
+                    if (keep > 0) {
+                        if (nb + keep > RB_CAP) {  // the buffer into the HBM array first
+                            scan = min(scan, flush_into_r<RVX_MERGE_RG_G>(rd, ri, rs, bfd, bfi, nb, lane));
+                            __threadfence_block();
+                            rs += nb;
+                            nb = 0;
+                        }
+                        merge_into_r<RVX_MERGE_LDS_G>(bfd, bfi, nb, sdb, sib, keep, nb + keep, lane);
+                        nb += keep;
+                    }
+                    PH_MARK(4);
+                }
+            }
+            if (nb > 0) {
+                flush_into_r<RVX_MERGE_RG_G>(rd, ri, rs, bfd, bfi, nb, lane);
+                __threadfence_block();
+                __builtin_amdgcn_wave_barrier();
+                rs += nb;
+            }
+            const int take = min(a.k, rs);
+            for (int s = lane; s < a.k; s += 64) {
+                a.out_d[qi * a.k + s] = s < take ? rd[s] : INFINITY;
+                a.out_i[qi * a.k + s] = s < take ? (int64_t)(ri[s] & ID_MASK) : (int64_t)-1;
+            }
+            if (lane == 0 && a.out_n) a.out_n[qi] = take;
+            __builtin_amdgcn_wave_barrier();
+            continue;
         }
 
         // ---- layer 0: search_layer (:913-1055) over R alone (hnsw_dev.hpp
@@ -409,7 +511,8 @@ size_t hnsw_search_lds(int d, int ef, bool coop) {
 int hnsw_rg_nst() { return env_int("RVX_HNSW_RG_NST", 2) == 1 ? 1 : 2; }
 size_t hnsw_search_lds_rg(int d, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)wd_lds(hnsw_rg_nst()) : 0) + (size_t)dq * 4 + 64 * 8;  // (no srk: decide_batch)
+    // + the union window's scratch (sdb / sib / origins) and R's LDS buffer (RB_CAP entries)
+    return (coop ? (size_t)wd_lds(hnsw_rg_nst()) : 0) + (size_t)dq * 4 + 64 * 12 + (size_t)RB_CAP * 8;
 }
 
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
@@ -480,7 +583,8 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
         rg_i = (int*)scratch_bytes("hnsw_rg_i", (int64_t)nslots * (ef + 1) * 4);
     }
     SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, vbits, vwords, nslots, vcap, out_d, out_i, out_n, status, stats,
-                 curv, hyper, coop ? 1 : 0, rg_d, rg_i, env_int("RVX_HNSW_PAR_DECIDE", 1) != 0 ? 1 : 0};
+                 curv, hyper, coop ? 1 : 0, rg_d, rg_i, env_int("RVX_HNSW_PAR_DECIDE", 1) != 0 ? 1 : 0,
+                 env_int("RVX_HNSW_RG_BUF", 1) != 0 ? 1 : 0};  // (read per call: tests and A/Bs run both)
     // RVX_HNSW_QG=1 (read per call): LDS-staged distances read the query from global memory (no LDS copy)
     const int nst_sel = rg ? hnsw_rg_nst() : hnsw_nst(coop, d, ef);
     const bool qg = coop && (rg ? nst_sel == 2 : (nst_sel == 1 || nst_sel == 2)) && env_int("RVX_HNSW_QG", 0) != 0 &&

@@ -1609,29 +1609,12 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
         attr = true;
     }
     const bool cos = metric == RVX_METRIC_COSINE;
-    rows_to_f16(q, nq, d, qh, qc, cos ? qnorm : nullptr, nullptr, nullptr, flags);
-    // the filter's shared bound needs eps from max |x|^2 over every row before
-    // the first chunk's filter (cosine: eps is a constant)
-    if (nchunks > 1 && !cos && !prb) row_sq_max(x, n, d, max_bits);
-    for (int64_t c = 0; c < nchunks; ++c) {
-        const int64_t c0 = c * chunk_rows, c1 = std::min(n, c0 + chunk_rows);
-        if (prb) {
-            const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((c1 - c0 + 3) / 4, 4096));
-            RVX_LAUNCH("scan_f16", k_rows_to_f16_pr, dim3((unsigned)blocks), dim3(256), 0, x + c0 * d, c1 - c0, d, xh, xc4,
-                       rb + c0, deleted ? deleted + c0 : nullptr, metric == RVX_METRIC_POINCARE ? curv : 0.0f, beta,
-                       flags);
-        } else {
-            rows_to_f16(x + c0 * d, c1 - c0, d, xh, xc, cos ? xnorm + c0 : nullptr, deleted ? deleted + c0 : nullptr,
-                        max_bits, flags);
-        }
-        FilterArgs fa{xh, xc, qh, qc, nq, c0, c1, d, rows_per_split, (int)(c * s_c), (int)qtiles, nsplit_total,
-                      part_v, part_r, gbound, k, max_bits, xc4, beta};
-        const dim3 grid((unsigned)(qtiles * s_c));
+    // list insertion: one lane per query (0, default) or 16-lane groups with one list
+    // slot per lane (1, opt-in: spills ~100 B/lane in the 256-register wide tile and ran
+    // 225 vs 173 ms at 10M x 768 / 10k, scripts/exp_scan_group.sh); read per call
+    const bool group = env_int("RVX_SCAN_GROUP", 0) != 0;
+    auto launch_filter = [&](FilterArgs& fa, dim3 grid) {
         const dim3 blk((unsigned)F_THREADS);
-        // list insertion: one lane per query (0, default) or 16-lane groups with one list
-        // slot per lane (1, opt-in: spills ~100 B/lane in the 256-register wide tile and ran
-        // 225 vs 173 ms at 10M x 768 / 10k, scripts/exp_scan_group.sh); read per call
-        const bool group = env_int("RVX_SCAN_GROUP", 0) != 0;
 #define RVX_FILTER_LAUNCH(C)                                                                                          \
     switch (metric) {                                                                                                 \
         case RVX_METRIC_L2: if (group) RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, C, true>), grid, blk, F_LDS, fa); else RVX_LAUNCH("scan_filter", (k_scan_filter<RVX_METRIC_L2, C, false>), grid, blk, F_LDS, fa); break; \
@@ -1669,20 +1652,44 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
             ++launch;
         }
 #endif
+    };
+    // the reference-order rerank of nqq queries' lists (qq rows, their norms and f16 constants)
+    auto launch_rerank = [&](const float* qq, const float* qqn, const float2* qqc, int64_t nqq, int nsplit,
+                             float* pv, int32_t* pr, float* od, int64_t* oi, int32_t* uns) {
+        const dim3 rg((unsigned)((nqq + 3) / 4));
+        if (prb) {
+            RerankPrArgs rp{qq, qqc, x, rb, nqq, d, k, nsplit, pv, pr, beta, curv, id_offset, od, oi, uns};
+            if (metric == RVX_METRIC_POINCARE) RVX_LAUNCH("scan_rerank", k_scan_rerank_pr<RVX_METRIC_POINCARE>, rg, dim3(256), 0, rp);
+            else RVX_LAUNCH("scan_rerank", k_scan_rerank_pr<METRIC_L2SQ>, rg, dim3(256), 0, rp);
+            return;
+        }
+        RerankArgs ra{qq, qqn, qqc, x, xnorm, nqq, d, k, nsplit, pv, pr, max_bits, id_offset, od, oi, uns};
+        switch (metric) {
+            case RVX_METRIC_L2: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_L2>, rg, dim3(256), 0, ra); break;
+            case RVX_METRIC_COSINE: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_COSINE>, rg, dim3(256), 0, ra); break;
+            default: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_DOT>, rg, dim3(256), 0, ra); break;
+        }
+    };
+    rows_to_f16(q, nq, d, qh, qc, cos ? qnorm : nullptr, nullptr, nullptr, flags);
+    // the filter's shared bound needs eps from max |x|^2 over every row before
+    // the first chunk's filter (cosine: eps is a constant)
+    if (nchunks > 1 && !cos && !prb) row_sq_max(x, n, d, max_bits);
+    for (int64_t c = 0; c < nchunks; ++c) {
+        const int64_t c0 = c * chunk_rows, c1 = std::min(n, c0 + chunk_rows);
+        if (prb) {
+            const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((c1 - c0 + 3) / 4, 4096));
+            RVX_LAUNCH("scan_f16", k_rows_to_f16_pr, dim3((unsigned)blocks), dim3(256), 0, x + c0 * d, c1 - c0, d, xh, xc4,
+                       rb + c0, deleted ? deleted + c0 : nullptr, metric == RVX_METRIC_POINCARE ? curv : 0.0f, beta,
+                       flags);
+        } else {
+            rows_to_f16(x + c0 * d, c1 - c0, d, xh, xc, cos ? xnorm + c0 : nullptr, deleted ? deleted + c0 : nullptr,
+                        max_bits, flags);
+        }
+        FilterArgs fa{xh, xc, qh, qc, nq, c0, c1, d, rows_per_split, (int)(c * s_c), (int)qtiles, nsplit_total,
+                      part_v, part_r, gbound, k, max_bits, xc4, beta};
+        launch_filter(fa, dim3((unsigned)(qtiles * s_c)));
     }
-    RerankArgs ra{q, qnorm, qc, x, xnorm, nq, d, k, nsplit_total, part_v, part_r, max_bits, id_offset, out_d, out_i,
-                  unsure};
-    const dim3 rg((unsigned)((nq + 3) / 4));
-    if (prb) {
-        RerankPrArgs rp{q, qc, x, rb, nq, d, k, nsplit_total, part_v, part_r, beta, curv, id_offset, out_d, out_i, unsure};
-        if (metric == RVX_METRIC_POINCARE) RVX_LAUNCH("scan_rerank", k_scan_rerank_pr<RVX_METRIC_POINCARE>, rg, dim3(256), 0, rp);
-        else RVX_LAUNCH("scan_rerank", k_scan_rerank_pr<METRIC_L2SQ>, rg, dim3(256), 0, rp);
-    } else
-    switch (metric) {
-        case RVX_METRIC_L2: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_L2>, rg, dim3(256), 0, ra); break;
-        case RVX_METRIC_COSINE: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_COSINE>, rg, dim3(256), 0, ra); break;
-        default: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_DOT>, rg, dim3(256), 0, ra); break;
-    }
+    launch_rerank(q, qnorm, qc, nq, nsplit_total, part_v, part_r, out_d, out_i, unsure);
     // flags[0] bad input, flags[2] unsure-query count: 16 B through a pinned
     // host word; the per-query flags come down only when some query is unsure
     static int32_t* hflags = nullptr;
@@ -1707,8 +1714,63 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
             if (h[i]) redo.push_back((int32_t)i);
     }
     last_scan_stats().mfma_queries += nq;
-    last_scan_stats().fallback_queries += (int64_t)redo.size();
     if (redo.empty()) return true;
+    // Second pass (one conversion chunk: the f16 image of every row is still in scratch): the
+    // queries whose lists could not prove completeness run the filter again on their own with as
+    // many splits as the rerank holds — each FKP-long list then covers fewer rows, so far fewer
+    // lists fill below the threshold — before the rest take the exact VALU scan over every row.
+    // C5's 6.25M x 1024 Poincaré scan: ~0.6% of 10k queries were unsure with 32 splits, and their
+    // VALU scan took 61 of 221 ms; their second filter streams the f16 image once. Results are the
+    // same bits either way (the rerank is the reference arithmetic); RVX_SCAN_SECOND=0 skips it.
+    if (nchunks == 1 && env_int("RVX_SCAN_SECOND", 1) != 0) {
+        const int64_t s2 = std::max<int64_t>(1, std::min<int64_t>(max_splits, (tiles + 1) / 2));
+        const int64_t rps2 = ((n + s2 - 1) / s2 + FR - 1) / FR * FR;
+        const int nsplit2 = (int)((n + rps2 - 1) / rps2);
+        if (nsplit2 > nsplit_total) {
+            const int64_t c2 = (int64_t)redo.size();
+            const int64_t qtiles2 = (c2 + FQ - 1) / FQ;
+            int32_t* didx2 = (int32_t*)scratch_bytes("mscan2_idx", c2 * 4);
+            RVX_HIP(hipMemcpyAsync(didx2, redo.data(), (size_t)c2 * 4, hipMemcpyHostToDevice, stream()));
+            float* q2 = scratch_f32("mscan2_q", c2 * d);
+            float* q2n = cos ? scratch_f32("mscan2_qn", c2) : nullptr;
+            RVX_LAUNCH("scan_gather", k_gather_rows, dim3((unsigned)((c2 * d + 255) / 256)), dim3(256), 0, q, didx2, c2, d,
+                       q2);
+            if (q2n)
+                RVX_LAUNCH("scan_gather", k_gather_rows, dim3((unsigned)((c2 + 255) / 256)), dim3(256), 0, qnorm, didx2, c2,
+                           1, q2n);
+            _Float16* qh2 = (_Float16*)scratch_bytes("mscan2_qh", c2 * d * 2);
+            float2* qc2 = (float2*)scratch_bytes("mscan2_qc", c2 * 8);
+            int32_t* flags2 = (int32_t*)scratch_bytes("mscan2_flags", 16 + c2 * 4);
+            RVX_HIP(hipMemsetAsync(flags2, 0, (size_t)(16 + c2 * 4), stream()));
+            unsigned* gbound2 = (unsigned*)scratch_bytes("mscan2_gbound", c2 * 4);
+            RVX_HIP(hipMemsetD32Async((hipDeviceptr_t)gbound2, 0xFF800000u, (size_t)c2, stream()));
+            float* pv2 = scratch_f32("mscan2_part_v", c2 * nsplit2 * FKP);
+            int32_t* pr2 = (int32_t*)scratch_bytes("mscan2_part_r", c2 * nsplit2 * FKP * 4);
+            float* rd2 = scratch_f32("mscan2_d", c2 * k);
+            int64_t* ri2 = (int64_t*)scratch_bytes("mscan2_i", c2 * k * 8);
+            rows_to_f16(q2, c2, d, qh2, qc2, q2n, nullptr, nullptr, flags2);
+            FilterArgs fa2{xh, xc, qh2, qc2, c2, 0, n, d, rps2, 0, (int)qtiles2, nsplit2, pv2, pr2, gbound2, k, max_bits,
+                           xc4, beta};
+            launch_filter(fa2, dim3((unsigned)(qtiles2 * nsplit2)));
+            launch_rerank(q2, q2n, qc2, c2, nsplit2, pv2, pr2, rd2, ri2, flags2 + 4);
+            RVX_LAUNCH("scan_gather", k_scatter_topk, dim3((unsigned)((c2 * k + 255) / 256)), dim3(256), 0, rd2, ri2,
+                       didx2, c2, k, out_d, out_i);
+            RVX_HIP(hipMemcpyAsync(hflags, flags2, 16, hipMemcpyDeviceToHost, stream()));
+            sync();
+            last_scan_stats().second_pass_queries += c2;
+            std::vector<int32_t> still;
+            if (hflags[2] > 0) {
+                std::vector<int32_t> h(c2);
+                RVX_HIP(hipMemcpyAsync(h.data(), flags2 + 4, (size_t)(c2 * 4), hipMemcpyDeviceToHost, stream()));
+                sync();
+                for (int64_t i = 0; i < c2; ++i)
+                    if (h[i]) still.push_back(redo[i]);
+            }
+            redo.swap(still);
+            if (redo.empty()) return true;
+        }
+    }
+    last_scan_stats().fallback_queries += (int64_t)redo.size();
     // queries whose lists could not prove completeness: exact VALU scan
     const int64_t cnt = (int64_t)redo.size();
     int32_t* didx = (int32_t*)scratch_bytes("mscan_redo_idx", cnt * 4);

@@ -15,6 +15,7 @@ constexpr int METRIC_L2SQ = 16;
 // Path of the most recent scan_topk call (rvx_scan_last_stats).
 struct ScanStats {
     int64_t mfma_queries = 0, valu_queries = 0, fallback_queries = 0;
+    int64_t second_pass_queries = 0;  // unsure after the first filter, run again with the most splits
 };
 ScanStats& last_scan_stats();
 

@@ -129,6 +129,24 @@ def test_hnsw_ef_past_8192_bit_exact(monkeypatch, wide_graph, k, ef, rg, bitmap)
     assert np.array_equal(dist, rd)
 
 
+@pytest.mark.parametrize("ef,k", [(2000, 300), (6000, 10)])
+def test_hnsw_hbm_r_buffer_and_merge_forms_bit_exact(monkeypatch, wide_graph, ef, k):
+    # R in HBM (forced): admissions buffered in LDS and flushed into the HBM array (default,
+    # RVX_HNSW_RG_BUF=1; many flushes at these ef on a 30k-node graph) and the one-merge-per-batch
+    # form (0) give the oracle's ids and distances
+    monkeypatch.setenv("RVX_HNSW_RG", "1")
+    x, h, idx = wide_graph
+    q = O.fill_uniform(24 * 32, 215).reshape(24, 32)
+    rids, rd, rc = h.search(q, k, ef)
+    for buf in ("1", "0"):
+        monkeypatch.setenv("RVX_HNSW_RG_BUF", buf)
+        ids, dist, cnt = idx.search_array(q, k, ef)
+        assert rv.hnsw_last_search_stats()["r_in_hbm"]
+        assert np.array_equal(cnt, rc), buf
+        assert np.array_equal(ids.astype(np.int64)[:, :k], rids), buf
+        assert np.array_equal(dist, rd), buf
+
+
 def test_flat_k_past_n_many_queries_small_budget(monkeypatch):
     # k > n over many queries — the wide scan's batches budget the whole per-query
     # footprint (row, selection histogram, min(k, n) keys) and select_topk sizes its keys by

@@ -283,10 +283,13 @@ def test_hnsw_rules_at_tuned_widths_bit_exact(monkeypatch, d):
             assert np.array_equal(dist, rd), (d, ef, k)
 
 
-def test_hnsw_search_tie_heavy_bit_exact():
+@pytest.mark.parametrize("rg", ["0", "1"])
+def test_hnsw_search_tie_heavy_bit_exact(monkeypatch, rg):
     # 3000 points on 12 distinct vectors: hundreds of exact distance ties at R's
     # farthest (the round-1 candidate list overflowed here and raised RVX_ERR_INDEX);
-    # ids and distances equal the oracle's (d, id)-ordered search on the same graph
+    # ids and distances equal the oracle's (d, id)-ordered search on the same graph.
+    # rg 1: R in HBM with its LDS admission buffer (ties between the buffer and the HBM array)
+    monkeypatch.setenv("RVX_HNSW_RG", rg)
     n, d = 3000, 16
     base = O.fill_uniform(12 * d, 21).reshape(12, d)
     x = np.ascontiguousarray(base[np.arange(n) % 12])

@@ -113,6 +113,7 @@ def test_duplicates_fall_back_and_stay_exact(monkeypatch):
         ids, dist = flat(x, metric).brute_force_array(q, 12)
         st = rv.scan_last_stats()
         assert st["mfma"] == 260 and st["fallback"] > 0, st
+        assert st["second_pass"] >= st["fallback"], st  # the unsure queries' second filter first
         rids, rd = O.flat_search(x, q, 12, name)
         assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd)
 
@@ -266,3 +267,27 @@ def test_tangent_pruned_scan_through_the_filter(monkeypatch, d):
     monkeypatch.setenv("RVX_SCAN_MFMA", "0")
     vids, vdist, _ = h.search_with_pruning_batch(q, 10)
     assert np.array_equal(ids, vids) and np.array_equal(dist, vdist)
+
+
+@pytest.mark.parametrize("second", ["1", "0"])
+def test_poincare_second_pass_same_bits(monkeypatch, second):
+    """Queries whose first-pass lists cannot prove completeness run the filter again with the most
+    splits the re-rank holds (RVX_SCAN_SECOND, default on) before any VALU fallback: the exact
+    Poincaré top-k is the oracle's bit for bit either way (C5-shaped ball data, d 256)."""
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    monkeypatch.setenv("RVX_SCAN_SECOND", second)
+    n, d, nq, k = 20000, 256, 300, 10
+    r = np.random.default_rng(216)
+    x = r.standard_normal((n, d)).astype(np.float32)
+    x = (x / np.linalg.norm(x, axis=1, keepdims=True) * (0.9 * r.random((n, 1)))).astype(np.float32)
+    q = r.standard_normal((nq, d)).astype(np.float32)
+    q = (q / np.linalg.norm(q, axis=1, keepdims=True) * (0.9 * r.random((nq, 1)))).astype(np.float32)
+    h = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=3), dim=d)
+    h.insert_batch(x)
+    ids, dist, _ = h.brute_force(q, k)
+    st = rv.scan_last_stats()
+    assert st["mfma"] == nq, st
+    if second == "0":
+        assert st["second_pass"] == 0, st
+    rids, rd = O.hyp_scan_rows(x, q, k, threads=8)  # the oracle's exact Poincaré scan (poincare.rs order)
+    assert np.array_equal(np.asarray(ids, np.int64), rids) and np.array_equal(dist, rd)
