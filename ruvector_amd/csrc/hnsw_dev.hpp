@@ -646,7 +646,10 @@ __device__ __forceinline__ int merge_into_r(float* rd, int* ri, int n, const flo
 // merges were 60-66% of the cycles and doubled the bytes, one merge at ef 12,288 reading and
 // rewriting ~98 KB). The search is the same set operations on R, so the same expansions, the
 // same admissions and the same result bits.
-constexpr int RB_CAP = 256;
+#ifndef RVX_RB_CAP
+#define RVX_RB_CAP 256
+#endif
+constexpr int RB_CAP = RVX_RB_CAP;
 
 // The union window: lane l < wn gets the (below + l)-th smallest entry of Rh ∪ B (id masked),
 // wsrc 1 when it comes from B. The union's largest 64 lie within Rh's largest 64 and B's largest

@@ -410,9 +410,13 @@ template <int METRIC, int NST, bool RG>
 __global__ __launch_bounds__(64) void k_hnsw_search_qg(SearchArgs a) {
     search_body<METRIC, ROW_BATCH, NST, RG, true>(a);
 }
-// ef past one wave's LDS: R in HBM (one distance stage when coop).
+// ef past one wave's LDS: R in HBM (one distance stage when coop). RVX_RG_WPE: occupancy
+// attribute for A/B builds (scripts/exp/build_variant.sh).
+#ifndef RVX_RG_WPE
+#define RVX_RG_WPE
+#endif
 template <int METRIC, int NST = 1>
-__global__ __launch_bounds__(64) void k_hnsw_search_rg(SearchArgs a) {
+__global__ __launch_bounds__(64) RVX_RG_WPE void k_hnsw_search_rg(SearchArgs a) {
     search_body<METRIC, ROW_BATCH, NST, true>(a);
 }
 

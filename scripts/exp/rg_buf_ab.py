@@ -24,6 +24,8 @@ def main():
     p.add_argument("--ef", default="8192,12288")
     p.add_argument("--queries", type=int, default=4096)
     p.add_argument("--reps", type=int, default=2)
+    p.add_argument("--forms", default="1,0", help="RVX_HNSW_RG_BUF settings to run")
+    p.add_argument("--arms", default="", help="instead of --forms: arms 'name:VAR=v,VAR=v;name2:...' (env read per call)")
     a = p.parse_args()
     import ruvector_amd as rv
     from benchutil import heartbeat
@@ -46,8 +48,12 @@ def main():
     for ef in [int(e) for e in a.ef.split(",")]:
         ref = None
         for rep in range(a.reps):
-            for buf in ("1", "0"):
-                os.environ["RVX_HNSW_RG_BUF"] = buf
+            arms = ([(f"buf{b}", {"RVX_HNSW_RG_BUF": b}) for b in a.forms.split(",")] if not a.arms else
+                    [(x.split(":")[0], dict(kv.split("=") for kv in x.split(":")[1].split(",") if kv))
+                     for x in a.arms.split(";")])
+            for buf, env in arms:
+                saved = {kk: os.environ.get(kk) for kk in env}
+                os.environ.update(env)
                 rv._lib.call("rvx_index_search_device", idx.handle, qb.handle, min(nq, 256), k, ef, ids_b.handle,
                              dist_b.handle)
                 rv.synchronize()
@@ -65,6 +71,11 @@ def main():
                 same = bool(np.array_equal(got[0], ref[0]) and np.array_equal(got[1].view(np.uint32),
                                                                              ref[1].view(np.uint32)))
                 rec = float(np.mean([len(set(x.tolist()) & set(y.tolist())) / k for x, y in zip(gt, got[0])]))
+                for kk, vv in saved.items():
+                    if vv is None:
+                        os.environ.pop(kk, None)
+                    else:
+                        os.environ[kk] = vv
                 row = {"ef": ef, "buf": buf, "rep": rep, "qps": round(nq / dt, 1), "kernel_ms": round(prof.query("hnsw_search")[0], 2),
                        "recall": round(rec, 4), "same_as_first": same, "r_in_hbm": st["r_in_hbm"], "stages": st["stages"],
                        "dist_per_query": round(st["n_dist"] / nq, 1), "expand_per_query": round(st["n_expand"] / nq, 1)}
