@@ -650,6 +650,9 @@ __device__ __forceinline__ int merge_into_r(float* rd, int* ri, int n, const flo
 #define RVX_RB_CAP 256
 #endif
 constexpr int RB_CAP = RVX_RB_CAP;
+// an expansion's fresh neighbours collected before admission (k_hnsw.hip collect_fresh): whole
+// layer-0 lists of up to this many entries (MAX_C0, the builder's cap), longer lists slice by slice
+constexpr int FRESH_CAP = 256;
 
 // The union window: lane l < wn gets the (below + l)-th smallest entry of Rh ∪ B (id masked),
 // wsrc 1 when it comes from B. The union's largest 64 lie within Rh's largest 64 and B's largest

@@ -57,6 +57,7 @@ struct SearchArgs {
     int* rg_i;         // ... and flagged ids (ef past one wave's LDS)
     int par_decide;    // hnsw_dev.hpp decide_par where R is in LDS
     int rg_buf;        // RG: R's admissions buffered in LDS (hnsw_dev.hpp RB_CAP); 0 = merge into HBM per batch
+    int collect;       // layer-0 lists of <= FRESH_CAP claimed whole, fresh neighbours batched (collect_fresh)
 };
 
 // Diagnostic build only (-DRVX_HNSW_PHASES, scripts/exp/build_variant.sh): shader-clock cycles
@@ -107,6 +108,7 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
     int* srk = sib + 64;  // the admitted batch's ranks in R (decide_par; R in LDS); RG: window origins
     float* bfd = reinterpret_cast<float*>(srk + 64);  // RG: R's LDS buffer (hnsw_dev.hpp RB_CAP) ...
     int* bfi = reinterpret_cast<int*>(bfd + RB_CAP);   // ... and its flagged ids
+    int* frs = RG ? bfi + RB_CAP : srk + 64;           // an expansion's fresh neighbours [FRESH_CAP]
 
     unsigned long long* vis = a.vbits ? nullptr : a.visited + (int64_t)blockIdx.x * a.vcap;
     const unsigned vmask = a.vcap - 1;
@@ -148,6 +150,34 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
                 }
             }
             return node >= 0 ? dist_of(node) : INFINITY;
+        };
+        // Claim a whole layer-0 list (up to FRESH_CAP neighbours, the loads and claims of its
+        // 64-entry slices issued back to back) and compact the fresh neighbours into frs in list
+        // order: the admissions then take batches of up to 64 FRESH neighbours, one distance
+        // pass each, instead of one pass per 64-entry slice of the list (M 128: 256-entry lists,
+        // ~55 fresh per expansion at high ef — one pass instead of four). Claims do not depend on
+        // admissions, so the admissions see the same neighbours in the same order.
+        auto collect_fresh = [&](int64_t b, int64_t e) -> int {
+            int nids[FRESH_CAP / 64];
+            bool fr[FRESH_CAP / 64];
+#pragma unroll
+            for (int sl = 0; sl < FRESH_CAP / 64; ++sl) {
+                const int64_t p = b + 64 * sl + lane;
+                nids[sl] = p < e ? a.g.col0[p] : -1;
+            }
+#pragma unroll
+            for (int sl = 0; sl < FRESH_CAP / 64; ++sl) fr[sl] = nids[sl] >= 0 && claim(nids[sl]);
+            int nf = 0;
+#pragma unroll
+            for (int sl = 0; sl < FRESH_CAP / 64; ++sl) {
+                const unsigned long long m = __ballot(fr[sl]);
+                const int before = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                if (fr[sl]) frs[nf + before] = nids[sl];
+                nf += __popcll(m);
+            }
+            __builtin_amdgcn_wave_barrier();
+            return nf;
         };
 
         // ---- upper layers: single pass per layer (search_filter :1499-1517)
@@ -238,12 +268,16 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
                 const int64_t b = a.g.rp0[c_id], e = a.g.rp0[c_id + 1];
                 n_expand += 1;
                 PH_MARK(0);
-                for (int64_t c0 = b; c0 < e; c0 += 64) {
-                    const int64_t p = c0 + lane;
+                const bool whole = a.collect && e - b <= FRESH_CAP;  // (wave-uniform) else slice by slice
+                const int nf = whole ? collect_fresh(b, e) : 0;
+                for (int64_t c0 = whole ? 0 : b, c1 = whole ? nf : e; c0 < c1; c0 += 64) {
                     int nid = -1;
                     bool fresh = false;
-                    if (p < e) {
-                        nid = a.g.col0[p];
+                    if (whole) {
+                        nid = c0 + lane < nf ? frs[c0 + lane] : -1;
+                        fresh = nid >= 0;
+                    } else if (c0 + lane < e) {
+                        nid = a.g.col0[c0 + lane];
                         fresh = claim(nid);
                     }
                     const unsigned long long fmask = __ballot(fresh);
@@ -326,12 +360,18 @@ __device__ __forceinline__ void search_body(const SearchArgs& a) {
             const int64_t b = a.g.rp0[c_id], e = a.g.rp0[c_id + 1];
             n_expand += 1;
             PH_MARK(0);
-            for (int64_t c0 = b; c0 < e; c0 += 64) {
-                const int64_t p = c0 + lane;
+            // (wave-uniform; with R in LDS only for the LDS-staged distances: per-lane distances over
+            // R in LDS ran 16% slower batched, 1M x 768 M 128 ef 1,600; profiles/r06_hnsw_collect_ab_1m.log)
+            const bool whole = a.collect && coop && e - b <= FRESH_CAP;
+            const int nf = whole ? collect_fresh(b, e) : 0;
+            for (int64_t c0 = whole ? 0 : b, c1 = whole ? nf : e; c0 < c1; c0 += 64) {
                 int nid = -1;
                 bool fresh = false;
-                if (p < e) {
-                    nid = a.g.col0[p];
+                if (whole) {
+                    nid = c0 + lane < nf ? frs[c0 + lane] : -1;
+                    fresh = nid >= 0;
+                } else if (c0 + lane < e) {
+                    nid = a.g.col0[c0 + lane];
                     fresh = claim(nid);
                 }
                 const unsigned long long fmask = __ballot(fresh);
@@ -485,7 +525,7 @@ bool hnsw_coop(int metric, int d, int64_t rows) {
 namespace {
 size_t search_lds_nst(int d, int ef, int nst) {
     const int dq = (d + 3) & ~3;
-    return (size_t)wd_lds(nst) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 12;
+    return (size_t)wd_lds(nst) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 12 + (size_t)FRESH_CAP * 4;
 }
 }  // namespace
 
@@ -507,16 +547,22 @@ int hnsw_nst(bool coop, int d, int ef) {
 
 size_t hnsw_search_lds(int d, int ef, bool coop) {
     const int dq = (d + 3) & ~3;
-    return (coop ? (size_t)wd_lds(hnsw_nst(coop, d, ef)) : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 12;
+    return (coop ? (size_t)wd_lds(hnsw_nst(coop, d, ef)) : 0) + (size_t)dq * 4 + (size_t)(ef + 1) * 8 + 64 * 12 +
+           (size_t)FRESH_CAP * 4;
 }
 // LDS of the RG kernel: distance stage + query + admitted batch (R is in HBM)
-// distance stages of the RG kernel, 2 unless RVX_HNSW_RG_NST=1 (read per call): with R out
-// of LDS the second stage costs no wave (ef 12288 above: 1134 -> 1266 QPS)
-int hnsw_rg_nst() { return env_int("RVX_HNSW_RG_NST", 2) == 1 ? 1 : 2; }
+// distance stages of the RG kernel: 1 unless RVX_HNSW_RG_NST=2 (read per call). Round 5 (R merged
+// into HBM per batch) preferred 2 (ef 12288: 1134 -> 1266 QPS); with R's LDS admission buffer
+// (2.3 KB more LDS per wave) one stage fits 11 waves per CU instead of 7: 1M x 768 M 128 (LDS-staged
+// forced) ef 8,192 1,405 -> 1,931 QPS, 12,288 995 -> 1,381; 10M x 768 M 128 (10k queries) within 1%
+// either way (1,104 vs 1,097 at ef 12,288; profiles/r06_hnsw_coop_ab_1m.log,
+// r06_c3_10m_m128_efc500_forms.log)
+int hnsw_rg_nst() { return env_int("RVX_HNSW_RG_NST", 1) == 2 ? 2 : 1; }
 size_t hnsw_search_lds_rg(int d, bool coop) {
     const int dq = (d + 3) & ~3;
     // + the union window's scratch (sdb / sib / origins) and R's LDS buffer (RB_CAP entries)
-    return (coop ? (size_t)wd_lds(hnsw_rg_nst()) : 0) + (size_t)dq * 4 + 64 * 12 + (size_t)RB_CAP * 8;
+    return (coop ? (size_t)wd_lds(hnsw_rg_nst()) : 0) + (size_t)dq * 4 + 64 * 12 + (size_t)RB_CAP * 8 +
+           (size_t)FRESH_CAP * 4;
 }
 
 void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnorm, int d, const float* q,
@@ -532,14 +578,28 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     // queries: ef 3200 8.7k -> 11.0k, 4096 5.0k -> 8.2k; 20M x 128 ef 4096 11.5k -> 14.2k;
     // scripts/exp/exp_hnsw_nst.py, profiles/r05_hnsw_rg_rule_*.txt).
     // RVX_HNSW_RG: 1 always, 0 only past the LDS, unset auto (read per call: tests force both)
-    const bool coop0 = hnsw_coop(metric, d, g.n);
+    // LDS-staged distances also for long rows on smaller tables when the layer-0 lists span several
+    // 64-entry slices (round 6: with whole lists batched they fill the DMA stages; 1M x 768 M 128,
+    // 2,048 queries: ef 1,600 8.71k -> 9.72k QPS, 4,096 4.20k -> 5.02k, 8,192 2.86k -> 3.22k,
+    // 12,288 2.27k -> 2.46k against per-lane distances, profiles/r06_hnsw_collect_ab_1m.log)
+    const bool coop0 = hnsw_coop(metric, d, g.n) ||
+                       (env_int("RVX_HNSW_COOP", 1) == 1 && d >= 512 && g.max_deg > 64 &&
+                        env_int("RVX_HNSW_COLLECT", 1) != 0 && hnsw_coop(metric, d, INT64_MAX / (4 * (int64_t)d)));
     const int rg_mode = env_int("RVX_HNSW_RG", -1);
     const size_t lds_r = hnsw_search_lds(d, ef, coop0);
     // waves per CU below which R moves to HBM: 4 (RVX_HNSW_RG_WAVES=W, read per call, for A/Bs),
     // on the footprint of the stage count hnsw_nst picks
     const int rg_waves = std::max(1, env_int("RVX_HNSW_RG_WAVES", 4));
     const bool rg_auto = lds_r * (size_t)rg_waves > 160 * 1024;
-    const bool rg = lds_r > 160 * 1024 || rg_mode == 1 || (rg_mode < 0 && coop0 && rg_auto);
+    // per-lane distances (tables below the translation reach, the Poincaré metrics): HBM R once
+    // an LDS R would leave fewer than 6 waves per CU (RVX_HNSW_RG_WAVES_LANE). Round 6, with R's
+    // admissions buffered in LDS (1M x 768 M 128, 2,048 queries, profiles/r06_hnsw_coop_ab_1m.log):
+    // ef 4,096 (LDS R: 4.4 waves) 3.05k -> 3.99k QPS, 8,192 846 -> 2.29k, 12,288 300 -> 1.66k;
+    // ef 1,600 (9 waves) stays in LDS (8.67k vs 8.18k)
+    const int rg_waves_lane = std::max(1, env_int("RVX_HNSW_RG_WAVES_LANE", 6));
+    const bool rg_auto_lane = lds_r * (size_t)rg_waves_lane > 160 * 1024;
+    const bool rg = lds_r > 160 * 1024 || rg_mode == 1 ||
+                    (rg_mode < 0 && (coop0 ? rg_auto : rg_auto_lane));
     const unsigned vcap = visited_capacity(ef, g.max_deg, g.n);
     // visited set: a per-slot bitmap over all n nodes (cleared per query by its
     // wave: no launch-wide memset, no probing, n/8 bytes touched) when at least
@@ -588,7 +648,8 @@ void hnsw_search(const HnswDev& g, int metric, const float* x, const float* xnor
     }
     SearchArgs a{g, x, xnorm, d, q, qnorm, nq, k, ef, vis, vbits, vwords, nslots, vcap, out_d, out_i, out_n, status, stats,
                  curv, hyper, coop ? 1 : 0, rg_d, rg_i, env_int("RVX_HNSW_PAR_DECIDE", 1) != 0 ? 1 : 0,
-                 env_int("RVX_HNSW_RG_BUF", 1) != 0 ? 1 : 0};  // (read per call: tests and A/Bs run both)
+                 env_int("RVX_HNSW_RG_BUF", 1) != 0 ? 1 : 0,  // (read per call: tests and A/Bs run both)
+                 env_int("RVX_HNSW_COLLECT", 1) != 0 ? 1 : 0};
     // RVX_HNSW_QG=1 (read per call): LDS-staged distances read the query from global memory (no LDS copy)
     const int nst_sel = rg ? hnsw_rg_nst() : hnsw_nst(coop, d, ef);
     const bool qg = coop && (rg ? nst_sel == 2 : (nst_sel == 1 || nst_sel == 2)) && env_int("RVX_HNSW_QG", 0) != 0 &&

@@ -51,6 +51,7 @@ struct BuildArgs {
     int coop;    // wave-cooperative LDS-staged distances in the layer searches
     float* rg_d; int* rg_i;  // RG: R in HBM, [nslots][ef_c + 1] (ef_c past one wave's LDS)
     int* vis_full;           // set when a visited table fills (hnsw_dev.hpp visit_claim): the batch fails
+    int collect;             // whole lists claimed first, fresh neighbours batched (RVX_HNSW_COLLECT, default 1)
 };
 
 __device__ __forceinline__ int list_get(const BuildGraph& G, int p, int l, const int** ids, const float** ds) {
@@ -104,11 +105,40 @@ __device__ int build_search_layer(const BuildArgs& a, const float* qs, float qn,
         const int* nbi;
         const float* nbd;
         const int cnt = list_get(a.G, c_id, l, &nbi, &nbd);
-        for (int c0 = 0; c0 < cnt; c0 += 64) {
+        // The whole list claimed first and its fresh neighbours compacted in list order, then
+        // admitted in batches of up to 64 (one distance pass each instead of one per 64-entry
+        // slice; as the query kernel's collect_fresh, k_hnsw.hip). The fresh ids sit in the parts
+        // of the selection arrays the search does not use: sd[64..MAX_C0) then si[64..MAX_C0).
+        int* const fsd = reinterpret_cast<int*>(sdb) + 64;
+        int* const fsi = sib + 64;
+        auto fslot = [&](int f) -> int* { return f < MAX_C0 - 64 ? fsd + f : fsi + (f - (MAX_C0 - 64)); };
+        const bool whole = a.collect && cnt <= MAX_C0 && cnt > 64;  // (wave-uniform; one slice needs no compaction)
+        int nf = 0;
+        if (whole) {
+            int nids[MAX_C0 / 64];
+            bool fr[MAX_C0 / 64];
+#pragma unroll
+            for (int sl = 0; sl < MAX_C0 / 64; ++sl) nids[sl] = 64 * sl + lane < cnt ? nbi[64 * sl + lane] : -1;
+#pragma unroll
+            for (int sl = 0; sl < MAX_C0 / 64; ++sl) fr[sl] = nids[sl] >= 0 && visit_claim(vis, vmask, tag, nids[sl], a.vis_full);
+#pragma unroll
+            for (int sl = 0; sl < MAX_C0 / 64; ++sl) {
+                const unsigned long long m = __ballot(fr[sl]);
+                const int before = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                if (fr[sl]) *fslot(nf + before) = nids[sl];
+                nf += __popcll(m);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        for (int c0 = 0, c1 = whole ? nf : cnt; c0 < c1; c0 += 64) {
             const int p = c0 + lane;
             int nid = -1;
             bool fresh = false;
-            if (p < cnt) {
+            if (whole) {
+                nid = p < nf ? *fslot(p) : -1;
+                fresh = nid >= 0;
+            } else if (p < cnt) {
                 nid = nbi[p];
                 fresh = visit_claim(vis, vmask, tag, nid, a.vis_full);
             }
@@ -420,6 +450,7 @@ void build_insert_batch(const BuildGraph& G, int metric, const float* x, const f
     a.rev_cap = rev_cap;
     a.nslots = nslots;
     a.vis_full = (int*)scratch_bytes("build_vis_full", 64);
+    a.collect = env_int("RVX_HNSW_COLLECT", 1) != 0 ? 1 : 0;  // (read per batch: tests build both ways)
     RVX_HIP(hipMemsetAsync(a.vis_full, 0, 4, stream()));
     RVX_HIP(hipMemsetAsync(a.visited, 0, (size_t)nslots * vcap * 8, stream()));
     const size_t lds = build_lds_bytes(d, ef_c, a.coop != 0, rg);

@@ -147,6 +147,46 @@ def test_hnsw_hbm_r_buffer_and_merge_forms_bit_exact(monkeypatch, wide_graph, ef
         assert np.array_equal(dist, rd), buf
 
 
+@pytest.fixture(scope="module")
+def long_list_graph():
+    return _hnsw_pair(6000, 32, 48, 100, 217)  # layer-0 lists of up to 96 > one 64-lane slice
+
+
+@pytest.mark.parametrize("rg", ["0", "1"])
+def test_hnsw_whole_list_fresh_batches_bit_exact(monkeypatch, long_list_graph, rg):
+    # a whole layer-0 list claimed first and its fresh neighbours admitted in batches of 64
+    # (RVX_HNSW_COLLECT=1, default) or slice by slice (0): the oracle's ids and distances, with R
+    # in LDS and in HBM
+    monkeypatch.setenv("RVX_HNSW_RG", rg)
+    x, h, idx = long_list_graph
+    q = O.fill_uniform(40 * 32, 218).reshape(40, 32)
+    for k, ef in ((10, 200), (50, 1500)):
+        rids, rd, rc = h.search(q, k, ef)
+        for col in ("1", "0"):
+            monkeypatch.setenv("RVX_HNSW_COLLECT", col)
+            ids, dist, cnt = idx.search_array(q, k, ef)
+            assert np.array_equal(cnt, rc), (col, k, ef)
+            assert np.array_equal(ids.astype(np.int64)[:, :k], rids), (col, k, ef)
+            assert np.array_equal(dist, rd), (col, k, ef)
+
+
+def test_hnsw_build_whole_list_batches_same_graph(monkeypatch):
+    # the builder's layer searches with whole lists claimed first and fresh neighbours batched
+    # (RVX_HNSW_COLLECT=1) build the same graph as slice by slice (0): layer-0 lists of up to 96
+    n, d = 5000, 32
+    x = O.fill_uniform(n * d, 219).reshape(n, d)
+    graphs = []
+    for col in ("1", "0"):
+        monkeypatch.setenv("RVX_HNSW_COLLECT", col)
+        idx = rv.HnswIndex(d, rv.DistanceMetric.Euclidean, rv.HnswConfig(m=48, ef_construction=120, ef_search=50),
+                           seed=5)
+        idx.add_array(x, np.arange(n, dtype=np.uint64))
+        graphs.append(idx.export_graph())
+    assert int(np.max(np.diff(np.asarray(graphs[0]["row_ptr0"])))) > 64
+    for key in ("levels", "row_ptr0", "col0"):
+        assert np.array_equal(np.asarray(graphs[0][key]), np.asarray(graphs[1][key])), key
+
+
 def test_flat_k_past_n_many_queries_small_budget(monkeypatch):
     # k > n over many queries — the wide scan's batches budget the whole per-query
     # footprint (row, selection histogram, min(k, n) keys) and select_topk sizes its keys by

@@ -255,11 +255,12 @@ def test_hnsw_search_query_global_bit_exact(monkeypatch, mode, d, metric):
 
 # (ef, LDS distance stages, R in HBM) the round-5 rules pick on the LDS-staged path (k_hnsw.hip
 # hnsw_nst / hnsw_search): d <= 768 one stage at ef 1,024..1,151, else two; R moves to HBM once an
-# LDS R leaves < 4 waves per CU (LDS bytes 8,192 * stages + 4d + 8 (ef + 1) + 768 > 40,960):
-# ef >= 2,592 at d 768, >= 2,464 at d 1,024 — each boundary straddled
-_WIDTH_RULES = {768: [(1023, 2, False), (1024, 1, False), (1151, 1, False), (1152, 2, False), (2591, 2, False),
-                      (2592, 2, True)],
-                1024: [(1023, 2, False), (1024, 2, False), (2463, 2, False), (2464, 2, True)]}
+# LDS R leaves < 4 waves per CU (LDS bytes 8,192 * stages + 4d + 8 (ef + 1) + 768 + 1,024 > 40,960):
+# ef >= 2,464 at d 768, >= 2,336 at d 1,024 — each boundary straddled; the HBM-R kernel runs one
+# distance stage (round 6, hnsw_rg_nst)
+_WIDTH_RULES = {768: [(1023, 2, False), (1024, 1, False), (1151, 1, False), (1152, 2, False), (2463, 2, False),
+                      (2464, 1, True)],
+                1024: [(1023, 2, False), (1024, 2, False), (2335, 2, False), (2336, 1, True)]}
 
 
 @pytest.mark.parametrize("d", [768, 1024])
