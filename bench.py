@@ -462,7 +462,8 @@ def c5_leg(a, comm, rank, world):
     all-gathered and merged on the GPU) in the exact mode (K10 Poincaré scan, the ground truth)
     and the tangent-pruned mode (search_with_pruning, hnsw.rs:450-490). The graph-search mode is
     left out: on this data the reference's graph rules give a non-navigable graph (recall@10
-    0.002 at 6.25M, DESIGN.md §6 C5 note), so pruned search is C5's fast path. value = exact
+    0.002 at 6.25M, DESIGN.md §6 C5 note); the pruned mode (recall 0.85) is reported beside the
+    exact one, which is as fast since the band pass (round 6). value = exact
     queries/s (recall 1.0) over the whole corpus; the exact mode's ids and distances are checked
     bit for bit against the oracle's scan of a query sample over every shard, whose rate on rank 0
     at N = 1 is the CPU baseline."""

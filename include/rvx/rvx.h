@@ -440,6 +440,11 @@ rvx_status rvx_scan_last_stats(int64_t* mfma_queries, int64_t* valu_queries, int
  * (one conversion chunk), after their first lists could not prove completeness; those still
  * unsure are the fallback queries above (an rvx extension for tests and benchmarks). */
 rvx_status rvx_scan_last_second_pass(int64_t* second_pass_queries);
+/* Queries of that scan still unsure after the list passes that took the band pass: every row whose
+ * filter value is within the bound the re-rank proved, then those rows' reference distances (one
+ * conversion chunk); a band past its capacity is a fallback query (an rvx extension for tests and
+ * benchmarks). */
+rvx_status rvx_scan_last_band(int64_t* band_queries);
 
 /* HNSW graph interchange (fixed-graph parity and GNN topology).
  * Layer 0: CSR over all n points in stored neighbour order (hnsw_rs keeps

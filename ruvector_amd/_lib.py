@@ -166,6 +166,7 @@ SIGNATURES = {
     "rvx_hnsw_last_search_visited": (None, [PI32, PI32]),
     "rvx_hnsw_last_search_form": (None, [PI32, PI32, PI32]),
     "rvx_scan_last_second_pass": (None, [PI64]),
+    "rvx_scan_last_band": (None, [PI64]),
     "rvx_index_sharded_search": (None, [P, P, PF32, I64, I32, I32, I32, PU64, PF32, PI32]),
     "rvx_index_sharded_search_device": (None, [P, P, P, I64, I32, I32, I32, P, P]),
     "rvx_index_load_graph": (None, [P, C.POINTER(HnswGraph)]),

@@ -252,7 +252,9 @@ def scan_last_stats() -> dict:
     _check("rvx_scan_last_stats", C.byref(a), C.byref(b), C.byref(c))
     s2 = C.c_int64()
     _check("rvx_scan_last_second_pass", C.byref(s2))
-    return {"mfma": a.value, "valu": b.value, "fallback": c.value, "second_pass": s2.value}
+    bd = C.c_int64()
+    _check("rvx_scan_last_band", C.byref(bd))
+    return {"mfma": a.value, "valu": b.value, "fallback": c.value, "second_pass": s2.value, "band": bd.value}
 
 
 class FlatIndex(_Index):

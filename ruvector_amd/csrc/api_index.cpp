@@ -563,6 +563,13 @@ rvx_status rvx_scan_last_second_pass(int64_t* second_pass_queries) {
     });
 }
 
+rvx_status rvx_scan_last_band(int64_t* band_queries) {
+    return guard([&] {
+        RVX_REQUIRE(band_queries, RVX_ERR_INVALID_PARAMETER, "null argument");
+        *band_queries = last_scan_stats().band_queries;
+    });
+}
+
 rvx_status rvx_hnsw_last_search_stats(int64_t* n_dist, int64_t* n_expand, int64_t* nq) {
     return guard([&] {
         ComputeLock cl;

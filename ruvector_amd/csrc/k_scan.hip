@@ -1088,6 +1088,7 @@ struct RerankArgs {
     const unsigned* xsq_max_bits;  // max_x |x|^2 (float bits)
     int64_t id_offset;
     float* out_d; int64_t* out_i; int32_t* unsure;
+    float* uthr;  // [nq] (nullable): an unsure query's proven bound D, for the band pass
 };
 
 template <int METRIC>
@@ -1140,6 +1141,7 @@ __global__ __launch_bounds__(256) void k_scan_rerank(RerankArgs a) {
         if (lane == 0) {
             a.unsure[qi] = 1;
             atomicAdd(a.unsure - 2, 1);  // flags[2]: how many queries need the VALU scan
+            if (a.uthr) a.uthr[qi] = D;
         }
         return;
     }
@@ -1281,6 +1283,7 @@ struct RerankPrArgs {
     float beta, curv;
     int64_t id_offset;
     float* out_d; int64_t* out_i; int32_t* unsure;
+    float* uthr;  // [nq] (nullable): an unsure query's proven bound thr, for the band pass
 };
 
 // one wave per query: Uk, candidates, reference distances, top-k by (distance, id)
@@ -1344,6 +1347,7 @@ __global__ __launch_bounds__(256) void k_scan_rerank_pr(RerankPrArgs a) {
         if (lane == 0) {
             a.unsure[qi] = 1;
             atomicAdd(a.unsure - 2, 1);
+            if (a.uthr) a.uthr[qi] = thr;
         }
         return;
     }
@@ -1397,6 +1401,177 @@ __global__ __launch_bounds__(256) void k_scan_rerank_pr(RerankPrArgs a) {
             if (better(od, oi, bd, bi)) { bd = od; bi = oi; }
         }
         if (lane == 0) { a.out_d[qi * a.k + s] = bd; a.out_i[qi * a.k + s] = bi; }
+        ld = bd;
+        li = bi;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Band pass: queries still unsure after the list passes (a split's FKP-long list
+// filled at or below the query's bound). The rerank proved a bound thr_q that every
+// row of the query's true top-k meets with its filter value (D = v_k + 2 eps; for the
+// per-row-bound metrics the tie-widened Uk, see k_scan_rerank_pr), and a lane's value
+// below meets the same error bound in any f32 summation order. So the band kernel
+// streams the f16 image once per 64 queries and appends EVERY row whose value is
+// <= thr_q — no list, nothing dropped — and the band rerank takes the reference
+// distances of exactly those rows: the same candidates' superset argument as the
+// lists, hence the same top-k bits as the VALU scan. A band longer than its capacity
+// sends the query on to the VALU scan. One wave: 32 rows x 64 queries per tile, the
+// f16 fragments straight from global memory (a row's 2 KB is read once per 64
+// queries; the query image stays in L2).
+struct BandArgs {
+    const _Float16* xh; const float2* xc; const float4* xc4;  // the whole table's f16 image and row factors
+    const _Float16* qh; const float2* qc;                      // band queries' f16 image and {1/t_q, |q|^2 or |q|}
+    int64_t nq, n; int d;
+    float beta;
+    const float* thr;  // [nq]
+    int32_t* cnt;      // [nq] band length (may exceed cap)
+    int32_t* cand;     // [nq][cap] rows
+    int cap;
+};
+
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_scan_band(BandArgs a) {
+    constexpr bool PRB = METRIC == RVX_METRIC_POINCARE || METRIC == METRIC_L2SQ;
+    const int lane = threadIdx.x & 63, lr = lane & 31, lh = lane >> 5;
+    const int64_t q0 = (int64_t)blockIdx.y * 64;
+    float qf[2], qs[2], qp[2], th[2];
+    int64_t qg[2];
+#pragma unroll
+    for (int fn = 0; fn < 2; ++fn) {
+        qg[fn] = q0 + fn * 32 + lr;
+        const int64_t qc = min(qg[fn], a.nq - 1);
+        const float2 c = a.qc[qc];
+        if constexpr (PRB) {
+            qf[fn] = -2.0f * c.x;
+            qs[fn] = c.y * (1.0f - a.beta);
+            qp[fn] = -0x1.8p-9f * sqrtf(c.y);
+        } else {
+            qf[fn] = query_factor<METRIC>(c.x, c.y);
+            qs[fn] = qp[fn] = 0.0f;
+        }
+        th[fn] = qg[fn] < a.nq ? a.thr[qc] : -INFINITY;  // padding query: nothing passes
+    }
+    const _Float16* qb0 = a.qh + min(q0 + lr, a.nq - 1) * a.d + 8 * lh;
+    const _Float16* qb1 = a.qh + min(q0 + 32 + lr, a.nq - 1) * a.d + 8 * lh;
+    const int64_t ntiles = (a.n + 31) / 32;
+    const int64_t wstride = (int64_t)gridDim.x * 4;
+    for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < ntiles; t += wstride) {
+        const int64_t r0 = t * 32;
+        const _Float16* xb = a.xh + min(r0 + lr, a.n - 1) * a.d + 8 * lh;
+        f32x16 acc0, acc1;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc0[e] = acc1[e] = 0.0f;
+#pragma unroll 4
+        for (int k0 = 0; k0 < a.d; k0 += 16) {
+            const h16x8 av = *reinterpret_cast<const h16x8*>(xb + k0);
+            const h16x8 b0 = *reinterpret_cast<const h16x8*>(qb0 + k0);
+            const h16x8 b1 = *reinterpret_cast<const h16x8*>(qb1 + k0);
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, b0, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, b1, acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int64_t row = r0 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+            if (row >= a.n) continue;
+            float v[2];
+            if constexpr (PRB) {
+                const float4 c = a.xc4[row];
+                v[0] = __builtin_fmaf(c.w, qp[0], __builtin_fmaf(c.z, qs[0], __builtin_fmaf(acc0[e] * c.x, qf[0], c.y)));
+                v[1] = __builtin_fmaf(c.w, qp[1], __builtin_fmaf(c.z, qs[1], __builtin_fmaf(acc1[e] * c.x, qf[1], c.y)));
+            } else {
+                const float2 f = row_factors<METRIC>(a.xc[row]);
+                v[0] = __builtin_fmaf(acc0[e] * f.x, qf[0], f.y);
+                v[1] = __builtin_fmaf(acc1[e] * f.x, qf[1], f.y);
+            }
+#pragma unroll
+            for (int fn = 0; fn < 2; ++fn)
+                if (v[fn] <= th[fn]) {  // NaN (deleted row) never passes
+                    const int pos = atomicAdd(a.cnt + qg[fn], 1);
+                    if (pos < a.cap) a.cand[qg[fn] * a.cap + pos] = (int32_t)row;
+                }
+        }
+    }
+}
+
+struct BandRerankArgs {
+    const float* q; const float* qnorm;  // band queries [nq][d]; reference norms (cosine)
+    const float* x; const float* xnorm;  // rows; reference norms (cosine)
+    const int32_t* cnt; const int32_t* cand; int cap;
+    float* dist;  // [nq][cap] scratch
+    int64_t nq; int d, k; float curv;
+    int64_t id_offset;
+    float* out_d; int64_t* out_i;  // [nq][k]
+};
+
+// one block per band query: the reference distance of every band row (the rerank's
+// arithmetic), then k rounds of a block-wide (distance, id) minimum
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_scan_band_rerank(BandRerankArgs a) {
+    const int64_t qi = blockIdx.x;
+    const int m = a.cnt[qi];
+    if (m > a.cap) return;  // the VALU scan owns this query
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float* qrow = a.q + qi * a.d;
+    const int32_t* cr = a.cand + qi * a.cap;
+    float* dr = a.dist + qi * a.cap;
+    for (int c = tid; c < m; c += 256) {
+        const float* xr = a.x + (int64_t)cr[c] * a.d;
+        float ex;
+        if constexpr (METRIC == RVX_METRIC_POINCARE) {  // fused_norms chunk order, then from_norms (as K8)
+            float ds = 0.0f, nu = 0.0f, nv = 0.0f;
+            for (int kk = 0; kk < a.d; kk += 4) {
+                const float4 qv = *reinterpret_cast<const float4*>(qrow + kk);
+                const float4 xv = *reinterpret_cast<const float4*>(xr + kk);
+                const float d0 = qv.x - xv.x, d1 = qv.y - xv.y, d2 = qv.z - xv.z, d3 = qv.w - xv.w;
+                ds = ds + (((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3);
+                nu = nu + (((qv.x * qv.x + qv.y * qv.y) + qv.z * qv.z) + qv.w * qv.w);
+                nv = nv + (((xv.x * xv.x + xv.y * xv.y) + xv.z * xv.z) + xv.w * xv.w);
+            }
+            ex = pdev::from_norms(ds, nu, nv, a.curv);
+        } else {  // sequential sum in the reference order (tangent_distance_squared: no finish)
+            float acc = 0.0f;
+            for (int kk = 0; kk < a.d; kk += 4) {
+                const float4 qv = *reinterpret_cast<const float4*>(qrow + kk);
+                const float4 xv = *reinterpret_cast<const float4*>(xr + kk);
+                acc = pair_step<METRIC>(acc, qv.x, xv.x);
+                acc = pair_step<METRIC>(acc, qv.y, xv.y);
+                acc = pair_step<METRIC>(acc, qv.z, xv.z);
+                acc = pair_step<METRIC>(acc, qv.w, xv.w);
+            }
+            if constexpr (METRIC == METRIC_L2SQ) ex = acc;
+            else ex = pair_finish<METRIC>(acc, METRIC == RVX_METRIC_COSINE ? a.qnorm[qi] : 0.0f,
+                                          METRIC == RVX_METRIC_COSINE ? a.xnorm[cr[c]] : 0.0f);
+        }
+        dr[c] = ex;
+    }
+    __syncthreads();
+    __shared__ float sd[4];
+    __shared__ int64_t si[4];
+    float ld = -INFINITY;
+    int64_t li = INT64_MIN;
+    for (int s = 0; s < a.k; ++s) {
+        float bd = INFINITY;
+        int64_t bi = INT64_MAX;
+        for (int c = tid; c < m; c += 256) {
+            const float dv = dr[c];
+            const int64_t id = (int64_t)cr[c] + a.id_offset;
+            const bool after = dv > ld || (dv == ld && id > li);
+            if (after && better(dv, id, bd, bi)) { bd = dv; bi = id; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float od = __shfl_xor(bd, o);
+            const int64_t oi = __shfl_xor(bi, o);
+            if (better(od, oi, bd, bi)) { bd = od; bi = oi; }
+        }
+        if (lane == 0) { sd[wave] = bd; si[wave] = bi; }
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (better(sd[w], si[w], bd, bi)) { bd = sd[w]; bi = si[w]; }
+        __syncthreads();  // every wave has read sd / si before the next round writes them
+        if (tid == 0) { a.out_d[qi * a.k + s] = bd; a.out_i[qi * a.k + s] = bi; }
         ld = bd;
         li = bi;
     }
@@ -1655,15 +1830,15 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     };
     // the reference-order rerank of nqq queries' lists (qq rows, their norms and f16 constants)
     auto launch_rerank = [&](const float* qq, const float* qqn, const float2* qqc, int64_t nqq, int nsplit,
-                             float* pv, int32_t* pr, float* od, int64_t* oi, int32_t* uns) {
+                             float* pv, int32_t* pr, float* od, int64_t* oi, int32_t* uns, float* ut) {
         const dim3 rg((unsigned)((nqq + 3) / 4));
         if (prb) {
-            RerankPrArgs rp{qq, qqc, x, rb, nqq, d, k, nsplit, pv, pr, beta, curv, id_offset, od, oi, uns};
+            RerankPrArgs rp{qq, qqc, x, rb, nqq, d, k, nsplit, pv, pr, beta, curv, id_offset, od, oi, uns, ut};
             if (metric == RVX_METRIC_POINCARE) RVX_LAUNCH("scan_rerank", k_scan_rerank_pr<RVX_METRIC_POINCARE>, rg, dim3(256), 0, rp);
             else RVX_LAUNCH("scan_rerank", k_scan_rerank_pr<METRIC_L2SQ>, rg, dim3(256), 0, rp);
             return;
         }
-        RerankArgs ra{qq, qqn, qqc, x, xnorm, nqq, d, k, nsplit, pv, pr, max_bits, id_offset, od, oi, uns};
+        RerankArgs ra{qq, qqn, qqc, x, xnorm, nqq, d, k, nsplit, pv, pr, max_bits, id_offset, od, oi, uns, ut};
         switch (metric) {
             case RVX_METRIC_L2: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_L2>, rg, dim3(256), 0, ra); break;
             case RVX_METRIC_COSINE: RVX_LAUNCH("scan_rerank", k_scan_rerank<RVX_METRIC_COSINE>, rg, dim3(256), 0, ra); break;
@@ -1689,7 +1864,10 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
                       part_v, part_r, gbound, k, max_bits, xc4, beta};
         launch_filter(fa, dim3((unsigned)(qtiles * s_c)));
     }
-    launch_rerank(q, qnorm, qc, nq, nsplit_total, part_v, part_r, out_d, out_i, unsure);
+    // the bound each unsure query proved (one conversion chunk: for the band pass)
+    const bool band = nchunks == 1 && env_int("RVX_SCAN_BAND", 1) != 0;
+    float* uthr = band ? scratch_f32("mscan_uthr", nq) : nullptr;
+    launch_rerank(q, qnorm, qc, nq, nsplit_total, part_v, part_r, out_d, out_i, unsure, uthr);
     // flags[0] bad input, flags[2] unsure-query count: 16 B through a pinned
     // host word; the per-query flags come down only when some query is unsure
     static int32_t* hflags = nullptr;
@@ -1715,6 +1893,9 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     }
     last_scan_stats().mfma_queries += nq;
     if (redo.empty()) return true;
+    // where each query left in redo has its bound: thr_src[thr_idx[i]]
+    const float* thr_src = uthr;
+    std::vector<int32_t> thr_idx = redo;
     // Second pass (one conversion chunk: the f16 image of every row is still in scratch): the
     // queries whose lists could not prove completeness run the filter again on their own with as
     // many splits as the rerank holds — each FKP-long list then covers fewer rows, so far fewer
@@ -1747,28 +1928,94 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
             float* pv2 = scratch_f32("mscan2_part_v", c2 * nsplit2 * FKP);
             int32_t* pr2 = (int32_t*)scratch_bytes("mscan2_part_r", c2 * nsplit2 * FKP * 4);
             float* rd2 = scratch_f32("mscan2_d", c2 * k);
+            float* uthr2 = band ? scratch_f32("mscan2_uthr", c2) : nullptr;
             int64_t* ri2 = (int64_t*)scratch_bytes("mscan2_i", c2 * k * 8);
             rows_to_f16(q2, c2, d, qh2, qc2, q2n, nullptr, nullptr, flags2);
             FilterArgs fa2{xh, xc, qh2, qc2, c2, 0, n, d, rps2, 0, (int)qtiles2, nsplit2, pv2, pr2, gbound2, k, max_bits,
                            xc4, beta};
             launch_filter(fa2, dim3((unsigned)(qtiles2 * nsplit2)));
-            launch_rerank(q2, q2n, qc2, c2, nsplit2, pv2, pr2, rd2, ri2, flags2 + 4);
+            launch_rerank(q2, q2n, qc2, c2, nsplit2, pv2, pr2, rd2, ri2, flags2 + 4, uthr2);
             RVX_LAUNCH("scan_gather", k_scatter_topk, dim3((unsigned)((c2 * k + 255) / 256)), dim3(256), 0, rd2, ri2,
                        didx2, c2, k, out_d, out_i);
             RVX_HIP(hipMemcpyAsync(hflags, flags2, 16, hipMemcpyDeviceToHost, stream()));
             sync();
             last_scan_stats().second_pass_queries += c2;
-            std::vector<int32_t> still;
+            std::vector<int32_t> still, still_i;
             if (hflags[2] > 0) {
                 std::vector<int32_t> h(c2);
                 RVX_HIP(hipMemcpyAsync(h.data(), flags2 + 4, (size_t)(c2 * 4), hipMemcpyDeviceToHost, stream()));
                 sync();
                 for (int64_t i = 0; i < c2; ++i)
-                    if (h[i]) still.push_back(redo[i]);
+                    if (h[i]) {
+                        still.push_back(redo[i]);
+                        still_i.push_back((int32_t)i);
+                    }
             }
             redo.swap(still);
+            thr_idx.swap(still_i);
+            thr_src = uthr2;
             if (redo.empty()) return true;
         }
+    }
+    // Band pass (k_scan_band): the queries still unsure take every row whose value is within
+    // their proven bound, and the reference distances of those rows (C5's 6.25M x 1024 exact
+    // Poincaré scan: 52 of 10k queries left after the second pass, whose VALU scan took 60 of
+    // 233 ms). Same bits as the VALU scan; a band past its capacity still goes there.
+    // RVX_SCAN_BAND=0 skips it, RVX_SCAN_BAND_CAP caps rows per query (tests).
+    if (band) {
+        const int64_t nb = (int64_t)redo.size();
+        const int64_t cap_env = env_int("RVX_SCAN_BAND_CAP", 65536);
+        const int cap = (int)std::max<int64_t>(
+            1, std::min<int64_t>(cap_env, std::max<int64_t>(1024, ((int64_t)1 << 30) / (8 * nb))));
+        int32_t* bidx = (int32_t*)scratch_bytes("mscanb_idx", nb * 4);
+        int32_t* btix = (int32_t*)scratch_bytes("mscanb_tidx", nb * 4);
+        RVX_HIP(hipMemcpyAsync(bidx, redo.data(), (size_t)nb * 4, hipMemcpyHostToDevice, stream()));
+        RVX_HIP(hipMemcpyAsync(btix, thr_idx.data(), (size_t)nb * 4, hipMemcpyHostToDevice, stream()));
+        float* bthr = scratch_f32("mscanb_thr", nb);
+        RVX_LAUNCH("scan_gather", k_gather_rows, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, thr_src, btix, nb, 1,
+                   bthr);
+        float* bq = scratch_f32("mscanb_q", nb * d);
+        RVX_LAUNCH("scan_gather", k_gather_rows, dim3((unsigned)((nb * d + 255) / 256)), dim3(256), 0, q, bidx, nb, d,
+                   bq);
+        float* bqn = nullptr;
+        if (cos) {
+            bqn = scratch_f32("mscanb_qn", nb);
+            RVX_LAUNCH("scan_gather", k_gather_rows, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, qnorm, bidx, nb,
+                       1, bqn);
+        }
+        _Float16* bqh = (_Float16*)scratch_bytes("mscanb_qh", nb * d * 2);
+        float2* bqc = (float2*)scratch_bytes("mscanb_qc", nb * 8);
+        int32_t* bcnt = (int32_t*)scratch_bytes("mscanb_cnt", 16 + nb * 4);  // [0..3] the conversion's bad flag
+        RVX_HIP(hipMemsetAsync(bcnt, 0, (size_t)(16 + nb * 4), stream()));
+        rows_to_f16(bq, nb, d, bqh, bqc, bqn, nullptr, nullptr, bcnt);
+        int32_t* bcand = (int32_t*)scratch_bytes("mscanb_cand", nb * cap * 4);
+        float* bdist = scratch_f32("mscanb_dist", nb * cap);
+        float* bd = scratch_f32("mscanb_d", nb * k);
+        int64_t* bi = (int64_t*)scratch_bytes("mscanb_i", nb * k * 8);
+        BandArgs ba{xh, xc, xc4, bqh, bqc, nb, n, d, beta, bthr, bcnt + 4, bcand, cap};
+        const int64_t wtiles = (n + 31) / 32;
+        const dim3 bg((unsigned)std::max<int64_t>(1, std::min<int64_t>((wtiles + 3) / 4, 2048)), (unsigned)((nb + 63) / 64));
+        BandRerankArgs br{bq, bqn, x, xnorm, bcnt + 4, bcand, cap, bdist, nb, d, k, curv, id_offset, bd, bi};
+        switch (metric) {
+#define RVX_BAND(M)                                                                                       RVX_LAUNCH("scan_band", k_scan_band<M>, bg, dim3(256), 0, ba);                                        RVX_LAUNCH("scan_band", k_scan_band_rerank<M>, dim3((unsigned)nb), dim3(256), 0, br);                 break;
+            case RVX_METRIC_L2: RVX_BAND(RVX_METRIC_L2)
+            case RVX_METRIC_COSINE: RVX_BAND(RVX_METRIC_COSINE)
+            case RVX_METRIC_POINCARE: RVX_BAND(RVX_METRIC_POINCARE)
+            case METRIC_L2SQ: RVX_BAND(METRIC_L2SQ)
+            default: RVX_BAND(RVX_METRIC_DOT)
+#undef RVX_BAND
+        }
+        RVX_LAUNCH("scan_gather", k_scatter_topk, dim3((unsigned)((nb * k + 255) / 256)), dim3(256), 0, bd, bi, bidx, nb,
+                   k, out_d, out_i);
+        std::vector<int32_t> h((size_t)nb);
+        RVX_HIP(hipMemcpyAsync(h.data(), bcnt + 4, (size_t)nb * 4, hipMemcpyDeviceToHost, stream()));
+        sync();
+        last_scan_stats().band_queries += nb;
+        std::vector<int32_t> still;
+        for (int64_t i = 0; i < nb; ++i)
+            if (h[(size_t)i] > cap) still.push_back(redo[(size_t)i]);  // band past capacity
+        redo.swap(still);
+        if (redo.empty()) return true;
     }
     last_scan_stats().fallback_queries += (int64_t)redo.size();
     // queries whose lists could not prove completeness: exact VALU scan

@@ -16,6 +16,7 @@ constexpr int METRIC_L2SQ = 16;
 struct ScanStats {
     int64_t mfma_queries = 0, valu_queries = 0, fallback_queries = 0;
     int64_t second_pass_queries = 0;  // unsure after the first filter, run again with the most splits
+    int64_t band_queries = 0;         // still unsure: every row within the proven bound (k_scan_band)
 };
 ScanStats& last_scan_stats();
 

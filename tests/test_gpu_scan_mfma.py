@@ -101,10 +101,16 @@ def test_removed_rows_are_skipped(monkeypatch):
     assert np.array_equal(ids.astype(np.int64), rids)
 
 
-def test_duplicates_fall_back_and_stay_exact(monkeypatch):
+@pytest.mark.parametrize("band,cap", [("1", None), ("1", "8"), ("0", None)])
+def test_duplicates_fall_back_and_stay_exact(monkeypatch, band, cap):
     # 40 copies of every base row: a split's list fills with equal values, so
-    # completeness cannot be proven and those queries take the exact VALU scan
+    # completeness cannot be proven from the lists; those queries take the band pass
+    # (every row within the proven bound, k_scan_band) or, band off or past its
+    # capacity (RVX_SCAN_BAND_CAP), the exact VALU scan — the same bits every way
     monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    monkeypatch.setenv("RVX_SCAN_BAND", band)
+    if cap:
+        monkeypatch.setenv("RVX_SCAN_BAND_CAP", cap)
     d = 32
     base = O.fill_uniform(150 * d, 9).reshape(150, d)
     x = np.repeat(base, 40, axis=0)
@@ -112,8 +118,12 @@ def test_duplicates_fall_back_and_stay_exact(monkeypatch):
     for metric, name in METRICS:
         ids, dist = flat(x, metric).brute_force_array(q, 12)
         st = rv.scan_last_stats()
-        assert st["mfma"] == 260 and st["fallback"] > 0, st
-        assert st["second_pass"] >= st["fallback"], st  # the unsure queries' second filter first
+        assert st["mfma"] == 260, st
+        assert st["second_pass"] >= st["band"] > 0 if band == "1" else st["band"] == 0, st
+        if band == "1" and not cap:
+            assert st["fallback"] == 0, st  # 40-row ties fit a band
+        else:
+            assert st["fallback"] > 0 and st["second_pass"] >= st["fallback"], st
         rids, rd = O.flat_search(x, q, 12, name)
         assert np.array_equal(ids.astype(np.int64), rids) and np.array_equal(dist, rd)
 
@@ -291,3 +301,34 @@ def test_poincare_second_pass_same_bits(monkeypatch, second):
         assert st["second_pass"] == 0, st
     rids, rd = O.hyp_scan_rows(x, q, k, threads=8)  # the oracle's exact Poincaré scan (poincare.rs order)
     assert np.array_equal(np.asarray(ids, np.int64), rids) and np.array_equal(dist, rd)
+
+
+@pytest.mark.parametrize("band", ["1", "0"])
+def test_poincare_band_pass_duplicates(monkeypatch, band):
+    """Ball rows repeated 40 times: the exact Poincaré scan (and the tangent-pruned scan's squared
+    L2) cannot prove completeness from FKP-long lists; the band pass (RVX_SCAN_BAND, default on)
+    resolves the queries from every row within the bound, RVX_SCAN_BAND=0 sends them to the VALU
+    scan: ids and distances are the oracle's (poincare.rs order) either way."""
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    monkeypatch.setenv("RVX_SCAN_BAND", band)
+    d, k = 64, 10
+    base = ball_points(500, d, 301)
+    x = np.repeat(base, 40, axis=0)
+    q = ball_points(300, d, 302)
+    h = rv.HyperbolicHnsw(rv.HyperbolicHnswConfig(seed=4, ef_construction=16, max_connections=4,
+                                                  max_connections_0=8), dim=d)
+    h.insert_batch(x)
+    ids, dist, _ = h.brute_force(q, k)
+    st = rv.scan_last_stats()
+    assert st["mfma"] == 300, st
+    if band == "1":
+        assert st["band"] > 0 and st["fallback"] == 0, st
+    else:
+        assert st["band"] == 0 and st["fallback"] > 0, st
+    rids, rd = O.hyp_scan_rows(x, q, k, threads=8)
+    assert np.array_equal(np.asarray(ids, np.int64), rids) and np.array_equal(dist, rd)
+    h.build_tangent_cache()
+    pids, pdist, _ = h.search_with_pruning_batch(q, k)
+    monkeypatch.setenv("RVX_SCAN_MFMA", "0")
+    vids, vdist, _ = h.search_with_pruning_batch(q, k)
+    assert np.array_equal(pids, vids) and np.array_equal(pdist, vdist)
