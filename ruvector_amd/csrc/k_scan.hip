@@ -1965,8 +1965,10 @@ bool scan_topk_mfma(int metric, const float* q, const float* qnorm, int64_t nq, 
     if (band) {
         const int64_t nb = (int64_t)redo.size();
         const int64_t cap_env = env_int("RVX_SCAN_BAND_CAP", 65536);
+        // rows per query: 64k by default, fewer when many queries are unsure (the row ids and
+        // their distances stay within ~1 GiB up to 2M band queries)
         const int cap = (int)std::max<int64_t>(
-            1, std::min<int64_t>(cap_env, std::max<int64_t>(1024, ((int64_t)1 << 30) / (8 * nb))));
+            1, std::min<int64_t>(cap_env, std::max<int64_t>(64, ((int64_t)1 << 30) / (8 * nb))));
         int32_t* bidx = (int32_t*)scratch_bytes("mscanb_idx", nb * 4);
         int32_t* btix = (int32_t*)scratch_bytes("mscanb_tidx", nb * 4);
         RVX_HIP(hipMemcpyAsync(bidx, redo.data(), (size_t)nb * 4, hipMemcpyHostToDevice, stream()));
