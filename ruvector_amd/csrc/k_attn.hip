@@ -70,7 +70,73 @@ __global__ __launch_bounds__(256) void k_edge_feat_scores(EfaArgs a) {
     }
 }
 
-// stable_softmax per (node, head), in place over the score scratch.
+// Scores and their stable_softmax in one pass (one wave per destination node): the lanes
+// take the node's (edge, head) scores in storage order (coalesced stores, neighbour head dots
+// read as runs), keep them in LDS, one lane per head runs the softmax's max / sequential sum /
+// normalisation in edge order exactly as k_edge_feat_softmax, and the lanes store the weights.
+// Same expressions, same order, same bits as the two-kernel form (RVX_EFA_FUSED=0); a node
+// with more than EFA_LCAP (edge, head) scores writes raw scores for k_edge_feat_softmax.
+constexpr int EFA_LCAP = 2048;
+__global__ __launch_bounds__(256) void k_edge_feat_scores_sm(EfaArgs a) {
+    __shared__ float sbuf[4][EFA_LCAP];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t i = (int64_t)blockIdx.x * 4 + w;
+    if (i >= a.n) return;
+    const int heads = a.heads, ed = a.edge_dim;
+    const int64_t beg = a.rp[i], end = a.rp[i + 1];
+    const int64_t cnt = end - beg, tot = cnt * heads;
+    const bool fused = tot <= EFA_LCAP;
+    float* sb = sbuf[w];
+    for (int64_t t = lane; t < tot; t += 64) {
+        const int64_t e = beg + t / heads;
+        const int h = (int)(t % heads);
+        const int64_t j = a.col[e];
+        float te = 0.0f;
+        if (a.edges) {
+            const float* ef = a.edges + e * (int64_t)ed;
+            for (int kk = 0; kk < ed; ++kk) te = te + ef[kk] * a.u[h * ed + kk];
+        }
+        const float score = (a.sq[i * heads + h] + a.sk[j * heads + h]) + te;
+        const float v = score < 0.0f ? a.slope * score : score;
+        if (fused) sb[t] = v;
+        else a.scores[beg * heads + t] = v;
+    }
+    if (!fused || cnt == 0) return;
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    for (int h = lane; h < heads; h += 64) {
+        float mx = -INFINITY;
+        for (int64_t e = 0; e < cnt; ++e) {
+            const float v = sb[e * heads + h];
+            if (isfinite(v)) mx = fmaxf(mx, v);
+        }
+        if (!isfinite(mx)) {
+            for (int64_t e = 0; e < cnt; ++e) sb[e * heads + h] = 1.0f / (float)cnt;
+            continue;
+        }
+        float sum = 0.0f;
+        for (int64_t e = 0; e < cnt; ++e) {
+            const float v = sb[e * heads + h];
+            sum = sum + (isfinite(v) ? expf(v - mx) : 0.0f);
+        }
+        if (sum <= 1e-10f || !isfinite(sum)) {
+            for (int64_t e = 0; e < cnt; ++e) sb[e * heads + h] = 1.0f / (float)cnt;
+            continue;
+        }
+        const float inv = 1.0f / sum;
+        for (int64_t e = 0; e < cnt; ++e) {
+            const float v = sb[e * heads + h];
+            sb[e * heads + h] = (isfinite(v) ? expf(v - mx) : 0.0f) * inv;
+        }
+    }
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    for (int64_t t = lane; t < tot; t += 64) a.scores[beg * heads + t] = sb[t];
+}
+
+// stable_softmax per (node, head), in place over the score scratch. SKIP: nodes the fused
+// kernel above already normalised (at most EFA_LCAP scores) are left alone.
+template <bool SKIP>
 __global__ void k_edge_feat_softmax(EfaArgs a) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= a.n * a.heads) return;
@@ -79,6 +145,7 @@ __global__ void k_edge_feat_softmax(EfaArgs a) {
     const int64_t beg = a.rp[i], end = a.rp[i + 1];
     const int64_t cnt = end - beg;
     if (cnt == 0) return;
+    if (SKIP && cnt * a.heads <= EFA_LCAP) return;
     float mx = -INFINITY;
     for (int64_t e = beg; e < end; ++e) {
         const float v = a.scores[e * a.heads + h];
@@ -368,8 +435,15 @@ void edge_feat_attention(const EfaArgs& a) {
         RVX_LAUNCH("efa_node_dots", k_efa_edge_u, dim3((unsigned)((nu + 255) / 256)), dim3(256), 0, a.w_edge, a.a_edge,
                    a.heads, a.hd, a.edge_dim, a.u);
     }
-    RVX_LAUNCH("efa_scores", k_edge_feat_scores, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, a);
-    RVX_LAUNCH("efa_softmax", k_edge_feat_softmax, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, a);
+    // scores + softmax fused (RVX_EFA_FUSED=1, default; read per call): the second kernel then only
+    // takes nodes past EFA_LCAP scores
+    if (env_int("RVX_EFA_FUSED", 1)) {
+        RVX_LAUNCH("efa_scores", k_edge_feat_scores_sm, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, a);
+        RVX_LAUNCH("efa_softmax", k_edge_feat_softmax<true>, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, a);
+    } else {
+        RVX_LAUNCH("efa_scores", k_edge_feat_scores, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, a);
+        RVX_LAUNCH("efa_softmax", k_edge_feat_softmax<false>, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, a);
+    }
     const bool vec = a.concat && a.hd % 4 == 0 && a.ldv % 4 == 0 && al16(a.tv) && al16(a.out) && D <= 1024 &&
                      env_int("RVX_EFA_VEC", 1);
     const dim3 og((unsigned)((a.n + 3) / 4)), ob(256);

@@ -1344,3 +1344,39 @@ def test_graphsage_gemm_helps_gather_bits(monkeypatch, aggregator, dims, n, deg,
     b = _sage_stack(layers, g, x, n, True)
     for u, v in zip(a, b):
         assert np.array_equal(u, v)
+
+
+@pytest.mark.parametrize("heads,edge_dim", [(8, 1), (4, 3), (5, 2)])
+def test_edge_attention_fused_softmax_bits(monkeypatch, heads, edge_dim):
+    """Scores and stable_softmax in one kernel (k_edge_feat_scores_sm, RVX_EFA_FUSED default on)
+    write the same bits as the score kernel + softmax kernel pair (RVX_EFA_FUSED=0): degrees 0 to
+    40, nodes whose (edge, head) scores exceed the LDS buffer (> 2048: the softmax kernel takes
+    them) or fill it exactly, a node whose neighbours are all one row (tied scores), and the oracle
+    on a sample."""
+    node_dim, n = 16 * heads, 300
+    att = rv.EdgeFeaturedAttention(rv.EdgeFeaturedConfig(node_dim=node_dim, edge_dim=edge_dim, num_heads=heads))
+    x = O.fill_uniform(n * node_dim, 41).reshape(n, node_dim)
+    rng = np.random.default_rng(heads)
+    degs = rng.integers(0, 41, n)
+    degs[::13] = 0
+    degs[7] = 2048 // heads + 5  # past the fused kernel's buffer
+    degs[8] = 2048 // heads      # exactly at it
+    rp = np.concatenate([[0], np.cumsum(degs)]).astype(np.int64)
+    col = rng.integers(0, n, int(rp[-1])).astype(np.int32)
+    col[rp[9]:rp[10]] = col[rp[9]]  # one node whose neighbours are all the same row
+    ef = O.fill_uniform(int(rp[-1]) * edge_dim, 42, 0.0, 1.0)
+    g = rv.Graph.from_csr(rp, col)
+    xb, eb = rv.Buffer.from_numpy(x), rv.Buffer.from_numpy(ef)
+    ys = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("RVX_EFA_FUSED", fused)
+        yb = rv.Buffer(x.nbytes)
+        att.forward_graph_device(xb, g, eb, yb)
+        ys.append(yb.download(np.float32, x.shape))
+    assert np.array_equal(ys[0], ys[1])
+    for i in (1, 7, 8, 9, 33):
+        nb = col[rp[i]:rp[i + 1]]
+        if len(nb):
+            ref = O.efa_compute(node_dim, edge_dim, heads, x[i], x[nb], x[nb],
+                                ef[rp[i] * edge_dim:rp[i + 1] * edge_dim].reshape(-1, edge_dim))
+            assert_close(ys[1][i], ref)
