@@ -237,11 +237,7 @@ __device__ __forceinline__ void build_insert_body(const BuildArgs& a) {
             if (rs == 0) continue;
             const int nb_conn = l == 0 ? a.G.C0 : a.G.M;
             int ss = 0;
-#ifdef RVX_BUILD_NOSEL  // timing diagnostic only (scripts/exp/build_variant.sh): closest nb_conn, no heuristic
-            if (true) {
-#else
             if (rs <= nb_conn || a.hyper) {
-#endif
                 // all of R, or (HyperbolicHnsw, hnsw.rs:225) its closest nb_conn
                 ss = min(rs, nb_conn);
                 for (int i = lane; i < ss; i += 64) { sd[i] = rd[i]; si[i] = ri[i]; }
