@@ -332,3 +332,29 @@ def test_poincare_band_pass_duplicates(monkeypatch, band):
     monkeypatch.setenv("RVX_SCAN_MFMA", "0")
     vids, vdist, _ = h.search_with_pruning_batch(q, k)
     assert np.array_equal(pids, vids) and np.array_equal(pdist, vdist)
+
+
+@pytest.mark.parametrize("metric,name", METRICS)
+def test_band_pass_skips_removed_rows(monkeypatch, metric, name):
+    """Duplicate-heavy rows (the lists cannot settle the queries, the band pass does) with every
+    third row removed: the band kernel must skip the removed rows exactly as the lists do
+    (NaN row factor), results equal to the oracle's scan over the live rows."""
+    monkeypatch.setenv("RVX_SCAN_MFMA", "2")
+    n_base, d = 200, 64
+    base = O.fill_uniform(n_base * d, 231).reshape(n_base, d)
+    x = np.repeat(base, 30, axis=0)
+    n = len(x)
+    idx = rv.FlatIndex(d, metric)
+    idx.add_batch([(f"v{i}", x[i]) for i in range(n)])
+    gone = list(range(0, n, 3))
+    for i in gone:
+        assert idx.remove(f"v{i}")
+    q = O.fill_uniform(300 * d, 232).reshape(300, d)
+    ids, dist, _ = idx.search_array(q, 10)
+    st = rv.scan_last_stats()
+    assert st["mfma"] == 300 and st["band"] > 0 and st["fallback"] == 0, st
+    deleted = np.zeros(n, np.uint8)
+    deleted[gone] = 1
+    rids, rd = O.flat_search(x, q, 10, name, deleted=deleted)
+    assert np.array_equal(dist, rd)
+    assert np.array_equal(ids.astype(np.int64), rids)
